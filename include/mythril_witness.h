@@ -1,0 +1,113 @@
+/* mythril_witness.h — C-ABI of the MI355X constraint-witness engine.
+ *
+ * Drop-in boundary.  The reference has no native FFI of its
+ * own on this path: Mythril is pure Python and crosses into native code only
+ * through z3-solver's and pysha3's ctypes/C-extension bindings.  Each entry
+ * point below replaces one of those crossings and is bound from Python with
+ * ctypes exactly the way z3's own bindings are:
+ *
+ *   mg_search     replaces z3 Optimize.check() for feasibility-only queries
+ *                 (mythril/laser/smt/solver/solver.py:50-66, reached from
+ *                  mythril/support/model.py:58 get_model)
+ *   mg_eval       replaces z3 ModelRef.eval / substitute+simplify for a batch
+ *                 of assignments (mythril/laser/smt/model.py:52-59)
+ *   mg_keccak256  replaces _pysha3.keccak_256 (mythril/support/support_utils.py:50-59,
+ *                 called by keccak_function_manager.py:57-69 find_concrete_keccak)
+ *
+ * Conventions: every call returns 0 on success or a negative MG_E* code; the
+ * message for the calling thread is in mg_last_error().  The caller owns all
+ * host buffers (copied in/out); program handles are library-owned until
+ * mg_prog_free.  Nothing throws across the ABI.  A context serialises its
+ * calls.  Programs are validated on load (slot ranges, constant offsets,
+ * opcodes) so a malformed program can never be launched.
+ */
+#ifndef MYTHRIL_WITNESS_H
+#define MYTHRIL_WITNESS_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MG_OK 0
+#define MG_E_ARG -1
+#define MG_E_HIP -2
+#define MG_E_PROG -3
+#define MG_E_NOMEM -4
+
+#define MG_NONE UINT64_MAX /* no witness in the searched range */
+
+/* search flags (same values as MW_FLAG_* in mw_isa.h) */
+#define MG_FLAG_EARLY_EXIT 1u
+#define MG_FLAG_STOP_AFTER_HIT 2u
+
+typedef struct mg_ctx mg_ctx;
+typedef struct mg_prog mg_prog;
+
+/* A compiled constraint program (produced by mythril_amd.compiler). */
+typedef struct {
+  const uint32_t* code;   /* 4 words per instruction, ends with MW_END */
+  size_t ncode_words;
+  const uint32_t* consts; /* constant pool words */
+  size_t nconst_words;
+  const uint32_t* leaves; /* MW_LEAF_WORDS words per free variable */
+  size_t nleaves;
+  const uint32_t* pool;   /* candidate pools, MW_POOL_ENTRY_WORDS per entry */
+  size_t npool_words;
+  uint32_t n_spill;       /* spill slots (8 limbs each) the program uses */
+  uint32_t n_trace_rows;  /* rows written by MW_STORE_* (mg_eval trace) */
+  uint32_t n_input_rows;  /* SoA leaf rows mg_eval reads */
+  uint32_t reserved;
+  uint64_t ops_per_eval;  /* algorithmic u32 ops per candidate */
+} mg_prog_desc;
+
+typedef struct {
+  double kernel_ms;      /* device time of the search/eval kernels (HIP events) */
+  double wall_ms;        /* host wall time of the call */
+  uint64_t evals;        /* program x candidate verdicts determined */
+  uint64_t launches;
+  double ops;            /* algorithmic u32 ops executed (evals x ops_per_eval) */
+} mg_stats;
+
+int mg_device_count(int* n);
+int mg_init(int device, mg_ctx** out);
+int mg_free(mg_ctx* ctx);
+
+int mg_prog_load(mg_ctx* ctx, const mg_prog_desc* desc, mg_prog** out);
+int mg_prog_free(mg_prog* prog);
+
+/* Search candidate indices [begin, begin+count) of every program; out_min_idx[i]
+ * receives the lowest index whose assignment satisfies program i, or MG_NONE. */
+int mg_search(mg_ctx* ctx, mg_prog* const* progs, size_t nprog, uint64_t seed,
+              uint64_t begin, uint64_t count, uint32_t flags, uint64_t* out_min_idx,
+              mg_stats* stats);
+
+/* Evaluate one program on explicit assignments: leaves_soa has n_input_rows
+ * rows of ncand u32 (row r, candidate i at [r*ncand + i]).  verdict[i] = 0/1;
+ * trace (may be NULL) receives n_trace_rows rows of ncand u32. */
+int mg_eval(mg_ctx* ctx, const mg_prog* prog, const uint32_t* leaves_soa, size_t ncand,
+            uint32_t* verdict, uint32_t* trace);
+
+/* Evaluate one program on generated candidates [begin, begin+count): the
+ * verdict/trace of exactly what mg_search explores (parity tests). */
+int mg_eval_generated(mg_ctx* ctx, const mg_prog* prog, uint64_t seed, uint64_t begin,
+                      size_t count, uint32_t* verdict, uint32_t* trace);
+
+/* Batched Keccak-256 (original 0x01 padding): message i is data[off[i] .. off[i]+len[i]). */
+int mg_keccak256(mg_ctx* ctx, const uint8_t* data, size_t ndata, const uint64_t* off,
+                 const uint32_t* len, size_t n, uint8_t* out32, mg_stats* stats);
+
+/* Device-resident variant for benchmarking with inputs already in HBM. */
+int mg_keccak256_device(mg_ctx* ctx, const uint8_t* d_data, const uint64_t* d_off,
+                        const uint32_t* d_len, size_t n, uint8_t* d_out32, mg_stats* stats);
+
+/* Validate a program without a device (the same check mg_prog_load runs). */
+int mg_validate_desc(const mg_prog_desc* desc);
+
+const char* mg_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

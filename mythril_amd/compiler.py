@@ -1,0 +1,647 @@
+"""Constraint DAG -> witness-engine bytecode.
+
+Input: the conjuncts of a Mythril constraint set (``Constraints`` list,
+``mythril/laser/ethereum/state/constraints.py:10-108``) as IR terms.  Output:
+a :class:`Program` — straight-line bytecode for ``csrc/mw_interp.h``, a
+constant pool, the leaf (free-variable) table with candidate pools, and the
+algorithmic op count per candidate (SURVEY.md §8(d) cost table).
+
+Passes
+  1. flatten top-level ``and`` into conjuncts (each becomes one CHECK so a
+     wavefront can stop at the first conjunct no lane satisfies);
+  2. lower every term to machine ops on virtual registers (W class: widths
+     33..256 in 8 limbs; N class: widths 1..32, Bools are width-1 N values);
+  3. schedule conjunct by conjunct in operand-first order, leaves at first use;
+  4. allocate the MW_NW W slots / MW_NN N slots with Belady (furthest next use)
+     eviction, emitting SPILL/FILL to a per-lane spill area when needed;
+  5. encode.
+
+Anything outside the supported vocabulary raises :class:`Unsupported`, which
+the drop-in ``get_model`` turns into "fall back to z3" (fail closed).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import isa
+from .ir import BOOL, Node, topo
+
+
+class Unsupported(Exception):
+    """The formula uses something the GPU path does not evaluate (-> z3)."""
+
+
+# --------------------------------------------------------------------------- machine IR
+class VReg:
+    __slots__ = ("id", "cls")
+
+    def __init__(self, vid: int, cls: str):
+        self.id = vid
+        self.cls = cls
+
+    def __repr__(self):  # pragma: no cover
+        return f"%{self.cls}{self.id}"
+
+
+class Const:
+    __slots__ = ("value", "cls")
+
+    def __init__(self, value: int, cls: str):
+        self.value = value
+        self.cls = cls
+
+    def __repr__(self):  # pragma: no cover
+        return f"${self.value:#x}"
+
+
+@dataclass
+class MInsn:
+    op: str
+    width: int = 0
+    dst: Optional[VReg] = None
+    srcs: List[object] = field(default_factory=list)
+    imm: int = 0
+
+
+def cls_of(width: int) -> str:
+    return "N" if width <= isa.NARROW_MAX else "W"
+
+
+def _w(n: Node) -> int:
+    """Machine width of a term (Bool -> 1)."""
+    return 1 if n.width == BOOL else n.width
+
+
+# --------------------------------------------------------------------------- leaves / pools
+@dataclass
+class LeafSpec:
+    """Candidate generator for one free variable (DESIGN.md "Candidate space")."""
+    name: str
+    width: int
+    pool: Optional[List[Optional[int]]] = None   # None entry = RANDOM; len must be 2**k
+    shift: int = 0
+    bits: int = 0
+
+
+@dataclass
+class Program:
+    code: np.ndarray
+    consts: np.ndarray
+    leaves: np.ndarray
+    pool: np.ndarray
+    n_spill: int
+    n_trace_rows: int
+    n_input_rows: int
+    ops_per_eval: int
+    leaf_specs: List[LeafSpec]
+    leaf_nodes: List[Node]
+    trace_map: Dict[int, Tuple[int, str]]
+    n_insn: int
+    n_conjuncts: int
+    stats: Dict[str, int] = field(default_factory=dict)
+
+    def input_rows_for(self, leaf_index: int) -> Tuple[int, int]:
+        off = int(self.leaves[leaf_index * isa.LEAF_WORDS + isa.LEAF_INROW])
+        return off, (self.leaf_specs[leaf_index].width + 31) // 32
+
+
+# --------------------------------------------------------------------------- cost model
+def node_cost(n: Node) -> int:
+    """Algorithmic u32 ops to evaluate one node once."""
+    op = n.op
+    if op in ("const", "var", "array", "apply"):
+        return 0
+    k = len(n.args)
+    if n.width == BOOL and op in ("and", "or", "not", "xor", "=>"):
+        return max(k, 1)
+    if op == "ite":
+        return max(1, (_w(n) + 31) // 32)
+    if op in ("=", "distinct") and n.args and n.args[0].width == BOOL:
+        return k
+    aw = _w(n.args[0]) if n.args else _w(n)
+    L = (aw + 31) // 32
+    Lo = (_w(n) + 31) // 32
+    if op in ("bvadd", "bvsub", "bvand", "bvor", "bvxor"):
+        return L * max(k - 1, 1)
+    if op in ("bvneg", "bvnot"):
+        return L
+    if op in ("bvnand", "bvnor", "bvxnor"):
+        return 2 * L
+    if op in ("=", "distinct"):
+        return 2 * L * max(k - 1, 1)
+    if op in ("bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge"):
+        return L + 1
+    if op in ("extract", "concat", "zero_extend", "sign_extend", "repeat", "rotate_left",
+              "rotate_right"):
+        return Lo
+    if op in ("bvshl", "bvlshr", "bvashr"):
+        return 2 * L + L * max(1, math.ceil(math.log2(L))) if L > 1 else 2
+    if op == "bvmul":
+        return 2 * L * (L + 1) * max(k - 1, 1)
+    if op == "bvumul_noovfl":
+        return 4 * L * L + L
+    if op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod"):
+        if L == 1:
+            base = 20
+        else:
+            lg = max(1, math.ceil(math.log2(L)))
+            base = L * (6 * L + 20) + 3 * (2 * L + L * lg)
+        return base + (4 * L if op in ("bvsdiv", "bvsrem", "bvsmod") else 0)
+    if op == "bvcomp":
+        return 2 * L
+    return L
+
+
+# --------------------------------------------------------------------------- compiler
+class _Lowerer:
+    def __init__(self):
+        self.insns: List[MInsn] = []
+        self.memo: Dict[int, object] = {}
+        self.nv = 0
+        self.leaf_index: Dict[str, int] = {}
+        self.leaf_nodes: List[Node] = []
+        self.trace_req: Dict[int, Node] = {}
+        self.trace_emitted: Dict[int, object] = {}
+
+    def vreg(self, cls: str) -> VReg:
+        self.nv += 1
+        return VReg(self.nv, cls)
+
+    def emit(self, op: str, width: int, srcs: Sequence[object] = (), imm: int = 0) -> VReg:
+        dcls = isa.SHAPES[op][0]
+        d = self.vreg(dcls) if dcls else None
+        self.insns.append(MInsn(op, width, d, list(srcs), imm))
+        return d
+
+    def emit_void(self, op: str, width: int, srcs: Sequence[object] = (), imm: int = 0):
+        self.insns.append(MInsn(op, width, None, list(srcs), imm))
+
+    @staticmethod
+    def k(value: int, width: int) -> Const:
+        return Const(value & ((1 << width) - 1), cls_of(width))
+
+    # ---- helpers producing values of a given machine width
+    def as_cls(self, v, width: int, want: str):
+        """Make sure operand v (a value of `width`) sits in class `want`."""
+        have = v.cls
+        if have == want:
+            return v
+        if want == "W":  # N -> W zero extension
+            if isinstance(v, Const):
+                return Const(v.value, "W")
+            return self.emit("W_ZEXTN", max(width, 33), [v])
+        raise Unsupported("narrowing class change")
+
+    def lower(self, n: Node):
+        if n.id in self.memo:
+            return self.memo[n.id]
+        v = self._lower(n)
+        self.memo[n.id] = v
+        if n.id in self.trace_req and n.id not in self.trace_emitted:
+            self.trace_emitted[n.id] = v
+            cls = v.cls
+            self.insns.append(MInsn("STORE_W" if cls == "W" else "STORE_N", _w(n), None, [v],
+                                    imm=-(n.id + 1)))  # row patched at encode time
+        return v
+
+    def _bin(self, op_w: str, op_n: str, width: int, a, b):
+        if cls_of(width) == "W":
+            return self.emit(op_w, width, [self.as_cls(a, width, "W"), self.as_cls(b, width, "W")])
+        return self.emit(op_n, width, [a, b])
+
+    def _lower(self, n: Node):
+        op = n.op
+        w = _w(n)
+        if n.is_array:
+            raise Unsupported("array term outside select (Ackermannisation pending)")
+        if op == "const":
+            return self.k(n.val, w)
+        if op == "var":
+            if w > isa.MAX_WIDTH:
+                raise Unsupported("free variable wider than 256 bits")
+            if n.name not in self.leaf_index:
+                self.leaf_index[n.name] = len(self.leaf_nodes)
+                self.leaf_nodes.append(n)
+            li = self.leaf_index[n.name]
+            return self.emit("LEAF_W" if cls_of(w) == "W" else "LEAF_N", w, [], imm=li)
+        if w > isa.MAX_WIDTH or any(_w(a) > isa.MAX_WIDTH for a in n.args if not a.is_array):
+            raise Unsupported(f"{op} wider than 256 bits")
+        if op in ("select", "store", "apply", "const_array"):
+            raise Unsupported(f"{op} (Ackermannisation pending)")
+
+        args = [self.lower(a) for a in n.args]
+        # ---------------- Bool connectives (width-1 N values)
+        if n.width == BOOL:
+            if op == "and":
+                return self._fold("N_AND", 1, args)
+            if op == "or":
+                return self._fold("N_OR", 1, args)
+            if op == "xor":
+                return self._fold("N_XOR", 1, args)
+            if op == "not":
+                return self.emit("N_XOR", 1, [args[0], self.k(1, 1)])
+            if op == "=>":
+                na = self.emit("N_XOR", 1, [args[0], self.k(1, 1)])
+                return self.emit("N_OR", 1, [na, args[1]])
+            if op in ("=", "distinct"):
+                aw = _w(n.args[0])
+                if n.args[0].is_array:
+                    raise Unsupported("array equality")
+                pairs = []
+                if op == "=":
+                    for b in args[1:]:
+                        pairs.append(self._eq(aw, args[0], b))
+                    r = self._fold("N_AND", 1, pairs)
+                    return r
+                for i in range(len(args)):
+                    for j in range(i + 1, len(args)):
+                        e = self._eq(aw, args[i], args[j])
+                        pairs.append(self.emit("N_XOR", 1, [e, self.k(1, 1)]))
+                return self._fold("N_AND", 1, pairs)
+            if op in ("bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge"):
+                aw = _w(n.args[0])
+                a, b = args
+                base = {"bvult": ("ULT", False), "bvule": ("ULE", False), "bvugt": ("ULT", True),
+                        "bvuge": ("ULE", True), "bvslt": ("SLT", False), "bvsle": ("SLE", False),
+                        "bvsgt": ("SLT", True), "bvsge": ("SLE", True)}[op]
+                name, swap = base
+                if swap:
+                    a, b = b, a
+                if cls_of(aw) == "W":
+                    return self.emit("N_" + name, aw, [self.as_cls(a, aw, "W"), self.as_cls(b, aw, "W")])
+                return self.emit("N_" + name + "N", aw, [a, b])
+            if op == "bvumul_noovfl":
+                aw = _w(n.args[0])
+                return self._bin("N_UMULNO", "N_UMULNON", aw, *args) if cls_of(aw) == "W" else \
+                    self.emit("N_UMULNON", aw, args)
+            if op == "ite":
+                return self.emit("N_ITE", 1, [args[1], args[2], args[0]])
+            raise Unsupported(f"bool op {op}")
+
+        # ---------------- bitvector ops
+        C = cls_of(w)
+        if op == "bvadd":
+            return self._fold("W_ADD" if C == "W" else "N_ADD", w, args)
+        if op == "bvmul":
+            return self._fold("W_MUL" if C == "W" else "N_MUL", w, args)
+        if op == "bvand":
+            return self._fold("W_AND" if C == "W" else "N_AND", w, args)
+        if op == "bvor":
+            return self._fold("W_OR" if C == "W" else "N_OR", w, args)
+        if op == "bvxor":
+            return self._fold("W_XOR" if C == "W" else "N_XOR", w, args)
+        if op == "bvsub":
+            return self._bin("W_SUB", "N_SUB", w, *args)
+        if op == "bvneg":
+            return self._bin("W_SUB", "N_SUB", w, self.k(0, w), args[0])
+        if op == "bvnot":
+            return self.emit("W_NOT" if C == "W" else "N_NOT", w, [args[0]])
+        if op in ("bvnand", "bvnor", "bvxnor"):
+            inner = {"bvnand": "AND", "bvnor": "OR", "bvxnor": "XOR"}[op]
+            t = self._bin("W_" + inner, "N_" + inner, w, *args)
+            return self.emit("W_NOT" if C == "W" else "N_NOT", w, [t])
+        if op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod"):
+            s = op[2:].upper()
+            return self._bin("W_" + s, "N_" + s, w, *args)
+        if op in ("bvshl", "bvlshr", "bvashr"):
+            a, b = args
+            if isinstance(b, Const) and op != "bvashr":
+                if b.value >= w:
+                    return self.k(0, w)
+                if b.value == 0:
+                    return a
+                name = ("W_" if C == "W" else "N_") + ("SHLI" if op == "bvshl" else "LSHRI")
+                return self.emit(name, w, [a], imm=b.value)
+            s = {"bvshl": "SHL", "bvlshr": "LSHR", "bvashr": "ASHR"}[op]
+            return self._bin("W_" + s, "N_" + s, w, a, b)
+        if op == "ite":
+            c, a, b = args
+            if C == "W":
+                return self.emit("W_ITE", w, [self.as_cls(a, w, "W"), self.as_cls(b, w, "W"), c])
+            return self.emit("N_ITE", w, [a, b, c])
+        if op == "bvcomp":
+            return self._eq(_w(n.args[0]), args[0], args[1])
+        if op == "extract":
+            hi, lo = n.params
+            a = args[0]
+            aw = _w(n.args[0])
+            if isinstance(a, Const):
+                return self.k(a.value >> lo, w)
+            if cls_of(aw) == "W":
+                if C == "N":
+                    return self.emit("N_EXTRACTW", w, [a], imm=lo)
+                if lo == 0 and w == aw:
+                    return a
+                return self.emit("W_LSHRI", w, [a], imm=lo)
+            if lo == 0 and w == aw:
+                return a
+            return self.emit("N_LSHRI", w, [a], imm=lo)
+        if op == "zero_extend":
+            a = args[0]
+            if isinstance(a, Const):
+                return Const(a.value, C)
+            return self.as_cls(a, _w(n.args[0]), C)
+        if op == "sign_extend":
+            a = args[0]
+            aw = _w(n.args[0])
+            if C == "N":
+                return self.emit("N_SEXT", w, [a], imm=aw)
+            if a.cls == "N":
+                return self.emit("W_SEXTN", w, [a], imm=aw)
+            return self.emit("W_SEXT", w, [a], imm=aw)
+        if op == "concat":
+            return self._concat([_w(x) for x in n.args], args, w)
+        if op == "repeat":
+            aw = _w(n.args[0])
+            return self._concat([aw] * n.params[0], [args[0]] * n.params[0], w)
+        if op in ("rotate_left", "rotate_right"):
+            r = n.params[0] % w
+            a = args[0]
+            if r == 0:
+                return a
+            left = r if op == "rotate_left" else w - r
+            p = "W_" if C == "W" else "N_"
+            hi = self.emit(p + "SHLI", w, [a], imm=left)
+            lo = self.emit(p + "LSHRI", w, [a], imm=w - left)
+            return self.emit(p + "OR", w, [hi, lo])
+        raise Unsupported(f"op {op}")
+
+    def _fold(self, op: str, w: int, args):
+        if len(args) == 1:
+            return args[0]
+        acc = args[0]
+        C = "W" if op.startswith("W_") else "N"
+        for b in args[1:]:
+            if C == "W":
+                acc = self.emit(op, w, [self.as_cls(acc, w, "W"), self.as_cls(b, w, "W")])
+            else:
+                acc = self.emit(op, w, [acc, b])
+        return acc
+
+    def _eq(self, aw: int, a, b):
+        if cls_of(aw) == "W":
+            return self.emit("N_EQ", aw, [self.as_cls(a, aw, "W"), self.as_cls(b, aw, "W")])
+        return self.emit("N_EQN", aw, [a, b])
+
+    def _concat(self, widths: List[int], vals: List[object], w: int):
+        # first argument is most significant; build from the least significant part up
+        parts = list(zip(widths, vals))[::-1]
+        off = 0
+        if cls_of(w) == "N":
+            acc = None
+            for pw, v in parts:
+                if acc is None:
+                    acc = v
+                else:
+                    sh = self.emit("N_SHLI", w, [v], imm=off) if off else v
+                    acc = self.emit("N_OR", w, [acc, sh])
+                off += pw
+            return acc
+        acc = None
+        for pw, v in parts:
+            if acc is None:
+                if isinstance(v, Const):
+                    acc = Const(v.value, "W")
+                elif v.cls == "W":
+                    acc = v
+                else:
+                    acc = self.emit("W_ZEXTN", w, [v])
+            elif isinstance(v, Const):
+                if v.value:
+                    acc = self.emit("W_OR", w, [self.as_cls(acc, w, "W"), Const(v.value << off, "W")])
+            elif v.cls == "N":
+                acc = self.emit("W_INSN", w, [self.as_cls(acc, w, "W"), v], imm=off)
+            else:
+                sh = self.emit("W_SHLI", w, [v], imm=off)
+                acc = self.emit("W_OR", w, [self.as_cls(acc, w, "W"), sh])
+            off += pw
+        return acc
+
+
+def _flatten(conjuncts: Iterable[Node]) -> List[Node]:
+    out: List[Node] = []
+    stack = list(conjuncts)[::-1]
+    while stack:
+        c = stack.pop()
+        if c.width != BOOL:
+            raise Unsupported("conjunct is not Bool")
+        if c.op == "and":
+            stack.extend(list(c.args)[::-1])
+        elif c.op == "const" and c.val:
+            continue
+        else:
+            out.append(c)
+    return out
+
+
+# --------------------------------------------------------------------------- register allocation
+def _allocate(insns: List[MInsn]):
+    """Belady allocation of W/N vregs to MW_NW/MW_NN slots; returns (insns, n_spill)."""
+    uses: Dict[int, List[int]] = {}
+    for i, ins in enumerate(insns):
+        for s in ins.srcs:
+            if isinstance(s, VReg):
+                uses.setdefault(s.id, []).append(i)
+    ptr: Dict[int, int] = {k: 0 for k in uses}
+
+    def next_use(vid: int, i: int) -> int:
+        lst = uses.get(vid)
+        if not lst:
+            return 1 << 60
+        p = ptr[vid]
+        while p < len(lst) and lst[p] < i:
+            p += 1
+        ptr[vid] = p
+        return lst[p] if p < len(lst) else 1 << 60
+
+    cap = {"W": isa.NW, "N": isa.NN}
+    free = {"W": list(range(isa.NW - 1, -1, -1)), "N": list(range(isa.NN - 1, -1, -1))}
+    reg_of: Dict[int, int] = {}
+    resident: Dict[str, Dict[int, VReg]] = {"W": {}, "N": {}}
+    spill_of: Dict[int, int] = {}
+    spill_free: List[int] = []
+    n_spill = 0
+    out: List[MInsn] = []
+
+    def get_spill_slot() -> int:
+        nonlocal n_spill
+        if spill_free:
+            return spill_free.pop()
+        n_spill += 1
+        return n_spill - 1
+
+    def evict(cls: str, i: int, pinned: set):
+        best, best_nu = None, -1
+        for vid, vr in resident[cls].items():
+            if vid in pinned:
+                continue
+            nu = next_use(vid, i)
+            if nu > best_nu:
+                best, best_nu = vr, nu
+        if best is None:
+            raise Unsupported("register pressure: too many simultaneous operands")
+        slot = reg_of.pop(best.id)
+        del resident[cls][best.id]
+        if best_nu < (1 << 60) and best.id not in spill_of:
+            sp = get_spill_slot()
+            spill_of[best.id] = sp
+            m = MInsn("SPILL_W" if cls == "W" else "SPILL_N", 0, None, [("phys", slot)], imm=sp)
+            out.append(m)
+        free[cls].append(slot)
+
+    def take(cls: str, i: int, pinned: set) -> int:
+        if not free[cls]:
+            evict(cls, i, pinned)
+        return free[cls].pop()
+
+    for i, ins in enumerate(insns):
+        pinned = {s.id for s in ins.srcs if isinstance(s, VReg)}
+        # bring every source into a register
+        for s in ins.srcs:
+            if isinstance(s, VReg) and s.id not in reg_of:
+                if s.id not in spill_of:
+                    raise AssertionError("use of undefined vreg")
+                slot = take(s.cls, i, pinned)
+                out.append(MInsn("FILL_W" if s.cls == "W" else "FILL_N", 0, ("phys", slot), [],
+                                 imm=spill_of[s.id]))
+                reg_of[s.id] = slot
+                resident[s.cls][s.id] = s
+        phys_srcs = []
+        for s in ins.srcs:
+            phys_srcs.append(("phys", reg_of[s.id]) if isinstance(s, VReg) else s)
+        # release sources that die here (the interpreter reads before it writes)
+        for s in ins.srcs:
+            if isinstance(s, VReg) and s.id in reg_of and next_use(s.id, i + 1) >= (1 << 60):
+                slot = reg_of.pop(s.id)
+                resident[s.cls].pop(s.id, None)
+                free[s.cls].append(slot)
+                if s.id in spill_of:
+                    spill_free.append(spill_of.pop(s.id))
+        dst = None
+        if ins.dst is not None:
+            d = ins.dst
+            slot = take(d.cls, i, set())
+            if next_use(d.id, i + 1) < (1 << 60):
+                reg_of[d.id] = slot
+                resident[d.cls][d.id] = d
+            else:
+                free[d.cls].append(slot)  # dead result (e.g. traced only) - slot reused
+            dst = ("phys", slot)
+        out.append(MInsn(ins.op, ins.width, dst, phys_srcs, ins.imm))
+    return out, n_spill
+
+
+# --------------------------------------------------------------------------- encode
+def _limbs(v: int) -> List[int]:
+    return [(v >> (32 * k)) & 0xFFFFFFFF for k in range(8)]
+
+
+def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, LeafSpec]] = None,
+                    trace: Sequence[Node] = (), pools: Optional[Dict[str, List[Optional[int]]]] = None
+                    ) -> Program:
+    """Compile the conjunction of `conjuncts` (IR Bool terms)."""
+    conj = _flatten(conjuncts)
+    lw = _Lowerer()
+    for t in trace:
+        lw.trace_req[t.id] = t
+    checks = 0
+    for c in conj:
+        if c.op == "const" and not c.val:
+            lw.emit_void("CHECK", 1, [Const(0, "N")])
+            checks += 1
+            continue
+        v = lw.lower(c)
+        lw.emit_void("CHECK", 1, [v])
+        checks += 1
+    for t in trace:  # traced nodes not reachable from the conjuncts
+        lw.lower(t)
+    lw.emit_void("END", 0, [])
+
+    insns, n_spill = _allocate(lw.insns)
+
+    # constant pool
+    consts: List[int] = []
+    kmap: Dict[Tuple[int, str], int] = {}
+
+    def kref(c: Const) -> int:
+        key = (c.value, c.cls)
+        if key not in kmap:
+            kmap[key] = len(consts)
+            consts.extend(_limbs(c.value) if c.cls == "W" else [c.value & 0xFFFFFFFF])
+        return isa.KBIT | kmap[key]
+
+    # trace rows
+    trace_map: Dict[int, Tuple[int, str]] = {}
+    rows = 0
+    code: List[int] = []
+    for ins in insns:
+        fields = []
+        for s in ins.srcs:
+            if isinstance(s, Const):
+                fields.append(kref(s))
+            else:
+                fields.append(s[1])
+        while len(fields) < 3:
+            fields.append(0)
+        imm = ins.imm
+        if ins.op in ("STORE_W", "STORE_N"):
+            nid = -imm - 1
+            cls = "W" if ins.op == "STORE_W" else "N"
+            trace_map[nid] = (rows, cls)
+            imm = rows
+            rows += 8 if cls == "W" else 1
+        dst = ins.dst[1] if ins.dst is not None else 0
+        code.extend(isa.encode(ins.op, ins.width, dst, fields[0], fields[1], fields[2], imm))
+    if len(consts) > 0x7FFF:
+        raise Unsupported("constant pool overflow")
+
+    # leaf table + pools
+    specs: List[LeafSpec] = []
+    leaf_words: List[int] = []
+    pool_words: List[int] = []
+    in_row = 0
+    bit = 0
+    user = dict(leaf_specs or {})
+    for li, n in enumerate(lw.leaf_nodes):
+        w = _w(n)
+        spec = user.get(n.name)
+        if spec is None and pools and n.name in pools:
+            spec = LeafSpec(n.name, w, pool=list(pools[n.name]))
+        if spec is None:
+            spec = LeafSpec(n.name, w)
+        spec.width = w
+        kind, pshift, pbits, poff = 0, 0, 0, 0
+        if spec.pool:
+            p = list(spec.pool)
+            nb = max(0, math.ceil(math.log2(len(p)))) if len(p) > 1 else 0
+            p += [None] * ((1 << nb) - len(p))
+            spec.pool = p
+            if spec.bits == 0 and spec.shift == 0:
+                spec.bits, spec.shift = nb, bit
+                bit += nb
+            kind, pshift, pbits, poff = 1, spec.shift, spec.bits, len(pool_words)
+            for e in p:
+                if e is None:
+                    pool_words.extend([1] + [0] * 8)
+                else:
+                    pool_words.extend([0] + _limbs(e & ((1 << w) - 1)))
+        leaf_words.extend([w, kind, li, pshift, pbits, poff, in_row, 0])
+        in_row += (w + 31) // 32
+        specs.append(spec)
+    if bit > 63:
+        raise Unsupported("pool digit fields exceed the 64-bit candidate index")
+
+    reach = topo(conj + list(trace))
+    ops = sum(node_cost(n) for n in reach)
+    arr = lambda x: np.asarray(x if x else [0], dtype=np.uint32)
+    stats = {"nodes": len(reach), "insns": len(code) // 4, "spills": sum(1 for i in insns if i.op.startswith("SPILL")),
+             "fills": sum(1 for i in insns if i.op.startswith("FILL"))}
+    return Program(code=np.asarray(code, dtype=np.uint32), consts=arr(consts),
+                   leaves=np.asarray(leaf_words, dtype=np.uint32), pool=arr(pool_words),
+                   n_spill=n_spill, n_trace_rows=rows, n_input_rows=in_row, ops_per_eval=ops,
+                   leaf_specs=specs, leaf_nodes=list(lw.leaf_nodes), trace_map=trace_map,
+                   n_insn=len(code) // 4, n_conjuncts=checks, stats=stats)

@@ -1,0 +1,458 @@
+// mw_alu.h — multi-limb bitvector ALU for the witness interpreter.
+//
+// One candidate per lane: a <=256-bit value is 8 x u32 limbs held in VGPRs
+// (limb 0 least significant); <=32-bit values are a single u32.  Semantics are
+// SMT-LIB 2.6 (z3 hi_div0=true), i.e. what z3 gives the terms Mythril builds:
+//   bvadd/bvsub/bvmul/bvsdiv     mythril/laser/smt/bitvec.py:126-166
+//   bvand/bvor/bvxor             bitvec.py:168-199
+//   bvslt/bvsgt/bvsle/bvsge      bitvec.py:201-243
+//   bvshl/bvashr, LShR           bitvec.py:295-309, bitvec_helper.py:30-31
+//   UDiv/URem/SRem               bitvec_helper.py:153-180
+//   BVMulNoOverflow(unsigned)    bitvec_helper.py:211-224
+// Division by zero: udiv -> all-ones, urem -> dividend, sdiv -> (s<0 ? 1 : -1),
+// srem/smod -> dividend.  Shifts by >= width: shl/lshr -> 0, ashr -> sign fill.
+//
+// Written as portable C++ (__host__ __device__) so the identical code is
+// checked on the CPU by tests/test_host_emulator.py before it runs on gfx950.
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+#define MW_HD __host__ __device__ __attribute__((always_inline)) inline
+
+namespace mw {
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+MW_HD u32 addc(u32 a, u32 b, u32& c) {
+  u32 co;
+  u32 r = __builtin_addc(a, b, c, &co);
+  c = co;
+  return r;
+}
+MW_HD u32 subb(u32 a, u32 b, u32& br) {
+  u32 bo;
+  u32 r = __builtin_subc(a, b, br, &bo);
+  br = bo;
+  return r;
+}
+
+// mask of limb k of a w-bit value
+MW_HD u32 limb_mask(u32 w, int k) {
+  int lo = 32 * k;
+  if ((int)w >= lo + 32) return 0xffffffffu;
+  if ((int)w <= lo) return 0u;
+  return (1u << (w - lo)) - 1u;
+}
+MW_HD u32 nmask(u32 w) { return w >= 32 ? 0xffffffffu : ((1u << w) - 1u); }
+
+MW_HD void canon(u32 r[8], u32 w) {
+  if (w < 256) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] &= limb_mask(w, k);
+  }
+}
+
+MW_HD void copy8(u32 d[8], const u32 s[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d[k] = s[k];
+}
+MW_HD void zero8(u32 d[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d[k] = 0;
+}
+
+// ---------------------------------------------------------------- add / sub
+MW_HD u32 add8(const u32 a[8], const u32 b[8], u32 r[8]) {
+  u32 c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = addc(a[k], b[k], c);
+  return c;
+}
+MW_HD u32 sub8(const u32 a[8], const u32 b[8], u32 r[8]) {
+  u32 br = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = subb(a[k], b[k], br);
+  return br;
+}
+// borrow of a - b  ==  a <u b
+MW_HD bool ult8(const u32 a[8], const u32 b[8]) {
+  u32 br = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) (void)subb(a[k], b[k], br);
+  return br != 0;
+}
+MW_HD bool eq8(const u32 a[8], const u32 b[8]) {
+  u32 x = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x |= a[k] ^ b[k];
+  return x == 0;
+}
+MW_HD bool is_zero8(const u32 a[8]) {
+  u32 x = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x |= a[k];
+  return x == 0;
+}
+
+// ---------------------------------------------------------------- multiply
+// low 256 bits of a*b (product scanning by rows)
+MW_HD void mul8(const u32 a[8], const u32 b[8], u32 r[8]) {
+  u32 acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    u32 carry = 0;
+#pragma unroll
+    for (int j = 0; j < 8 - i; ++j) {
+      if (i + j < 7) {
+        u64 p = (u64)a[i] * b[j] + acc[i + j] + carry;
+        acc[i + j] = (u32)p;
+        carry = (u32)(p >> 32);
+      } else {
+        acc[i + j] += a[i] * b[j] + carry;
+      }
+    }
+  }
+  copy8(r, acc);
+}
+// full 512-bit product high half (limbs 8..15)
+MW_HD void mulhi8(const u32 a[8], const u32 b[8], u32 lo[8], u32 hi[8]) {
+  u32 acc[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    u32 carry = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      u64 p = (u64)a[i] * b[j] + acc[i + j] + carry;
+      acc[i + j] = (u32)p;
+      carry = (u32)(p >> 32);
+    }
+    acc[i + 8] = carry;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    lo[k] = acc[k];
+    hi[k] = acc[k + 8];
+  }
+}
+
+// ---------------------------------------------------------------- shifts
+// funnel shifts on 32-bit limbs, b in [0,31]
+MW_HD u32 fshr32(u32 hi, u32 lo, u32 b) { return (u32)((((u64)hi << 32) | lo) >> b); }
+MW_HD u32 fshl32(u32 hi, u32 lo, u32 b) { return (u32)((((u64)hi << 32) | lo) >> (32 - b)) ; }
+// note fshl32 with b == 0 shifts the pair right by 32 and returns hi: correct.
+
+// r = a << s for s in [0,255] (bits shifted past 256 dropped)
+MW_HD void shl8(const u32 a[8], u32 s, u32 r[8]) {
+  u32 t[8];
+  copy8(t, a);
+  u32 q = s >> 5, b = s & 31;
+#pragma unroll
+  for (int st = 0; st < 3; ++st) {
+    int n = 1 << st;
+    bool c = (q >> st) & 1;
+#pragma unroll
+    for (int k = 7; k >= 0; --k) t[k] = c ? (k >= n ? t[k - n] : 0u) : t[k];
+  }
+#pragma unroll
+  for (int k = 7; k >= 1; --k) r[k] = fshl32(t[k], t[k - 1], b);
+  r[0] = t[0] << b;
+}
+// r = a >> s (fill = 0 or all-ones for arithmetic), s in [0,255]
+MW_HD void shr8(const u32 a[8], u32 s, u32 fill, u32 r[8]) {
+  u32 t[8];
+  copy8(t, a);
+  u32 q = s >> 5, b = s & 31;
+#pragma unroll
+  for (int st = 0; st < 3; ++st) {
+    int n = 1 << st;
+    bool c = (q >> st) & 1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[k] = c ? (k + n < 8 ? t[k + n] : fill) : t[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) r[k] = fshr32(t[k + 1], t[k], b);
+  r[7] = fshr32(fill, t[7], b);
+}
+// 16-limb result of x << s, s in [0,255]
+MW_HD void shl8to16(const u32 x[8], u32 s, u32 u[16]) {
+  u32 t[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    t[k] = x[k];
+    t[k + 8] = 0;
+  }
+  u32 q = s >> 5, b = s & 31;
+#pragma unroll
+  for (int st = 0; st < 3; ++st) {
+    int n = 1 << st;
+    bool c = (q >> st) & 1;
+#pragma unroll
+    for (int k = 15; k >= 0; --k) t[k] = c ? (k >= n ? t[k - n] : 0u) : t[k];
+  }
+#pragma unroll
+  for (int k = 15; k >= 1; --k) u[k] = fshl32(t[k], t[k - 1], b);
+  u[0] = t[0] << b;
+}
+
+// amount >= w ?  (amount is a w-bit canonical value held in 8 limbs)
+MW_HD bool amount_ge(const u32 b[8], u32 w) {
+  u32 hi = b[1] | b[2] | b[3] | b[4] | b[5] | b[6] | b[7];
+  return hi != 0 || b[0] >= w;
+}
+
+// sign bit of a w-bit value (w in 33..256) / sign fill word
+MW_HD bool signbit8(const u32 a[8], u32 w) {
+  u32 x = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    int bit = (int)w - 1 - 32 * k;
+    x |= (bit >= 0 && bit < 32) ? ((a[k] >> bit) & 1u) : 0u;
+  }
+  return x != 0;
+}
+// sign-extend a w_from-bit value in place to 256 bits
+MW_HD void sext8(u32 a[8], u32 w_from) {
+  bool s = signbit8(a, w_from);
+  if (w_from < 256) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] |= s ? ~limb_mask(w_from, k) : 0u;
+  }
+}
+
+MW_HD void wshl(const u32 a[8], const u32 b[8], u32 w, u32 r[8]) {
+  if (amount_ge(b, w)) {
+    zero8(r);
+  } else {
+    shl8(a, b[0], r);
+    canon(r, w);
+  }
+}
+MW_HD void wlshr(const u32 a[8], const u32 b[8], u32 w, u32 r[8]) {
+  if (amount_ge(b, w)) {
+    zero8(r);
+  } else {
+    shr8(a, b[0], 0u, r);
+  }
+}
+MW_HD void washr(const u32 a[8], const u32 b[8], u32 w, u32 r[8]) {
+  u32 t[8];
+  copy8(t, a);
+  sext8(t, w);
+  u32 fill = signbit8(a, w) ? 0xffffffffu : 0u;
+  u32 s = amount_ge(b, w) ? 255u : b[0];
+  shr8(t, s, fill, r);
+  canon(r, w);
+}
+
+// ---------------------------------------------------------------- division
+MW_HD u32 clz32(u32 x) { return x ? (u32)__builtin_clz(x) : 32u; }
+MW_HD u32 clz256(const u32 y[8]) {
+  u32 n = 0;
+  bool found = false;
+#pragma unroll
+  for (int k = 7; k >= 0; --k) {
+    u32 c = found ? 0u : clz32(y[k]);
+    n += c;
+    found = found || (y[k] != 0);
+  }
+  return n;
+}
+// Moller-Granlund reciprocal of a normalized divisor d (top bit set)
+MW_HD u32 recip32(u32 d) { return (u32)(~0ull / (u64)d - (1ull << 32)); }
+// (u1:u0) / d with u1 < d, d normalized, v = recip32(d)  (Moller & Granlund 2011, Alg. 4)
+MW_HD u32 div2by1(u32 u1, u32 u0, u32 d, u32 v) {
+  u64 q = (u64)v * u1 + ((((u64)u1) << 32) | u0);
+  u32 q1 = (u32)(q >> 32) + 1u, q0 = (u32)q;
+  u32 r = u0 - q1 * d;
+  bool adj1 = r > q0;
+  q1 = adj1 ? q1 - 1u : q1;
+  r = adj1 ? r + d : r;
+  bool adj2 = r >= d;
+  q1 = adj2 ? q1 + 1u : q1;
+  return q1;
+}
+
+// q = x / y, r = x % y for y != 0 (Knuth Alg. D, base 2^32, fixed 8x8 shape:
+// the divisor is normalized to a full 8-limb value so every index is static)
+MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
+  u32 s = clz256(y);
+  u32 v[8];
+  shl8(y, s, v);
+  u32 u[16];
+  shl8to16(x, s, u);
+  u32 d = v[7];
+  u32 rec = recip32(d);
+#pragma unroll
+  for (int j = 7; j >= 0; --j) {
+    u32 u1 = u[j + 8], u0 = u[j + 7];
+    bool sat = (u1 == d);
+    u32 qh = div2by1(sat ? 0u : u1, u0, d, rec);
+    qh = sat ? 0xffffffffu : qh;
+    // u[j..j+8] -= qh * v
+    u32 carry = 0, br = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      u64 p = (u64)qh * v[k] + carry;
+      carry = (u32)(p >> 32);
+      u[j + k] = subb(u[j + k], (u32)p, br);
+    }
+    u[j + 8] = subb(u[j + 8], carry, br);
+    u32 neg = br;
+    // at most two add-backs (Knuth Thm B: qhat - 2 <= q <= qhat)
+#pragma unroll
+    for (int ab = 0; ab < 2; ++ab) {
+      u32 c = 0, t[9];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t[k] = addc(u[j + k], v[k], c);
+      t[8] = addc(u[j + 8], 0u, c);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) u[j + k] = neg ? t[k] : u[j + k];
+      qh -= neg;
+      neg = neg & (c ^ 1u);
+    }
+    q[j] = qh;
+  }
+  u32 rn[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) rn[k] = u[k];
+  shr8(rn, s, 0u, r);
+}
+
+MW_HD void neg8(const u32 a[8], u32 r[8]) {
+  u32 br = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = subb(0u, a[k], br);
+}
+
+// kind: 0 udiv, 1 urem, 2 sdiv, 3 srem, 4 smod
+MW_HD void wdiv(int kind, const u32 a[8], const u32 b[8], u32 w, u32 r[8]) {
+  bool sa = false, sb = false;
+  u32 x[8], y[8];
+  copy8(x, a);
+  copy8(y, b);
+  if (kind >= 2) {
+    sa = signbit8(a, w);
+    sb = signbit8(b, w);
+    u32 t[8];
+    neg8(a, t);
+    canon(t, w);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = sa ? t[k] : x[k];
+    neg8(b, t);
+    canon(t, w);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) y[k] = sb ? t[k] : y[k];
+  }
+  bool yz = is_zero8(y);
+  u32 q[8], rm[8];
+  u32 one[8] = {1u, 0, 0, 0, 0, 0, 0, 0};
+  udivrem8(x, yz ? one : y, q, rm);
+  // SMT-LIB division-by-zero results on the magnitudes
+  if (yz) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      q[k] = limb_mask(w, k);  // all ones
+      rm[k] = x[k];
+    }
+  }
+  u32 t[8];
+  switch (kind) {
+    case 0:
+      copy8(r, q);
+      break;
+    case 1:
+      copy8(r, rm);
+      break;
+    case 2: {  // negate quotient when signs differ
+      neg8(q, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = (sa != sb) ? t[k] : q[k];
+      break;
+    }
+    case 3: {  // remainder takes the dividend's sign
+      neg8(rm, t);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = sa ? t[k] : rm[k];
+      break;
+    }
+    default: {  // smod: sign of divisor
+      bool uz = is_zero8(rm);
+      u32 nu[8], s1[8], s2[8];
+      neg8(rm, nu);
+      add8(nu, b, s1);   // -u + t
+      add8(rm, b, s2);   //  u + t
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        u32 v = rm[k];
+        v = (!uz && sa && !sb) ? s1[k] : v;
+        v = (!uz && !sa && sb) ? s2[k] : v;
+        v = (!uz && sa && sb) ? nu[k] : v;
+        r[k] = v;
+      }
+      break;
+    }
+  }
+  canon(r, w);
+}
+
+// ---------------------------------------------------------------- narrow (<= 32 bit)
+MW_HD u32 n_sext(u32 a, u32 wfrom) {
+  if (wfrom >= 32) return a;
+  u32 s = (a >> (wfrom - 1)) & 1u;
+  return s ? (a | ~nmask(wfrom)) : a;
+}
+MW_HD u32 n_div(int kind, u32 a, u32 b, u32 w) {
+  u32 m = nmask(w);
+  bool sa = false, sb = false;
+  u32 x = a, y = b;
+  if (kind >= 2) {
+    sa = (a >> (w - 1)) & 1u;
+    sb = (b >> (w - 1)) & 1u;
+    x = sa ? ((0u - a) & m) : a;
+    y = sb ? ((0u - b) & m) : b;
+  }
+  u32 q, rm;
+  if (y == 0) {
+    q = m;
+    rm = x;
+  } else {
+    q = x / y;
+    rm = x - q * y;
+  }
+  u32 r;
+  switch (kind) {
+    case 0: r = q; break;
+    case 1: r = rm; break;
+    case 2: r = (sa != sb) ? (0u - q) : q; break;
+    case 3: r = sa ? (0u - rm) : rm; break;
+    default: {
+      if (rm == 0) r = 0;
+      else if (!sa && !sb) r = rm;
+      else if (sa && !sb) r = (0u - rm) + b;
+      else if (!sa && sb) r = rm + b;
+      else r = 0u - rm;
+      break;
+    }
+  }
+  return r & m;
+}
+MW_HD u32 n_shl(u32 a, u32 b, u32 w) { return b >= w ? 0u : ((a << b) & nmask(w)); }
+MW_HD u32 n_lshr(u32 a, u32 b, u32 w) { return b >= w ? 0u : (a >> b); }
+MW_HD u32 n_ashr(u32 a, u32 b, u32 w) {
+  int32_t sa = (int32_t)n_sext(a, w);
+  u32 s = b >= w ? 31u : b;
+  return ((u32)(sa >> s)) & nmask(w);
+}
+MW_HD bool n_slt(u32 a, u32 b, u32 w) { return (int32_t)n_sext(a, w) < (int32_t)n_sext(b, w); }
+MW_HD bool n_sle(u32 a, u32 b, u32 w) { return (int32_t)n_sext(a, w) <= (int32_t)n_sext(b, w); }
+MW_HD bool n_umulno(u32 a, u32 b, u32 w) {
+  u64 p = (u64)a * b;
+  return w >= 32 ? (p >> 32) == 0 : (p >> w) == 0;
+}
+
+}  // namespace mw

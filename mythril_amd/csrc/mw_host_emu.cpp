@@ -1,0 +1,80 @@
+// mw_host_emu.cpp — CPU build of the *same* interpreter/ALU/leaf code that runs
+// on gfx950 (mw_interp.h, mw_alu.h, mw_leaf.h, mw_keccak.h), one candidate at a
+// time.  TEST/DEVELOPMENT ONLY: lets tests/ check compiler + bytecode + ALU
+// semantics against the oracle on a machine without a GPU.  The product path
+// (mythril_amd.runtime) never loads this library.
+#include <cstring>
+#include <vector>
+
+#include "../../include/mythril_witness.h"
+#include "mw_interp.h"
+#include "mw_keccak.h"
+#include "mw_leaf.h"
+
+using namespace mw;
+
+namespace {
+struct HostEnv {
+  const u32* leaves;
+  const u32* pool;
+  const u32* in;  // SoA rows or null
+  u32* trace;
+  u64 ncand, idx, seed, cand;
+  std::vector<u32>* spillv;
+  void leaf(u32 li, u32 out[8]) {
+    const u32* L = leaves + (u64)li * MW_LEAF_WORDS;
+    if (in) {
+      const u32 w = L[MW_LEAF_WIDTH], row = L[MW_LEAF_INROW];
+      const int nl = (int)((w + 31) / 32);
+      for (int k = 0; k < 8; ++k) out[k] = k < nl ? in[((u64)row + k) * ncand + idx] : 0u;
+      canon(out, w);
+    } else {
+      leaf_value(L, pool, seed, cand, out);
+    }
+  }
+  void store(u32 row, const u32* v, int n) {
+    if (trace)
+      for (int k = 0; k < n; ++k) trace[((u64)row + k) * ncand + idx] = v[k];
+  }
+  void spill(u32 slot, const u32* v, int n) {
+    if (spillv->size() < (slot + 1) * 8) spillv->resize((slot + 1) * 8, 0u);
+    for (int k = 0; k < n; ++k) (*spillv)[slot * 8 + k] = v[k];
+  }
+  void fill(u32 slot, u32* v, int n) {
+    if (spillv->size() < (slot + 1) * 8) spillv->resize((slot + 1) * 8, 0u);
+    for (int k = 0; k < 8; ++k) v[k] = k < n ? (*spillv)[slot * 8 + k] : 0u;
+  }
+  bool none(bool alive) { return !alive; }
+};
+}  // namespace
+
+extern "C" {
+
+int mg_validate_desc(const mg_prog_desc* d);
+
+// Evaluate candidates [0, ncand) (explicit SoA inputs) or generated candidates
+// [begin, begin+ncand) when leaves_soa == NULL.
+int mwh_eval(const mg_prog_desc* d, const uint32_t* leaves_soa, uint64_t seed, uint64_t begin, size_t ncand,
+             uint32_t flags, uint32_t* verdict, uint32_t* trace) {
+  int rc = mg_validate_desc(d);
+  if (rc) return rc;
+  std::vector<u32> consts(d->nconst_words + 8, 0u);
+  if (d->nconst_words) std::memcpy(consts.data(), d->consts, d->nconst_words * 4);
+  std::vector<u32> spill;
+  for (size_t i = 0; i < ncand; ++i) {
+    HostEnv env{d->leaves, d->pool, leaves_soa, trace, (u64)ncand, (u64)i, seed, begin + i, &spill};
+    verdict[i] = mw_run(d->code, consts.data(), env, true, flags) ? 1u : 0u;
+  }
+  return 0;
+}
+
+int mwh_keccak256(const uint8_t* data, const uint64_t* off, const uint32_t* len, size_t n, uint8_t* out32) {
+  for (size_t i = 0; i < n; ++i) {
+    u64 h[4];
+    keccak256_msg(data + off[i], len[i], h);
+    std::memcpy(out32 + 32 * i, h, 32);
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,394 @@
+// mw_interp.h — bytecode interpreter for one candidate per lane.
+//
+// The instruction stream is wave-uniform: every lane of a wavefront executes
+// the same program on its own candidate assignment, so `pc`, the opcode and
+// every slot index live in SGPRs (s_load_dwordx4 per instruction) and the
+// dispatch `switch` is a scalar branch tree.  The W file (MW_NW x 8 limbs) and
+// N file (MW_NN x 1) are ext_vector values indexed by a uniform slot number,
+// which hipcc lowers to `s_set_gpr_idx_on` + v_mov — the file never leaves the
+// VGPRs (checked in tests/test_build.py against the gfx950 ISA: no scratch).
+//
+// Env policy (device kernel or host emulator) supplies:
+//   void leaf(u32 idx, u32 out[8]);            candidate value of leaf `idx`
+//   void store(u32 row, const u32* v, int n);  trace rows (mg_eval)
+//   void spill(u32 slot, const u32* v, int n); void fill(u32 slot, u32* v, int n);
+//   bool none(bool alive);                     wave-wide "no lane alive"
+#pragma once
+#include "mw_alu.h"
+#include "mw_isa.h"
+
+namespace mw {
+
+typedef u32 u32x16 __attribute__((ext_vector_type(16)));
+typedef u32 u32x32 __attribute__((ext_vector_type(32)));
+
+#define MW_FETCH_W(opnd, x)                                                   \
+  do {                                                                        \
+    u32 _o = (opnd);                                                          \
+    if (_o & MW_KBIT) {                                                       \
+      const u32* _p = cpool + (_o & 0x7fffu);                                 \
+      x[0] = _p[0]; x[1] = _p[1]; x[2] = _p[2]; x[3] = _p[3];                 \
+      x[4] = _p[4]; x[5] = _p[5]; x[6] = _p[6]; x[7] = _p[7];                 \
+    } else {                                                                  \
+      _o &= (MW_NW - 1);                                                      \
+      x[0] = F0[_o]; x[1] = F1[_o]; x[2] = F2[_o]; x[3] = F3[_o];             \
+      x[4] = F4[_o]; x[5] = F5[_o]; x[6] = F6[_o]; x[7] = F7[_o];             \
+    }                                                                         \
+  } while (0)
+
+#define MW_FETCH_N(opnd, v)                                                   \
+  do {                                                                        \
+    u32 _o = (opnd);                                                          \
+    if (_o & MW_KBIT) v = cpool[_o & 0x7fffu];                                \
+    else v = NF[_o & (MW_NN - 1)];                                            \
+  } while (0)
+
+#define MW_WRITE_W(d, r)                                                      \
+  do {                                                                        \
+    u32 _d = (d) & (MW_NW - 1);                                               \
+    F0[_d] = r[0]; F1[_d] = r[1]; F2[_d] = r[2]; F3[_d] = r[3];               \
+    F4[_d] = r[4]; F5[_d] = r[5]; F6[_d] = r[6]; F7[_d] = r[7];               \
+  } while (0)
+
+#define MW_WRITE_N(d, v) NF[(d) & (MW_NN - 1)] = (v)
+
+template <class Env>
+MW_HD bool mw_run(const u32* __restrict__ code, const u32* __restrict__ cpool, Env& env,
+                  bool alive, u32 flags) {
+  u32x16 F0 = 0, F1 = 0, F2 = 0, F3 = 0, F4 = 0, F5 = 0, F6 = 0, F7 = 0;
+  u32x32 NF = 0;
+  for (u32 pc = 0;; pc += 4) {
+    const u32 w0 = code[pc], w1 = code[pc + 1], w2 = code[pc + 2], w3 = code[pc + 3];
+    const u32 op = w0 & 0xffu;
+    const u32 w = w0 >> 16;
+    const u32 dst = w1 & 0xffffu, oa = w1 >> 16, ob = w2 & 0xffffu, oc = w2 >> 16;
+    u32 x[8], y[8], r[8];
+    u32 wk = 0;  // 1: write W[dst] = r, 2: write N[dst] = r[0]
+    switch (op) {
+      case MW_END:
+        return alive;
+      case MW_CHECK: {
+        u32 v;
+        MW_FETCH_N(oa, v);
+        alive = alive && (v != 0);
+        if ((flags & MW_FLAG_EARLY_EXIT) && env.none(alive)) return false;
+        break;
+      }
+      case MW_LEAF_W:
+        env.leaf(w3, r);
+        wk = 1;
+        break;
+      case MW_LEAF_N:
+        env.leaf(w3, r);
+        wk = 2;
+        break;
+      case MW_STORE_W:
+        MW_FETCH_W(oa, x);
+        env.store(w3, x, 8);
+        break;
+      case MW_STORE_N: {
+        MW_FETCH_N(oa, x[0]);
+        env.store(w3, x, 1);
+        break;
+      }
+      case MW_SPILL_W:
+        MW_FETCH_W(oa, x);
+        env.spill(w3, x, 8);
+        break;
+      case MW_FILL_W:
+        env.fill(w3, r, 8);
+        wk = 1;
+        break;
+      case MW_SPILL_N:
+        MW_FETCH_N(oa, x[0]);
+        env.spill(w3, x, 1);
+        break;
+      case MW_FILL_N:
+        env.fill(w3, r, 1);
+        wk = 2;
+        break;
+      case MW_MOV_W:
+        MW_FETCH_W(oa, x);
+        copy8(r, x);
+        wk = 1;
+        break;
+      case MW_MOV_N: {
+        u32 v;
+        MW_FETCH_N(oa, v);
+        r[0] = v;
+        wk = 2;
+        break;
+      }
+
+      // ---------------------------------------------------------- wide
+      case MW_W_ADD:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        add8(x, y, r);
+        canon(r, w);
+        wk = 1;
+        break;
+      case MW_W_SUB:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        sub8(x, y, r);
+        canon(r, w);
+        wk = 1;
+        break;
+      case MW_W_MUL:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        mul8(x, y, r);
+        canon(r, w);
+        wk = 1;
+        break;
+      case MW_W_AND:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = x[k] & y[k];
+        wk = 1;
+        break;
+      case MW_W_OR:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = x[k] | y[k];
+        wk = 1;
+        break;
+      case MW_W_XOR:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = x[k] ^ y[k];
+        wk = 1;
+        break;
+      case MW_W_NOT:
+        MW_FETCH_W(oa, x);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = ~x[k];
+        canon(r, w);
+        wk = 1;
+        break;
+      case MW_W_SHL:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        wshl(x, y, w, r);
+        wk = 1;
+        break;
+      case MW_W_LSHR:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        wlshr(x, y, w, r);
+        wk = 1;
+        break;
+      case MW_W_ASHR:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        washr(x, y, w, r);
+        wk = 1;
+        break;
+      case MW_W_UDIV:
+      case MW_W_UREM:
+      case MW_W_SDIV:
+      case MW_W_SREM:
+      case MW_W_SMOD:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        wdiv((int)(op - MW_W_UDIV), x, y, w, r);
+        wk = 1;
+        break;
+      case MW_W_ITE: {
+        u32 c;
+        MW_FETCH_N(oc, c);
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = c ? x[k] : y[k];
+        wk = 1;
+        break;
+      }
+      case MW_W_SHLI:
+        MW_FETCH_W(oa, x);
+        shl8(x, w3, r);
+        canon(r, w);
+        wk = 1;
+        break;
+      case MW_W_LSHRI:
+        MW_FETCH_W(oa, x);
+        shr8(x, w3, 0u, r);
+        canon(r, w);
+        wk = 1;
+        break;
+      case MW_W_ZEXTN: {
+        u32 v;
+        MW_FETCH_N(oa, v);
+        zero8(r);
+        r[0] = v;
+        wk = 1;
+        break;
+      }
+      case MW_W_SEXT:
+        MW_FETCH_W(oa, x);
+        sext8(x, w3);
+        canon(x, w);
+        copy8(r, x);
+        wk = 1;
+        break;
+      case MW_W_SEXTN: {
+        u32 v;
+        MW_FETCH_N(oa, v);
+        zero8(r);
+        r[0] = v;
+        sext8(r, w3);
+        canon(r, w);
+        wk = 1;
+        break;
+      }
+      case MW_W_INSN: {
+        u32 v;
+        MW_FETCH_W(oa, x);
+        MW_FETCH_N(ob, v);
+        zero8(y);
+        y[0] = v;
+        shl8(y, w3, r);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] |= x[k];
+        canon(r, w);
+        wk = 1;
+        break;
+      }
+
+      // ---------------------------------------------------------- wide -> narrow
+      case MW_N_EXTRACTW: {
+        MW_FETCH_W(oa, x);
+        shr8(x, w3, 0u, r);
+        r[0] = r[0] & nmask(w);
+        wk = 2;
+        break;
+      }
+      case MW_N_ULT:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        r[0] = ult8(x, y) ? 1u : 0u;
+        wk = 2;
+        break;
+      case MW_N_ULE:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        r[0] = ult8(y, x) ? 0u : 1u;
+        wk = 2;
+        break;
+      case MW_N_SLT:
+      case MW_N_SLE: {
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        // flip the sign bit (bit w-1) of both, then compare unsigned
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          int bit = (int)w - 1 - 32 * k;
+          u32 m = (bit >= 0 && bit < 32) ? (1u << bit) : 0u;
+          x[k] ^= m;
+          y[k] ^= m;
+        }
+        bool lt = (op == MW_N_SLT) ? ult8(x, y) : !ult8(y, x);
+        r[0] = lt ? 1u : 0u;
+        wk = 2;
+        break;
+      }
+      case MW_N_EQ:
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        r[0] = eq8(x, y) ? 1u : 0u;
+        wk = 2;
+        break;
+      case MW_N_UMULNO: {
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        u32 hi[8];
+        mulhi8(x, y, r, hi);
+        u32 ov = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ov |= (r[k] & ~limb_mask(w, k)) | hi[k];
+        r[0] = ov ? 0u : 1u;
+        wk = 2;
+        break;
+      }
+      case MW_N_ADDC: {
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);
+        u32 c = add8(x, y, r);
+        u32 bit = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          int b = (int)w - 32 * k;
+          bit |= (b >= 0 && b < 32) ? ((r[k] >> b) & 1u) : 0u;
+        }
+        r[0] = (w >= 256) ? c : bit;
+        wk = 2;
+        break;
+      }
+
+      // ---------------------------------------------------------- narrow
+      default: {
+        u32 a = 0, b = 0, v = 0;
+        const u32 m = nmask(w);
+        if (op >= MW_N_ADD) {
+          MW_FETCH_N(oa, a);
+          MW_FETCH_N(ob, b);
+        }
+        switch (op) {
+          case MW_N_ADD: v = (a + b) & m; break;
+          case MW_N_SUB: v = (a - b) & m; break;
+          case MW_N_MUL: v = (a * b) & m; break;
+          case MW_N_AND: v = a & b; break;
+          case MW_N_OR: v = a | b; break;
+          case MW_N_XOR: v = a ^ b; break;
+          case MW_N_NOT: v = (~a) & m; break;
+          case MW_N_SHL: v = n_shl(a, b, w); break;
+          case MW_N_LSHR: v = n_lshr(a, b, w); break;
+          case MW_N_ASHR: v = n_ashr(a, b, w); break;
+          case MW_N_UDIV:
+          case MW_N_UREM:
+          case MW_N_SDIV:
+          case MW_N_SREM:
+          case MW_N_SMOD: v = n_div((int)(op - MW_N_UDIV), a, b, w); break;
+          case MW_N_ITE: {
+            u32 c;
+            MW_FETCH_N(oc, c);
+            v = c ? a : b;
+            break;
+          }
+          case MW_N_SHLI: v = (w3 >= 32 ? 0u : (a << w3)) & m; break;
+          case MW_N_LSHRI: v = (w3 >= 32 ? 0u : (a >> w3)) & m; break;
+          case MW_N_SEXT: v = n_sext(a, w3) & m; break;
+          case MW_N_ULTN: v = a < b; break;
+          case MW_N_ULEN: v = a <= b; break;
+          case MW_N_SLTN: v = n_slt(a, b, w); break;
+          case MW_N_SLEN: v = n_sle(a, b, w); break;
+          case MW_N_EQN: v = a == b; break;
+          case MW_N_UMULNON: v = n_umulno(a, b, w); break;
+          case MW_N_ADDCN: {
+            u64 s = (u64)a + b;
+            v = (u32)((s >> w) & 1u);
+            break;
+          }
+          default:
+            return false;  // unknown opcode: verdict false (validated on load)
+        }
+        r[0] = v;
+        wk = 2;
+        break;
+      }
+    }
+    // single write-back point: keeps one SSA version of each register-file
+    // vector live across the dispatch (otherwise hipcc duplicates the files)
+    if (wk == 1) {
+      MW_WRITE_W(dst, r);
+    } else if (wk == 2) {
+      MW_WRITE_N(dst, r[0]);
+    }
+  }
+}
+
+}  // namespace mw

@@ -1,0 +1,87 @@
+// mw_keccak.h — Keccak-256 (original 0x01 padding, rate 136 B) for one message
+// per lane.  Replaces _pysha3.keccak_256 on the concrete-hash path
+// (mythril/support/support_utils.py:50-59; keccak_function_manager.py:57-69).
+// State: 25 x u64 lanes in VGPRs, fully unrolled permutation (static indices).
+#pragma once
+#include "mw_alu.h"
+
+namespace mw {
+
+MW_HD u64 rotl64(u64 x, int n) { return (x << n) | (x >> (64 - n)); }
+
+MW_HD void keccak_f1600(u64 A[25]) {
+  const u64 RC[24] = {
+      0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+      0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+      0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+      0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+      0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+      0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+  // rho offsets and pi lane order along the (x,y) -> (y, 2x+3y) cycle starting at lane 1
+  const int RHO[24] = {1, 3, 6, 10, 15, 21, 28, 36, 45, 55, 2, 14,
+                       27, 41, 56, 8, 25, 43, 62, 18, 39, 61, 20, 44};
+  const int PI[24] = {10, 7, 11, 17, 18, 3, 5, 16, 8, 21, 24, 4,
+                      15, 23, 19, 13, 12, 2, 20, 14, 22, 9, 6, 1};
+#pragma unroll 1
+  for (int rnd = 0; rnd < 24; ++rnd) {
+    u64 C[5];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) C[x] = A[x] ^ A[x + 5] ^ A[x + 10] ^ A[x + 15] ^ A[x + 20];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+      u64 D = C[(x + 4) % 5] ^ rotl64(C[(x + 1) % 5], 1);
+#pragma unroll
+      for (int y = 0; y < 25; y += 5) A[y + x] ^= D;
+    }
+    u64 t = A[1];
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      int j = PI[i];
+      u64 tmp = A[j];
+      A[j] = rotl64(t, RHO[i]);
+      t = tmp;
+    }
+#pragma unroll
+    for (int y = 0; y < 25; y += 5) {
+      u64 r0 = A[y], r1 = A[y + 1], r2 = A[y + 2], r3 = A[y + 3], r4 = A[y + 4];
+      A[y] = r0 ^ (~r1 & r2);
+      A[y + 1] = r1 ^ (~r2 & r3);
+      A[y + 2] = r2 ^ (~r3 & r4);
+      A[y + 3] = r3 ^ (~r4 & r0);
+      A[y + 4] = r4 ^ (~r0 & r1);
+    }
+    A[0] ^= RC[rnd];
+  }
+}
+
+// absorb + squeeze one message; out = 32 digest bytes as 4 little-endian u64 lanes
+MW_HD void keccak256_msg(const uint8_t* __restrict__ msg, u32 len, u64 out[4]) {
+  u64 A[25];
+#pragma unroll
+  for (int i = 0; i < 25; ++i) A[i] = 0;
+  const u32 nblk = len / 136u + 1u;
+  for (u32 blk = 0; blk < nblk; ++blk) {
+    const u32 base = blk * 136u;
+    const bool last = (blk + 1u == nblk);
+#pragma unroll
+    for (int lane = 0; lane < 17; ++lane) {
+      u64 v = 0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        u32 pos = base + (u32)(lane * 8 + b);
+        u32 byte = pos < len ? (u32)msg[pos] : 0u;
+        if (last && pos == len) byte ^= 0x01u;
+        if (last && (lane * 8 + b) == 135) byte ^= 0x80u;
+        v |= (u64)byte << (8 * b);
+      }
+      A[lane] ^= v;
+    }
+    keccak_f1600(A);
+  }
+  out[0] = A[0];
+  out[1] = A[1];
+  out[2] = A[2];
+  out[3] = A[3];
+}
+
+}  // namespace mw

@@ -1,0 +1,494 @@
+// mw_kernels.hip — gfx950 kernels and the C-ABI (include/mythril_witness.h).
+//
+// Kernels
+//   mw_search_kernel  grid (x: candidate chunks, y: programs), 256-thread blocks,
+//                     one candidate per lane; per-wave ballot -> lowest satisfying
+//                     lane -> atomicMin(u64) on the program's witness index.
+//   mw_eval_kernel    same interpreter on explicit (SoA) or generated assignments,
+//                     writing per-candidate verdicts and traced node values.
+//   mw_keccak_kernel  one message per lane, Keccak-256.
+// Host side: context (device, stream, events, spill/min/counter buffers),
+// program upload with full validation, thread-local error strings.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mythril_witness.h"
+#include "mw_interp.h"
+#include "mw_keccak.h"
+#include "mw_leaf.h"
+
+extern "C" int mw_fail(int code, const char* msg);
+extern "C" int mg_validate_desc(const mg_prog_desc* d);
+
+using namespace mw;
+
+namespace {
+
+struct ProgDev {
+  const u32* code;
+  const u32* consts;
+  const u32* leaves;
+  const u32* pool;
+  u32 n_spill;
+  u32 pad;
+};
+
+constexpr int kBlock = 256;
+
+struct SearchEnv {
+  const u32* __restrict__ leaves;
+  const u32* __restrict__ pool;
+  u64 seed;
+  u64 cand;
+  u32* __restrict__ spillbuf;
+  u64 nthreads;
+  u64 gtid;
+  __device__ void leaf(u32 idx, u32 out[8]) {
+    leaf_value(leaves + (u64)idx * MW_LEAF_WORDS, pool, seed, cand, out);
+  }
+  __device__ void store(u32, const u32*, int) {}
+  __device__ void spill(u32 slot, const u32* v, int n) {
+    for (int k = 0; k < n; ++k) spillbuf[((u64)slot * 8 + k) * nthreads + gtid] = v[k];
+  }
+  __device__ void fill(u32 slot, u32* v, int n) {
+    for (int k = 0; k < 8; ++k) v[k] = k < n ? spillbuf[((u64)slot * 8 + k) * nthreads + gtid] : 0u;
+  }
+  __device__ bool none(bool alive) { return __ballot(alive) == 0ull; }
+};
+
+struct EvalEnv {
+  const u32* __restrict__ leaves;
+  const u32* __restrict__ pool;
+  const u32* __restrict__ in;  // SoA rows, or null -> generated
+  u32* __restrict__ trace;
+  u64 ncand;
+  u64 idx;   // candidate position within this call
+  u64 seed;
+  u64 cand;  // generated candidate index
+  u32* __restrict__ spillbuf;
+  u64 nthreads;
+  u64 gtid;
+  __device__ void leaf(u32 li, u32 out[8]) {
+    const u32* L = leaves + (u64)li * MW_LEAF_WORDS;
+    if (in) {
+      const u32 w = L[MW_LEAF_WIDTH];
+      const u32 row = L[MW_LEAF_INROW];
+      const int nl = (int)((w + 31) / 32);
+      for (int k = 0; k < 8; ++k) out[k] = k < nl ? in[((u64)row + k) * ncand + idx] : 0u;
+      canon(out, w);
+    } else {
+      leaf_value(L, pool, seed, cand, out);
+    }
+  }
+  __device__ void store(u32 row, const u32* v, int n) {
+    if (trace)
+      for (int k = 0; k < n; ++k) trace[((u64)row + k) * ncand + idx] = v[k];
+  }
+  __device__ void spill(u32 slot, const u32* v, int n) {
+    for (int k = 0; k < n; ++k) spillbuf[((u64)slot * 8 + k) * nthreads + gtid] = v[k];
+  }
+  __device__ void fill(u32 slot, u32* v, int n) {
+    for (int k = 0; k < 8; ++k) v[k] = k < n ? spillbuf[((u64)slot * 8 + k) * nthreads + gtid] : 0u;
+  }
+  __device__ bool none(bool) { return false; }  // eval: never exit early
+};
+
+}  // namespace
+
+__global__ __launch_bounds__(kBlock) void mw_search_kernel(const ProgDev* __restrict__ progs, u64 seed,
+                                                           u64 begin, u64 count, u32 flags,
+                                                           u64* __restrict__ out_min,
+                                                           u64* __restrict__ counter,
+                                                           u32* __restrict__ spillbuf) {
+  const ProgDev P = progs[blockIdx.y];
+  const u64 nchunks = (count + kBlock - 1) / kBlock;
+  const u64 end = begin + count;
+  const u64 nthreads = (u64)gridDim.x * gridDim.y * kBlock;
+  const u64 gtid = ((u64)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x;
+  const u32 lane = threadIdx.x & 63u;
+  u64 evals = 0;
+  for (u64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const u64 base = begin + ch * kBlock;
+    if (flags & MW_FLAG_STOP_AFTER_HIT) {
+      u64 m = __hip_atomic_load(&out_min[blockIdx.y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (m <= base) break;
+    }
+    const u64 cand = base + threadIdx.x;
+    const bool valid = cand < end;
+    SearchEnv env{P.leaves, P.pool, seed, cand, spillbuf, nthreads, gtid};
+    const bool ok = mw_run(P.code, P.consts, env, valid, flags);
+    const u64 hit = __ballot(ok);
+    if (hit) {
+      const u32 first = (u32)__ffsll((unsigned long long)hit) - 1u;
+      if (lane == first) atomicMin((unsigned long long*)&out_min[blockIdx.y], (unsigned long long)cand);
+    }
+    evals += (u64)__popcll(__ballot(valid));
+  }
+  if (lane == 0 && evals) atomicAdd((unsigned long long*)counter, (unsigned long long)evals);
+}
+
+__global__ __launch_bounds__(kBlock) void mw_eval_kernel(ProgDev P, const u32* __restrict__ in,
+                                                         u64 ncand, u64 seed, u64 begin,
+                                                         u32* __restrict__ verdict,
+                                                         u32* __restrict__ trace,
+                                                         u32* __restrict__ spillbuf) {
+  const u64 nthreads = (u64)gridDim.x * kBlock;
+  const u64 gtid = (u64)blockIdx.x * kBlock + threadIdx.x;
+  const u64 nchunks = (ncand + kBlock - 1) / kBlock;
+  for (u64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const u64 idx = ch * kBlock + threadIdx.x;
+    const bool valid = idx < ncand;
+    EvalEnv env{P.leaves, P.pool, in, valid ? trace : nullptr, ncand, valid ? idx : 0,
+                seed, begin + idx, spillbuf, nthreads, gtid};
+    const bool ok = mw_run(P.code, P.consts, env, valid, 0u);
+    if (valid) verdict[idx] = ok ? 1u : 0u;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void mw_keccak_kernel(const uint8_t* __restrict__ data,
+                                                           const u64* __restrict__ off,
+                                                           const u32* __restrict__ len, u64 n,
+                                                           uint8_t* __restrict__ out) {
+  for (u64 i = (u64)blockIdx.x * kBlock + threadIdx.x; i < n; i += (u64)gridDim.x * kBlock) {
+    u64 h[4];
+    keccak256_msg(data + off[i], len[i], h);
+    u64* o = (u64*)(out + 32 * i);
+    o[0] = h[0];
+    o[1] = h[1];
+    o[2] = h[2];
+    o[3] = h[3];
+  }
+}
+
+// =============================================================== host side
+namespace {
+
+int fail(int code, const std::string& msg) { return mw_fail(code, msg.c_str()); }
+
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t _e = (x);                                                            \
+    if (_e != hipSuccess) return fail(MG_E_HIP, std::string(#x ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+}  // namespace
+
+struct mg_ctx {
+  int dev = 0;
+  int ncu = 256;
+  hipStream_t stream = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  u32* d_spill = nullptr;
+  size_t spill_bytes = 0;
+  u64* d_min = nullptr;
+  size_t nmin = 0;
+  u64* d_counter = nullptr;
+  ProgDev* d_progs = nullptr;
+  size_t nprogs_cap = 0;
+  std::mutex mu;
+};
+
+struct mg_prog {
+  mg_ctx* ctx = nullptr;
+  u32* d_buf = nullptr;
+  ProgDev dev{};
+  mg_prog_desc desc{};
+  u64 ops_per_eval = 0;
+};
+
+namespace {
+
+int ensure_spill(mg_ctx* c, size_t bytes) {
+  if (bytes <= c->spill_bytes) return 0;
+  if (c->d_spill) HIPCHK(hipFree(c->d_spill));
+  c->d_spill = nullptr;
+  c->spill_bytes = 0;
+  HIPCHK(hipMalloc(&c->d_spill, bytes));
+  c->spill_bytes = bytes;
+  return 0;
+}
+
+int ensure_min(mg_ctx* c, size_t n) {
+  if (n <= c->nmin) return 0;
+  if (c->d_min) HIPCHK(hipFree(c->d_min));
+  if (c->d_progs) HIPCHK(hipFree(c->d_progs));
+  c->d_min = nullptr;
+  c->d_progs = nullptr;
+  HIPCHK(hipMalloc(&c->d_min, n * sizeof(u64)));
+  HIPCHK(hipMalloc(&c->d_progs, n * sizeof(ProgDev)));
+  c->nmin = n;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mg_device_count(int* n) {
+  if (!n) return fail(MG_E_ARG, "null out");
+  int c = 0;
+  HIPCHK(hipGetDeviceCount(&c));
+  *n = c;
+  return 0;
+}
+
+int mg_init(int device, mg_ctx** out) {
+  if (!out) return fail(MG_E_ARG, "null out");
+  *out = nullptr;
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(MG_E_ARG, "no such device");
+  HIPCHK(hipSetDevice(device));
+  mg_ctx* c = new mg_ctx();
+  c->dev = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    c->ncu = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
+      hipMalloc(&c->d_counter, sizeof(u64)) != hipSuccess) {
+    delete c;
+    return fail(MG_E_HIP, "context setup failed");
+  }
+  *out = c;
+  return 0;
+}
+
+int mg_free(mg_ctx* c) {
+  if (!c) return 0;
+  hipSetDevice(c->dev);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->d_spill) hipFree(c->d_spill);
+  if (c->d_min) hipFree(c->d_min);
+  if (c->d_progs) hipFree(c->d_progs);
+  if (c->d_counter) hipFree(c->d_counter);
+  if (c->e0) hipEventDestroy(c->e0);
+  if (c->e1) hipEventDestroy(c->e1);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
+  if (!c || !d || !out) return fail(MG_E_ARG, "null argument");
+  *out = nullptr;
+  int rc = mg_validate_desc(d);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  const size_t nc = d->ncode_words, nk = d->nconst_words + 8, nl = d->nleaves * MW_LEAF_WORDS + 8,
+               np = d->npool_words + 8;
+  const size_t total = nc + nk + nl + np;
+  mg_prog* p = new mg_prog();
+  p->ctx = c;
+  p->desc = *d;
+  p->ops_per_eval = d->ops_per_eval;
+  if (hipMalloc(&p->d_buf, total * sizeof(u32)) != hipSuccess) {
+    delete p;
+    return fail(MG_E_NOMEM, "program upload allocation failed");
+  }
+  std::vector<u32> h(total, 0u);
+  std::memcpy(h.data(), d->code, nc * 4);
+  if (d->nconst_words) std::memcpy(h.data() + nc, d->consts, d->nconst_words * 4);
+  if (d->nleaves) std::memcpy(h.data() + nc + nk, d->leaves, d->nleaves * MW_LEAF_WORDS * 4);
+  if (d->npool_words) std::memcpy(h.data() + nc + nk + nl, d->pool, d->npool_words * 4);
+  if (hipMemcpy(p->d_buf, h.data(), total * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(p->d_buf);
+    delete p;
+    return fail(MG_E_HIP, "program upload copy failed");
+  }
+  p->dev.code = p->d_buf;
+  p->dev.consts = p->d_buf + nc;
+  p->dev.leaves = p->d_buf + nc + nk;
+  p->dev.pool = p->d_buf + nc + nk + nl;
+  p->dev.n_spill = d->n_spill;
+  // the desc's host pointers are not retained
+  p->desc.code = nullptr;
+  p->desc.consts = nullptr;
+  p->desc.leaves = nullptr;
+  p->desc.pool = nullptr;
+  *out = p;
+  return 0;
+}
+
+int mg_prog_free(mg_prog* p) {
+  if (!p) return 0;
+  hipSetDevice(p->ctx->dev);
+  if (p->d_buf) hipFree(p->d_buf);
+  delete p;
+  return 0;
+}
+
+int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uint64_t begin,
+              uint64_t count, uint32_t flags, uint64_t* out_min_idx, mg_stats* st) {
+  if (!c || !progs || !out_min_idx || nprog == 0) return fail(MG_E_ARG, "null argument");
+  if (nprog > 65535) return fail(MG_E_ARG, "too many programs per launch");
+  if (count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad candidate range");
+  std::lock_guard<std::mutex> lk(c->mu);
+  const double t0 = now_ms();
+  HIPCHK(hipSetDevice(c->dev));
+  int rc = ensure_min(c, nprog);
+  if (rc) return rc;
+  std::vector<ProgDev> hp(nprog);
+  u32 max_spill = 0;
+  u64 ops = 0;
+  for (size_t i = 0; i < nprog; ++i) {
+    if (!progs[i] || progs[i]->ctx != c) return fail(MG_E_ARG, "program from another context");
+    hp[i] = progs[i]->dev;
+    max_spill = std::max(max_spill, progs[i]->dev.n_spill);
+    ops += progs[i]->ops_per_eval;
+  }
+  const u64 nchunks = (count + kBlock - 1) / kBlock;
+  // enough blocks to fill the chip several times over, split across programs
+  u64 gx = std::max<u64>(1, (u64)c->ncu * 8 / nprog);
+  gx = std::min<u64>(gx, nchunks);
+  const u64 nthreads = gx * nprog * kBlock;
+  rc = ensure_spill(c, std::max<size_t>(4, (size_t)max_spill * 8 * nthreads * sizeof(u32)));
+  if (rc) return rc;
+  std::vector<u64> init(nprog, MG_NONE);
+  HIPCHK(hipMemcpyAsync(c->d_progs, hp.data(), nprog * sizeof(ProgDev), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_min, init.data(), nprog * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_counter, 0, sizeof(u64), c->stream));
+  HIPCHK(hipEventRecord(c->e0, c->stream));
+  hipLaunchKernelGGL(mw_search_kernel, dim3((u32)gx, (u32)nprog), dim3(kBlock), 0, c->stream, c->d_progs,
+                     seed, begin, count, flags, c->d_min, c->d_counter, c->d_spill);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->e1, c->stream));
+  u64 evals = 0;
+  HIPCHK(hipMemcpyAsync(out_min_idx, c->d_min, nprog * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(&evals, c->d_counter, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (st) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
+    st->kernel_ms = ms;
+    st->wall_ms = now_ms() - t0;
+    st->evals = evals;  // summed over every program's blocks
+    st->launches = 1;
+    st->ops = (double)evals / (double)nprog * (double)ops;
+  }
+  return 0;
+}
+
+static int eval_common(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncand, uint64_t seed,
+                       uint64_t begin, uint32_t* verdict, uint32_t* trace) {
+  if (!c || !p || !verdict || ncand == 0) return fail(MG_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  const u64 nchunks = (ncand + kBlock - 1) / kBlock;
+  const u64 gx = std::min<u64>(nchunks, (u64)c->ncu * 8);
+  const u64 nthreads = gx * kBlock;
+  int rc = ensure_spill(c, std::max<size_t>(4, (size_t)p->dev.n_spill * 8 * nthreads * sizeof(u32)));
+  if (rc) return rc;
+  u32 *d_in = nullptr, *d_v = nullptr, *d_t = nullptr;
+  const size_t nin = leaves_soa ? (size_t)p->desc.n_input_rows * ncand : 0;
+  const size_t ntr = trace ? (size_t)p->desc.n_trace_rows * ncand : 0;
+  auto cleanup = [&]() {
+    if (d_in) hipFree(d_in);
+    if (d_v) hipFree(d_v);
+    if (d_t) hipFree(d_t);
+  };
+  if (nin && hipMalloc(&d_in, nin * 4) != hipSuccess) { cleanup(); return fail(MG_E_NOMEM, "eval input alloc"); }
+  if (hipMalloc(&d_v, ncand * 4) != hipSuccess) { cleanup(); return fail(MG_E_NOMEM, "eval verdict alloc"); }
+  if (ntr && hipMalloc(&d_t, ntr * 4) != hipSuccess) { cleanup(); return fail(MG_E_NOMEM, "eval trace alloc"); }
+  if (nin && hipMemcpyAsync(d_in, leaves_soa, nin * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+    cleanup(); return fail(MG_E_HIP, "eval input copy");
+  }
+  if (ntr) hipMemsetAsync(d_t, 0, ntr * 4, c->stream);
+  hipLaunchKernelGGL(mw_eval_kernel, dim3((u32)gx), dim3(kBlock), 0, c->stream, p->dev, (const u32*)d_in,
+                     (u64)ncand, seed, begin, d_v, d_t, c->d_spill);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, ncand * 4, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && ntr) e = hipMemcpyAsync(trace, d_t, ntr * 4, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  cleanup();
+  if (e != hipSuccess) return fail(MG_E_HIP, std::string("eval: ") + hipGetErrorString(e));
+  return 0;
+}
+
+int mg_eval(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncand, uint32_t* verdict,
+            uint32_t* trace) {
+  if (p && p->desc.nleaves && p->desc.n_input_rows && !leaves_soa) return fail(MG_E_ARG, "leaves_soa required");
+  if (p && p->desc.nleaves && !p->desc.n_input_rows) return fail(MG_E_ARG, "program has no input rows");
+  static const u32 dummy = 0;
+  return eval_common(c, p, leaves_soa ? leaves_soa : (p && p->desc.nleaves ? nullptr : &dummy), ncand, 0, 0,
+                     verdict, trace);
+}
+
+int mg_eval_generated(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, size_t count,
+                      uint32_t* verdict, uint32_t* trace) {
+  return eval_common(c, p, nullptr, count, seed, begin, verdict, trace);
+}
+
+int mg_keccak256_device(mg_ctx* c, const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len, size_t n,
+                        uint8_t* d_out32, mg_stats* st) {
+  if (!c || (!n)) return fail(MG_E_ARG, "bad argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  const double t0 = now_ms();
+  const u64 gx = std::min<u64>((n + kBlock - 1) / kBlock, (u64)c->ncu * 16);
+  HIPCHK(hipEventRecord(c->e0, c->stream));
+  hipLaunchKernelGGL(mw_keccak_kernel, dim3((u32)gx), dim3(kBlock), 0, c->stream, d_data, (const u64*)d_off,
+                     (const u32*)d_len, (u64)n, d_out32);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->e1, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (st) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
+    st->kernel_ms = ms;
+    st->wall_ms = now_ms() - t0;
+    st->evals = n;
+    st->launches = 1;
+    st->ops = 0;
+  }
+  return 0;
+}
+
+int mg_keccak256(mg_ctx* c, const uint8_t* data, size_t ndata, const uint64_t* off, const uint32_t* len, size_t n,
+                 uint8_t* out32, mg_stats* st) {
+  if (!c || !off || !len || !out32) return fail(MG_E_ARG, "null argument");
+  if (n == 0) return 0;
+  for (size_t i = 0; i < n; ++i)
+    if (off[i] + len[i] > ndata) return fail(MG_E_ARG, "message out of range");
+  HIPCHK(hipSetDevice(c->dev));
+  uint8_t *dd = nullptr, *dout = nullptr;
+  u64* doff = nullptr;
+  u32* dlen = nullptr;
+  auto cleanup = [&]() {
+    if (dd) hipFree(dd);
+    if (dout) hipFree(dout);
+    if (doff) hipFree(doff);
+    if (dlen) hipFree(dlen);
+  };
+  if (hipMalloc(&dd, std::max<size_t>(ndata, 1)) != hipSuccess || hipMalloc(&dout, 32 * n) != hipSuccess ||
+      hipMalloc(&doff, 8 * n) != hipSuccess || hipMalloc(&dlen, 4 * n) != hipSuccess) {
+    cleanup();
+    return fail(MG_E_NOMEM, "keccak alloc");
+  }
+  hipError_t e = hipSuccess;
+  if (ndata) e = hipMemcpy(dd, data, ndata, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(doff, off, 8 * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(dlen, len, 4 * n, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    cleanup();
+    return fail(MG_E_HIP, "keccak copy-in");
+  }
+  int rc = mg_keccak256_device(c, dd, doff, dlen, n, dout, st);
+  if (rc == 0 && hipMemcpy(out32, dout, 32 * n, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(MG_E_HIP, "keccak copy-out");
+  cleanup();
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+// mw_leaf.h — on-device candidate generation (never materialised in HBM).
+//
+// Candidate index c (u64) -> value of each free variable ("leaf": sender_N,
+// call_valueN, N_calldata bytes, calldatasize, storage/balance reads,
+// keccak UF results — the leaf schema of SURVEY.md §8a row A8,
+// mythril/laser/ethereum/transaction/symbolic.py:118-136, calldata.py:214-215).
+//   random leaf: Philox4x32-10(key=(seed_lo ^ id, seed_hi), ctr=(c_lo, c_hi, blk, 0)),
+//                blk 0 -> limbs 0..3, blk 1 -> limbs 4..7, masked to width
+//   pool leaf:   digit = (c >> shift) & (2^bits - 1); entry = pool[digit];
+//                entry flag RANDOM -> random value above, else the constant.
+// Restated independently in oracle/philox.py (pinned by Random123 KATs).
+#pragma once
+#include "mw_alu.h"
+#include "mw_isa.h"
+
+namespace mw {
+
+MW_HD void philox4x32_10(u32 c[4], u32 k0, u32 k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    u64 p0 = (u64)0xD2511F53u * c[0];
+    u64 p1 = (u64)0xCD9E8D57u * c[2];
+    u32 hi0 = (u32)(p0 >> 32), lo0 = (u32)p0;
+    u32 hi1 = (u32)(p1 >> 32), lo1 = (u32)p1;
+    u32 n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+MW_HD void random_leaf(u32 id, u32 w, u64 seed, u64 cand, u32 out[8]) {
+  u32 k0 = (u32)seed ^ id, k1 = (u32)(seed >> 32);
+  u32 c[4] = {(u32)cand, (u32)(cand >> 32), 0u, 0u};
+  philox4x32_10(c, k0, k1);
+  out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = c[3];
+  if (w > 128) {
+    u32 d[4] = {(u32)cand, (u32)(cand >> 32), 1u, 0u};
+    philox4x32_10(d, k0, k1);
+    out[4] = d[0]; out[5] = d[1]; out[6] = d[2]; out[7] = d[3];
+  } else {
+    out[4] = out[5] = out[6] = out[7] = 0u;
+  }
+  canon(out, w);
+}
+
+// leaf: MW_LEAF_WORDS words (uniform); pool: per-lane gather
+MW_HD void leaf_value(const u32* __restrict__ leaf, const u32* __restrict__ pool, u64 seed,
+                      u64 cand, u32 out[8]) {
+  const u32 w = leaf[MW_LEAF_WIDTH];
+  const u32 id = leaf[MW_LEAF_ID];
+  if (leaf[MW_LEAF_KIND] == 1u) {
+    const u32 bits = leaf[MW_LEAF_BITS];
+    const u32 digit = (u32)(cand >> leaf[MW_LEAF_SHIFT]) & ((bits >= 32) ? 0xffffffffu : ((1u << bits) - 1u));
+    const u32* e = pool + leaf[MW_LEAF_POOL] + (u64)digit * MW_POOL_ENTRY_WORDS;
+    if (e[0] & 1u) {
+      random_leaf(id, w, seed, cand, out);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) out[k] = e[1 + k];
+      canon(out, w);
+    }
+  } else {
+    random_leaf(id, w, seed, cand, out);
+  }
+}
+
+}  // namespace mw

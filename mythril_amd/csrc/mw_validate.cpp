@@ -1,0 +1,156 @@
+// mw_validate.cpp — program validation and error reporting shared by the
+// device library (libmythril_witness.so) and the host emulator.  Every program
+// is checked before upload: opcodes, operand slots, constant-pool offsets,
+// widths, leaf/pool/trace/spill ranges, and a terminating END — so the
+// interpreter loop can never run off the stream or index out of its files.
+#include <stdint.h>
+
+#include <algorithm>
+#include <string>
+
+#include "../../include/mythril_witness.h"
+#include "mw_isa.h"
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+// operand classes per opcode: returns false for unknown opcodes
+// kinds: 0 none, 1 W-or-K source, 2 N-or-K source, 3 W dst, 4 N dst
+struct OpShape {
+  int dst, a, b, c;
+  bool wide;  // width rules: wide ops 1..256, narrow 1..32
+};
+
+bool op_shape(u32 op, OpShape& s) {
+  s = OpShape{0, 0, 0, 0, false};
+  switch (op) {
+    case MW_END: return true;
+    case MW_CHECK: s.a = 2; return true;
+    case MW_LEAF_W: s.dst = 3; return true;
+    case MW_LEAF_N: s.dst = 4; return true;
+    case MW_STORE_W: s.a = 1; return true;
+    case MW_STORE_N: s.a = 2; return true;
+    case MW_SPILL_W: s.a = 1; return true;
+    case MW_FILL_W: s.dst = 3; return true;
+    case MW_SPILL_N: s.a = 2; return true;
+    case MW_FILL_N: s.dst = 4; return true;
+    case MW_MOV_W: s.dst = 3; s.a = 1; return true;
+    case MW_MOV_N: s.dst = 4; s.a = 2; return true;
+    case MW_W_ADD: case MW_W_SUB: case MW_W_MUL: case MW_W_AND: case MW_W_OR: case MW_W_XOR:
+    case MW_W_SHL: case MW_W_LSHR: case MW_W_ASHR: case MW_W_UDIV: case MW_W_UREM:
+    case MW_W_SDIV: case MW_W_SREM: case MW_W_SMOD:
+      s.dst = 3; s.a = 1; s.b = 1; s.wide = true; return true;
+    case MW_W_NOT: case MW_W_SHLI: case MW_W_LSHRI: case MW_W_SEXT:
+      s.dst = 3; s.a = 1; s.wide = true; return true;
+    case MW_W_ITE: s.dst = 3; s.a = 1; s.b = 1; s.c = 2; s.wide = true; return true;
+    case MW_W_ZEXTN: case MW_W_SEXTN: s.dst = 3; s.a = 2; s.wide = true; return true;
+    case MW_W_INSN: s.dst = 3; s.a = 1; s.b = 2; s.wide = true; return true;
+    case MW_N_EXTRACTW: s.dst = 4; s.a = 1; return true;
+    case MW_N_ULT: case MW_N_ULE: case MW_N_SLT: case MW_N_SLE: case MW_N_EQ:
+    case MW_N_UMULNO: case MW_N_ADDC:
+      s.dst = 4; s.a = 1; s.b = 1; s.wide = true; return true;
+    case MW_N_ADD: case MW_N_SUB: case MW_N_MUL: case MW_N_AND: case MW_N_OR: case MW_N_XOR:
+    case MW_N_SHL: case MW_N_LSHR: case MW_N_ASHR: case MW_N_UDIV: case MW_N_UREM:
+    case MW_N_SDIV: case MW_N_SREM: case MW_N_SMOD: case MW_N_ULTN: case MW_N_ULEN:
+    case MW_N_SLTN: case MW_N_SLEN: case MW_N_EQN: case MW_N_UMULNON: case MW_N_ADDCN:
+      s.dst = 4; s.a = 2; s.b = 2; return true;
+    case MW_N_NOT: case MW_N_SHLI: case MW_N_LSHRI: case MW_N_SEXT:
+      s.dst = 4; s.a = 2; return true;
+    case MW_N_ITE: s.dst = 4; s.a = 2; s.b = 2; s.c = 2; return true;
+    default: return false;
+  }
+}
+
+bool check_operand(int kind, u32 f, size_t nconst) {
+  if (kind == 0) return true;
+  if (kind == 3) return f < MW_NW;
+  if (kind == 4) return f < MW_NN;
+  if (f & MW_KBIT) {
+    size_t o = f & 0x7fffu;
+    return o + (kind == 1 ? 8 : 1) <= nconst;
+  }
+  return kind == 1 ? f < MW_NW : f < MW_NN;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mw_fail(int code, const char* msg) {
+  g_err = msg ? msg : "";
+  return code;
+}
+
+const char* mg_last_error(void) { return g_err.c_str(); }
+
+int mg_validate_desc(const mg_prog_desc* d) {
+  if (!d || !d->code || d->ncode_words < 4 || d->ncode_words % 4)
+    return fail(MG_E_PROG, "code must be a non-empty multiple of 4 words");
+  if (d->nleaves && !d->leaves) return fail(MG_E_PROG, "leaf table missing");
+  if (d->nconst_words > 0x8000) return fail(MG_E_PROG, "constant pool exceeds 32768 words");
+  const size_t n = d->ncode_words / 4;
+  if ((d->code[4 * (n - 1)] & 0xffu) != MW_END) return fail(MG_E_PROG, "program must end with END");
+  for (size_t i = 0; i < n; ++i) {
+    const u32* I = d->code + 4 * i;
+    const u32 op = I[0] & 0xffu, w = I[0] >> 16;
+    OpShape s;
+    if (!op_shape(op, s)) return fail(MG_E_PROG, "unknown opcode " + std::to_string(op) + " at " + std::to_string(i));
+    if (op == MW_END && i != n - 1) return fail(MG_E_PROG, "END before the last instruction");
+    const u32 dst = I[1] & 0xffffu, a = I[1] >> 16, b = I[2] & 0xffffu, c = I[2] >> 16;
+    if (!check_operand(s.dst, dst, d->nconst_words) || !check_operand(s.a, a, d->nconst_words) ||
+        !check_operand(s.b, b, d->nconst_words) || !check_operand(s.c, c, d->nconst_words))
+      return fail(MG_E_PROG, "operand out of range at instruction " + std::to_string(i));
+    if (s.dst == 3 || s.dst == 4 || s.a || s.b) {
+      const u32 maxw = (s.wide || s.dst == 3) ? 256u : 32u;
+      if (op != MW_CHECK && op != MW_STORE_W && op != MW_STORE_N && op != MW_SPILL_W &&
+          op != MW_SPILL_N && op != MW_FILL_W && op != MW_FILL_N && op != MW_MOV_W && op != MW_MOV_N &&
+          op != MW_LEAF_W && op != MW_LEAF_N && (w < 1 || w > maxw))
+        return fail(MG_E_PROG, "bad width " + std::to_string(w) + " at instruction " + std::to_string(i));
+    }
+    switch (op) {
+      case MW_LEAF_W: case MW_LEAF_N:
+        if (I[3] >= d->nleaves) return fail(MG_E_PROG, "leaf index out of range");
+        break;
+      case MW_STORE_W:
+        if ((u64)I[3] + 8 > d->n_trace_rows) return fail(MG_E_PROG, "trace row out of range");
+        break;
+      case MW_STORE_N:
+        if ((u64)I[3] + 1 > d->n_trace_rows) return fail(MG_E_PROG, "trace row out of range");
+        break;
+      case MW_SPILL_W: case MW_FILL_W: case MW_SPILL_N: case MW_FILL_N:
+        if (I[3] >= d->n_spill) return fail(MG_E_PROG, "spill slot out of range");
+        break;
+      case MW_W_SHLI: case MW_W_LSHRI: case MW_N_EXTRACTW: case MW_W_INSN:
+        if (I[3] >= 256) return fail(MG_E_PROG, "immediate shift out of range");
+        break;
+      case MW_W_SEXT: case MW_W_SEXTN: case MW_N_SEXT:
+        if (I[3] < 1 || I[3] > w) return fail(MG_E_PROG, "bad sign-extension source width");
+        break;
+      default: break;
+    }
+  }
+  for (size_t l = 0; l < d->nleaves; ++l) {
+    const u32* L = d->leaves + l * MW_LEAF_WORDS;
+    if (L[MW_LEAF_WIDTH] < 1 || L[MW_LEAF_WIDTH] > 256) return fail(MG_E_PROG, "bad leaf width");
+    if (L[MW_LEAF_KIND] == 1) {
+      if (L[MW_LEAF_BITS] > 24 || L[MW_LEAF_SHIFT] > 63) return fail(MG_E_PROG, "bad pool digit field");
+      u64 need = (u64)L[MW_LEAF_POOL] + ((u64)1 << L[MW_LEAF_BITS]) * MW_POOL_ENTRY_WORDS;
+      if (need > d->npool_words) return fail(MG_E_PROG, "pool out of range");
+    } else if (L[MW_LEAF_KIND] != 0) {
+      return fail(MG_E_PROG, "bad leaf kind");
+    }
+    if ((u64)L[MW_LEAF_INROW] + (L[MW_LEAF_WIDTH] + 31) / 32 > d->n_input_rows && d->n_input_rows)
+      return fail(MG_E_PROG, "leaf input row out of range");
+  }
+  return 0;
+}
+
+}  // extern "C"

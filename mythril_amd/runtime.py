@@ -1,0 +1,237 @@
+"""ctypes binding of ``libmythril_witness.so`` (include/mythril_witness.h).
+
+This is the only way the product reaches the device.  There is no CPU
+fallback: if the library or a GPU is missing, :func:`load_library` /
+:class:`Device` raise :class:`EngineUnavailable`, and callers (the drop-in
+``get_model``) route the query to z3 exactly as the reference does.  ctypes
+releases the GIL for the duration of each call, like z3's own bindings.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .compiler import Program
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmythril_witness.so")
+MG_NONE = (1 << 64) - 1
+
+
+class EngineUnavailable(RuntimeError):
+    """The HIP extension or the device is not available."""
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class MgProgDesc(ctypes.Structure):
+    _fields_ = [
+        ("code", ctypes.c_void_p), ("ncode_words", ctypes.c_size_t),
+        ("consts", ctypes.c_void_p), ("nconst_words", ctypes.c_size_t),
+        ("leaves", ctypes.c_void_p), ("nleaves", ctypes.c_size_t),
+        ("pool", ctypes.c_void_p), ("npool_words", ctypes.c_size_t),
+        ("n_spill", ctypes.c_uint32), ("n_trace_rows", ctypes.c_uint32),
+        ("n_input_rows", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+        ("ops_per_eval", ctypes.c_uint64),
+    ]
+
+
+class MgStats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_double), ("wall_ms", ctypes.c_double),
+                ("evals", ctypes.c_uint64), ("launches", ctypes.c_uint64), ("ops", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_P = ctypes.c_void_p
+_lib = None
+_lib_lock = threading.Lock()
+
+SIGNATURES = {
+    "mg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "mg_init": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_P)]),
+    "mg_free": (ctypes.c_int, [_P]),
+    "mg_prog_load": (ctypes.c_int, [_P, ctypes.POINTER(MgProgDesc), ctypes.POINTER(_P)]),
+    "mg_prog_free": (ctypes.c_int, [_P]),
+    "mg_search": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
+                                 ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
+                                 ctypes.POINTER(MgStats)]),
+    "mg_eval": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t, _P, _P]),
+    "mg_eval_generated": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, _P, _P]),
+    "mg_keccak256": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _P, _P, ctypes.c_size_t, _P, ctypes.POINTER(MgStats)]),
+    "mg_keccak256_device": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_size_t, _P, ctypes.POINTER(MgStats)]),
+    "mg_validate_desc": (ctypes.c_int, [ctypes.POINTER(MgProgDesc)]),
+    "mg_last_error": (ctypes.c_char_p, []),
+}
+
+
+def bind(lib):
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+def load_library(path: str = LIB_PATH):
+    """Load the HIP library; raises EngineUnavailable (never falls back)."""
+    global _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise EngineUnavailable(f"HIP extension not built: {path} (run python -m mythril_amd.build)")
+            try:
+                _lib = bind(ctypes.CDLL(path))
+            except OSError as e:
+                raise EngineUnavailable(f"cannot load {path}: {e}") from e
+        return _lib
+
+
+def _ptr(a: np.ndarray) -> Optional[int]:
+    return a.ctypes.data if a is not None and a.size else None
+
+
+def make_desc(p: Program) -> Tuple[MgProgDesc, list]:
+    keep = [np.ascontiguousarray(x, dtype=np.uint32) for x in (p.code, p.consts, p.leaves, p.pool)]
+    code, consts, leaves, pool = keep
+    d = MgProgDesc(
+        code=_ptr(code), ncode_words=code.size,
+        consts=_ptr(consts), nconst_words=consts.size,
+        leaves=_ptr(leaves), nleaves=leaves.size // 8,
+        pool=_ptr(pool), npool_words=pool.size,
+        n_spill=p.n_spill, n_trace_rows=p.n_trace_rows, n_input_rows=p.n_input_rows, reserved=0,
+        ops_per_eval=p.ops_per_eval)
+    return d, keep
+
+
+def _check(lib, rc: int, what: str):
+    if rc != 0:
+        msg = lib.mg_last_error()
+        raise EngineError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+class DeviceProgram:
+    def __init__(self, dev: "Device", handle: int, prog: Program):
+        self.dev = dev
+        self.handle = handle
+        self.prog = prog
+
+    def free(self):
+        if self.handle:
+            self.dev.lib.mg_prog_free(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Device:
+    """One HIP device context (one process per GPU; see mythril_amd.distributed)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        n = ctypes.c_int(0)
+        rc = self.lib.mg_device_count(ctypes.byref(n))
+        if rc != 0 or n.value == 0:
+            raise EngineUnavailable("no HIP device visible")
+        h = _P()
+        _check(self.lib, self.lib.mg_init(device, ctypes.byref(h)), "mg_init")
+        self.handle = h.value
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            self.lib.mg_free(self.handle)
+            self.handle = None
+
+    def load(self, p: Program) -> DeviceProgram:
+        d, keep = make_desc(p)
+        h = _P()
+        _check(self.lib, self.lib.mg_prog_load(self.handle, ctypes.byref(d), ctypes.byref(h)), "mg_prog_load")
+        return DeviceProgram(self, h.value, p)
+
+    def search(self, progs: Sequence[DeviceProgram], seed: int, begin: int, count: int,
+               flags: int = 0) -> Tuple[List[Optional[int]], dict]:
+        arr = (_P * len(progs))(*[dp.handle for dp in progs])
+        out = (ctypes.c_uint64 * len(progs))()
+        st = MgStats()
+        _check(self.lib, self.lib.mg_search(self.handle, arr, len(progs), seed & ((1 << 64) - 1), begin, count,
+                                            flags, out, ctypes.byref(st)), "mg_search")
+        res = [None if v == MG_NONE else int(v) for v in out]
+        return res, st.as_dict()
+
+    def eval(self, dp: DeviceProgram, leaves_soa: Optional[np.ndarray], ncand: int,
+             trace: bool = True) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+        v = np.zeros(ncand, dtype=np.uint32)
+        t = np.zeros(dp.prog.n_trace_rows * ncand, dtype=np.uint32) if trace and dp.prog.n_trace_rows else None
+        inp = np.ascontiguousarray(leaves_soa, dtype=np.uint32) if leaves_soa is not None else None
+        _check(self.lib, self.lib.mg_eval(self.handle, dp.handle, _ptr(inp) if inp is not None else None, ncand,
+                                          v.ctypes.data, _ptr(t) if t is not None else None), "mg_eval")
+        return v, (t.reshape(dp.prog.n_trace_rows, ncand) if t is not None else None)
+
+    def eval_generated(self, dp: DeviceProgram, seed: int, begin: int, count: int,
+                       trace: bool = True) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+        v = np.zeros(count, dtype=np.uint32)
+        t = np.zeros(dp.prog.n_trace_rows * count, dtype=np.uint32) if trace and dp.prog.n_trace_rows else None
+        _check(self.lib, self.lib.mg_eval_generated(self.handle, dp.handle, seed & ((1 << 64) - 1), begin, count,
+                                                    v.ctypes.data, _ptr(t) if t is not None else None),
+               "mg_eval_generated")
+        return v, (t.reshape(dp.prog.n_trace_rows, count) if t is not None else None)
+
+    def keccak256(self, msgs: Sequence[bytes]) -> Tuple[List[bytes], dict]:
+        n = len(msgs)
+        if n == 0:
+            return [], {}
+        data = np.frombuffer(b"".join(msgs) or b"\0", dtype=np.uint8)
+        lens = np.array([len(m) for m in msgs], dtype=np.uint32)
+        offs = np.zeros(n, dtype=np.uint64)
+        if n > 1:
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        out = np.zeros(32 * n, dtype=np.uint8)
+        st = MgStats()
+        _check(self.lib, self.lib.mg_keccak256(self.handle, data.ctypes.data, sum(len(m) for m in msgs),
+                                               offs.ctypes.data, lens.ctypes.data, n, out.ctypes.data,
+                                               ctypes.byref(st)), "mg_keccak256")
+        return [out[32 * i:32 * i + 32].tobytes() for i in range(n)], st.as_dict()
+
+
+def validate(p: Program) -> None:
+    lib = load_library()
+    d, keep = make_desc(p)
+    _check(lib, lib.mg_validate_desc(ctypes.byref(d)), "mg_validate_desc")
+
+
+def pack_inputs(p: Program, assignments: Sequence[dict]) -> np.ndarray:
+    """SoA leaf rows for mg_eval from per-candidate {name: int} dicts."""
+    n = len(assignments)
+    rows = np.zeros((max(p.n_input_rows, 1), n), dtype=np.uint32)
+    for li, node in enumerate(p.leaf_nodes):
+        r0, nl = p.input_rows_for(li)
+        w = p.leaf_specs[li].width
+        for j, a in enumerate(assignments):
+            v = int(a.get(node.name, 0)) & ((1 << w) - 1)
+            for k in range(nl):
+                rows[r0 + k, j] = (v >> (32 * k)) & 0xFFFFFFFF
+    return rows
+
+
+def unpack_trace(p: Program, trace: np.ndarray, node) -> List[int]:
+    row, cls = p.trace_map[node.id]
+    n = trace.shape[1]
+    nl = 8 if cls == "W" else 1
+    out = []
+    for j in range(n):
+        v = 0
+        for k in range(nl):
+            v |= int(trace[row + k, j]) << (32 * k)
+        out.append(v)
+    return out

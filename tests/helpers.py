@@ -1,0 +1,164 @@
+"""Test helpers: host-emulator binding, oracle candidate models, random DAGs."""
+from __future__ import annotations
+
+import ctypes
+import os
+import random
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from mythril_amd.compiler import Program
+from mythril_amd.ir import BOOL, Ctx, Node
+from mythril_amd.runtime import MgProgDesc, make_desc
+from oracle.philox import leaf_value
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HOST_EMU = os.path.join(ROOT, "build", "host", "libmw_host_emu.so")
+_emu = None
+
+
+def host_emu():
+    global _emu
+    if _emu is None:
+        if not os.path.exists(HOST_EMU):
+            from mythril_amd.build import build_host_emu
+            build_host_emu()
+        lib = ctypes.CDLL(HOST_EMU)
+        lib.mwh_eval.restype = ctypes.c_int
+        lib.mwh_eval.argtypes = [ctypes.POINTER(MgProgDesc), ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                 ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        lib.mwh_keccak256.restype = ctypes.c_int
+        lib.mwh_keccak256.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                      ctypes.c_void_p]
+        lib.mg_validate_desc.restype = ctypes.c_int
+        lib.mg_validate_desc.argtypes = [ctypes.POINTER(MgProgDesc)]
+        lib.mg_last_error.restype = ctypes.c_char_p
+        _emu = lib
+    return _emu
+
+
+def emu_eval(p: Program, inputs: Optional[np.ndarray], n: int, seed: int = 0, begin: int = 0, flags: int = 0):
+    lib = host_emu()
+    d, keep = make_desc(p)
+    v = np.zeros(n, dtype=np.uint32)
+    t = np.zeros(max(p.n_trace_rows, 1) * n, dtype=np.uint32)
+    inp = np.ascontiguousarray(inputs, dtype=np.uint32) if inputs is not None else None
+    rc = lib.mwh_eval(ctypes.byref(d), inp.ctypes.data if inp is not None else None, seed, begin, n, flags,
+                      v.ctypes.data, t.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(lib.mg_last_error().decode())
+    return v, t.reshape(max(p.n_trace_rows, 1), n)
+
+
+def oracle_models(p: Program, seed: int, begin: int, n: int) -> List[Dict[str, int]]:
+    """Leaf assignments of generated candidates, restated by the oracle (oracle/philox.py)."""
+    out = []
+    for j in range(n):
+        m = {}
+        for li, (node, spec) in enumerate(zip(p.leaf_nodes, p.leaf_specs)):
+            sd = {"id": li, "width": spec.width, "shift": spec.shift, "bits": spec.bits, "pool": spec.pool}
+            m[node.name] = leaf_value(sd, seed, begin + j)
+        out.append(m)
+    return out
+
+
+WIDTHS = [1, 5, 8, 31, 32, 33, 64, 100, 160, 255, 256]
+
+
+class RandDag:
+    """Random well-typed terms over every op the compiler lowers."""
+
+    def __init__(self, seed: int, widths: Sequence[int] = WIDTHS, nvars: int = 6):
+        self.r = random.Random(seed)
+        self.ctx = Ctx()
+        self.widths = list(widths)
+        self.vars = [self.ctx.var(f"v{i}_{w}", w) for i, w in enumerate(self.r.choice(self.widths) for _ in range(nvars))]
+        self.bvars = [self.ctx.var(f"b{i}", BOOL) for i in range(2)]
+
+    def special(self, w):
+        r = self.r.random()
+        m = (1 << w) - 1
+        if r < 0.15:
+            return 0
+        if r < 0.3:
+            return m
+        if r < 0.4:
+            return 1 << (w - 1)
+        if r < 0.5:
+            return self.r.randrange(0, min(w + 3, m + 1))
+        return self.r.getrandbits(w)
+
+    def const(self, w):
+        return self.ctx.const(self.special(w), w)
+
+    def leaf(self, w):
+        cands = [v for v in self.vars if v.width == w]
+        if cands and self.r.random() < 0.7:
+            return self.r.choice(cands)
+        return self.const(w)
+
+    def bv(self, w: int, depth: int) -> Node:
+        c, r = self.ctx, self.r
+        if depth <= 0 or r.random() < 0.15:
+            return self.leaf(w)
+        k = r.random()
+        d = depth - 1
+        if k < 0.40:
+            op = r.choice(["bvadd", "bvsub", "bvmul", "bvand", "bvor", "bvxor", "bvudiv", "bvurem",
+                           "bvsdiv", "bvsrem", "bvsmod", "bvshl", "bvlshr", "bvashr", "bvnand", "bvnor",
+                           "bvxnor"])
+            a = self.bv(w, d)
+            b = self.bv(w, d) if op not in ("bvshl", "bvlshr", "bvashr") or r.random() < 0.5 else \
+                c.const(r.choice([0, 1, w - 1, w, w + 1, r.randrange(0, w)]) & ((1 << w) - 1), w)
+            if op in ("bvadd", "bvmul", "bvand", "bvor", "bvxor") and r.random() < 0.3:
+                return c.app(op, a, b, self.bv(w, d))
+            return c.app(op, a, b)
+        if k < 0.48:
+            return c.app(r.choice(["bvneg", "bvnot"]), self.bv(w, d))
+        if k < 0.58:
+            return c.app("ite", self.boolean(d), self.bv(w, d), self.bv(w, d))
+        if k < 0.68 and w > 1:  # concat
+            cut = r.randrange(1, w)
+            return c.app("concat", self.bv(w - cut, d), self.bv(cut, d))
+        if k < 0.78:  # extract from something wider
+            big = r.choice([x for x in self.widths if x >= w])
+            lo = r.randrange(0, big - w + 1)
+            return c.app("extract", self.bv(big, d), params=(lo + w - 1, lo))
+        if k < 0.86 and w > 1:
+            small = r.choice([x for x in self.widths if x < w] or [1])
+            return c.app(r.choice(["zero_extend", "sign_extend"]), self.bv(small, d), params=(w - small,))
+        if k < 0.92:
+            return c.app(r.choice(["rotate_left", "rotate_right"]), self.bv(w, d), params=(r.randrange(0, 2 * w),))
+        if k < 0.95 and w % 2 == 0 and w >= 2:
+            return c.app("repeat", self.bv(w // 2, d), params=(2,))
+        return c.app("bvcomp", self.bv(w, d), self.bv(w, d)) if w == 1 else self.leaf(w)
+
+    def boolean(self, depth: int) -> Node:
+        c, r = self.ctx, self.r
+        if depth <= 0 or r.random() < 0.1:
+            return r.choice(self.bvars + [c.true(), c.false()])
+        k = r.random()
+        d = depth - 1
+        if k < 0.5:
+            w = r.choice(self.widths)
+            op = r.choice(["bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge", "=",
+                           "distinct", "bvumul_noovfl"])
+            return c.app(op, self.bv(w, d), self.bv(w, d))
+        if k < 0.8:
+            op = r.choice(["and", "or", "xor", "=>", "=", "distinct"])
+            return c.app(op, self.boolean(d), self.boolean(d))
+        if k < 0.9:
+            return c.app("not", self.boolean(d))
+        return c.app("ite", self.boolean(d), self.boolean(d), self.boolean(d))
+
+
+def random_assignments(vars_: Sequence[Node], n: int, rng: random.Random, dag: RandDag) -> List[Dict[str, int]]:
+    out = []
+    for _ in range(n):
+        m = {}
+        for v in vars_:
+            w = 1 if v.width == BOOL else v.width
+            m[v.name] = dag.special(w)
+        out.append(m)
+    return out
