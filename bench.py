@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Benchmark: candidate-assignment evals/sec of the witness search (BASELINE.json).
+
+Workload (BASELINE.json config C5, the metric's multi-GPU config): a synthetic
+10k-node 256-bit bitvector DAG over 16 free 256-bit variables whose root is
+the AND of 32 comparisons with a planted witness (mythril_amd/synth.py).  A
+step is one exhaustive search launch over a batch of candidate indices per GPU
+(early exit off, so every verdict is fully determined — SURVEY.md §8(d)).
+Candidates are generated on the device from the index (Philox4x32-10); the
+program is uploaded once before timing.
+
+Multi-GPU: one process per GPU (torchrun); rank r searches its own contiguous
+slice of the index space each step (weak scaling, no data-path collective);
+the per-step witness minimum is combined with one RCCL all-reduce(MIN) of a
+single int64, as the engine's multi-GPU search does (mythril_amd/distributed.py).
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+NOMINAL_PEAK = 256 * 64 * 2.4e9  # SURVEY.md §8(d) derived INT32 VALU peak (u32 ops/s)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch-log2", type=int, default=22, help="candidates per GPU per step = 2**k")
+    ap.add_argument("--nodes", type=int, default=10000)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    from mythril_amd.compiler import compile_program
+    from mythril_amd.runtime import Device, unpack_trace
+    from mythril_amd.synth import build_c5
+
+    dev = Device(local)
+
+    def gpu_eval(terms, index, seed):
+        p = compile_program([], trace=list(terms))
+        dp = dev.load(p)
+        _, tr = dev.eval_generated(dp, seed, index, 1)
+        dp.free()
+        return [unpack_trace(p, tr, t)[0] for t in terms]
+
+    syn = build_c5(gpu_eval, n_nodes=args.nodes)
+    prog = compile_program(syn.conjuncts)
+    dp = dev.load(prog)
+    batch = 1 << args.batch_log2
+
+    def step(k):
+        begin = ((k * world + rank) * batch) % (1 << 62)
+        (found,), st = dev.search([dp], syn.seed, begin, batch, 0)
+        return found, st
+
+    for k in range(args.warmup):
+        step(k)
+
+    def barrier():
+        if dist is not None:
+            import torch
+            t = torch.zeros(1, device=f"cuda:{local}")
+            dist.all_reduce(t)
+            torch.cuda.synchronize()
+
+    barrier()
+    kms = []
+    found_any = None
+    t0 = time.perf_counter()
+    for k in range(args.warmup, args.warmup + args.steps):
+        found, st = step(k)
+        kms.append(st["kernel_ms"])
+        if found is not None:
+            found_any = found if found_any is None else min(found_any, found)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        w = torch.tensor([found_any if found_any is not None else (1 << 63) - 1], dtype=torch.int64,
+                         device=f"cuda:{local}")
+        dist.all_reduce(w, op=dist.ReduceOp.MIN)  # RCCL MIN of the witness index
+        found_any = None if int(w.item()) == (1 << 63) - 1 else int(w.item())
+
+    total_evals = world * args.steps * batch
+    value = total_evals / elapsed
+    avg_kernel_s = sum(kms) / len(kms) / 1e3
+    ops_launch = prog.ops_per_eval * batch
+    achieved = ops_launch / avg_kernel_s
+    peak_info = load_peak()
+    peak = peak_info["peak"]
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline(syn, prog, args.cpu_seconds)
+
+    out = {
+        "metric": "candidate-assignment evals/sec",
+        "value": value,
+        "unit": "evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u256 (u32 limbs)",
+        "data": "synthetic (Philox-generated candidates, planted witness)",
+        "config": {
+            "workload": "C5: synthetic 256-bit bitvector DAG, 16 free 256-bit vars, AND of 32 comparisons, "
+                        "exhaustive search (BASELINE.json configs[4], per-GPU shard)",
+            "dag_nodes": len(__import__("mythril_amd.ir", fromlist=["topo"]).topo(syn.conjuncts)),
+            "candidates_per_gpu_step": batch,
+            "ops_per_eval": prog.ops_per_eval,
+            "program_insns": prog.n_insn,
+            "spill_slots": prog.n_spill,
+            "parallelism": f"candidate-shard x{world}",
+            "witness_found_in_timed_range": found_any,
+        },
+        "roofline": {
+            "bound": "valu-int32",
+            "achieved": achieved / 1e12,
+            "peak": peak / 1e12,
+            "unit": "Tops/s (u32)",
+            "frac": achieved / peak,
+            "traffic": load_traffic(prog, batch),
+            "kernel_ms_avg": avg_kernel_s * 1e3,
+            "peak_source": peak_info["source"],
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def load_peak():
+    """INT32 VALU peak: the measured v_add_u32 microbenchmark (profiles/valu_peak.json) when
+    present and above the derived figure, else SURVEY.md §8(d)'s derived 39.3 T u32-ops/s."""
+    path = os.path.join(ROOT, "profiles", "valu_peak.json")
+    if os.path.exists(path):
+        try:
+            d = json.load(open(path))
+            m = float(d["measured_ops_per_s"])
+            if m > NOMINAL_PEAK:
+                return {"peak": m, "source": "measured v_add_u32 microbenchmark (profiles/valu_peak.json)"}
+        except Exception:
+            pass
+    return {"peak": NOMINAL_PEAK, "source": "derived 256 CU x 64 lanes x 2.4 GHz (SURVEY.md 8d)"}
+
+
+def load_traffic(prog, batch):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass for this workload, else None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        if d.get("ops_per_eval") == prog.ops_per_eval and d.get("batch") == batch:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        pass
+    return None
+
+
+def cpu_baseline(syn, prog, budget_s):
+    """Oracle on the host cores over a bounded sample of the same candidate indices."""
+    from oracle import cbaseline
+    return cbaseline.run(syn, prog, budget_s)
+
+
+if __name__ == "__main__":
+    main()

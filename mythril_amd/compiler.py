@@ -22,6 +22,7 @@ the drop-in ``get_model`` turns into "fall back to z3" (fail closed).
 from __future__ import annotations
 
 import math
+import zlib
 from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -85,6 +86,11 @@ class LeafSpec:
     pool: Optional[List[Optional[int]]] = None   # None entry = RANDOM; len must be 2**k
     shift: int = 0
     bits: int = 0
+    salt: Optional[int] = None   # Philox key salt; default crc32(name) so a variable
+                                 # draws the same value in every program for an index
+
+    def key_salt(self) -> int:
+        return self.salt if self.salt is not None else zlib.crc32(self.name.encode()) & 0xFFFFFFFF
 
 
 @dataclass
@@ -629,7 +635,7 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
                     pool_words.extend([1] + [0] * 8)
                 else:
                     pool_words.extend([0] + _limbs(e & ((1 << w) - 1)))
-        leaf_words.extend([w, kind, li, pshift, pbits, poff, in_row, 0])
+        leaf_words.extend([w, kind, spec.key_salt(), pshift, pbits, poff, in_row, 0])
         in_row += (w + 31) // 32
         specs.append(spec)
     if bit > 63:

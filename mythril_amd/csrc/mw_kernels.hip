@@ -40,6 +40,11 @@ struct ProgDev {
 };
 
 constexpr int kBlock = 256;
+// LDS spill area: up to kLdsSpillSlots W-sized slots per lane, [slot][limb][lane]
+// (consecutive lanes -> consecutive banks).  10 slots = 80 KiB per 256-lane
+// block, so two blocks (8 waves) still fit a CU's 160 KiB.
+constexpr u32 kLdsSpillSlots = 10;
+extern __shared__ u32 lds_spill[];
 
 struct SearchEnv {
   const u32* __restrict__ leaves;
@@ -53,11 +58,20 @@ struct SearchEnv {
     leaf_value(leaves + (u64)idx * MW_LEAF_WORDS, pool, seed, cand, out);
   }
   __device__ void store(u32, const u32*, int) {}
+  u32 nlds;  // spill slots [0, nlds) live in LDS, the rest in the global spill buffer
   __device__ void spill(u32 slot, const u32* v, int n) {
-    for (int k = 0; k < n; ++k) spillbuf[((u64)slot * 8 + k) * nthreads + gtid] = v[k];
+    if (slot < nlds) {
+      for (int k = 0; k < n; ++k) lds_spill[(slot * 8 + k) * kBlock + threadIdx.x] = v[k];
+    } else {
+      for (int k = 0; k < n; ++k) spillbuf[((u64)(slot - nlds) * 8 + k) * nthreads + gtid] = v[k];
+    }
   }
   __device__ void fill(u32 slot, u32* v, int n) {
-    for (int k = 0; k < 8; ++k) v[k] = k < n ? spillbuf[((u64)slot * 8 + k) * nthreads + gtid] : 0u;
+    if (slot < nlds) {
+      for (int k = 0; k < 8; ++k) v[k] = k < n ? lds_spill[(slot * 8 + k) * kBlock + threadIdx.x] : 0u;
+    } else {
+      for (int k = 0; k < 8; ++k) v[k] = k < n ? spillbuf[((u64)(slot - nlds) * 8 + k) * nthreads + gtid] : 0u;
+    }
   }
   __device__ bool none(bool alive) { return __ballot(alive) == 0ull; }
 };
@@ -90,11 +104,20 @@ struct EvalEnv {
     if (trace)
       for (int k = 0; k < n; ++k) trace[((u64)row + k) * ncand + idx] = v[k];
   }
+  u32 nlds;  // spill slots [0, nlds) live in LDS, the rest in the global spill buffer
   __device__ void spill(u32 slot, const u32* v, int n) {
-    for (int k = 0; k < n; ++k) spillbuf[((u64)slot * 8 + k) * nthreads + gtid] = v[k];
+    if (slot < nlds) {
+      for (int k = 0; k < n; ++k) lds_spill[(slot * 8 + k) * kBlock + threadIdx.x] = v[k];
+    } else {
+      for (int k = 0; k < n; ++k) spillbuf[((u64)(slot - nlds) * 8 + k) * nthreads + gtid] = v[k];
+    }
   }
   __device__ void fill(u32 slot, u32* v, int n) {
-    for (int k = 0; k < 8; ++k) v[k] = k < n ? spillbuf[((u64)slot * 8 + k) * nthreads + gtid] : 0u;
+    if (slot < nlds) {
+      for (int k = 0; k < 8; ++k) v[k] = k < n ? lds_spill[(slot * 8 + k) * kBlock + threadIdx.x] : 0u;
+    } else {
+      for (int k = 0; k < 8; ++k) v[k] = k < n ? spillbuf[((u64)(slot - nlds) * 8 + k) * nthreads + gtid] : 0u;
+    }
   }
   __device__ bool none(bool) { return false; }  // eval: never exit early
 };
@@ -105,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void mw_search_kernel(const ProgDev* __rest
                                                            u64 begin, u64 count, u32 flags,
                                                            u64* __restrict__ out_min,
                                                            u64* __restrict__ counter,
-                                                           u32* __restrict__ spillbuf) {
+                                                           u32* __restrict__ spillbuf, u32 nlds) {
   const ProgDev P = progs[blockIdx.y];
   const u64 nchunks = (count + kBlock - 1) / kBlock;
   const u64 end = begin + count;
@@ -121,7 +144,7 @@ __global__ __launch_bounds__(kBlock) void mw_search_kernel(const ProgDev* __rest
     }
     const u64 cand = base + threadIdx.x;
     const bool valid = cand < end;
-    SearchEnv env{P.leaves, P.pool, seed, cand, spillbuf, nthreads, gtid};
+    SearchEnv env{P.leaves, P.pool, seed, cand, spillbuf, nthreads, gtid, nlds};
     const bool ok = mw_run(P.code, P.consts, env, valid, flags);
     const u64 hit = __ballot(ok);
     if (hit) {
@@ -137,7 +160,7 @@ __global__ __launch_bounds__(kBlock) void mw_eval_kernel(ProgDev P, const u32* _
                                                          u64 ncand, u64 seed, u64 begin,
                                                          u32* __restrict__ verdict,
                                                          u32* __restrict__ trace,
-                                                         u32* __restrict__ spillbuf) {
+                                                         u32* __restrict__ spillbuf, u32 nlds) {
   const u64 nthreads = (u64)gridDim.x * kBlock;
   const u64 gtid = (u64)blockIdx.x * kBlock + threadIdx.x;
   const u64 nchunks = (ncand + kBlock - 1) / kBlock;
@@ -145,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void mw_eval_kernel(ProgDev P, const u32* _
     const u64 idx = ch * kBlock + threadIdx.x;
     const bool valid = idx < ncand;
     EvalEnv env{P.leaves, P.pool, in, valid ? trace : nullptr, ncand, valid ? idx : 0,
-                seed, begin + idx, spillbuf, nthreads, gtid};
+                seed, begin + idx, spillbuf, nthreads, gtid, nlds};
     const bool ok = mw_run(P.code, P.consts, env, valid, 0u);
     if (valid) verdict[idx] = ok ? 1u : 0u;
   }
@@ -354,15 +377,17 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   u64 gx = std::max<u64>(1, (u64)c->ncu * 8 / nprog);
   gx = std::min<u64>(gx, nchunks);
   const u64 nthreads = gx * nprog * kBlock;
-  rc = ensure_spill(c, std::max<size_t>(4, (size_t)max_spill * 8 * nthreads * sizeof(u32)));
+  const u32 nlds = std::min(max_spill, kLdsSpillSlots);
+  const u32 nglob = max_spill - nlds;
+  rc = ensure_spill(c, std::max<size_t>(4, (size_t)nglob * 8 * nthreads * sizeof(u32)));
   if (rc) return rc;
   std::vector<u64> init(nprog, MG_NONE);
   HIPCHK(hipMemcpyAsync(c->d_progs, hp.data(), nprog * sizeof(ProgDev), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_min, init.data(), nprog * sizeof(u64), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemsetAsync(c->d_counter, 0, sizeof(u64), c->stream));
   HIPCHK(hipEventRecord(c->e0, c->stream));
-  hipLaunchKernelGGL(mw_search_kernel, dim3((u32)gx, (u32)nprog), dim3(kBlock), 0, c->stream, c->d_progs,
-                     seed, begin, count, flags, c->d_min, c->d_counter, c->d_spill);
+  hipLaunchKernelGGL(mw_search_kernel, dim3((u32)gx, (u32)nprog), dim3(kBlock), (size_t)nlds * 8 * kBlock * 4,
+                     c->stream, c->d_progs, seed, begin, count, flags, c->d_min, c->d_counter, c->d_spill, nlds);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->e1, c->stream));
   u64 evals = 0;
@@ -389,7 +414,8 @@ static int eval_common(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, 
   const u64 nchunks = (ncand + kBlock - 1) / kBlock;
   const u64 gx = std::min<u64>(nchunks, (u64)c->ncu * 8);
   const u64 nthreads = gx * kBlock;
-  int rc = ensure_spill(c, std::max<size_t>(4, (size_t)p->dev.n_spill * 8 * nthreads * sizeof(u32)));
+  const u32 nlds = std::min(p->dev.n_spill, kLdsSpillSlots);
+  int rc = ensure_spill(c, std::max<size_t>(4, (size_t)(p->dev.n_spill - nlds) * 8 * nthreads * sizeof(u32)));
   if (rc) return rc;
   u32 *d_in = nullptr, *d_v = nullptr, *d_t = nullptr;
   const size_t nin = leaves_soa ? (size_t)p->desc.n_input_rows * ncand : 0;
@@ -406,8 +432,8 @@ static int eval_common(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, 
     cleanup(); return fail(MG_E_HIP, "eval input copy");
   }
   if (ntr) hipMemsetAsync(d_t, 0, ntr * 4, c->stream);
-  hipLaunchKernelGGL(mw_eval_kernel, dim3((u32)gx), dim3(kBlock), 0, c->stream, p->dev, (const u32*)d_in,
-                     (u64)ncand, seed, begin, d_v, d_t, c->d_spill);
+  hipLaunchKernelGGL(mw_eval_kernel, dim3((u32)gx), dim3(kBlock), (size_t)nlds * 8 * kBlock * 4, c->stream,
+                     p->dev, (const u32*)d_in, (u64)ncand, seed, begin, d_v, d_t, c->d_spill, nlds);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, ncand * 4, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess && ntr) e = hipMemcpyAsync(trace, d_t, ntr * 4, hipMemcpyDeviceToHost, c->stream);
