@@ -284,6 +284,14 @@ int mg_init(int device, mg_ctx** out) {
     delete c;
     return fail(MG_E_HIP, "context setup failed");
   }
+  // allow the LDS spill area (up to kLdsSpillSlots x 8 KiB) beyond the 64 KiB default
+  const int lds_max = (int)(kLdsSpillSlots * 8 * kBlock * sizeof(u32));
+  if (hipFuncSetAttribute((const void*)mw_search_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
+          hipSuccess ||
+      hipFuncSetAttribute((const void*)mw_eval_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
+          hipSuccess) {
+    (void)hipGetLastError();  // older runtimes: the default limit already covers it
+  }
   *out = c;
   return 0;
 }
