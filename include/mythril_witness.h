@@ -102,6 +102,10 @@ int mg_keccak256(mg_ctx* ctx, const uint8_t* data, size_t ndata, const uint64_t*
 int mg_keccak256_device(mg_ctx* ctx, const uint8_t* d_data, const uint64_t* d_off,
                         const uint32_t* d_len, size_t n, uint8_t* d_out32, mg_stats* stats);
 
+/* Diagnostic: measured INT32 VALU issue rate of the device (v_add_u32, or
+ * v_mul_lo_u32 when mul != 0), u32 ops/s — the roofline peak bench.py reports. */
+int mg_valu_peak(mg_ctx* ctx, uint32_t mul, double* ops_per_s, double* kernel_ms);
+
 /* Validate a program without a device (the same check mg_prog_load runs). */
 int mg_validate_desc(const mg_prog_desc* desc);
 

@@ -189,6 +189,44 @@ __global__ __launch_bounds__(kBlock) void mw_keccak_kernel(const uint8_t* __rest
   }
 }
 
+// INT32 VALU peak microbenchmark: 8 independent v_add_u32 chains per lane
+// (or v_mul_lo_u32 when mul != 0), all CUs, 8 waves per SIMD.
+__global__ __launch_bounds__(kBlock) void mw_valu_peak_kernel(u32* __restrict__ out, u32 iters, u32 mul) {
+  u32 a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
+      a7 = a0 + 7;
+  const u32 b = blockIdx.x | 1u;
+  if (mul) {
+    for (u32 i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a0) : "v"(b));
+        asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a1) : "v"(b));
+        asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a2) : "v"(b));
+        asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a3) : "v"(b));
+        asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a4) : "v"(b));
+        asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a5) : "v"(b));
+        asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a6) : "v"(b));
+        asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a7) : "v"(b));
+      }
+    }
+  } else {
+    for (u32 i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(a0) : "v"(b));
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(a1) : "v"(b));
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(a2) : "v"(b));
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(a3) : "v"(b));
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(a4) : "v"(b));
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(a5) : "v"(b));
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(a6) : "v"(b));
+        asm volatile("v_add_u32 %0, %0, %1" : "+v"(a7) : "v"(b));
+      }
+    }
+  }
+  out[(u64)blockIdx.x * kBlock + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+}
+
 // =============================================================== host side
 namespace {
 
@@ -463,6 +501,26 @@ int mg_eval(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncan
 int mg_eval_generated(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, size_t count,
                       uint32_t* verdict, uint32_t* trace) {
   return eval_common(c, p, nullptr, count, seed, begin, verdict, trace);
+}
+
+int mg_valu_peak(mg_ctx* c, uint32_t mul, double* ops_per_s, double* kernel_ms) {
+  if (!c || !ops_per_s) return fail(MG_E_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  const u32 blocks = (u32)c->ncu * 8, iters = 4096;
+  u32* d = nullptr;
+  HIPCHK(hipMalloc(&d, (size_t)blocks * kBlock * 4));
+  hipLaunchKernelGGL(mw_valu_peak_kernel, dim3(blocks), dim3(kBlock), 0, c->stream, d, 16u, mul);  // warm
+  HIPCHK(hipEventRecord(c->e0, c->stream));
+  hipLaunchKernelGGL(mw_valu_peak_kernel, dim3(blocks), dim3(kBlock), 0, c->stream, d, iters, mul);
+  HIPCHK(hipEventRecord(c->e1, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
+  hipFree(d);
+  *ops_per_s = (double)blocks * kBlock * iters * 32.0 / (ms * 1e-3);
+  if (kernel_ms) *kernel_ms = ms;
+  return 0;
 }
 
 int mg_keccak256_device(mg_ctx* c, const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len, size_t n,

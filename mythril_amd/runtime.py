@@ -67,6 +67,8 @@ SIGNATURES = {
     "mg_keccak256": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _P, _P, ctypes.c_size_t, _P, ctypes.POINTER(MgStats)]),
     "mg_keccak256_device": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_size_t, _P, ctypes.POINTER(MgStats)]),
     "mg_validate_desc": (ctypes.c_int, [ctypes.POINTER(MgProgDesc)]),
+    "mg_valu_peak": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
+                                    ctypes.POINTER(ctypes.c_double)]),
     "mg_last_error": (ctypes.c_char_p, []),
 }
 
@@ -202,6 +204,13 @@ class Device:
                                                offs.ctypes.data, lens.ctypes.data, n, out.ctypes.data,
                                                ctypes.byref(st)), "mg_keccak256")
         return [out[32 * i:32 * i + 32].tobytes() for i in range(n)], st.as_dict()
+
+
+    def valu_peak(self, mul: bool = False) -> Tuple[float, float]:
+        ops, ms = ctypes.c_double(0), ctypes.c_double(0)
+        _check(self.lib, self.lib.mg_valu_peak(self.handle, 1 if mul else 0, ctypes.byref(ops), ctypes.byref(ms)),
+               "mg_valu_peak")
+        return ops.value, ms.value
 
 
 def validate(p: Program) -> None:

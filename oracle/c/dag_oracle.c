@@ -1,0 +1,256 @@
+/* ORACLE (test infrastructure only) — C restatement of the DAG semantics.
+ *
+ * Plain C99 + OpenMP.  Evaluates a constraint DAG (serialised by oracle/cdag.py
+ * from the IR) for candidate indices [begin, begin+n): leaves drawn with
+ * Philox4x32-10 exactly as oracle/philox.py specifies, every op with SMT-LIB
+ * 2.6 semantics (oracle/bvsem.py is the reference for this file; both restate
+ * z3's bitvector theory as Mythril uses it, mythril/laser/smt/bitvec.py,
+ * bitvec_helper.py, bool.py).  Widths 1..256; values are 8 x u32 limbs,
+ * canonical (bits >= width are zero).  Written independently of the product
+ * ALU (mythril_amd/csrc): simple schoolbook arithmetic, bit-serial division.
+ *
+ * Used by bench.py's cpu_baseline leg and by tests for large parity sweeps.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+enum {
+  O_CONST = 0, O_VAR, O_ADD, O_SUB, O_MUL, O_UDIV, O_UREM, O_SDIV, O_SREM, O_SMOD,
+  O_AND, O_OR, O_XOR, O_NOT, O_NEG, O_SHL, O_LSHR, O_ASHR, O_CONCAT, O_EXTRACT,
+  O_ZEXT, O_SEXT, O_ITE, O_EQ, O_ULT, O_ULE, O_SLT, O_SLE, O_UMULNO, O_ROTL, O_ROTR
+};
+
+/* node record: op, width, a, b, c, p0, p1, salt (8 x i32) */
+typedef struct { int32_t op, w, a, b, c, p0, p1, salt; } onode;
+
+static void mask(u32* v, int w) {
+  for (int k = 0; k < 8; ++k) {
+    int lo = 32 * k;
+    if (w >= lo + 32) continue;
+    if (w <= lo) v[k] = 0;
+    else v[k] &= (1u << (w - lo)) - 1u;
+  }
+}
+static int bit(const u32* v, int i) { return (v[i >> 5] >> (i & 31)) & 1; }
+static int iszero(const u32* v) { for (int k = 0; k < 8; ++k) if (v[k]) return 0; return 1; }
+static int cmpu(const u32* a, const u32* b) {
+  for (int k = 7; k >= 0; --k) { if (a[k] != b[k]) return a[k] < b[k] ? -1 : 1; }
+  return 0;
+}
+static void add(const u32* a, const u32* b, u32* r) {
+  u64 c = 0;
+  for (int k = 0; k < 8; ++k) { c += (u64)a[k] + b[k]; r[k] = (u32)c; c >>= 32; }
+}
+static void sub(const u32* a, const u32* b, u32* r) {
+  u64 br = 0;
+  for (int k = 0; k < 8; ++k) { u64 t = (u64)a[k] - b[k] - br; r[k] = (u32)t; br = (t >> 63) & 1; }
+}
+static void neg(const u32* a, u32* r, int w) { u32 z[8] = {0}; sub(z, a, r); mask(r, w); }
+static void mul(const u32* a, const u32* b, u32* r) {
+  u32 t[16]; memset(t, 0, sizeof t);
+  for (int i = 0; i < 8; ++i) {
+    u64 c = 0;
+    for (int j = 0; j < 8; ++j) { c += (u64)a[i] * b[j] + t[i + j]; t[i + j] = (u32)c; c >>= 32; }
+    t[i + 8] = (u32)c;
+  }
+  memcpy(r, t, 32);
+}
+static void shl1(u32* v) { for (int k = 7; k > 0; --k) v[k] = (v[k] << 1) | (v[k - 1] >> 31); v[0] <<= 1; }
+static void shl(const u32* a, int s, u32* r) {  /* 0 <= s < 256 */
+  u32 t[8] = {0}; int q = s >> 5, b = s & 31;
+  for (int k = 7; k >= 0; --k) {
+    if (k - q < 0) continue;
+    u32 v = a[k - q] << b;
+    if (b && k - q - 1 >= 0) v |= a[k - q - 1] >> (32 - b);
+    t[k] = v;
+  }
+  memcpy(r, t, 32);
+}
+static void shr(const u32* a, int s, u32 fill, u32* r) { /* 0 <= s < 256, fill = 0 or ~0 */
+  u32 t[8]; int q = s >> 5, b = s & 31;
+  for (int k = 0; k < 8; ++k) {
+    u32 lo = (k + q < 8) ? a[k + q] : fill;
+    u32 hi = (k + q + 1 < 8) ? a[k + q + 1] : fill;
+    t[k] = b ? (lo >> b) | (hi << (32 - b)) : lo;
+  }
+  memcpy(r, t, 32);
+}
+/* bit-serial restoring division, y != 0 */
+static void udivrem(const u32* x, const u32* y, u32* q, u32* r) {
+  u32 rr[8] = {0}, qq[8] = {0};
+  int top = 255;
+  while (top >= 0 && !bit(x, top)) --top;
+  for (int i = top; i >= 0; --i) {
+    shl1(rr);
+    rr[0] |= (u32)bit(x, i);
+    if (cmpu(rr, y) >= 0) { sub(rr, y, rr); qq[i >> 5] |= 1u << (i & 31); }
+  }
+  memcpy(q, qq, 32); memcpy(r, rr, 32);
+}
+static int sgnbit(const u32* a, int w) { return bit(a, w - 1); }
+static void sext_to256(u32* a, int w) {
+  if (w < 256 && sgnbit(a, w)) {
+    for (int i = w; i < 256; ++i) a[i >> 5] |= 1u << (i & 31);
+  }
+}
+static void ones(u32* r, int w) { for (int k = 0; k < 8; ++k) r[k] = 0xffffffffu; mask(r, w); }
+static int amount_ge(const u32* b, int w) {
+  for (int k = 1; k < 8; ++k) if (b[k]) return 1;
+  return b[0] >= (u32)w;
+}
+
+static void divop(int op, const u32* s, const u32* t, int w, u32* r) {
+  u32 q[8], m[8], x[8], y[8], tmp[8];
+  if (op == O_UDIV || op == O_UREM) {
+    if (iszero(t)) { if (op == O_UDIV) ones(r, w); else memcpy(r, s, 32); return; }
+    udivrem(s, t, q, m);
+    memcpy(r, op == O_UDIV ? q : m, 32);
+    return;
+  }
+  int ms = sgnbit(s, w), mt = sgnbit(t, w);
+  if (ms) neg(s, x, w); else memcpy(x, s, 32);
+  if (mt) neg(t, y, w); else memcpy(y, t, 32);
+  if (iszero(y)) { ones(q, w); memcpy(m, x, 32); } else udivrem(x, y, q, m);
+  if (op == O_SDIV) {
+    if (ms != mt) neg(q, r, w); else memcpy(r, q, 32);
+  } else if (op == O_SREM) {
+    if (ms) neg(m, r, w); else memcpy(r, m, 32);
+  } else { /* smod: sign follows the divisor */
+    if (iszero(m)) { memset(r, 0, 32); }
+    else if (!ms && !mt) memcpy(r, m, 32);
+    else if (ms && !mt) { neg(m, tmp, w); add(tmp, t, r); }
+    else if (!ms && mt) add(m, t, r);
+    else neg(m, r, w);
+  }
+  mask(r, w);
+}
+
+static void philox(u32 c[4], u32 k0, u32 k1) {
+  for (int i = 0; i < 10; ++i) {
+    u64 p0 = (u64)0xD2511F53u * c[0], p1 = (u64)0xCD9E8D57u * c[2];
+    u32 n0 = (u32)(p1 >> 32) ^ c[1] ^ k0, n2 = (u32)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (u32)p1; c[3] = (u32)p0; c[0] = n0; c[2] = n2;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+static void leaf(u64 seed, u32 salt, u64 cand, int w, u32* out) {
+  u32 k0 = (u32)seed ^ salt, k1 = (u32)(seed >> 32);
+  for (u32 blk = 0; blk < 2; ++blk) {
+    u32 c[4] = {(u32)cand, (u32)(cand >> 32), blk, 0};
+    philox(c, k0, k1);
+    for (int i = 0; i < 4; ++i) out[4 * blk + i] = c[i];
+  }
+  mask(out, w);
+}
+
+static void eval1(const onode* g, const u32* consts, int i, u32* V, u64 seed, u64 cand) {
+  const onode* n = &g[i];
+  u32* r = V + 8 * (size_t)i;
+  const u32* a = n->a >= 0 ? V + 8 * (size_t)n->a : 0;
+  const u32* b = n->b >= 0 ? V + 8 * (size_t)n->b : 0;
+  const u32* c = n->c >= 0 ? V + 8 * (size_t)n->c : 0;
+  int w = n->w;
+  int aw = n->a >= 0 ? g[n->a].w : w;
+  u32 t[8], u[8];
+  switch (n->op) {
+    case O_CONST: memcpy(r, consts + 8 * (size_t)n->p0, 32); break;
+    case O_VAR: leaf(seed, (u32)n->salt, cand, w, r); break;
+    case O_ADD: add(a, b, r); mask(r, w); break;
+    case O_SUB: sub(a, b, r); mask(r, w); break;
+    case O_MUL: mul(a, b, r); mask(r, w); break;
+    case O_UDIV: case O_UREM: case O_SDIV: case O_SREM: case O_SMOD: divop(n->op, a, b, w, r); break;
+    case O_AND: for (int k = 0; k < 8; ++k) r[k] = a[k] & b[k]; break;
+    case O_OR: for (int k = 0; k < 8; ++k) r[k] = a[k] | b[k]; break;
+    case O_XOR: for (int k = 0; k < 8; ++k) r[k] = a[k] ^ b[k]; break;
+    case O_NOT: for (int k = 0; k < 8; ++k) r[k] = ~a[k]; mask(r, w); break;
+    case O_NEG: neg(a, r, w); break;
+    case O_SHL: if (amount_ge(b, w)) memset(r, 0, 32); else { shl(a, (int)b[0], r); mask(r, w); } break;
+    case O_LSHR: if (amount_ge(b, w)) memset(r, 0, 32); else shr(a, (int)b[0], 0, r); break;
+    case O_ASHR: {
+      memcpy(t, a, 32); sext_to256(t, w);
+      u32 fill = sgnbit(a, w) ? 0xffffffffu : 0u;
+      shr(t, amount_ge(b, w) ? 255 : (int)b[0], fill, r); mask(r, w); break;
+    }
+    case O_CONCAT: /* a = high part, b = low part of width g[b].w */
+      shl(a, g[n->b].w, t); for (int k = 0; k < 8; ++k) r[k] = t[k] | b[k]; mask(r, w); break;
+    case O_EXTRACT: shr(a, n->p1, 0, r); mask(r, w); break;
+    case O_ZEXT: memcpy(r, a, 32); break;
+    case O_SEXT: memcpy(r, a, 32); sext_to256(r, aw); mask(r, w); break;
+    case O_ITE: memcpy(r, a[0] ? b : c, 32); break;
+    case O_EQ: memset(r, 0, 32); r[0] = cmpu(a, b) == 0; break;
+    case O_ULT: memset(r, 0, 32); r[0] = cmpu(a, b) < 0; break;
+    case O_ULE: memset(r, 0, 32); r[0] = cmpu(a, b) <= 0; break;
+    case O_SLT: case O_SLE: {
+      memcpy(t, a, 32); memcpy(u, b, 32);
+      t[(aw - 1) >> 5] ^= 1u << ((aw - 1) & 31); u[(aw - 1) >> 5] ^= 1u << ((aw - 1) & 31);
+      int cmp = cmpu(t, u);
+      memset(r, 0, 32); r[0] = n->op == O_SLT ? cmp < 0 : cmp <= 0; break;
+    }
+    case O_UMULNO: { /* full product < 2^aw */
+      u32 full[16]; memset(full, 0, sizeof full);
+      for (int i2 = 0; i2 < 8; ++i2) {
+        u64 cc = 0;
+        for (int j = 0; j < 8; ++j) { cc += (u64)a[i2] * b[j] + full[i2 + j]; full[i2 + j] = (u32)cc; cc >>= 32; }
+        full[i2 + 8] = (u32)cc;
+      }
+      int ok = 1;
+      for (int bi = aw; bi < 512; ++bi) if ((full[bi >> 5] >> (bi & 31)) & 1) { ok = 0; break; }
+      memset(r, 0, 32); r[0] = ok; break;
+    }
+    case O_ROTL: case O_ROTR: {
+      int s = n->p0 % w; if (n->op == O_ROTR) s = (w - s) % w;
+      if (!s) { memcpy(r, a, 32); break; }
+      shl(a, s, t); mask(t, w); shr(a, w - s, 0, u);
+      for (int k = 0; k < 8; ++k) r[k] = t[k] | u[k];
+      break;
+    }
+    default: memset(r, 0, 32); break;
+  }
+}
+
+/* Evaluate candidates [begin, begin+n); roots are Bool nodes (conjuncts).
+ * verdict (may be NULL) receives 0/1; returns the number satisfied, or -1. */
+long long odag_eval(const int32_t* nodes, int nn, const u32* consts, const int32_t* roots, int nroots,
+                    u64 seed, u64 begin, u64 n, uint8_t* verdict, int nthreads, u64* first_sat) {
+  const onode* g = (const onode*)nodes;
+  long long total = 0;
+  u64 best = ~0ull;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel reduction(+ : total)
+  {
+    u32* V = (u32*)malloc(sizeof(u32) * 8 * (size_t)nn);
+    u64 mybest = ~0ull;
+#pragma omp for schedule(dynamic, 64)
+    for (long long j = 0; j < (long long)n; ++j) {
+      u64 cand = begin + (u64)j;
+      for (int i = 0; i < nn; ++i) eval1(g, consts, i, V, seed, cand);
+      int ok = 1;
+      for (int k = 0; k < nroots; ++k) ok &= (V[8 * (size_t)roots[k]] & 1u) != 0;
+      if (verdict) verdict[j] = (uint8_t)ok;
+      total += ok;
+      if (ok && cand < mybest) mybest = cand;
+    }
+#pragma omp critical
+    { if (mybest < best) best = mybest; }
+    free(V);
+  }
+  if (first_sat) *first_sat = best;
+  return total;
+}
+
+int odag_max_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
