@@ -205,6 +205,24 @@ class _Lowerer:
     def lower(self, n: Node):
         if n.id in self.memo:
             return self.memo[n.id]
+        # operand-first (post-order) without recursion: DAGs can be thousands deep
+        stack = [(n, False)]
+        while stack:
+            m, expanded = stack.pop()
+            if m.id in self.memo:
+                continue
+            if expanded:
+                self._lower_one(m)
+                continue
+            stack.append((m, True))
+            for a in reversed(m.args):
+                if a.id not in self.memo:
+                    stack.append((a, False))
+        return self.memo[n.id]
+
+    def _lower_one(self, n: Node):
+        if n.id in self.memo:
+            return self.memo[n.id]
         v = self._lower(n)
         self.memo[n.id] = v
         if n.id in self.trace_req and n.id not in self.trace_emitted:

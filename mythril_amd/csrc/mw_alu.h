@@ -37,12 +37,12 @@ MW_HD u32 subb(u32 a, u32 b, u32& br) {
   return r;
 }
 
-// mask of limb k of a w-bit value
+// mask of limb k of a w-bit value (branch-free, so a uniform w stays on the SALU)
 MW_HD u32 limb_mask(u32 w, int k) {
-  int lo = 32 * k;
-  if ((int)w >= lo + 32) return 0xffffffffu;
-  if ((int)w <= lo) return 0u;
-  return (1u << (w - lo)) - 1u;
+  const int lo = 32 * k;
+  const int rem = (int)w - lo;  // bits of this limb that belong to the value
+  const u32 part = 0xffffffffu >> ((32 - (rem > 0 ? (rem < 32 ? rem : 32) : 32)) & 31);
+  return rem >= 32 ? 0xffffffffu : (rem > 0 ? part : 0u);
 }
 MW_HD u32 nmask(u32 w) { return w >= 32 ? 0xffffffffu : ((1u << w) - 1u); }
 
@@ -278,19 +278,22 @@ MW_HD u32 div2by1(u32 u1, u32 u0, u32 d, u32 v) {
 }
 
 // q = x / y, r = x % y for y != 0 (Knuth Alg. D, base 2^32, fixed 8x8 shape:
-// the divisor is normalized to a full 8-limb value so every index is static)
+// the divisor is normalized to a full 8-limb value so every index is static).
+// Written to keep the live set small next to the interpreter's register file:
+// y and x are consumed by the normalising shifts, the add-backs are applied
+// limb by limb, and the remainder is de-normalised in place.
 MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
-  u32 s = clz256(y);
+  const u32 s = clz256(y);
   u32 v[8];
   shl8(y, s, v);
   u32 u[16];
   shl8to16(x, s, u);
-  u32 d = v[7];
-  u32 rec = recip32(d);
+  const u32 d = v[7];
+  const u32 rec = recip32(d);
 #pragma unroll
   for (int j = 7; j >= 0; --j) {
-    u32 u1 = u[j + 8], u0 = u[j + 7];
-    bool sat = (u1 == d);
+    const u32 u1 = u[j + 8], u0 = u[j + 7];
+    const bool sat = (u1 == d);
     u32 qh = div2by1(sat ? 0u : u1, u0, d, rec);
     qh = sat ? 0xffffffffu : qh;
     // u[j..j+8] -= qh * v
@@ -303,24 +306,23 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
     }
     u[j + 8] = subb(u[j + 8], carry, br);
     u32 neg = br;
-    // at most two add-backs (Knuth Thm B: qhat - 2 <= q <= qhat)
+    // at most two add-backs (Knuth Thm B: qhat - 2 <= q <= qhat), applied in place
 #pragma unroll
     for (int ab = 0; ab < 2; ++ab) {
-      u32 c = 0, t[9];
+      u32 c = 0;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) t[k] = addc(u[j + k], v[k], c);
-      t[8] = addc(u[j + 8], 0u, c);
-#pragma unroll
-      for (int k = 0; k < 9; ++k) u[j + k] = neg ? t[k] : u[j + k];
+      for (int k = 0; k < 8; ++k) {
+        const u32 t = addc(u[j + k], v[k], c);
+        u[j + k] = neg ? t : u[j + k];
+      }
+      const u32 t8 = addc(u[j + 8], 0u, c);
+      u[j + 8] = neg ? t8 : u[j + 8];
       qh -= neg;
       neg = neg & (c ^ 1u);
     }
     q[j] = qh;
   }
-  u32 rn[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) rn[k] = u[k];
-  shr8(rn, s, 0u, r);
+  shr8(u, s, 0u, r);
 }
 
 MW_HD void neg8(const u32 a[8], u32 r[8]) {
@@ -328,71 +330,63 @@ MW_HD void neg8(const u32 a[8], u32 r[8]) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) r[k] = subb(0u, a[k], br);
 }
-
-// kind: 0 udiv, 1 urem, 2 sdiv, 3 srem, 4 smod
-MW_HD void wdiv(int kind, const u32 a[8], const u32 b[8], u32 w, u32 r[8]) {
-  bool sa = false, sb = false;
-  u32 x[8], y[8];
-  copy8(x, a);
-  copy8(y, b);
-  if (kind >= 2) {
-    sa = signbit8(a, w);
-    sb = signbit8(b, w);
-    u32 t[8];
-    neg8(a, t);
-    canon(t, w);
+MW_HD void cneg8(u32 a[8], bool c, u32 w) {  // a = c ? -a mod 2^w : a
+  u32 br = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = sa ? t[k] : x[k];
-    neg8(b, t);
-    canon(t, w);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) y[k] = sb ? t[k] : y[k];
+  for (int k = 0; k < 8; ++k) {
+    const u32 t = subb(0u, a[k], br);
+    a[k] = c ? t : a[k];
   }
-  bool yz = is_zero8(y);
-  u32 q[8], rm[8];
-  u32 one[8] = {1u, 0, 0, 0, 0, 0, 0, 0};
-  udivrem8(x, yz ? one : y, q, rm);
-  // SMT-LIB division-by-zero results on the magnitudes
-  if (yz) {
+  canon(a, w);
+}
+
+// kind: 0 udiv, 1 urem, 2 sdiv, 3 srem, 4 smod.  x, y are consumed (overwritten).
+MW_HD void wdiv(int kind, u32 x[8], u32 y[8], u32 w, u32 r[8]) {
+  bool sa = false, sb = false;
+  if (kind >= 2) {
+    sa = signbit8(x, w);
+    sb = signbit8(y, w);
+    cneg8(x, sa, w);  // |s|
+    cneg8(y, sb, w);  // |t|
+  }
+  const bool yz = is_zero8(y);
+  y[0] |= yz ? 1u : 0u;  // divide by 1 instead; result replaced below
+  u32 q[8];
+  udivrem8(x, y, q, r);  // r = |s| mod |t|
+  if (yz) {  // SMT-LIB: q = all ones, r = dividend magnitude
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      q[k] = limb_mask(w, k);  // all ones
-      rm[k] = x[k];
+      q[k] = limb_mask(w, k);
+      r[k] = x[k];
     }
   }
-  u32 t[8];
   switch (kind) {
     case 0:
       copy8(r, q);
       break;
     case 1:
-      copy8(r, rm);
       break;
-    case 2: {  // negate quotient when signs differ
-      neg8(q, t);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) r[k] = (sa != sb) ? t[k] : q[k];
+    case 2:  // quotient negated when the signs differ
+      copy8(r, q);
+      cneg8(r, sa != sb, w);
       break;
-    }
-    case 3: {  // remainder takes the dividend's sign
-      neg8(rm, t);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) r[k] = sa ? t[k] : rm[k];
+    case 3:  // remainder takes the dividend's sign
+      cneg8(r, sa, w);
       break;
-    }
-    default: {  // smod: sign of divisor
-      bool uz = is_zero8(rm);
-      u32 nu[8], s1[8], s2[8];
-      neg8(rm, nu);
-      add8(nu, b, s1);   // -u + t
-      add8(rm, b, s2);   //  u + t
+    default: {  // smod: u = |s| mod |t|; result follows the divisor's sign
+      const bool uz = is_zero8(r);
+      // t (the signed divisor) = sb ? -|t| : |t|  (y still holds |t|, or 1 if t == 0)
+      if (yz) y[0] = 0u;
+      cneg8(y, sb, w);
+      // sa & !sb : t - u ; !sa & sb : u + t ; sa & sb : -u
+      const bool negu = sa;
+      cneg8(r, negu, w);  // r = sa ? -u : u
+      const bool addt = !uz && (sa != sb);
+      u32 c = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        u32 v = rm[k];
-        v = (!uz && sa && !sb) ? s1[k] : v;
-        v = (!uz && !sa && sb) ? s2[k] : v;
-        v = (!uz && sa && sb) ? nu[k] : v;
-        r[k] = v;
+        const u32 t = addc(r[k], y[k], c);
+        r[k] = addt ? t : r[k];
       }
       break;
     }

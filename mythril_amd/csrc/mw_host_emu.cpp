@@ -60,10 +60,12 @@ int mwh_eval(const mg_prog_desc* d, const uint32_t* leaves_soa, uint64_t seed, u
   if (rc) return rc;
   std::vector<u32> consts(d->nconst_words + 8, 0u);
   if (d->nconst_words) std::memcpy(consts.data(), d->consts, d->nconst_words * 4);
+  std::vector<u32> code(d->ncode_words + 8, 0u);  // padded: the interpreter prefetches past END
+  std::memcpy(code.data(), d->code, d->ncode_words * 4);
   std::vector<u32> spill;
   for (size_t i = 0; i < ncand; ++i) {
     HostEnv env{d->leaves, d->pool, leaves_soa, trace, (u64)ncand, (u64)i, seed, begin + i, &spill};
-    verdict[i] = mw_run(d->code, consts.data(), env, true, flags) ? 1u : 0u;
+    verdict[i] = mw_run(code.data(), consts.data(), env, true, flags) ? 1u : 0u;
   }
   return 0;
 }

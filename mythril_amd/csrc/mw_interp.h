@@ -19,6 +19,18 @@
 
 namespace mw {
 
+// The program and its constant pool are read through the constant address
+// space on the device: with a uniform index that makes every instruction fetch
+// an s_load into SGPRs and keeps the opcode, slot numbers and constants
+// wave-uniform (a generic pointer read from a struct would compile to a vector
+// load and a divergent, exec-masked dispatch with waterfall register indexing).
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) u32* kptr;
+#else
+typedef const u32* kptr;
+#endif
+#define MW_KPTR(p) ((kptr)(p))
+
 typedef u32 u32x16 __attribute__((ext_vector_type(16)));
 typedef u32 u32x32 __attribute__((ext_vector_type(32)));
 
@@ -26,7 +38,7 @@ typedef u32 u32x32 __attribute__((ext_vector_type(32)));
   do {                                                                        \
     u32 _o = (opnd);                                                          \
     if (_o & MW_KBIT) {                                                       \
-      const u32* _p = cpool + (_o & 0x7fffu);                                 \
+      kptr _p = cpool + (_o & 0x7fffu);                                       \
       x[0] = _p[0]; x[1] = _p[1]; x[2] = _p[2]; x[3] = _p[3];                 \
       x[4] = _p[4]; x[5] = _p[5]; x[6] = _p[6]; x[7] = _p[7];                 \
     } else {                                                                  \
@@ -53,15 +65,26 @@ typedef u32 u32x32 __attribute__((ext_vector_type(32)));
 #define MW_WRITE_N(d, v) NF[(d) & (MW_NN - 1)] = (v)
 
 template <class Env>
-MW_HD bool mw_run(const u32* __restrict__ code, const u32* __restrict__ cpool, Env& env,
+MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_, Env& env,
                   bool alive, u32 flags) {
+  const kptr code = MW_KPTR(code_);
+  const kptr cpool = MW_KPTR(cpool_);
   u32x16 F0 = 0, F1 = 0, F2 = 0, F3 = 0, F4 = 0, F5 = 0, F6 = 0, F7 = 0;
   u32x32 NF = 0;
-  for (u32 pc = 0;; pc += 4) {
-    const u32 w0 = code[pc], w1 = code[pc + 1], w2 = code[pc + 2], w3 = code[pc + 3];
+  // Instruction fetch is software-pipelined: the next instruction's s_load is in
+  // flight while the current one executes (the words after END are always
+  // readable: the constant pool follows the code in the program buffer).
+  u32 w0 = code[0], w1 = code[1], w2 = code[2], w3 = code[3];
+  for (u32 pc = 4;; pc += 4) {
     const u32 op = w0 & 0xffu;
     const u32 w = w0 >> 16;
     const u32 dst = w1 & 0xffffu, oa = w1 >> 16, ob = w2 & 0xffffu, oc = w2 >> 16;
+    const u32 imm = w3;
+    // decode above, prefetch below: scalar loads return out of order, so the
+    // lgkmcnt(0) guarding this instruction's words must not also cover the
+    // next instruction's load (the barrier stops the load being hoisted).
+    asm volatile("" ::: "memory");
+    const u32 n0 = code[pc], n1 = code[pc + 1], n2 = code[pc + 2], n3 = code[pc + 3];
     u32 x[8], y[8], r[8];
     u32 wk = 0;  // 1: write W[dst] = r, 2: write N[dst] = r[0]
     switch (op) {
@@ -75,36 +98,36 @@ MW_HD bool mw_run(const u32* __restrict__ code, const u32* __restrict__ cpool, E
         break;
       }
       case MW_LEAF_W:
-        env.leaf(w3, r);
+        env.leaf(imm, r);
         wk = 1;
         break;
       case MW_LEAF_N:
-        env.leaf(w3, r);
+        env.leaf(imm, r);
         wk = 2;
         break;
       case MW_STORE_W:
         MW_FETCH_W(oa, x);
-        env.store(w3, x, 8);
+        env.store(imm, x, 8);
         break;
       case MW_STORE_N: {
         MW_FETCH_N(oa, x[0]);
-        env.store(w3, x, 1);
+        env.store(imm, x, 1);
         break;
       }
       case MW_SPILL_W:
         MW_FETCH_W(oa, x);
-        env.spill(w3, x, 8);
+        env.spill(imm, x, 8);
         break;
       case MW_FILL_W:
-        env.fill(w3, r, 8);
+        env.fill(imm, r, 8);
         wk = 1;
         break;
       case MW_SPILL_N:
         MW_FETCH_N(oa, x[0]);
-        env.spill(w3, x, 1);
+        env.spill(imm, x, 1);
         break;
       case MW_FILL_N:
-        env.fill(w3, r, 1);
+        env.fill(imm, r, 1);
         wk = 2;
         break;
       case MW_MOV_W:
@@ -125,21 +148,18 @@ MW_HD bool mw_run(const u32* __restrict__ code, const u32* __restrict__ cpool, E
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         add8(x, y, r);
-        canon(r, w);
         wk = 1;
         break;
       case MW_W_SUB:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         sub8(x, y, r);
-        canon(r, w);
         wk = 1;
         break;
       case MW_W_MUL:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         mul8(x, y, r);
-        canon(r, w);
         wk = 1;
         break;
       case MW_W_AND:
@@ -167,7 +187,6 @@ MW_HD bool mw_run(const u32* __restrict__ code, const u32* __restrict__ cpool, E
         MW_FETCH_W(oa, x);
 #pragma unroll
         for (int k = 0; k < 8; ++k) r[k] = ~x[k];
-        canon(r, w);
         wk = 1;
         break;
       case MW_W_SHL:
@@ -210,14 +229,12 @@ MW_HD bool mw_run(const u32* __restrict__ code, const u32* __restrict__ cpool, E
       }
       case MW_W_SHLI:
         MW_FETCH_W(oa, x);
-        shl8(x, w3, r);
-        canon(r, w);
+        shl8(x, imm, r);
         wk = 1;
         break;
       case MW_W_LSHRI:
         MW_FETCH_W(oa, x);
-        shr8(x, w3, 0u, r);
-        canon(r, w);
+        shr8(x, imm, 0u, r);
         wk = 1;
         break;
       case MW_W_ZEXTN: {
@@ -230,8 +247,7 @@ MW_HD bool mw_run(const u32* __restrict__ code, const u32* __restrict__ cpool, E
       }
       case MW_W_SEXT:
         MW_FETCH_W(oa, x);
-        sext8(x, w3);
-        canon(x, w);
+        sext8(x, imm);
         copy8(r, x);
         wk = 1;
         break;
@@ -240,8 +256,7 @@ MW_HD bool mw_run(const u32* __restrict__ code, const u32* __restrict__ cpool, E
         MW_FETCH_N(oa, v);
         zero8(r);
         r[0] = v;
-        sext8(r, w3);
-        canon(r, w);
+        sext8(r, imm);
         wk = 1;
         break;
       }
@@ -251,10 +266,9 @@ MW_HD bool mw_run(const u32* __restrict__ code, const u32* __restrict__ cpool, E
         MW_FETCH_N(ob, v);
         zero8(y);
         y[0] = v;
-        shl8(y, w3, r);
+        shl8(y, imm, r);
 #pragma unroll
         for (int k = 0; k < 8; ++k) r[k] |= x[k];
-        canon(r, w);
         wk = 1;
         break;
       }
@@ -262,7 +276,7 @@ MW_HD bool mw_run(const u32* __restrict__ code, const u32* __restrict__ cpool, E
       // ---------------------------------------------------------- wide -> narrow
       case MW_N_EXTRACTW: {
         MW_FETCH_W(oa, x);
-        shr8(x, w3, 0u, r);
+        shr8(x, imm, 0u, r);
         r[0] = r[0] & nmask(w);
         wk = 2;
         break;
@@ -359,9 +373,9 @@ MW_HD bool mw_run(const u32* __restrict__ code, const u32* __restrict__ cpool, E
             v = c ? a : b;
             break;
           }
-          case MW_N_SHLI: v = (w3 >= 32 ? 0u : (a << w3)) & m; break;
-          case MW_N_LSHRI: v = (w3 >= 32 ? 0u : (a >> w3)) & m; break;
-          case MW_N_SEXT: v = n_sext(a, w3) & m; break;
+          case MW_N_SHLI: v = (imm >= 32 ? 0u : (a << imm)) & m; break;
+          case MW_N_LSHRI: v = (imm >= 32 ? 0u : (a >> imm)) & m; break;
+          case MW_N_SEXT: v = n_sext(a, imm) & m; break;
           case MW_N_ULTN: v = a < b; break;
           case MW_N_ULEN: v = a <= b; break;
           case MW_N_SLTN: v = n_slt(a, b, w); break;
@@ -384,10 +398,15 @@ MW_HD bool mw_run(const u32* __restrict__ code, const u32* __restrict__ cpool, E
     // single write-back point: keeps one SSA version of each register-file
     // vector live across the dispatch (otherwise hipcc duplicates the files)
     if (wk == 1) {
+      if (w - 1u < 255u) canon(r, w);  // results of width 1..255: clear bits >= w (FILL/MOV carry 0)
       MW_WRITE_W(dst, r);
     } else if (wk == 2) {
       MW_WRITE_N(dst, r[0]);
     }
+    w0 = n0;
+    w1 = n1;
+    w2 = n2;
+    w3 = n3;
   }
 }
 

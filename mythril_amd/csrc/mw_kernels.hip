@@ -124,7 +124,7 @@ struct EvalEnv {
 
 }  // namespace
 
-__global__ __launch_bounds__(kBlock) void mw_search_kernel(const ProgDev* __restrict__ progs, u64 seed,
+__global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __restrict__ progs, u64 seed,
                                                            u64 begin, u64 count, u32 flags,
                                                            u64* __restrict__ out_min,
                                                            u64* __restrict__ counter,
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kBlock) void mw_search_kernel(const ProgDev* __rest
   if (lane == 0 && evals) atomicAdd((unsigned long long*)counter, (unsigned long long)evals);
 }
 
-__global__ __launch_bounds__(kBlock) void mw_eval_kernel(ProgDev P, const u32* __restrict__ in,
+__global__ __launch_bounds__(kBlock, 2) void mw_eval_kernel(ProgDev P, const u32* __restrict__ in,
                                                          u64 ncand, u64 seed, u64 begin,
                                                          u32* __restrict__ verdict,
                                                          u32* __restrict__ trace,

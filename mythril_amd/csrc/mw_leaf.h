@@ -48,8 +48,13 @@ MW_HD void random_leaf(u32 id, u32 w, u64 seed, u64 cand, u32 out[8]) {
 }
 
 // leaf: MW_LEAF_WORDS words (uniform); pool: per-lane gather
-MW_HD void leaf_value(const u32* __restrict__ leaf, const u32* __restrict__ pool, u64 seed,
+MW_HD void leaf_value(const u32* __restrict__ leaf_, const u32* __restrict__ pool, u64 seed,
                       u64 cand, u32 out[8]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __attribute__((address_space(4))) u32* leaf = (const __attribute__((address_space(4))) u32*)leaf_;
+#else
+  const u32* leaf = leaf_;
+#endif
   const u32 w = leaf[MW_LEAF_WIDTH];
   const u32 id = leaf[MW_LEAF_ID];
   if (leaf[MW_LEAF_KIND] == 1u) {
