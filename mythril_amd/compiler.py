@@ -32,6 +32,11 @@ from . import isa
 from .ir import BOOL, Node, topo
 
 
+# candidate-index bits available to exhaustive pool digits; the bits above
+# them enumerate "rounds" that re-draw every RANDOM entry
+INDEX_FIELD_BITS = 40
+
+
 class Unsupported(Exception):
     """The formula uses something the GPU path does not evaluate (-> z3)."""
 
@@ -86,6 +91,7 @@ class LeafSpec:
     pool: Optional[List[Optional[int]]] = None   # None entry = RANDOM; len must be 2**k
     shift: int = 0
     bits: int = 0
+    hashed: bool = False         # pool digit from a hash of the index instead of a bit-field
     salt: Optional[int] = None   # Philox key salt; default crc32(name) so a variable
                                  # draws the same value in every program for an index
 
@@ -644,10 +650,15 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
             nb = max(0, math.ceil(math.log2(len(p)))) if len(p) > 1 else 0
             p += [None] * ((1 << nb) - len(p))
             spec.pool = p
-            if spec.bits == 0 and spec.shift == 0:
-                spec.bits, spec.shift = nb, bit
-                bit += nb
-            kind, pshift, pbits, poff = 1, spec.shift, spec.bits, len(pool_words)
+            if not spec.hashed and spec.bits == 0 and spec.shift == 0:
+                if bit + nb > INDEX_FIELD_BITS:
+                    spec.hashed = True  # index bits exhausted: sample this pool instead
+                else:
+                    spec.bits, spec.shift = nb, bit
+                    bit += nb
+            if spec.hashed:
+                spec.bits, spec.shift = nb, 0
+            kind, pshift, pbits, poff = (2 if spec.hashed else 1), spec.shift, spec.bits, len(pool_words)
             for e in p:
                 if e is None:
                     pool_words.extend([1] + [0] * 8)

@@ -28,7 +28,7 @@
 
 // leaf table entry (MW_LEAF_WORDS u32 per leaf)
 #define MW_LEAF_WIDTH 0
-#define MW_LEAF_KIND 1   // 0 = random (Philox), 1 = pool
+#define MW_LEAF_KIND 1   // 0 = random (Philox), 1 = pool (index bit-field), 2 = pool (hashed digit)
 #define MW_LEAF_ID 2     // Philox key salt
 #define MW_LEAF_SHIFT 3  // candidate-index bit offset of the pool digit
 #define MW_LEAF_BITS 4   // log2(pool entries)

@@ -8,6 +8,9 @@
 //                blk 0 -> limbs 0..3, blk 1 -> limbs 4..7, masked to width
 //   pool leaf:   digit = (c >> shift) & (2^bits - 1); entry = pool[digit];
 //                entry flag RANDOM -> random value above, else the constant.
+//   hashed pool: digit = fmix64(c ^ (salt * 0x9E3779B97F4A7C15)) & (2^bits - 1)
+//                (MurmurHash3 finalizer), then as a pool leaf: samples large
+//                pools when the index bits cannot enumerate every leaf.
 // Restated independently in oracle/philox.py (pinned by Random123 KATs).
 #pragma once
 #include "mw_alu.h"
@@ -47,6 +50,15 @@ MW_HD void random_leaf(u32 id, u32 w, u64 seed, u64 cand, u32 out[8]) {
   canon(out, w);
 }
 
+MW_HD u64 fmix64(u64 h) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  h ^= h >> 33;
+  return h;
+}
+
 // leaf: MW_LEAF_WORDS words (uniform); pool: per-lane gather
 MW_HD void leaf_value(const u32* __restrict__ leaf_, const u32* __restrict__ pool, u64 seed,
                       u64 cand, u32 out[8]) {
@@ -57,9 +69,12 @@ MW_HD void leaf_value(const u32* __restrict__ leaf_, const u32* __restrict__ poo
 #endif
   const u32 w = leaf[MW_LEAF_WIDTH];
   const u32 id = leaf[MW_LEAF_ID];
-  if (leaf[MW_LEAF_KIND] == 1u) {
+  const u32 kind = leaf[MW_LEAF_KIND];
+  if (kind == 1u || kind == 2u) {
     const u32 bits = leaf[MW_LEAF_BITS];
-    const u32 digit = (u32)(cand >> leaf[MW_LEAF_SHIFT]) & ((bits >= 32) ? 0xffffffffu : ((1u << bits) - 1u));
+    const u64 src = kind == 1u ? (cand >> leaf[MW_LEAF_SHIFT])
+                               : fmix64(cand ^ ((u64)id * 0x9E3779B97F4A7C15ull));
+    const u32 digit = (u32)src & ((bits >= 32) ? 0xffffffffu : ((1u << bits) - 1u));
     const u32* e = pool + leaf[MW_LEAF_POOL] + (u64)digit * MW_POOL_ENTRY_WORDS;
     if (e[0] & 1u) {
       random_leaf(id, w, seed, cand, out);

@@ -13,6 +13,7 @@ for candidate index ``c`` (u64), leaf ``j`` of width ``w``:
 * ``pool`` leaf with 2**b entries at bit-field ``s``: digit = (c >> s) & (2**b-1);
   entry = pool[digit]; an entry flagged RANDOM yields the random value above,
   otherwise its constant (masked to ``w``).
+* ``hashed`` pool leaf: digit = fmix64(c ^ (salt * 0x9E3779B97F4A7C15)) & (2**b-1).
 """
 from __future__ import annotations
 
@@ -46,12 +47,27 @@ def random_leaf(seed: int, leaf_id: int, c: int, width: int) -> int:
     return v & ((1 << width) - 1)
 
 
+def fmix64(h: int) -> int:
+    """MurmurHash3 64-bit finalizer (Appleby, public domain)."""
+    M = (1 << 64) - 1
+    h ^= h >> 33
+    h = (h * 0xFF51AFD7ED558CCD) & M
+    h ^= h >> 33
+    h = (h * 0xC4CEB9FE1A85EC53) & M
+    h ^= h >> 33
+    return h
+
+
 def leaf_value(spec: dict, seed: int, c: int) -> int:
-    """spec: {'id','width','shift','bits','pool': [int or None]}  (None = RANDOM)."""
+    """spec: {'id','width','shift','bits','pool': [int or None], 'hashed': bool}  (None = RANDOM)."""
     w = spec["width"]
     pool = spec.get("pool")
     if pool:
-        d = (c >> spec["shift"]) & ((1 << spec["bits"]) - 1)
+        if spec.get("hashed"):
+            src = fmix64(c ^ ((spec["id"] * 0x9E3779B97F4A7C15) & ((1 << 64) - 1)))
+        else:
+            src = c >> spec["shift"]
+        d = src & ((1 << spec["bits"]) - 1)
         e = pool[d]
         if e is not None:
             return e & ((1 << w) - 1)

@@ -57,7 +57,8 @@ def oracle_models(p: Program, seed: int, begin: int, n: int) -> List[Dict[str, i
     for j in range(n):
         m = {}
         for li, (node, spec) in enumerate(zip(p.leaf_nodes, p.leaf_specs)):
-            sd = {"id": spec.key_salt(), "width": spec.width, "shift": spec.shift, "bits": spec.bits, "pool": spec.pool}
+            sd = {"id": spec.key_salt(), "width": spec.width, "shift": spec.shift, "bits": spec.bits, "pool": spec.pool,
+                  "hashed": spec.hashed}
             m[node.name] = leaf_value(sd, seed, begin + j)
         out.append(m)
     return out

@@ -88,6 +88,22 @@ def test_generated_candidates_match_oracle_philox_and_pools():
         assert verdict[j] == int(m["x"] < (1 << 255) and m["y"] == 3)
 
 
+def test_hashed_pools_match_oracle():
+    from mythril_amd.compiler import LeafSpec
+    dag = RandDag(8, widths=[8, 256])
+    c = dag.ctx
+    xs = [c.var(f"h{i}", 8) for i in range(6)]
+    big = c.var("big", 256)
+    specs = {f"h{i}": LeafSpec(f"h{i}", 8, pool=[i, 0x41, None, 0xFF, 7], hashed=True) for i in range(6)}
+    specs["big"] = LeafSpec("big", 256, pool=[None, 1 << 200, 5], hashed=True)
+    p = compile_program([c.true()], trace=xs + [big], leaf_specs=specs)
+    seed, begin, n = 3, (1 << 50) + 9, 300
+    _, trace = emu_eval(p, None, n, seed=seed, begin=begin)
+    models = oracle_models(p, seed, begin, n)
+    for node in xs + [big]:
+        assert unpack_trace(p, trace, node) == [m[node.name] for m in models]
+
+
 def test_spilling_under_pressure():
     """More simultaneously-live wide values than W slots forces SPILL/FILL."""
     dag = RandDag(3, widths=[256])
