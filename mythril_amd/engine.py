@@ -1,0 +1,164 @@
+"""Witness engine: constraint sets -> batched GPU search -> concrete witnesses.
+
+``prepare`` lowers one constraint set (Ackermannisation, width legalisation,
+candidate pools) and compiles it twice with identical leaf layouts: a search
+program (verdicts only) and a materialisation program that also traces every
+leaf and every array index / function argument.  ``WitnessEngine.search``
+launches many programs in one ``mg_search`` call (one grid row per program,
+SURVEY.md §8a row A9 batching) and turns each lowest satisfying index back
+into a :class:`Witness` by re-evaluating that single candidate on the device.
+"""
+from __future__ import annotations
+
+import copy
+import logging
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from . import isa
+from .compiler import LeafSpec, Program, Unsupported, compile_program
+from .ir import BOOL, Ctx, Node
+from .lower import Lowered, lower_constraints, needs_lowering
+from .pools import harvest
+
+log = logging.getLogger(__name__)
+
+DEFAULT_SEED = 0x5EED_0001
+DEFAULT_BUDGET = 1 << 22  # candidates per query (early exit + stop-after-hit)
+
+
+@dataclass
+class Witness:
+    index: int
+    values: Dict[str, int]                           # every scalar leaf (incl. Ackermann leaves)
+    arrays: Dict[str, Dict[int, int]] = field(default_factory=dict)
+    functions: Dict[str, Dict[Tuple[int, ...], int]] = field(default_factory=dict)
+
+
+@dataclass
+class Query:
+    ctx: Ctx
+    conjuncts: List[Node]
+    lowered: Lowered
+    program: Program
+    trace_program: Program
+    arg_terms: List[Node]
+    arg_chunks: Dict[str, List[List[Node]]] = field(default_factory=dict)
+
+    @property
+    def ops_per_eval(self) -> int:
+        return self.program.ops_per_eval
+
+
+def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True) -> Query:
+    conj = list(conjuncts)
+    low = lower_constraints(conj, ctx) if needs_lowering(conj) else Lowered(conj)
+    leaves = []
+    seen = set()
+    from .ir import topo
+    for n in topo(low.conjuncts):
+        if n.op == "var" and n.name not in seen:
+            seen.add(n.name)
+            leaves.append(n)
+    specs = harvest(low.conjuncts, leaves) if use_pools else {}
+    prog = compile_program(low.conjuncts, leaf_specs=specs)
+    # identical leaf layout (pool fields already assigned) for the materialisation program
+    fixed = {s.name: copy.deepcopy(s) for s in prog.leaf_specs}
+    # trace every array index / function argument (wider than 256 bits: as 256-bit chunks)
+    from .lower import _Rewriter
+    chunker = _Rewriter(ctx)
+    arg_chunks: Dict[str, List[List[Node]]] = {}
+    arg_terms: List[Node] = []
+    for al in low.ack.values():
+        per = []
+        terms = list(al.args) + ([al.value] if al.value is not None else [])
+        for a in terms:
+            parts = [a] if a.width <= 256 else chunker.chunks(a)
+            per.append(parts)
+            arg_terms.extend(parts)
+        arg_chunks[al.name] = per
+    tprog = compile_program(low.conjuncts, leaf_specs=fixed, trace=list(prog.leaf_nodes) + arg_terms)
+    q = Query(ctx, conj, low, prog, tprog, arg_terms)
+    q.arg_chunks = arg_chunks
+    return q
+
+
+def _combine_chunks(values: Dict[str, int], name: str, width: int) -> int:
+    if name in values:
+        return values[name]
+    v, lo, k = 0, 0, 0
+    while lo < width:
+        v |= values.get(f"{name}#{k}", 0) << lo
+        lo += 256
+        k += 1
+    return v
+
+
+class WitnessEngine:
+    """Owns one device context; everything goes through the C-ABI."""
+
+    def __init__(self, device: int = 0, seed: int = DEFAULT_SEED, budget: int = DEFAULT_BUDGET, dev=None):
+        if dev is None:
+            from .runtime import Device  # raises EngineUnavailable without the HIP library / GPU
+            dev = Device(device)
+        self.dev = dev
+        self.seed = seed
+        self.budget = budget
+        self.stats = {"searches": 0, "programs": 0, "hits": 0, "evals": 0, "kernel_ms": 0.0}
+
+    def close(self):
+        self.dev.close()
+
+    def search(self, queries: Sequence[Query], count: Optional[int] = None, begin: int = 0,
+               flags: int = isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT) -> List[Optional[Witness]]:
+        if not queries:
+            return []
+        count = count or self.budget
+        dps = [self.dev.load(q.program) for q in queries]
+        try:
+            found, st = self.dev.search(dps, self.seed, begin, count, flags)
+        finally:
+            for dp in dps:
+                dp.free()
+        self.stats["searches"] += 1
+        self.stats["programs"] += len(queries)
+        self.stats["evals"] += st["evals"]
+        self.stats["kernel_ms"] += st["kernel_ms"]
+        out: List[Optional[Witness]] = []
+        for q, idx in zip(queries, found):
+            w = self.materialize(q, idx) if idx is not None else None
+            if w is not None:
+                self.stats["hits"] += 1
+            out.append(w)
+        return out
+
+    def materialize(self, q: Query, index: int) -> Optional[Witness]:
+        from .runtime import unpack_trace
+        dp = self.dev.load(q.trace_program)
+        try:
+            verdict, trace = self.dev.eval_generated(dp, self.seed, index, 1)
+        finally:
+            dp.free()
+        if int(verdict[0]) != 1:
+            log.error("witness %d failed device re-evaluation; discarded", index)
+            return None
+        p = q.trace_program
+        values = {n.name: unpack_trace(p, trace, n)[0] for n in p.leaf_nodes}
+        w = Witness(index, values)
+        for al in q.lowered.ack.values():
+            args = []
+            for parts in q.arg_chunks[al.name]:
+                v = 0
+                for k, t in enumerate(parts):
+                    v |= (t.val if t.op == "const" else unpack_trace(p, trace, t)[0]) << (256 * k)
+                args.append(v)
+            if al.value is not None:
+                val = args.pop()  # defined value (keccak inverse = hashed input)
+            else:
+                val = _combine_chunks(values, al.name, al.width)
+            args = tuple(args)
+            if al.kind == "select":
+                w.arrays.setdefault(al.base, {})[args[0]] = val
+            else:
+                w.functions.setdefault(al.base, {})[args] = val
+        return w

@@ -44,6 +44,7 @@ class AckLeaf:
     base: str             # array or function name
     args: Tuple[Node, ...]  # index term(s) in the rewritten formula
     width: int
+    value: Optional[Node] = None  # defined (not free) value: keccak inverse = the hashed input
 
 
 @dataclass
@@ -60,6 +61,7 @@ class _Rewriter:
         self.ack: Dict[str, AckLeaf] = {}
         self.by_base: Dict[str, List[AckLeaf]] = {}
         self.leaf_of_key: Dict[tuple, Node] = {}
+        self.inner_apply: Dict[int, tuple] = {}   # leaf id of f(x) -> (f, x)
         self.nsym = 0
 
     # -- extract simplification (pushes extracts towards leaves) ------------------
@@ -135,6 +137,18 @@ class _Rewriter:
             self.by_base.setdefault((kind, base), []).append(al)
         return leaf
 
+    def defined_leaf(self, base: str, args: Tuple[Node, ...], width: int, value: Node) -> Node:
+        """An application whose value is a term (no free leaf); still congruence-checked."""
+        key = ("def", base) + tuple(("t", a.id) for a in args)
+        if key not in self.leaf_of_key:
+            self.nsym += 1
+            nm = f"{base}@d{self.nsym}"
+            al = AckLeaf(nm, "apply", base, args, width, value=value)
+            self.ack[nm] = al
+            self.by_base.setdefault(("apply", base), []).append(al)
+            self.leaf_of_key[key] = value
+        return self.leaf_of_key[key]
+
     def wide_var(self, nm: str, width: int) -> Node:
         """A leaf; wider than 256 bits it is the concat of 256-bit chunk leaves nm#0 (LSB).."""
         if width <= MAXW:
@@ -190,7 +204,19 @@ class _Rewriter:
         if op == "ite" and n.is_array:
             return c._mk("ite", n.width, tuple(args), dom=n.dom)
         if op == "apply":
-            return self.read_leaf("apply", n.name, tuple(args), n.width)
+            # Mythril's keccak inverse (keccak_function_manager.py:80-81): inv(keccak256_N(x)) is
+            # *defined* as x.  Sound: every inverse application sits on a keccak application
+            # here, and the inverse congruence (k_t = k_u) => (x_t = x_u) is still emitted, so
+            # any witness extends to a model with inv(k_t) = x_t (the condition
+            # inv(func(x)) == x of :169-179 then holds by construction).
+            if n.name.endswith("-1") and len(args) == 1:
+                inner = self.inner_apply.get(args[0].id)
+                if inner is not None and inner[0] == n.name[:-2] and inner[1].width == n.width:
+                    return self.defined_leaf(n.name, (args[0],), n.width, inner[1])
+            leaf = self.read_leaf("apply", n.name, tuple(args), n.width)
+            if len(args) == 1:
+                self.inner_apply[leaf.id] = (n.name, args[0])
+            return leaf
         if op in ("=", "distinct") and args and args[0].is_array:
             raise Unsupported("array equality")
         if op == "=" and args[0].width > MAXW:
@@ -218,7 +244,8 @@ class _Rewriter:
                         continue  # distinct concrete cells: nothing to relate
                     same = [self.eq(x, y) for x, y in zip(t.args, u.args)]
                     prem = c.app("and", *same) if len(same) > 1 else same[0]
-                    vt, vu = self.wide_var(t.name, t.width), self.wide_var(u.name, u.width)
+                    vt = t.value if t.value is not None else self.wide_var(t.name, t.width)
+                    vu = u.value if u.value is not None else self.wide_var(u.name, u.width)
                     out.append(c.app("=>", prem, self.eq(vt, vu)))
         return out
 

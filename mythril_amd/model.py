@@ -1,0 +1,207 @@
+"""Drop-in replacement for ``mythril.support.model.get_model``.
+
+Same signature, same ``@lru_cache(maxsize=2**23)``, same error behaviour as
+``mythril/support/model.py:15-63``:
+
+* the solver timeout is clamped to the remaining execution budget and
+  ``UnsatError`` is raised when it is <= 0 (``:26-31``);
+* a Python ``False`` constraint raises ``UnsatError`` (``:32-34``);
+* a ``Constraints`` object is expanded with the keccak conditions via
+  ``get_all_constraints()`` (``:35-36``); Python bools are dropped (``:37``);
+* ``--solver-log`` dumps are written exactly as the reference writes them
+  (``:45-56``), whether or not the GPU answers;
+* only *returned models* are cached; ``UnsatError`` is never cached.
+
+New: when ``minimize == maximize == ()`` (feasibility-only queries: LASER's
+``is_possible`` pruning, the detection modules' checks)
+and the formula lowers to the witness engine, a batched GPU search runs first.
+A witness is re-checked by z3 on the exact same constraints and z3's model of
+that check is returned.  On a miss, an unsupported formula, an unavailable
+engine, or a witness z3 does not confirm, the *unchanged* reference function
+answers (``minimize`` queries from ``get_transaction_sequence``,
+``analysis/solver.py:68``, always go to the reference).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+from functools import lru_cache
+from pathlib import Path
+from typing import Callable, Dict, Optional
+
+from .compiler import Unsupported
+
+log = logging.getLogger(__name__)
+
+STATS: Dict[str, int] = {"queries": 0, "gpu_attempts": 0, "gpu_witnesses": 0, "z3_confirmed": 0,
+                         "unsupported": 0, "fallbacks": 0, "memo_hits": 0}
+
+# injection points (set by install(); replaced by tests)
+_reference: Optional[Callable] = None   # the reference get_model, uncached (__wrapped__)
+_engine = None
+_engine_lock = threading.Lock()
+_engine_failed = False
+_memo: Dict[tuple, tuple] = {}          # z3 AST-id key -> (witness, script)
+MEMO_MAX = 1 << 16
+
+
+def _env():
+    from mythril.exceptions import UnsatError
+    from mythril.laser.ethereum.time_handler import time_handler
+    from mythril.support.support_args import args
+    return args, time_handler, UnsatError
+
+
+def engine():
+    """The process's WitnessEngine, or None if the HIP engine is unavailable."""
+    global _engine, _engine_failed
+    if _engine is None and not _engine_failed:
+        with _engine_lock:
+            if _engine is None and not _engine_failed:
+                if os.environ.get("MYTHRIL_AMD_DISABLE"):
+                    _engine_failed = True
+                    return None
+                try:
+                    from .engine import WitnessEngine
+                    dev = int(os.environ.get("LOCAL_RANK", os.environ.get("MYTHRIL_AMD_DEVICE", "0")))
+                    budget = int(os.environ.get("MYTHRIL_AMD_BUDGET", str(1 << 22)))
+                    _engine = WitnessEngine(device=dev, budget=budget)
+                except Exception as e:  # EngineUnavailable / EngineError
+                    log.warning("MI355X witness engine unavailable (%s); using z3 only", e)
+                    _engine_failed = True
+    return _engine
+
+
+def memo_key(raws) -> tuple:
+    return tuple(r.get_id() for r in raws)
+
+
+def _solver_log(constraints, minimize, maximize, args, timeout):
+    """Write the .smt2 dump exactly as mythril/support/model.py:45-56 does."""
+    from mythril.laser.smt import Optimize
+    s = Optimize()
+    s.set_timeout(timeout)
+    for c in constraints:
+        s.add(c)
+    for e in minimize:
+        s.minimize(e)
+    for e in maximize:
+        s.maximize(e)
+    Path(args.solver_log).mkdir(parents=True, exist_ok=True)
+    key = tuple(list(constraints) + list(minimize) + list(maximize)
+                + [len(constraints), len(minimize), len(maximize)])
+    with open(args.solver_log + f"/{abs(hash(key))}.smt2", "w") as f:
+        f.write(s.sexpr())
+
+
+def _gpu_model(constraints, timeout):
+    from . import z3bridge
+    raws = [c.raw for c in constraints]
+    key = memo_key(raws)
+    hit = _memo.get(key)
+    if hit is not None:
+        STATS["memo_hits"] += 1
+        witness, script = hit
+    else:
+        eng = engine()
+        if eng is None:
+            return None
+        try:
+            script = z3bridge.to_ir(raws)
+            from .engine import prepare
+            q = prepare(script.asserts, script.ctx)
+        except (Unsupported, RecursionError, ValueError, KeyError) as e:
+            STATS["unsupported"] += 1
+            log.debug("witness engine: unsupported formula (%s)", e)
+            return None
+        STATS["gpu_attempts"] += 1
+        witness = eng.search([q])[0]
+    if witness is None:
+        return None
+    STATS["gpu_witnesses"] += 1
+    zm = z3bridge.model_from_witness(raws, script, witness, timeout)
+    if zm is None:
+        return None
+    STATS["z3_confirmed"] += 1
+    from mythril.laser.smt.model import Model
+    return Model([zm])
+
+
+@lru_cache(maxsize=2 ** 23)
+def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True):
+    """mythril.support.model.get_model with a GPU witness fast path (see module doc)."""
+    args, time_handler, UnsatError = _env()
+    STATS["queries"] += 1
+    timeout = args.solver_timeout
+    if enforce_execution_time:
+        timeout = min(timeout, time_handler.time_remaining() - 500)
+        if timeout <= 0:
+            raise UnsatError
+    for constraint in constraints:
+        if type(constraint) == bool and not constraint:
+            raise UnsatError
+    if minimize == () and maximize == ():
+        cl = constraints if type(constraints) == tuple else constraints.get_all_constraints()
+        cl = [c for c in cl if type(c) != bool]
+        model = _gpu_model(cl, timeout)
+        if model is not None:
+            if args.solver_log:
+                _solver_log(cl, minimize, maximize, args, timeout)
+            return model
+    STATS["fallbacks"] += 1
+    return _reference(constraints, minimize, maximize, enforce_execution_time)
+
+
+def prefetch(constraint_sets) -> int:
+    """Batch feasibility search for many constraint sets in one launch (LaserEVM
+    open states at a transaction boundary, svm.py:216-223); fills the memo that
+    get_model consults.  Returns the number of witnesses found."""
+    eng = engine()
+    if eng is None:
+        return 0
+    from . import z3bridge
+    from .engine import prepare
+    items = []
+    for cs in constraint_sets:
+        try:
+            cl = cs if type(cs) == tuple else cs.get_all_constraints()
+            raws = [c.raw for c in cl if type(c) != bool]
+            key = memo_key(raws)
+            if key in _memo:
+                continue
+            script = z3bridge.to_ir(raws)
+            items.append((key, script, prepare(script.asserts, script.ctx)))
+        except (Unsupported, RecursionError, ValueError, KeyError):
+            STATS["unsupported"] += 1
+    if not items:
+        return 0
+    found = eng.search([q for _, _, q in items])
+    n = 0
+    for (key, script, _), w in zip(items, found):
+        if w is not None:
+            if len(_memo) >= MEMO_MAX:
+                _memo.clear()
+            _memo[key] = (w, script)
+            n += 1
+    return n
+
+
+def install() -> bool:
+    """Rebind every import site of get_model (SURVEY.md §8b "Who calls it")."""
+    global _reference
+    try:
+        import mythril.analysis.solver as a_solver
+        import mythril.laser.ethereum.state.constraints as l_constraints
+        import mythril.support.model as s_model
+    except ImportError:
+        return False
+    if getattr(s_model.get_model, "__module__", "") == __name__:
+        return True
+    ref = s_model.get_model
+    _reference = getattr(ref, "__wrapped__", ref)
+    s_model.get_model = get_model
+    a_solver.get_model = get_model
+    l_constraints.get_model = get_model
+    log.info("MI355X witness engine installed behind mythril get_model")
+    return True

@@ -1,0 +1,158 @@
+"""Engine end-to-end on CPU (host emulator behind a fake device): lowering of
+arrays/UFs/keccak conditions, pools, batched search, witness materialisation.
+
+Soundness is checked against the oracle on the ORIGINAL formula: every witness
+is turned into a full model (scalars + array cells + function points) and must
+satisfy every original conjunct.  Sat/unsat expectations come from the
+reference's own tests (tests/laser/keccak_tests.py:7-145,
+tests/laser/state/calldata_test.py:42-91): an UNSAT formula must never yield a
+witness.
+"""
+import pytest
+
+from mythril_amd.engine import WitnessEngine, prepare
+from mythril_amd.ir import Ctx
+from oracle.dag_eval import ArrayVal, eval_nodes
+from tests.fakedev import FakeDevice
+from tests.mythril_shapes import KeccakManager, calldata_load, calldata_word
+
+
+def engine(budget=1 << 14):
+    return WitnessEngine(dev=FakeDevice(), seed=0x5EED0001, budget=budget)
+
+
+def holds(conj, w):
+    model = dict(w.values)
+    for name, cells in w.arrays.items():
+        model[name] = ArrayVal(cells, 0)
+    for name, pts in w.functions.items():
+        model[name] = (pts, 0)
+    vals = eval_nodes(conj, model)
+    return all(vals[c.id] for c in conj)
+
+
+def run(conj, ctx, budget=1 << 14):
+    q = prepare(conj, ctx)
+    (w,) = engine(budget).search([q])
+    if w is not None:
+        assert holds(conj, w), "witness does not satisfy the original formula"
+    return w
+
+
+# ---- keccak UF expectations (tests/laser/keccak_tests.py) --------------------------
+def _kbasic(make1, make2):
+    c = Ctx()
+    km = KeccakManager(c)
+    o1 = km.create_keccak(make1(c))
+    o2 = km.create_keccak(make2(c))
+    return c, [km.create_conditions(), c.app("=", o1, o2)]
+
+
+@pytest.mark.parametrize("make1,make2,sat", [
+    (lambda c: c.const(100, 8), lambda c: c.const(101, 8), False),
+    (lambda c: c.const(100, 8), lambda c: c.const(100, 16), False),
+    (lambda c: c.const(100, 8), lambda c: c.const(100, 8), True),
+    (lambda c: c.var("N1", 256), lambda c: c.var("N2", 256), True),
+    (lambda c: c.const(100, 256), lambda c: c.var("N1", 256), True),
+    (lambda c: c.const(100, 8), lambda c: c.var("N1", 256), False),
+], ids=["100_8-101_8", "100_8-100_16", "100_8-100_8", "N1-N2", "100_256-N1", "100_8-N1"])
+def test_keccak_basic(make1, make2, sat):
+    # keccak_tests.py:7-38 — equal 8/16-bit inputs of different width hash via different UFs
+    if make1.__code__ == make2.__code__ and False:
+        pass
+    c, conj = _kbasic(make1, make2)
+    try:
+        w = run(conj, c)
+    except Exception as e:  # width-mismatched '=' of the two hashes is a Python error in z3 too
+        pytest.fail(f"engine raised {e!r}")
+    if not sat:
+        assert w is None
+    elif sat and conj:
+        # concrete/identical cases must be found; symbolic ones are found with the pools
+        assert w is not None
+
+
+def test_keccak_symbol_and_val_unsat():
+    # keccak_tests.py:41-56: keccak(100) == keccak(n) && n == 10 -> unsat
+    c = Ctx()
+    km = KeccakManager(c)
+    o1 = km.create_keccak(c.const(100, 256))
+    n = c.var("n", 256)
+    o2 = km.create_keccak(n)
+    conj = [km.create_conditions(), c.app("=", o1, o2), c.app("=", n, c.const(10, 256))]
+    assert run(conj, c) is None
+
+
+def test_keccak_simple_number_unsat():
+    # keccak_tests.py:110-124: keccak(a) == 10 -> unsat (10 is outside every interval, not aligned)
+    c = Ctx()
+    km = KeccakManager(c)
+    o = km.create_keccak(c.var("a", 160))
+    conj = [km.create_conditions(), c.app("=", c.const(10, 256), o)]
+    assert run(conj, c) is None
+
+
+def test_keccak_complex_eq_unsat():
+    # keccak_tests.py:59-81: keccak(2*keccak(a)) == keccak(2*keccak(b)) && a != b -> unsat
+    c = Ctx()
+    km = KeccakManager(c)
+    a, b = c.var("a", 160), c.var("b", 160)
+    o1 = km.create_keccak(c.app("bvmul", c.const(2, 256), km.create_keccak(a)))
+    o2 = km.create_keccak(c.app("bvmul", c.const(2, 256), km.create_keccak(b)))
+    conj = [km.create_conditions(), c.app("=", o1, o2), c.app("not", c.app("=", a, b))]
+    assert run(conj, c) is None
+
+
+def test_keccak_other_num_sat_witness_is_sound():
+    # keccak_tests.py:127-145: keccak(2*keccak(a)) == b -> sat
+    c = Ctx()
+    km = KeccakManager(c)
+    a, b = c.var("a", 160), c.var("b", 256)
+    o = km.create_keccak(c.app("bvmul", c.const(2, 256), km.create_keccak(a)))
+    conj = [km.create_conditions(), c.app("=", b, o)]
+    w = run(conj, c, budget=1 << 15)
+    assert w is not None
+
+
+# ---- calldata expectations (tests/laser/state/calldata_test.py) --------------------
+def test_symbolic_calldata_constrain_index_unsat():
+    # calldata_test.py:62-74: calldata[51] == 1 && calldatasize == 50 -> unsat
+    c = Ctx()
+    v = calldata_load(c, "0", c.const(51, 256))
+    conj = [c.app("=", v, c.const(1, 8)), c.app("=", c.var("0_calldatasize", 256), c.const(50, 256))]
+    assert run(conj, c) is None
+
+
+def test_symbolic_calldata_equal_indices_unsat():
+    # calldata_test.py:77-91: index_a == index_b && calldata[a] != calldata[b] -> unsat
+    c = Ctx()
+    ia, ib = c.var("index_a", 256), c.var("index_b", 256)
+    a, b = calldata_load(c, "0", ia), calldata_load(c, "0", ib)
+    conj = [c.app("=", ia, ib), c.app("not", c.app("=", a, b))]
+    assert run(conj, c) is None
+
+
+def test_function_selector_dispatch_sat():
+    # the shape of every dispatcher JUMPI: extract(255,224, calldataload(0)) == selector
+    c = Ctx()
+    word = calldata_word(c, "1", 0)
+    sel = c.app("extract", word, params=(255, 224))
+    conj = [c.app("=", sel, c.const(0xA9059CBB, 32)),
+            c.app("bvule", c.const(4, 256), c.var("1_calldatasize", 256)),
+            c.app("bvult", c.var("1_calldatasize", 256), c.const(1 << 16, 256))]
+    w = run(conj, c, budget=1 << 16)
+    assert w is not None
+    cells = w.arrays["1_calldata"]
+    assert [cells[i] for i in range(4)] == [0xA9, 0x05, 0x9C, 0xBB]
+
+
+def test_batched_search_equals_individual():
+    c = Ctx()
+    x = c.var("x", 256)
+    qs = [prepare([c.app("bvult", x, c.const(1 << k, 256)), c.app("bvugt", x, c.const(3, 256))], c)
+          for k in (4, 8, 200)]
+    e = engine(1 << 12)
+    batched = e.search(qs)
+    single = [e.search([q])[0] for q in qs]
+    assert [w and w.index for w in batched] == [w and w.index for w in single]
+    assert all(w is not None for w in batched)
