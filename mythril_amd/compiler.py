@@ -92,6 +92,7 @@ class LeafSpec:
     shift: int = 0
     bits: int = 0
     hashed: bool = False         # pool digit from a hash of the index instead of a bit-field
+    stride: int = 0              # >0: bit-interleaved digit (index bits shift, shift+stride, ...)
     salt: Optional[int] = None   # Philox key salt; default crc32(name) so a variable
                                  # draws the same value in every program for an index
 
@@ -629,14 +630,17 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
     if len(consts) > 0x7FFF:
         raise Unsupported("constant pool overflow")
 
-    # leaf table + pools
+    # leaf table + pools.  Default layout: bit-interleaved (Morton) digits over the
+    # first INDEX_FIELD_BITS index bits, so every pool varies at small indices and
+    # the best proposals of all leaves are tried together first; leaves that do
+    # not fit are sampled with hashed digits.
     specs: List[LeafSpec] = []
     leaf_words: List[int] = []
     pool_words: List[int] = []
     in_row = 0
-    bit = 0
     user = dict(leaf_specs or {})
-    for li, n in enumerate(lw.leaf_nodes):
+    resolved: List[LeafSpec] = []
+    for n in lw.leaf_nodes:
         w = _w(n)
         spec = user.get(n.name)
         if spec is None and pools and n.name in pools:
@@ -644,27 +648,51 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
         if spec is None:
             spec = LeafSpec(n.name, w)
         spec.width = w
-        kind, pshift, pbits, poff = 0, 0, 0, 0
         if spec.pool:
             p = list(spec.pool)
             nb = max(0, math.ceil(math.log2(len(p)))) if len(p) > 1 else 0
             p += [None] * ((1 << nb) - len(p))
             spec.pool = p
-            if not spec.hashed and spec.bits == 0 and spec.shift == 0:
-                if bit + nb > INDEX_FIELD_BITS:
-                    spec.hashed = True  # index bits exhausted: sample this pool instead
+        resolved.append(spec)
+    fresh = [s for s in resolved if s.pool and len(s.pool) > 1 and not s.hashed and s.bits == 0
+             and s.shift == 0 and s.stride == 0]
+    if fresh:
+        stride = len(fresh)
+        for j, spec in enumerate(fresh):
+            nb = int(math.log2(len(spec.pool)))
+            top = j + (nb - 1) * stride
+            if top < INDEX_FIELD_BITS:
+                spec.bits, spec.shift, spec.stride = nb, j, stride
+            else:
+                fit = max(0, (INDEX_FIELD_BITS - 1 - j) // stride + 1)
+                if fit >= 2:  # interleave the first 2^fit entries, hash nothing
+                    spec.bits, spec.shift, spec.stride = fit, j, stride
+                    spec.pool = spec.pool[:1 << fit]
                 else:
-                    spec.bits, spec.shift = nb, bit
-                    bit += nb
+                    spec.hashed = True
+    bit = 0
+    for li, (n, spec) in enumerate(zip(lw.leaf_nodes, resolved)):
+        w = spec.width
+        kind, pshift, pbits, poff, pstride = 0, 0, 0, 0, 0
+        if spec.pool:
+            nb = int(math.log2(len(spec.pool))) if len(spec.pool) > 1 else 0
             if spec.hashed:
-                spec.bits, spec.shift = nb, 0
-            kind, pshift, pbits, poff = (2 if spec.hashed else 1), spec.shift, spec.bits, len(pool_words)
-            for e in p:
+                spec.bits, spec.shift, spec.stride = nb, 0, 0
+                kind = 2
+            elif spec.stride:
+                kind = 3
+            else:
+                kind = 1
+                if spec.bits == 0 and spec.shift == 0:
+                    spec.bits = nb
+            pshift, pbits, poff, pstride = spec.shift, spec.bits, len(pool_words), spec.stride
+            bit = max(bit, spec.shift + (spec.bits - 1) * max(spec.stride, 1) + 1 if spec.bits else 0)
+            for e in spec.pool:
                 if e is None:
                     pool_words.extend([1] + [0] * 8)
                 else:
                     pool_words.extend([0] + _limbs(e & ((1 << w) - 1)))
-        leaf_words.extend([w, kind, spec.key_salt(), pshift, pbits, poff, in_row, 0])
+        leaf_words.extend([w, kind, spec.key_salt(), pshift, pbits, poff, in_row, pstride])
         in_row += (w + 31) // 32
         specs.append(spec)
     if bit > 63:

@@ -28,12 +28,14 @@
 
 // leaf table entry (MW_LEAF_WORDS u32 per leaf)
 #define MW_LEAF_WIDTH 0
-#define MW_LEAF_KIND 1   // 0 = random (Philox), 1 = pool (index bit-field), 2 = pool (hashed digit)
+#define MW_LEAF_KIND 1   // 0 random (Philox), 1 pool (index bit-field), 2 pool (hashed digit),
+                         // 3 pool (bit-interleaved digit: bits SHIFT, SHIFT+STRIDE, ...)
 #define MW_LEAF_ID 2     // Philox key salt
 #define MW_LEAF_SHIFT 3  // candidate-index bit offset of the pool digit
 #define MW_LEAF_BITS 4   // log2(pool entries)
 #define MW_LEAF_POOL 5   // word offset of entry 0 in the pool buffer
 #define MW_LEAF_INROW 6  // first SoA input row (mg_eval)
+#define MW_LEAF_STRIDE 7 // kind 3: index-bit stride between consecutive digit bits
 // pool entry: word 0 = flags (bit0: RANDOM), words 1..8 = limbs
 
 enum mw_opcode {

@@ -8,6 +8,9 @@
 //                blk 0 -> limbs 0..3, blk 1 -> limbs 4..7, masked to width
 //   pool leaf:   digit = (c >> shift) & (2^bits - 1); entry = pool[digit];
 //                entry flag RANDOM -> random value above, else the constant.
+//   interleaved: digit bit b = index bit (shift + b*stride)  (Morton order: indices
+//                below 2^(n*k) cover every combination of the first 2^k entries
+//                of n pools, so the strongest proposals are tried together first)
 //   hashed pool: digit = fmix64(c ^ (salt * 0x9E3779B97F4A7C15)) & (2^bits - 1)
 //                (MurmurHash3 finalizer), then as a pool leaf: samples large
 //                pools when the index bits cannot enumerate every leaf.
@@ -70,11 +73,18 @@ MW_HD void leaf_value(const u32* __restrict__ leaf_, const u32* __restrict__ poo
   const u32 w = leaf[MW_LEAF_WIDTH];
   const u32 id = leaf[MW_LEAF_ID];
   const u32 kind = leaf[MW_LEAF_KIND];
-  if (kind == 1u || kind == 2u) {
+  if (kind >= 1u && kind <= 3u) {
     const u32 bits = leaf[MW_LEAF_BITS];
-    const u64 src = kind == 1u ? (cand >> leaf[MW_LEAF_SHIFT])
-                               : fmix64(cand ^ ((u64)id * 0x9E3779B97F4A7C15ull));
-    const u32 digit = (u32)src & ((bits >= 32) ? 0xffffffffu : ((1u << bits) - 1u));
+    u32 digit;
+    if (kind == 3u) {
+      const u32 sh = leaf[MW_LEAF_SHIFT], st = leaf[MW_LEAF_STRIDE];
+      digit = 0;
+      for (u32 b = 0; b < bits; ++b) digit |= (u32)((cand >> (sh + b * st)) & 1u) << b;
+    } else {
+      const u64 src = kind == 1u ? (cand >> leaf[MW_LEAF_SHIFT])
+                                 : fmix64(cand ^ ((u64)id * 0x9E3779B97F4A7C15ull));
+      digit = (u32)src & ((bits >= 32) ? 0xffffffffu : ((1u << bits) - 1u));
+    }
     const u32* e = pool + leaf[MW_LEAF_POOL] + (u64)digit * MW_POOL_ENTRY_WORDS;
     if (e[0] & 1u) {
       random_leaf(id, w, seed, cand, out);

@@ -140,8 +140,11 @@ int mg_validate_desc(const mg_prog_desc* d) {
   for (size_t l = 0; l < d->nleaves; ++l) {
     const u32* L = d->leaves + l * MW_LEAF_WORDS;
     if (L[MW_LEAF_WIDTH] < 1 || L[MW_LEAF_WIDTH] > 256) return fail(MG_E_PROG, "bad leaf width");
-    if (L[MW_LEAF_KIND] == 1 || L[MW_LEAF_KIND] == 2) {
+    if (L[MW_LEAF_KIND] >= 1 && L[MW_LEAF_KIND] <= 3) {
       if (L[MW_LEAF_BITS] > 24 || L[MW_LEAF_SHIFT] > 63) return fail(MG_E_PROG, "bad pool digit field");
+      if (L[MW_LEAF_KIND] == 3 && L[MW_LEAF_BITS] &&
+          (u64)L[MW_LEAF_SHIFT] + (u64)(L[MW_LEAF_BITS] - 1) * L[MW_LEAF_STRIDE] > 63)
+        return fail(MG_E_PROG, "interleaved digit beyond the 64-bit index");
       u64 need = (u64)L[MW_LEAF_POOL] + ((u64)1 << L[MW_LEAF_BITS]) * MW_POOL_ENTRY_WORDS;
       if (need > d->npool_words) return fail(MG_E_PROG, "pool out of range");
     } else if (L[MW_LEAF_KIND] != 0) {

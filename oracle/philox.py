@@ -13,6 +13,7 @@ for candidate index ``c`` (u64), leaf ``j`` of width ``w``:
 * ``pool`` leaf with 2**b entries at bit-field ``s``: digit = (c >> s) & (2**b-1);
   entry = pool[digit]; an entry flagged RANDOM yields the random value above,
   otherwise its constant (masked to ``w``).
+* ``interleaved`` pool leaf (stride n): digit bit b = index bit (shift + b*n).
 * ``hashed`` pool leaf: digit = fmix64(c ^ (salt * 0x9E3779B97F4A7C15)) & (2**b-1).
 """
 from __future__ import annotations
@@ -65,9 +66,13 @@ def leaf_value(spec: dict, seed: int, c: int) -> int:
     if pool:
         if spec.get("hashed"):
             src = fmix64(c ^ ((spec["id"] * 0x9E3779B97F4A7C15) & ((1 << 64) - 1)))
+            d = src & ((1 << spec["bits"]) - 1)
+        elif spec.get("stride"):
+            d = 0
+            for b in range(spec["bits"]):
+                d |= ((c >> (spec["shift"] + b * spec["stride"])) & 1) << b
         else:
-            src = c >> spec["shift"]
-        d = src & ((1 << spec["bits"]) - 1)
+            d = (c >> spec["shift"]) & ((1 << spec["bits"]) - 1)
         e = pool[d]
         if e is not None:
             return e & ((1 << w) - 1)

@@ -58,7 +58,7 @@ def oracle_models(p: Program, seed: int, begin: int, n: int) -> List[Dict[str, i
         m = {}
         for li, (node, spec) in enumerate(zip(p.leaf_nodes, p.leaf_specs)):
             sd = {"id": spec.key_salt(), "width": spec.width, "shift": spec.shift, "bits": spec.bits, "pool": spec.pool,
-                  "hashed": spec.hashed}
+                  "hashed": spec.hashed, "stride": spec.stride}
             m[node.name] = leaf_value(sd, seed, begin + j)
         out.append(m)
     return out

@@ -1,0 +1,89 @@
+"""SMT-LIB2 front end (the --solver-log format, mythril/support/model.py:45-56)."""
+import pytest
+
+from mythril_amd.compiler import Unsupported
+from mythril_amd.engine import prepare
+from mythril_amd.smt2 import parse_script
+from oracle.dag_eval import ArrayVal, eval_nodes
+from tests.test_engine_cpu import engine, holds
+
+DUMP = r"""
+; z3 Optimize.sexpr() as written by --solver-log
+(declare-fun |1_calldata| () (Array (_ BitVec 256) (_ BitVec 8)))
+(declare-fun |1_calldatasize| () (_ BitVec 256))
+(declare-fun sender_1 () (_ BitVec 256))
+(declare-fun call_value1 () (_ BitVec 256))
+(declare-fun keccak256_512 ((_ BitVec 512)) (_ BitVec 256))
+(declare-fun |keccak256_512-1| ((_ BitVec 256)) (_ BitVec 512))
+(assert (let ((a!1 (concat (select |1_calldata| #x0000000000000000000000000000000000000000000000000000000000000000)
+                           (select |1_calldata| (_ bv1 256))
+                           (select |1_calldata| (_ bv2 256))
+                           (select |1_calldata| (_ bv3 256)))))
+  (= a!1 #xa9059cbb)))
+(assert (bvule (_ bv4 256) |1_calldatasize|))
+(assert (or (= sender_1 #x000000000000000000000000affeaffeaffeaffeaffeaffeaffeaffeaffeaffe)
+            (= sender_1 #x000000000000000000000000deadbeefdeadbeefdeadbeefdeadbeefdeadbeef)
+            (= sender_1 #x000000000000000000000000aaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaa)))
+(assert (not (bvumul_noovfl call_value1 (_ bv2 256))))
+(assert (let ((a!1 (keccak256_512 (concat sender_1 #x0000000000000000000000000000000000000000000000000000000000000000))))
+  (and (= (|keccak256_512-1| a!1) (concat sender_1 #x0000000000000000000000000000000000000000000000000000000000000000))
+       (= ((_ extract 5 0) a!1) #b000000))))
+(minimize |1_calldatasize|)
+(minimize call_value1)
+(check-sat)
+"""
+
+
+def test_parse_dump_structure():
+    s = parse_script(DUMP)
+    assert len(s.asserts) == 5 and len(s.minimize) == 2
+    assert s.decls["1_calldata"].sort.kind == "array" and s.decls["1_calldata"].sort.dom == 256
+    assert s.decls["keccak256_512"].args[0].width == 512
+
+
+def test_parsed_terms_evaluate_like_hand_built():
+    s = parse_script(DUMP)
+    cd = ArrayVal({0: 0xA9, 1: 0x05, 2: 0x9C, 3: 0xBB})
+    m = {"1_calldata": cd, "1_calldatasize": 4, "sender_1": 0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF,
+         "call_value1": 1 << 255,
+         "keccak256_512": ({((0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF << 256),): 64 * 12345}, 0),
+         "keccak256_512-1": ({(64 * 12345,): 0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF << 256}, 0)}
+    vals = eval_nodes(s.asserts, m)
+    assert all(vals[a.id] for a in s.asserts)
+    m["call_value1"] = 5  # 5*2 does not overflow -> the Not(noovfl) conjunct fails
+    vals = eval_nodes(s.asserts, m)
+    assert [vals[a.id] for a in s.asserts] == [1, 1, 1, 0, 1]
+
+
+def test_engine_solves_parsed_dump():
+    s = parse_script(DUMP)
+    q = prepare(s.asserts, s.ctx)
+    (w,) = engine(1 << 16).search([q])
+    assert w is not None and holds(s.asserts, w)
+    assert w.values["sender_1"] in (0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE,
+                                    0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF,
+                                    0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA)
+
+
+@pytest.mark.parametrize("text", [
+    "(declare-fun x () Int)(assert (> x 0))",                       # outside QF_ABV
+    "(declare-fun x () (_ BitVec 8))(assert (bvfoo x x))",          # unknown op
+    "(declare-fun x () (_ BitVec 8))(assert (= x #x01)",            # unbalanced
+    "(assert (forall ((x (_ BitVec 8))) (= x x)))",                 # quantifier
+])
+def test_fail_closed(text):
+    with pytest.raises(Unsupported):
+        parse_script(text)
+
+
+def test_numerals_and_indexed_ops():
+    s = parse_script("""
+(declare-fun x () (_ BitVec 16))
+(assert (= ((_ zero_extend 16) x) (_ bv258 32)))
+(assert (= ((_ sign_extend 8) ((_ extract 15 8) x)) #x0001))
+(assert (= ((_ rotate_left 4) x) #x1020))
+(assert (= ((_ repeat 2) ((_ extract 7 0) x)) #x0202))
+(assert (= (bvredor x) #b1))
+""")
+    vals = eval_nodes(s.asserts, {"x": 0x0102})
+    assert all(vals[a.id] for a in s.asserts)
