@@ -1,0 +1,210 @@
+"""The drop-in get_model (mythril_amd/model.py) against a stand-in Mythril.
+
+Neither mythril nor z3 is installable here, so the Mythril
+modules get_model touches are replaced by minimal stand-ins with the
+reference's semantics (mythril/support/model.py:15-63: timeout clamp,
+UnsatError, Python-bool handling, lru_cache of returned models) and the z3
+bridge by an IR pass-through whose "z3 re-check" is the oracle.  What is
+tested is the drop-in's control flow: GPU answer vs fallback, caching,
+error behaviour, rebinding of all three import sites, batched prefetch.
+"""
+import sys
+import types
+from functools import lru_cache
+
+import pytest
+
+from mythril_amd import model as dropin
+from mythril_amd import z3bridge
+from mythril_amd.compiler import Unsupported
+from mythril_amd.engine import WitnessEngine
+from mythril_amd.ir import Ctx
+from mythril_amd.smt2 import Script
+from oracle.dag_eval import ArrayVal, eval_nodes
+from tests.fakedev import FakeDevice
+
+
+class UnsatError(Exception):
+    pass
+
+
+class FakeRaw:
+    def __init__(self, node):
+        self.node = node
+
+    def get_id(self):
+        return self.node.id
+
+
+class FakeBool:
+    def __init__(self, node):
+        self.raw = FakeRaw(node)
+
+    def __hash__(self):
+        return self.raw.node.id
+
+    def __eq__(self, other):
+        return isinstance(other, FakeBool) and other.raw.node.id == self.raw.node.id
+
+
+class Model:
+    def __init__(self, raw):
+        self.raw = raw
+
+
+@pytest.fixture
+def mythril(monkeypatch):
+    calls = {"reference": 0}
+    args = types.SimpleNamespace(solver_timeout=10000, solver_log=None)
+    th = types.SimpleNamespace(remaining=100000)
+    th.time_remaining = lambda: th.remaining
+
+    @lru_cache(maxsize=2 ** 23)
+    def reference_get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True):
+        calls["reference"] += 1
+        timeout = args.solver_timeout
+        if enforce_execution_time:
+            timeout = min(timeout, th.time_remaining() - 500)
+            if timeout <= 0:
+                raise UnsatError
+        for c in constraints:
+            if type(c) == bool and not c:
+                raise UnsatError
+        cl = [c for c in constraints if type(c) != bool]
+        # stand-in "z3": brute force over the small domains used below
+        for v in range(256):
+            m = {"x": v, "y": v}
+            vals = eval_nodes([c.raw.node for c in cl], m)
+            if all(vals[c.raw.node.id] for c in cl):
+                return Model(["ref", m])
+        raise UnsatError
+
+    mods = {
+        "mythril": types.ModuleType("mythril"),
+        "mythril.exceptions": types.SimpleNamespace(UnsatError=UnsatError),
+        "mythril.support": types.ModuleType("mythril.support"),
+        "mythril.support.support_args": types.SimpleNamespace(args=args),
+        "mythril.support.model": types.SimpleNamespace(get_model=reference_get_model),
+        "mythril.laser": types.ModuleType("mythril.laser"),
+        "mythril.laser.ethereum": types.ModuleType("mythril.laser.ethereum"),
+        "mythril.laser.ethereum.time_handler": types.SimpleNamespace(time_handler=th),
+        "mythril.laser.ethereum.state": types.ModuleType("mythril.laser.ethereum.state"),
+        "mythril.laser.ethereum.state.constraints": types.SimpleNamespace(get_model=reference_get_model),
+        "mythril.analysis": types.ModuleType("mythril.analysis"),
+        "mythril.analysis.solver": types.SimpleNamespace(get_model=reference_get_model),
+        "mythril.laser.smt": types.ModuleType("mythril.laser.smt"),
+        "mythril.laser.smt.model": types.SimpleNamespace(Model=Model),
+    }
+    for k, v in mods.items():
+        monkeypatch.setitem(sys.modules, k, v)
+    mods["mythril"].support = mods["mythril.support"]
+    mods["mythril"].analysis = mods["mythril.analysis"]
+    mods["mythril"].laser = mods["mythril.laser"]
+    mods["mythril.support"].model = mods["mythril.support.model"]
+    mods["mythril.analysis"].solver = mods["mythril.analysis.solver"]
+    mods["mythril.laser"].ethereum = mods["mythril.laser.ethereum"]
+    mods["mythril.laser.ethereum"].state = mods["mythril.laser.ethereum.state"]
+    mods["mythril.laser.ethereum.state"].constraints = mods["mythril.laser.ethereum.state.constraints"]
+
+    def to_ir(raws, ctx=None):
+        s = Script(ctx or CTX)
+        s.asserts = [r.node for r in raws]
+        return s
+
+    def confirm(raws, script, w, timeout_ms=2000):
+        model = dict(w.values)
+        for n, cells in w.arrays.items():
+            model[n] = ArrayVal(cells)
+        vals = eval_nodes([r.node for r in raws], model)
+        return ("z3", model) if all(vals[r.node.id] for r in raws) else None
+
+    monkeypatch.setattr(z3bridge, "to_ir", to_ir)
+    monkeypatch.setattr(z3bridge, "model_from_witness", confirm)
+    monkeypatch.setattr(dropin, "_engine", WitnessEngine(dev=FakeDevice(chunk=1024), budget=1 << 12))
+    monkeypatch.setattr(dropin, "_engine_failed", False)
+    monkeypatch.setattr(dropin, "_reference", None)
+    dropin._memo.clear()
+    dropin.get_model.cache_clear()
+    assert dropin.install()
+    yield types.SimpleNamespace(calls=calls, args=args, th=th, mods=mods)
+    dropin.get_model.cache_clear()
+
+
+CTX = Ctx()
+X = CTX.var("x", 8)
+
+
+def fb(node):
+    return FakeBool(node)
+
+
+SAT = (fb(CTX.app("bvugt", X, CTX.const(200, 8))), fb(CTX.app("bvult", X, CTX.const(203, 8))))
+UNSAT = (fb(CTX.app("bvugt", X, CTX.const(200, 8))), fb(CTX.app("bvult", X, CTX.const(150, 8))))
+
+
+def test_install_rebinds_all_three_call_sites(mythril):
+    m = mythril.mods
+    assert m["mythril.support.model"].get_model is dropin.get_model
+    assert m["mythril.analysis.solver"].get_model is dropin.get_model
+    assert m["mythril.laser.ethereum.state.constraints"].get_model is dropin.get_model
+
+
+def test_feasible_query_answered_by_gpu_and_confirmed(mythril):
+    res = dropin.get_model(SAT)
+    assert res.raw[0][0] == "z3" and 200 < res.raw[0][1]["x"] < 203
+    assert mythril.calls["reference"] == 0
+    assert dropin.STATS["z3_confirmed"] >= 1
+
+
+def test_unsat_falls_back_to_reference_and_raises(mythril):
+    with pytest.raises(UnsatError):
+        dropin.get_model(UNSAT)
+    assert mythril.calls["reference"] == 1
+
+
+def test_minimize_always_goes_to_reference(mythril):
+    res = dropin.get_model(SAT, minimize=(fb(X),))
+    assert res.raw[0] == "ref"
+
+
+def test_python_false_and_exhausted_budget_raise_unsat(mythril):
+    with pytest.raises(UnsatError):
+        dropin.get_model(SAT + (False,))
+    mythril.th.remaining = 400
+    with pytest.raises(UnsatError):
+        dropin.get_model((fb(CTX.app("bvugt", X, CTX.const(10, 8))),))
+
+
+def test_returned_models_are_cached_unsat_is_not(mythril):
+    a = dropin.get_model(SAT)
+    n = dropin._engine.stats["searches"]
+    assert dropin.get_model(SAT) is a
+    assert dropin._engine.stats["searches"] == n
+    for _ in range(2):
+        with pytest.raises(UnsatError):
+            dropin.get_model(UNSAT)
+    assert mythril.calls["reference"] == 2  # UnsatError is not cached (reference behaviour)
+
+
+def test_engine_unavailable_or_unsupported_uses_reference(mythril, monkeypatch):
+    monkeypatch.setattr(dropin, "_engine", None)
+    monkeypatch.setattr(dropin, "_engine_failed", True)
+    assert dropin.get_model(SAT).raw[0] == "ref"
+    dropin.get_model.cache_clear()
+    monkeypatch.setattr(dropin, "_engine_failed", False)
+    monkeypatch.setattr(dropin, "_engine", WitnessEngine(dev=FakeDevice(), budget=1 << 10))
+
+    def boom(raws, ctx=None):
+        raise Unsupported("z3 op outside the vocabulary")
+    monkeypatch.setattr(z3bridge, "to_ir", boom)
+    assert dropin.get_model(SAT).raw[0] == "ref"
+
+
+def test_prefetch_batches_and_feeds_the_memo(mythril):
+    sets = [SAT, (fb(CTX.app("=", X, CTX.const(77, 8))),), UNSAT]
+    found = dropin.prefetch(sets)
+    assert found == 2
+    searches = dropin._engine.stats["searches"]
+    assert dropin.get_model(sets[1]).raw[0][1]["x"] == 77
+    assert dropin._engine.stats["searches"] == searches  # answered from the memo
+    assert dropin.STATS["memo_hits"] >= 1
