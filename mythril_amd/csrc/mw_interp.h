@@ -75,8 +75,13 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
   // flight while the current one executes (the words after END are always
   // readable: the constant pool follows the code in the program buffer).
   u32 w0 = code[0], w1 = code[1], w2 = code[2], w3 = code[3];
+  bool stop = false;
+  // ONE loop exit (END or a uniform early stop): a return inside the switch
+  // would make LLVM's CFG structurizer thread flag variables and exec-mask
+  // arithmetic through every iteration.
   for (u32 pc = 4;; pc += 4) {
     const u32 op = w0 & 0xffu;
+    if (op == MW_END || stop) break;
     const u32 w = w0 >> 16;
     const u32 dst = w1 & 0xffffu, oa = w1 >> 16, ob = w2 & 0xffffu, oc = w2 >> 16;
     const u32 imm = w3;
@@ -88,13 +93,12 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
     u32 x[8], y[8], r[8];
     u32 wk = 0;  // 1: write W[dst] = r, 2: write N[dst] = r[0]
     switch (op) {
-      case MW_END:
-        return alive;
       case MW_CHECK: {
         u32 v;
         MW_FETCH_N(oa, v);
         alive = alive && (v != 0);
-        if ((flags & MW_FLAG_EARLY_EXIT) && env.none(alive)) return false;
+        // wave-uniform: stop at the next loop top (keeps one loop exit)
+        if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
         break;
       }
       case MW_LEAF_W:
@@ -388,7 +392,7 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
             break;
           }
           default:
-            return false;  // unknown opcode: verdict false (validated on load)
+            break;  // unreachable: opcodes are validated on load
         }
         r[0] = v;
         wk = 2;
@@ -408,6 +412,7 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
     w2 = n2;
     w3 = n3;
   }
+  return alive && !stop;
 }
 
 }  // namespace mw
