@@ -116,6 +116,7 @@ class Program:
     n_insn: int
     n_conjuncts: int
     stats: Dict[str, int] = field(default_factory=dict)
+    ssa: List[MInsn] = field(default_factory=list)   # machine IR before slot allocation (jit.py)
 
     def input_rows_for(self, leaf_index: int) -> Tuple[int, int]:
         off = int(self.leaves[leaf_index * isa.LEAF_WORDS + isa.LEAF_INROW])
@@ -174,6 +175,8 @@ class _Lowerer:
     def __init__(self):
         self.insns: List[MInsn] = []
         self.memo: Dict[int, object] = {}
+        self.memo_scope: Dict[int, int] = {}   # node id -> conjunct in which it was computed
+        self.scope = 0
         self.nv = 0
         self.leaf_index: Dict[str, int] = {}
         self.leaf_nodes: List[Node] = []
@@ -209,21 +212,40 @@ class _Lowerer:
             return self.emit("W_ZEXTN", max(width, 33), [v])
         raise Unsupported("narrowing class change")
 
+    # Cheap terms over leaves/constants (e.g. ``bvor(x, 1)``, ``extract(x)``) are
+    # hash-consed across conjuncts; keeping one computed copy live from its first
+    # to its last conjunct costs 8 registers for the whole span.  Such terms are
+    # recomputed once per conjunct instead (REMAT_MAX_COST u32 ops at most).
+    REMAT_MAX_COST = 16
+
+    def _fresh(self, m: Node) -> bool:
+        if m.id not in self.memo:
+            return False
+        if self.memo_scope.get(m.id, self.scope) == self.scope:
+            return True
+        if m.op in ("var", "const") or not m.args or node_cost(m) > self.REMAT_MAX_COST:
+            return True
+        if not all(a.op in ("var", "const") for a in m.args):
+            return True
+        del self.memo[m.id]  # recompute in this conjunct
+        return False
+
     def lower(self, n: Node):
-        if n.id in self.memo:
+        if self._fresh(n):
             return self.memo[n.id]
         # operand-first (post-order) without recursion: DAGs can be thousands deep
         stack = [(n, False)]
         while stack:
             m, expanded = stack.pop()
-            if m.id in self.memo:
-                continue
             if expanded:
-                self._lower_one(m)
+                if m.id not in self.memo:
+                    self._lower_one(m)
+                continue
+            if self._fresh(m):
                 continue
             stack.append((m, True))
             for a in reversed(m.args):
-                if a.id not in self.memo:
+                if not self._fresh(a):
                     stack.append((a, False))
         return self.memo[n.id]
 
@@ -232,6 +254,7 @@ class _Lowerer:
             return self.memo[n.id]
         v = self._lower(n)
         self.memo[n.id] = v
+        self.memo_scope[n.id] = self.scope
         if n.id in self.trace_req and n.id not in self.trace_emitted:
             self.trace_emitted[n.id] = v
             cls = v.cls
@@ -469,6 +492,44 @@ def _flatten(conjuncts: Iterable[Node]) -> List[Node]:
     return out
 
 
+# --------------------------------------------------------------------------- scheduling
+def _schedule_narrow_early(insns: List[MInsn]) -> List[MInsn]:
+    """Move every instruction with a narrow (N) result right after the last
+    definition of its operands.
+
+    The operand-first order evaluates a conjunct's comparisons only when the
+    conjunct's ``and`` tree is reached, so the wide values they read stay live
+    across the rest of the chain (in C5, most of the spill traffic).  A
+    narrow result costs one register, so evaluating it as soon as its operands
+    exist never raises the wide live set and usually ends a wide operand's
+    life.  Leaves (no operands) stay at their first use; CHECK/STORE/END keep
+    their place, so the conjunct order (and early exit) is unchanged.
+    """
+    anchor: Dict[int, int] = {}           # vreg id -> index of the insn after which it is defined
+    after: Dict[int, List[MInsn]] = {}    # original index -> hoisted insns emitted right after it
+    head: List[MInsn] = []
+    keep: List[bool] = []
+    for i, ins in enumerate(insns):
+        srcs = [s for s in ins.srcs if isinstance(s, VReg)]
+        movable = (ins.dst is not None and ins.dst.cls == "N" and srcs
+                   and not ins.op.startswith(("LEAF", "FILL", "MOV")))
+        if movable:
+            a = max(anchor[s.id] for s in srcs)
+            after.setdefault(a, []).append(ins)
+            anchor[ins.dst.id] = a
+            keep.append(False)
+        else:
+            if ins.dst is not None:
+                anchor[ins.dst.id] = i
+            keep.append(True)
+    out: List[MInsn] = list(head)
+    for i, ins in enumerate(insns):
+        if keep[i]:
+            out.append(ins)
+        out.extend(after.get(i, ()))
+    return out
+
+
 # --------------------------------------------------------------------------- register allocation
 def _allocate(insns: List[MInsn]):
     """Belady allocation of W/N vregs to MW_NW/MW_NN slots; returns (insns, n_spill)."""
@@ -581,6 +642,7 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
         lw.trace_req[t.id] = t
     checks = 0
     for c in conj:
+        lw.scope += 1
         if c.op == "const" and not c.val:
             lw.emit_void("CHECK", 1, [Const(0, "N")])
             checks += 1
@@ -592,6 +654,7 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
         lw.lower(t)
     lw.emit_void("END", 0, [])
 
+    lw.insns = _schedule_narrow_early(lw.insns)
     insns, n_spill = _allocate(lw.insns)
 
     # constant pool
@@ -707,4 +770,4 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
                    leaves=np.asarray(leaf_words, dtype=np.uint32), pool=arr(pool_words),
                    n_spill=n_spill, n_trace_rows=rows, n_input_rows=in_row, ops_per_eval=ops,
                    leaf_specs=specs, leaf_nodes=list(lw.leaf_nodes), trace_map=trace_map,
-                   n_insn=len(code) // 4, n_conjuncts=checks, stats=stats)
+                   n_insn=len(code) // 4, n_conjuncts=checks, stats=stats, ssa=list(lw.insns))

@@ -1,0 +1,244 @@
+// mw_jit.h — support header for specialised (per-program) search kernels.
+//
+// mythril_amd/jit.py emits one straight-line function per program from the
+// compiler's SSA machine IR (mythril_amd/compiler.py, before slot
+// allocation): every value is a register array, every constant a literal and
+// every leaf descriptor folded into the call.  There is no dispatch, no
+// register-file indexing and no spill area: LLVM schedules and allocates the
+// whole program for gfx950.
+//
+// Each helper below has exactly the semantics of the matching interpreter case
+// in mw_interp.h (same ALU, same canonicalisation), and the candidate
+// generator is the interpreter's (mw_leaf.h), so a specialised kernel returns
+// the interpreter's verdict for every candidate index.  tests/test_jit.py
+// checks both against the oracle on the CPU (a host build of the generated
+// source) and tests/test_gpu_jit.py on gfx950.
+#pragma once
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MW_LEAF_KEY_FENCE(k) asm volatile("" : "+s"(k))
+#endif
+#include "mw_alu.h"
+#include "mw_isa.h"
+#include "mw_leaf.h"
+
+namespace mw {
+namespace jit {
+
+// ------------------------------------------------------------------ wide
+MW_HD void w_add(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { add8(x, y, r); canon(r, w); }
+MW_HD void w_sub(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { sub8(x, y, r); canon(r, w); }
+MW_HD void w_mul(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { mul8(x, y, r); canon(r, w); }
+MW_HD void w_and(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = x[k] & y[k];
+  canon(r, w);
+}
+MW_HD void w_or(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = x[k] | y[k];
+  canon(r, w);
+}
+MW_HD void w_xor(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = x[k] ^ y[k];
+  canon(r, w);
+}
+MW_HD void w_not(const u32 x[8], u32 w, u32 r[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = ~x[k];
+  canon(r, w);
+}
+MW_HD void w_shl(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { wshl(x, y, w, r); canon(r, w); }
+MW_HD void w_lshr(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { wlshr(x, y, w, r); canon(r, w); }
+MW_HD void w_ashr(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { washr(x, y, w, r); canon(r, w); }
+// kind: 0 udiv, 1 urem, 2 sdiv, 3 srem, 4 smod (wdiv consumes its operands)
+MW_HD void w_div(int kind, const u32 x[8], const u32 y[8], u32 w, u32 r[8]) {
+  u32 a[8], b[8];
+  copy8(a, x);
+  copy8(b, y);
+  wdiv(kind, a, b, w, r);
+  canon(r, w);
+}
+MW_HD void w_ite(u32 c, const u32 x[8], const u32 y[8], u32 w, u32 r[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = c ? x[k] : y[k];
+  canon(r, w);
+}
+MW_HD void w_shli(const u32 x[8], u32 imm, u32 w, u32 r[8]) { shl8(x, imm, r); canon(r, w); }
+MW_HD void w_lshri(const u32 x[8], u32 imm, u32 w, u32 r[8]) { shr8(x, imm, 0u, r); canon(r, w); }
+MW_HD void w_zextn(u32 v, u32 w, u32 r[8]) {
+  zero8(r);
+  r[0] = v;
+  canon(r, w);
+}
+MW_HD void w_sext(const u32 x[8], u32 imm, u32 w, u32 r[8]) {
+  copy8(r, x);
+  sext8(r, imm);
+  canon(r, w);
+}
+MW_HD void w_sextn(u32 v, u32 imm, u32 w, u32 r[8]) {
+  zero8(r);
+  r[0] = v;
+  sext8(r, imm);
+  canon(r, w);
+}
+MW_HD void w_insn(const u32 x[8], u32 v, u32 imm, u32 w, u32 r[8]) {
+  u32 y[8];
+  zero8(y);
+  y[0] = v;
+  shl8(y, imm, r);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] |= x[k];
+  canon(r, w);
+}
+MW_HD void w_mov(const u32 x[8], u32 w, u32 r[8]) {
+  copy8(r, x);
+  canon(r, w);
+}
+
+// ------------------------------------------------------------------ wide -> narrow
+MW_HD u32 n_extractw(const u32 x[8], u32 imm, u32 w) {
+  u32 r[8];
+  shr8(x, imm, 0u, r);
+  return r[0] & nmask(w);
+}
+MW_HD u32 n_ult(const u32 x[8], const u32 y[8]) { return ult8(x, y) ? 1u : 0u; }
+MW_HD u32 n_ule(const u32 x[8], const u32 y[8]) { return ult8(y, x) ? 0u : 1u; }
+// signed compare at width w: flip the sign bit (bit w-1) of both, compare unsigned
+MW_HD u32 n_scmp(const u32 x_[8], const u32 y_[8], u32 w, bool le) {
+  u32 x[8], y[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int bit = (int)w - 1 - 32 * k;
+    const u32 m = (bit >= 0 && bit < 32) ? (1u << bit) : 0u;
+    x[k] = x_[k] ^ m;
+    y[k] = y_[k] ^ m;
+  }
+  return (le ? !ult8(y, x) : ult8(x, y)) ? 1u : 0u;
+}
+MW_HD u32 n_eq(const u32 x[8], const u32 y[8]) { return eq8(x, y) ? 1u : 0u; }
+MW_HD u32 n_umulno(const u32 x[8], const u32 y[8], u32 w) {
+  u32 lo[8], hi[8];
+  mulhi8(x, y, lo, hi);
+  u32 ov = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ov |= (lo[k] & ~limb_mask(w, k)) | hi[k];
+  return ov ? 0u : 1u;
+}
+MW_HD u32 n_addc(const u32 x[8], const u32 y[8], u32 w) {
+  u32 r[8];
+  const u32 c = add8(x, y, r);
+  u32 bit = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int b = (int)w - 32 * k;
+    bit |= (b >= 0 && b < 32) ? ((r[k] >> b) & 1u) : 0u;
+  }
+  return (w >= 256) ? c : bit;
+}
+
+// ------------------------------------------------------------------ narrow (<= 32 bit)
+MW_HD u32 nn_add(u32 a, u32 b, u32 w) { return (a + b) & nmask(w); }
+MW_HD u32 nn_sub(u32 a, u32 b, u32 w) { return (a - b) & nmask(w); }
+MW_HD u32 nn_mul(u32 a, u32 b, u32 w) { return (a * b) & nmask(w); }
+MW_HD u32 nn_not(u32 a, u32 w) { return (~a) & nmask(w); }
+MW_HD u32 nn_shli(u32 a, u32 imm, u32 w) { return (imm >= 32 ? 0u : (a << imm)) & nmask(w); }
+MW_HD u32 nn_lshri(u32 a, u32 imm, u32 w) { return (imm >= 32 ? 0u : (a >> imm)) & nmask(w); }
+MW_HD u32 nn_sext(u32 a, u32 imm, u32 w) { return n_sext(a, imm) & nmask(w); }
+MW_HD u32 nn_addc(u32 a, u32 b, u32 w) { return (u32)((((u64)a + b) >> w) & 1u); }
+
+// ------------------------------------------------------------------ control
+// wave-wide "no lane alive" (per candidate in the host build)
+MW_HD bool none(bool alive) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ballot(alive) == 0ull;
+#else
+  return !alive;
+#endif
+}
+
+// trace rows (host build only; device bodies are instantiated with trace == nullptr)
+MW_HD void tstore(u32* trace, u64 stride, u64 idx, u32 row, const u32* v, int n) {
+  if (trace)
+    for (int k = 0; k < n; ++k) trace[((u64)row + k) * stride + idx] = v[k];
+}
+
+// Basic-block boundary for straight-line bodies (jit.py SPLIT_EVERY): a branch
+// on a control bit the host never sets (ctl is the launch's flags word), around
+// a side effect the compiler must keep.  Costs one scalar test and branch; stops
+// LLVM from scheduling the whole program as one region.
+#define MW_JIT_NEVER 0x80000000u
+#if defined(__HIP_DEVICE_COMPILE__)
+#define JIT_SPLIT()                                        \
+  do {                                                     \
+    if (__builtin_expect((ctl & MW_JIT_NEVER) != 0u, 0))   \
+      asm volatile("s_nop 0");                             \
+  } while (0)
+#else
+#define JIT_SPLIT() ((void)ctl)
+#endif
+
+typedef bool (*body_fn)(const u32* __restrict__, u64, u64, bool, u32, u32*, u64, u64);
+
+#if !defined(MW_JIT_HOST)
+// One 256-candidate chunk per block (chunk = chunk0 + blockIdx.x), with the
+// interpreter's result protocol (mw_search_kernel): per-wave ballot -> lowest
+// satisfying lane -> atomicMin on the program's witness index; optional
+// per-candidate verdicts (mg_eval_generated).  No grid-stride loop on purpose:
+// inside a loop LLVM hoists every leaf's Philox key schedule (uniform, loop
+// invariant) into SGPRs and spills hundreds of them into VGPR lanes.
+template <body_fn BODY>
+__device__ __attribute__((always_inline)) inline void search(const u32* __restrict__ pool, u64 seed, u64 begin,
+                                                             u64 count, u64 chunk0, u32 flags,
+                                                             u64* __restrict__ out_min, u64* __restrict__ counter,
+                                                             u32* __restrict__ verdict) {
+  const u64 base = begin + (chunk0 + blockIdx.x) * 256;
+  if (flags & MW_FLAG_STOP_AFTER_HIT) {
+    const u64 m = __hip_atomic_load(out_min, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (m <= base) return;
+  }
+  const u32 lane = threadIdx.x & 63u;
+  const u64 cand = base + threadIdx.x;
+  const bool valid = cand < begin + count;
+  const bool ok = BODY(pool, seed, cand, valid, flags, nullptr, 0, 0);
+  if (verdict && valid) verdict[cand - begin] = ok ? 1u : 0u;
+  const u64 hit = __ballot(ok);
+  if (hit) {
+    const u32 first = (u32)__ffsll((unsigned long long)hit) - 1u;
+    if (lane == first) atomicMin((unsigned long long*)out_min, (unsigned long long)cand);
+  }
+  const u64 evals = (u64)__popcll(__ballot(valid));
+  if (lane == 0 && evals) atomicAdd((unsigned long long*)counter, (unsigned long long)evals);
+}
+
+// <name>_x: exhaustive; <name>_e: per-wave early exit after a failing CHECK.
+// <name>_sig: FNV-1a 64 of the program words, checked by mg_prog_attach_kernel.
+#define MW_JIT_KERNEL(NAME, SUFFIX, BODY, EARLY)                                                     \
+  extern "C" __global__ __launch_bounds__(256, 2) void NAME##SUFFIX(                                 \
+      const mw::u32* __restrict__ pool, mw::u64 seed, mw::u64 begin, mw::u64 count, mw::u64 chunk0,  \
+      mw::u32 flags, mw::u64* __restrict__ out_min, mw::u64* __restrict__ counter,                   \
+      mw::u32* __restrict__ verdict) {                                                               \
+    mw::jit::search<BODY<EARLY>>(pool, seed, begin, count, chunk0, flags, out_min, counter, verdict); \
+  }
+#define MW_JIT_SIG(NAME, SIG) extern "C" __device__ const mw::u64 NAME##_sig = SIG;
+#else
+#define MW_JIT_KERNEL(NAME, SUFFIX, BODY, EARLY)
+#define MW_JIT_SIG(NAME, SIG)
+#endif
+
+// host build (tests only): verdicts (+ trace rows) of candidates [begin, begin+count)
+#if defined(MW_JIT_HOST)
+#define MW_JIT_HOST_ENTRY(NAME, BODY)                                                                \
+  extern "C" int NAME##_host(const mw::u32* pool, mw::u64 seed, mw::u64 begin, mw::u64 count,        \
+                             mw::u32 early, mw::u32* verdict, mw::u32* trace) {                      \
+    for (mw::u64 i = 0; i < count; ++i)                                                              \
+      verdict[i] = (early ? BODY<true>(pool, seed, begin + i, true, 0u, trace, count, i)                 \
+                          : BODY<false>(pool, seed, begin + i, true, 0u, trace, count, i)) ? 1u : 0u;    \
+    return 0;                                                                                        \
+  }
+#else
+#define MW_JIT_HOST_ENTRY(NAME, BODY)
+#endif
+
+}  // namespace jit
+}  // namespace mw

@@ -19,6 +19,13 @@
 #include "mw_alu.h"
 #include "mw_isa.h"
 
+// Hook for specialised kernels (mw_jit.h): pins a leaf's Philox key where the
+// leaf is generated, so LLVM cannot hoist every leaf's key schedule to the
+// top of a straight-line kernel and spill it.  No-op for the interpreter.
+#ifndef MW_LEAF_KEY_FENCE
+#define MW_LEAF_KEY_FENCE(k) ((void)0)
+#endif
+
 namespace mw {
 
 MW_HD void philox4x32_10(u32 c[4], u32 k0, u32 k1) {
@@ -40,6 +47,8 @@ MW_HD void philox4x32_10(u32 c[4], u32 k0, u32 k1) {
 
 MW_HD void random_leaf(u32 id, u32 w, u64 seed, u64 cand, u32 out[8]) {
   u32 k0 = (u32)seed ^ id, k1 = (u32)(seed >> 32);
+  MW_LEAF_KEY_FENCE(k0);
+  MW_LEAF_KEY_FENCE(k1);
   u32 c[4] = {(u32)cand, (u32)(cand >> 32), 0u, 0u};
   philox4x32_10(c, k0, k1);
   out[0] = c[0]; out[1] = c[1]; out[2] = c[2]; out[3] = c[3];
@@ -60,6 +69,33 @@ MW_HD u64 fmix64(u64 h) {
   h *= 0xc4ceb9fe1a85ec53ull;
   h ^= h >> 33;
   return h;
+}
+
+// Candidate value of one leaf from its descriptor fields (the interpreter
+// reads them from the leaf table below; specialised kernels, mw_jit.h, pass
+// them as literals).
+MW_HD void leaf_fields(u32 w, u32 kind, u32 id, u32 shift, u32 bits, u32 poff, u32 stride,
+                       const u32* __restrict__ pool, u64 seed, u64 cand, u32 out[8]) {
+  if (kind >= 1u && kind <= 3u) {
+    u32 digit;
+    if (kind == 3u) {
+      digit = 0;
+      for (u32 b = 0; b < bits; ++b) digit |= (u32)((cand >> (shift + b * stride)) & 1u) << b;
+    } else {
+      const u64 src = kind == 1u ? (cand >> shift) : fmix64(cand ^ ((u64)id * 0x9E3779B97F4A7C15ull));
+      digit = (u32)src & ((bits >= 32) ? 0xffffffffu : ((1u << bits) - 1u));
+    }
+    const u32* e = pool + poff + (u64)digit * MW_POOL_ENTRY_WORDS;
+    if (e[0] & 1u) {
+      random_leaf(id, w, seed, cand, out);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) out[k] = e[1 + k];
+      canon(out, w);
+    }
+  } else {
+    random_leaf(id, w, seed, cand, out);
+  }
 }
 
 // leaf: MW_LEAF_WORDS words (uniform); pool: per-lane gather

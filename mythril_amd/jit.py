@@ -1,0 +1,298 @@
+"""Specialised search kernels: one straight-line gfx950 kernel per program.
+
+The interpreter (``csrc/mw_interp.h``) runs any program, but for every
+bytecode instruction it pays a scalar dispatch and indexed register-file
+moves (``s_set_gpr_idx``) around a handful of VALU ops.  On the C5 workload
+that overhead is about two thirds of the kernel time (performance
+log).  For long searches the program is instead emitted as HIP source: one
+straight-line function over the compiler's SSA machine IR (``Program.ssa``),
+every value a register array, every constant a literal, every leaf
+descriptor folded into the generator call.  hipcc compiles it for gfx950 into
+a code object, and ``mg_prog_attach_kernel`` binds it to the loaded program;
+``mg_search`` / ``mg_eval_generated`` then launch it instead of the
+interpreter.  The op helpers (``csrc/mw_jit.h``) have the interpreter's exact
+semantics over the same ALU and candidate generator, so verdicts and witness
+indices are identical (tests/test_jit.py on the CPU, tests/test_gpu_jit.py on
+the device).
+
+The code object carries the program's signature (FNV-1a 64 over its code,
+constant, leaf and pool words); the library refuses to attach it to any
+other program.  Compiles are cached on disk by source hash (``MW_JIT_CACHE``,
+default ``build/jit``).
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import subprocess
+import tempfile
+import time
+from pathlib import Path
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import isa
+from .compiler import Const, Program, VReg
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "mythril_amd" / "csrc"
+ARCH = os.environ.get("MW_OFFLOAD_ARCH", "gfx950")
+HEADERS = ["mw_jit.h", "mw_alu.h", "mw_isa.h", "mw_leaf.h"]
+M256 = (1 << 256) - 1
+# A straight-line body is cut into basic blocks at every CHECK and at least every
+# SPLIT_EVERY instructions (JIT_SPLIT, mw_jit.h).  In one giant block LLVM's
+# scheduler interleaves far-apart computations and spills heavily (C5-1k:
+# 1121 VGPR spills in one block, 25 with a block per conjunct).
+SPLIT_EVERY = 48
+M32 = 0xFFFFFFFF
+
+_WBIN = {"W_ADD": "w_add", "W_SUB": "w_sub", "W_MUL": "w_mul", "W_AND": "w_and", "W_OR": "w_or",
+         "W_XOR": "w_xor", "W_SHL": "w_shl", "W_LSHR": "w_lshr", "W_ASHR": "w_ashr"}
+_DIV = {"UDIV": 0, "UREM": 1, "SDIV": 2, "SREM": 3, "SMOD": 4}
+_NBIN = {"N_ADD": "jit::nn_add({a}, {b}, {w})", "N_SUB": "jit::nn_sub({a}, {b}, {w})",
+         "N_MUL": "jit::nn_mul({a}, {b}, {w})", "N_AND": "({a} & {b})", "N_OR": "({a} | {b})",
+         "N_XOR": "({a} ^ {b})", "N_SHL": "n_shl({a}, {b}, {w})", "N_LSHR": "n_lshr({a}, {b}, {w})",
+         "N_ASHR": "n_ashr({a}, {b}, {w})", "N_ULTN": "(u32)({a} < {b})", "N_ULEN": "(u32)({a} <= {b})",
+         "N_SLTN": "(u32)n_slt({a}, {b}, {w})", "N_SLEN": "(u32)n_sle({a}, {b}, {w})",
+         "N_EQN": "(u32)({a} == {b})", "N_UMULNON": "(u32)n_umulno({a}, {b}, {w})",
+         "N_ADDCN": "jit::nn_addc({a}, {b}, {w})"}
+
+
+def _cache_dir() -> Path:
+    return Path(os.environ.get("MW_JIT_CACHE", str(ROOT / "build" / "jit")))
+
+
+def signature(p: Program) -> int:
+    """FNV-1a 64 over the program's words, as mg_prog_load computes it."""
+    h = 0xCBF29CE484222325
+    for arr in (p.code, p.consts, p.leaves, p.pool):
+        a = np.ascontiguousarray(arr, dtype=np.uint32)
+        h = _fnv_words(h, a)
+    return h
+
+
+def _fnv_words(h: int, a: np.ndarray) -> int:
+    # FNV-1a over the little-endian bytes of each word; vectorised per byte lane
+    b = a.astype("<u4").view(np.uint8)
+    P = 0x100000001B3
+    M = (1 << 64) - 1
+    for x in b.tobytes():
+        h = ((h ^ x) * P) & M
+    return h
+
+
+class _Gen:
+    """Emit the body of one program as straight-line HIP."""
+
+    def __init__(self, p: Program, name: str):
+        self.p = p
+        self.name = name
+        self.wconst: Dict[int, str] = {}
+        self.lines: List[str] = []
+        self.since_split = 0
+
+    def W(self, s) -> str:
+        if isinstance(s, Const):
+            v = s.value & M256
+            n = self.wconst.get(v)
+            if n is None:
+                n = f"k{len(self.wconst)}"
+                self.wconst[v] = n
+            return n
+        if s.cls != "W":
+            raise ValueError("N register in a W operand")
+        return f"v{s.id}"
+
+    def N(self, s) -> str:
+        if isinstance(s, Const):
+            return f"{s.value & M32:#x}u"
+        if s.cls != "N":
+            raise ValueError("W register in an N operand")
+        return f"n{s.id}"
+
+    def leaf(self, li: int, dst: str):
+        L = [int(x) for x in self.p.leaves[li * isa.LEAF_WORDS:(li + 1) * isa.LEAF_WORDS]]
+        w, kind, lid, shift, bits, poff, _inrow, stride = L
+        return (f"leaf_fields({w}u, {kind}u, {lid:#x}u, {shift}u, {bits}u, {poff}u, {stride}u, "
+                f"pool, seed, cand, {dst});")
+
+    def emit(self, ins) -> None:
+        op, w, d, S, imm = ins.op, ins.width, ins.dst, ins.srcs, ins.imm
+        self.since_split += 1
+        if self.since_split > SPLIT_EVERY and op != "CHECK":
+            self.lines.append("JIT_SPLIT();")
+            self.since_split = 0
+        if op == "END":
+            return
+        shape = isa.SHAPES[op]
+        A = [self.W(s) if c == "W" else self.N(s) for s, c in zip(S, shape[1])]
+        out = self.lines.append
+        dn = None
+        if d is not None:
+            dn = f"v{d.id}" if d.cls == "W" else f"n{d.id}"
+        if op == "CHECK":
+            out(f"alive = alive && ({A[0]} != 0u); if (EARLY) {{ if (jit::none(alive)) break; }} else JIT_SPLIT();")
+            self.since_split = 0
+        elif op == "LEAF_W":
+            out(f"u32 {dn}[8]; {self.leaf(imm, dn)}")
+        elif op == "LEAF_N":
+            out(f"u32 {dn}; {{ u32 t_[8]; {self.leaf(imm, 't_')} {dn} = t_[0]; }}")
+        elif op in ("STORE_W", "STORE_N"):
+            row = self.p.trace_map[-imm - 1][0]
+            if op == "STORE_W":
+                out(f"jit::tstore(trace, tstride, tidx, {row}u, {A[0]}, 8);")
+            else:
+                out(f"{{ const u32 t_ = {A[0]}; jit::tstore(trace, tstride, tidx, {row}u, &t_, 1); }}")
+        elif op == "MOV_W":
+            out(f"u32 {dn}[8]; jit::w_mov({A[0]}, {w}u, {dn});")
+        elif op == "MOV_N":
+            out(f"const u32 {dn} = {A[0]};")
+        elif op in _WBIN:
+            out(f"u32 {dn}[8]; jit::{_WBIN[op]}({A[0]}, {A[1]}, {w}u, {dn});")
+        elif op.startswith("W_") and op[2:] in _DIV:
+            out(f"u32 {dn}[8]; jit::w_div({_DIV[op[2:]]}, {A[0]}, {A[1]}, {w}u, {dn});")
+        elif op == "W_NOT":
+            out(f"u32 {dn}[8]; jit::w_not({A[0]}, {w}u, {dn});")
+        elif op == "W_ITE":
+            out(f"u32 {dn}[8]; jit::w_ite({A[2]}, {A[0]}, {A[1]}, {w}u, {dn});")
+        elif op == "W_SHLI":
+            out(f"u32 {dn}[8]; jit::w_shli({A[0]}, {imm}u, {w}u, {dn});")
+        elif op == "W_LSHRI":
+            out(f"u32 {dn}[8]; jit::w_lshri({A[0]}, {imm}u, {w}u, {dn});")
+        elif op == "W_ZEXTN":
+            out(f"u32 {dn}[8]; jit::w_zextn({A[0]}, {w}u, {dn});")
+        elif op == "W_SEXT":
+            out(f"u32 {dn}[8]; jit::w_sext({A[0]}, {imm}u, {w}u, {dn});")
+        elif op == "W_SEXTN":
+            out(f"u32 {dn}[8]; jit::w_sextn({A[0]}, {imm}u, {w}u, {dn});")
+        elif op == "W_INSN":
+            out(f"u32 {dn}[8]; jit::w_insn({A[0]}, {A[1]}, {imm}u, {w}u, {dn});")
+        elif op == "N_EXTRACTW":
+            out(f"const u32 {dn} = jit::n_extractw({A[0]}, {imm}u, {w}u);")
+        elif op == "N_ULT":
+            out(f"const u32 {dn} = jit::n_ult({A[0]}, {A[1]});")
+        elif op == "N_ULE":
+            out(f"const u32 {dn} = jit::n_ule({A[0]}, {A[1]});")
+        elif op in ("N_SLT", "N_SLE"):
+            le = "true" if op == "N_SLE" else "false"
+            out(f"const u32 {dn} = jit::n_scmp({A[0]}, {A[1]}, {w}u, {le});")
+        elif op == "N_EQ":
+            out(f"const u32 {dn} = jit::n_eq({A[0]}, {A[1]});")
+        elif op == "N_UMULNO":
+            out(f"const u32 {dn} = jit::n_umulno({A[0]}, {A[1]}, {w}u);")
+        elif op == "N_ADDC":
+            out(f"const u32 {dn} = jit::n_addc({A[0]}, {A[1]}, {w}u);")
+        elif op in _NBIN:
+            out(f"const u32 {dn} = " + _NBIN[op].format(a=A[0], b=A[1], w=f"{w}u") + ";")
+        elif op.startswith("N_") and op[2:] in _DIV:
+            out(f"const u32 {dn} = n_div({_DIV[op[2:]]}, {A[0]}, {A[1]}, {w}u);")
+        elif op == "N_NOT":
+            out(f"const u32 {dn} = jit::nn_not({A[0]}, {w}u);")
+        elif op == "N_ITE":
+            out(f"const u32 {dn} = {A[2]} ? {A[0]} : {A[1]};")
+        elif op == "N_SHLI":
+            out(f"const u32 {dn} = jit::nn_shli({A[0]}, {imm}u, {w}u);")
+        elif op == "N_LSHRI":
+            out(f"const u32 {dn} = jit::nn_lshri({A[0]}, {imm}u, {w}u);")
+        elif op == "N_SEXT":
+            out(f"const u32 {dn} = jit::nn_sext({A[0]}, {imm}u, {w}u);")
+        else:
+            raise ValueError(f"jit: no emitter for {op}")
+
+    def body(self) -> str:
+        for ins in self.p.ssa:
+            self.emit(ins)
+        head = [f"template <bool EARLY>",
+                f"MW_HD bool {self.name}_body(const u32* __restrict__ pool, u64 seed, u64 cand, bool alive,",
+                f"                             u32 ctl, u32* __restrict__ trace, u64 tstride, u64 tidx) {{"]
+        consts = []
+        for v, n in self.wconst.items():
+            limbs = ", ".join(f"{(v >> (32 * k)) & M32:#x}u" for k in range(8))
+            consts.append(f"  const u32 {n}[8] = {{{limbs}}};")
+        return "\n".join(head + consts + ["  do {"] + ["    " + x for x in self.lines] +
+                         ["  } while (0);", "  return alive;", "}"])
+
+
+def generate(progs: Sequence[Program], names: Sequence[str], variants: str = "xe") -> str:
+    """HIP source for a module holding one specialised kernel set per program."""
+    parts = ["// generated by mythril_amd/jit.py: specialised witness-search kernels",
+             '#include "mw_jit.h"', "using namespace mw;", ""]
+    for p, name in zip(progs, names):
+        if not p.ssa:
+            raise ValueError("program has no SSA machine IR (compiled by an older compiler?)")
+        parts.append(f"// program {name}: {p.n_insn} bytecode insns, {p.ops_per_eval} u32 ops/eval")
+        parts.append(_Gen(p, name).body())
+        parts.append(f"MW_JIT_SIG({name}, {signature(p):#x}ull)")
+        if "x" in variants:
+            parts.append(f"MW_JIT_KERNEL({name}, _x, {name}_body, false)")
+        if "e" in variants:
+            parts.append(f"MW_JIT_KERNEL({name}, _e, {name}_body, true)")
+        parts.append(f"MW_JIT_HOST_ENTRY({name}, {name}_body)")
+        parts.append("")
+    return "\n".join(parts)
+
+
+def kernel_name(p: Program) -> str:
+    return f"mwj_{signature(p):016x}"
+
+
+def _hipcc() -> str:
+    return "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else "hipcc"
+
+
+def _key(src: str, flags: Sequence[str]) -> str:
+    h = hashlib.sha256(src.encode())
+    h.update(" ".join(flags).encode())
+    for hd in HEADERS:
+        h.update((CSRC / hd).read_bytes())
+    return h.hexdigest()[:24]
+
+
+DEVICE_FLAGS = ["--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-Wno-unused-variable"]
+HOST_FLAGS = ["-O1", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__", "-DMW_JIT_HOST",
+              "-Wno-unused-variable"]
+
+
+def _compile(src: str, flags: Sequence[str], suffix: str, ext: str) -> Tuple[Path, float]:
+    cache = _cache_dir()
+    cache.mkdir(parents=True, exist_ok=True)
+    out = cache / f"{_key(src, flags)}{suffix}"
+    if out.exists():
+        return out, 0.0
+    t0 = time.perf_counter()
+    with tempfile.TemporaryDirectory() as td:
+        f = Path(td) / f"k{ext}"
+        f.write_text(src)
+        tmp = Path(td) / ("out" + suffix)
+        r = subprocess.run([_hipcc(), *flags, f"-I{CSRC}", str(f), "-o", str(tmp)], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"jit compile failed:\n{r.stderr[-4000:]}")
+        os.replace(tmp, out)
+    return out, time.perf_counter() - t0
+
+
+def compile_device(progs: Sequence[Program], variants: str = "xe") -> Tuple[bytes, List[str], float]:
+    """gfx950 code object for `progs`; returns (image, kernel names, compile seconds; 0 if cached)."""
+    names = [kernel_name(p) for p in progs]
+    src = generate(progs, names, variants)
+    path, dt = _compile(src, DEVICE_FLAGS, ".hsaco", ".hip")
+    return path.read_bytes(), names, dt
+
+
+def compile_host(progs: Sequence[Program]) -> Tuple[Path, List[str]]:
+    """TEST ONLY: x86 build of the same generated source (verdicts + trace rows)."""
+    names = [kernel_name(p) for p in progs]
+    src = generate(progs, names, "")
+    path, _ = _compile(src, HOST_FLAGS, ".so", ".cpp")
+    return path, names
+
+
+def attach(dev, dps, variants: str = "xe") -> float:
+    """Compile and attach specialised kernels to loaded programs (DevicePrograms); returns
+    the compile seconds (0 when every code object came from the cache)."""
+    dps = list(dps)
+    image, names, dt = compile_device([dp.prog for dp in dps], variants)
+    for dp, name in zip(dps, names):
+        dev.attach_kernel(dp, image, name)
+    return dt
