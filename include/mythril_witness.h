@@ -94,6 +94,20 @@ int mg_eval(mg_ctx* ctx, const mg_prog* prog, const uint32_t* leaves_soa, size_t
 int mg_eval_generated(mg_ctx* ctx, const mg_prog* prog, uint64_t seed, uint64_t begin,
                       size_t count, uint32_t* verdict, uint32_t* trace);
 
+/* Attach a specialised kernel to a loaded program: `image` is a gfx950 code
+ * object generated from this program's own IR by mythril_amd/jit.py (one
+ * straight-line kernel per program, csrc/mw_jit.h).  It must export
+ * `<name>_sig` (the program signature, checked against the loaded program:
+ * a code object made for any other program is refused) and `<name>_x`
+ * (exhaustive), optionally `<name>_e` (early exit).  mg_search and
+ * mg_eval_generated (verdicts only) then launch it instead of the
+ * interpreter; witness indices and verdicts are identical.  Same crossing as
+ * mg_search (z3 Optimize.check, mythril/laser/smt/solver/solver.py:50-66). */
+int mg_prog_attach_kernel(mg_prog* prog, const void* image, size_t size, const char* name);
+
+/* 1 if a specialised kernel is attached to the program, else 0. */
+int mg_prog_has_kernel(const mg_prog* prog);
+
 /* Batched Keccak-256 (original 0x01 padding): message i is data[off[i] .. off[i]+len[i]). */
 int mg_keccak256(mg_ctx* ctx, const uint8_t* data, size_t ndata, const uint64_t* off,
                  const uint32_t* len, size_t n, uint8_t* out32, mg_stats* stats);

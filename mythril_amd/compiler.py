@@ -71,6 +71,7 @@ class MInsn:
     dst: Optional[VReg] = None
     srcs: List[object] = field(default_factory=list)
     imm: int = 0
+    remat: bool = False   # recomputation of a term from an earlier conjunct (jit.py fences its inputs)
 
 
 def cls_of(width: int) -> str:
@@ -252,7 +253,11 @@ class _Lowerer:
     def _lower_one(self, n: Node):
         if n.id in self.memo:
             return self.memo[n.id]
+        first = len(self.insns)
         v = self._lower(n)
+        if n.id in self.memo_scope:  # lowered before, in an earlier conjunct
+            for ins in self.insns[first:]:
+                ins.remat = True
         self.memo[n.id] = v
         self.memo_scope[n.id] = self.scope
         if n.id in self.trace_req and n.id not in self.trace_emitted:

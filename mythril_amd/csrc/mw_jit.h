@@ -157,6 +157,36 @@ MW_HD bool none(bool alive) {
 #endif
 }
 
+// Opaque copy of a value: a recomputed term (compiler.py remat) reads its
+// operands through it, so LLVM cannot CSE the recomputation with the copy of
+// an earlier conjunct and stretch that copy's live range back across both.
+MW_HD void fence8(const u32 x[8], u32 r[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    r[k] = x[k];
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(r[k]));
+#endif
+  }
+}
+MW_HD u32 fence1(u32 x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(x));
+#endif
+  return x;
+}
+
+// alive &= (v != 0), materialised at this point: without the fence LLVM sinks
+// every comparison of an exhaustive body to its single use (the final return),
+// keeping all compared wide values live to the end of the program.
+MW_HD bool check(bool alive, u32 v) {
+  u32 a = (alive && v != 0u) ? 1u : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(a));
+#endif
+  return a != 0u;
+}
+
 // trace rows (host build only; device bodies are instantiated with trace == nullptr)
 MW_HD void tstore(u32* trace, u64 stride, u64 idx, u32 row, const u32* v, int n) {
   if (trace)
@@ -165,12 +195,15 @@ MW_HD void tstore(u32* trace, u64 stride, u64 idx, u32 row, const u32* v, int n)
 
 // Basic-block boundary for straight-line bodies (jit.py SPLIT_EVERY): a branch
 // on a control bit the host never sets (ctl is the launch's flags word), around
-// a side effect the compiler must keep.  Costs one scalar test and branch; stops
-// LLVM from scheduling the whole program as one region.
+// a side effect the compiler must keep.  The empty asm re-defines ctl at every
+// boundary, so jump threading cannot prove the later tests false from the first
+// one and fold the blocks back together.  Costs one scalar test and branch;
+// stops LLVM from scheduling the whole program as one region.
 #define MW_JIT_NEVER 0x80000000u
 #if defined(__HIP_DEVICE_COMPILE__)
 #define JIT_SPLIT()                                        \
   do {                                                     \
+    asm volatile("" : "+s"(ctl));                          \
     if (__builtin_expect((ctl & MW_JIT_NEVER) != 0u, 0))   \
       asm volatile("s_nop 0");                             \
   } while (0)

@@ -266,9 +266,52 @@ struct mg_prog {
   ProgDev dev{};
   mg_prog_desc desc{};
   u64 ops_per_eval = 0;
+  u64 sig = 0;                  // FNV-1a 64 of the program words (mythril_amd/jit.py signature)
+  hipModule_t mod = nullptr;    // specialised kernels (mg_prog_attach_kernel), or none
+  hipFunction_t fx = nullptr;   // exhaustive
+  hipFunction_t fe = nullptr;   // early exit (optional)
 };
 
 namespace {
+
+u64 fnv1a(u64 h, const u32* w, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    for (int b = 0; b < 4; ++b) {
+      h ^= (w[i] >> (8 * b)) & 0xffu;
+      h *= 0x100000001b3ull;
+    }
+  return h;
+}
+
+u64 prog_signature(const mg_prog_desc* d) {
+  u64 h = 0xcbf29ce484222325ull;
+  h = fnv1a(h, d->code, d->ncode_words);
+  if (d->consts) h = fnv1a(h, d->consts, d->nconst_words);
+  if (d->leaves) h = fnv1a(h, d->leaves, d->nleaves * MW_LEAF_WORDS);
+  if (d->pool) h = fnv1a(h, d->pool, d->npool_words);
+  return h;
+}
+
+// Launch a program's specialised kernel over [begin, begin+count): one block
+// per 256-candidate chunk (mw_jit.h), split into launches of <= 2^30 blocks.
+int launch_jit(mg_ctx* c, const mg_prog* p, u64 seed, u64 begin, u64 count, u32 flags, u64* d_min,
+               u32* d_verdict) {
+  hipFunction_t f = ((flags & MW_FLAG_EARLY_EXIT) && p->fe) ? p->fe : p->fx;
+  const u64 nchunks = (count + kBlock - 1) / kBlock;
+  const u64 kMaxBlocks = 1ull << 30;
+  for (u64 chunk0 = 0; chunk0 < nchunks; chunk0 += kMaxBlocks) {
+    const u32 nb = (u32)std::min<u64>(kMaxBlocks, nchunks - chunk0);
+    const u32* pool = p->dev.pool;
+    u64 sd = seed, bg = begin, ct = count, c0 = chunk0;
+    u32 fl = flags;
+    u64* mn = d_min;
+    u64* ctr = c->d_counter;
+    u32* vd = d_verdict;
+    void* args[] = {&pool, &sd, &bg, &ct, &c0, &fl, &mn, &ctr, &vd};
+    HIPCHK(hipModuleLaunchKernel(f, nb, 1, 1, kBlock, 1, 1, 0, c->stream, args, nullptr));
+  }
+  return 0;
+}
 
 int ensure_spill(mg_ctx* c, size_t bytes) {
   if (bytes <= c->spill_bytes) return 0;
@@ -363,6 +406,7 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
   p->ctx = c;
   p->desc = *d;
   p->ops_per_eval = d->ops_per_eval;
+  p->sig = prog_signature(d);
   if (hipMalloc(&p->d_buf, total * sizeof(u32)) != hipSuccess) {
     delete p;
     return fail(MG_E_NOMEM, "program upload allocation failed");
@@ -394,10 +438,50 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
 int mg_prog_free(mg_prog* p) {
   if (!p) return 0;
   hipSetDevice(p->ctx->dev);
+  if (p->mod) hipModuleUnload(p->mod);
   if (p->d_buf) hipFree(p->d_buf);
   delete p;
   return 0;
 }
+
+int mg_prog_attach_kernel(mg_prog* p, const void* image, size_t size, const char* name) {
+  if (!p || !image || !size || !name) return fail(MG_E_ARG, "null argument");
+  if (std::strlen(name) > 200) return fail(MG_E_ARG, "kernel name too long");
+  mg_ctx* c = p->ctx;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  hipModule_t mod = nullptr;
+  HIPCHK(hipModuleLoadData(&mod, image));
+  const std::string base(name);
+  hipDeviceptr_t dsig = nullptr;
+  size_t nsig = 0;
+  u64 sig = 0;
+  hipFunction_t fx = nullptr, fe = nullptr;
+  if (hipModuleGetGlobal(&dsig, &nsig, mod, (base + "_sig").c_str()) != hipSuccess || nsig != sizeof(u64) ||
+      hipMemcpyDtoH(&sig, dsig, sizeof(u64)) != hipSuccess) {
+    hipModuleUnload(mod);
+    return fail(MG_E_PROG, "code object has no program signature " + base + "_sig");
+  }
+  if (sig != p->sig) {
+    hipModuleUnload(mod);
+    return fail(MG_E_PROG, "code object was generated for another program (signature mismatch)");
+  }
+  if (hipModuleGetFunction(&fx, mod, (base + "_x").c_str()) != hipSuccess) {
+    hipModuleUnload(mod);
+    return fail(MG_E_PROG, "code object lacks kernel " + base + "_x");
+  }
+  if (hipModuleGetFunction(&fe, mod, (base + "_e").c_str()) != hipSuccess) {
+    (void)hipGetLastError();
+    fe = nullptr;  // early exit is an optimisation only: the exhaustive kernel gives the same results
+  }
+  if (p->mod) hipModuleUnload(p->mod);
+  p->mod = mod;
+  p->fx = fx;
+  p->fe = fe;
+  return 0;
+}
+
+int mg_prog_has_kernel(const mg_prog* p) { return p && p->fx ? 1 : 0; }
 
 int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uint64_t begin,
               uint64_t count, uint32_t flags, uint64_t* out_min_idx, mg_stats* st) {
@@ -409,44 +493,65 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   HIPCHK(hipSetDevice(c->dev));
   int rc = ensure_min(c, nprog);
   if (rc) return rc;
-  std::vector<ProgDev> hp(nprog);
+  // Programs with a specialised kernel (mg_prog_attach_kernel) get one launch
+  // each; the rest share one interpreter launch (grid row per program).
+  // d_min holds the interpreted programs first, then the specialised ones.
+  std::vector<size_t> interp, special;
   u32 max_spill = 0;
   u64 ops = 0;
   for (size_t i = 0; i < nprog; ++i) {
     if (!progs[i] || progs[i]->ctx != c) return fail(MG_E_ARG, "program from another context");
-    hp[i] = progs[i]->dev;
-    max_spill = std::max(max_spill, progs[i]->dev.n_spill);
+    (progs[i]->fx ? special : interp).push_back(i);
     ops += progs[i]->ops_per_eval;
   }
+  std::vector<ProgDev> hp;
+  for (size_t i : interp) {
+    hp.push_back(progs[i]->dev);
+    max_spill = std::max(max_spill, progs[i]->dev.n_spill);
+  }
   const u64 nchunks = (count + kBlock - 1) / kBlock;
-  // enough blocks to fill the chip several times over, split across programs
-  u64 gx = std::max<u64>(1, (u64)c->ncu * 8 / nprog);
-  gx = std::min<u64>(gx, nchunks);
-  const u64 nthreads = gx * nprog * kBlock;
-  const u32 nlds = std::min(max_spill, kLdsSpillSlots);
-  const u32 nglob = max_spill - nlds;
-  rc = ensure_spill(c, std::max<size_t>(4, (size_t)nglob * 8 * nthreads * sizeof(u32)));
-  if (rc) return rc;
+  const size_t ni = interp.size();
+  u64 gx = 1;
+  u32 nlds = 0;
+  if (ni) {
+    // enough blocks to fill the chip several times over, split across programs
+    gx = std::max<u64>(1, (u64)c->ncu * 8 / ni);
+    gx = std::min<u64>(gx, nchunks);
+    const u64 nthreads = gx * ni * kBlock;
+    nlds = std::min(max_spill, kLdsSpillSlots);
+    const u32 nglob = max_spill - nlds;
+    rc = ensure_spill(c, std::max<size_t>(4, (size_t)nglob * 8 * nthreads * sizeof(u32)));
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(c->d_progs, hp.data(), ni * sizeof(ProgDev), hipMemcpyHostToDevice, c->stream));
+  }
   std::vector<u64> init(nprog, MG_NONE);
-  HIPCHK(hipMemcpyAsync(c->d_progs, hp.data(), nprog * sizeof(ProgDev), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->d_min, init.data(), nprog * sizeof(u64), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemsetAsync(c->d_counter, 0, sizeof(u64), c->stream));
   HIPCHK(hipEventRecord(c->e0, c->stream));
-  hipLaunchKernelGGL(mw_search_kernel, dim3((u32)gx, (u32)nprog), dim3(kBlock), (size_t)nlds * 8 * kBlock * 4,
-                     c->stream, c->d_progs, seed, begin, count, flags, c->d_min, c->d_counter, c->d_spill, nlds);
-  HIPCHK(hipGetLastError());
+  if (ni) {
+    hipLaunchKernelGGL(mw_search_kernel, dim3((u32)gx, (u32)ni), dim3(kBlock), (size_t)nlds * 8 * kBlock * 4,
+                       c->stream, c->d_progs, seed, begin, count, flags, c->d_min, c->d_counter, c->d_spill, nlds);
+    HIPCHK(hipGetLastError());
+  }
+  for (size_t j = 0; j < special.size(); ++j) {
+    rc = launch_jit(c, progs[special[j]], seed, begin, count, flags, c->d_min + ni + j, nullptr);
+    if (rc) return rc;
+  }
   HIPCHK(hipEventRecord(c->e1, c->stream));
   u64 evals = 0;
-  HIPCHK(hipMemcpyAsync(out_min_idx, c->d_min, nprog * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  std::vector<u64> mins(nprog);
+  HIPCHK(hipMemcpyAsync(mins.data(), c->d_min, nprog * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipMemcpyAsync(&evals, c->d_counter, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  for (size_t j = 0; j < ni; ++j) out_min_idx[interp[j]] = mins[j];
+  for (size_t j = 0; j < special.size(); ++j) out_min_idx[special[j]] = mins[ni + j];
   if (st) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
     st->kernel_ms = ms;
     st->wall_ms = now_ms() - t0;
     st->evals = evals;  // summed over every program's blocks
-    st->launches = 1;
+    st->launches = (ni ? 1 : 0) + special.size();
     st->ops = (double)evals / (double)nprog * (double)ops;
   }
   return 0;
@@ -500,7 +605,30 @@ int mg_eval(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncan
 
 int mg_eval_generated(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, size_t count,
                       uint32_t* verdict, uint32_t* trace) {
-  return eval_common(c, p, nullptr, count, seed, begin, verdict, trace);
+  if (!p || !p->fx || trace) return eval_common(c, p, nullptr, count, seed, begin, verdict, trace);
+  // verdicts only, on the program's specialised kernel
+  if (!c || !verdict || count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  int rc = ensure_min(c, 1);
+  if (rc) return rc;
+  u32* d_v = nullptr;
+  if (hipMalloc(&d_v, count * 4) != hipSuccess) return fail(MG_E_NOMEM, "eval verdict alloc");
+  const u64 none = MG_NONE;
+  hipError_t e = hipMemcpyAsync(c->d_min, &none, sizeof(u64), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, sizeof(u64), c->stream);
+  if (e == hipSuccess) {
+    rc = launch_jit(c, p, seed, begin, count, 0u, c->d_min, d_v);
+    if (rc) {
+      hipFree(d_v);
+      return rc;
+    }
+    e = hipMemcpyAsync(verdict, d_v, count * 4, hipMemcpyDeviceToHost, c->stream);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(d_v);
+  if (e != hipSuccess) return fail(MG_E_HIP, std::string("eval (specialised): ") + hipGetErrorString(e));
+  return 0;
 }
 
 int mg_valu_peak(mg_ctx* c, uint32_t mul, double* ops_per_s, double* kernel_ms) {

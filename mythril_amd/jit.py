@@ -25,6 +25,7 @@ from __future__ import annotations
 import hashlib
 import os
 import subprocess
+import sys
 import tempfile
 import time
 from pathlib import Path
@@ -33,7 +34,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import isa
-from .compiler import Const, Program, VReg
+from .compiler import Const, Program, VReg, compile_program
 
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "mythril_amd" / "csrc"
@@ -91,6 +92,7 @@ class _Gen:
         self.wconst: Dict[int, str] = {}
         self.lines: List[str] = []
         self.since_split = 0
+        self.nf = 0
 
     def W(self, s) -> str:
         if isinstance(s, Const):
@@ -128,11 +130,21 @@ class _Gen:
         shape = isa.SHAPES[op]
         A = [self.W(s) if c == "W" else self.N(s) for s, c in zip(S, shape[1])]
         out = self.lines.append
+        if getattr(ins, "remat", False):
+            for j, (s, c) in enumerate(zip(S, shape[1])):
+                if isinstance(s, VReg):
+                    self.nf += 1
+                    if c == "W":
+                        out(f"u32 f{self.nf}[8]; jit::fence8({A[j]}, f{self.nf});")
+                        A[j] = f"f{self.nf}"
+                    else:
+                        out(f"const u32 f{self.nf} = jit::fence1({A[j]});")
+                        A[j] = f"f{self.nf}"
         dn = None
         if d is not None:
             dn = f"v{d.id}" if d.cls == "W" else f"n{d.id}"
         if op == "CHECK":
-            out(f"alive = alive && ({A[0]} != 0u); if (EARLY) {{ if (jit::none(alive)) break; }} else JIT_SPLIT();")
+            out(f"alive = jit::check(alive, {A[0]}); if (EARLY) {{ if (jit::none(alive)) break; }} else JIT_SPLIT();")
             self.since_split = 0
         elif op == "LEAF_W":
             out(f"u32 {dn}[8]; {self.leaf(imm, dn)}")
@@ -265,9 +277,17 @@ def _compile(src: str, flags: Sequence[str], suffix: str, ext: str) -> Tuple[Pat
         f = Path(td) / f"k{ext}"
         f.write_text(src)
         tmp = Path(td) / ("out" + suffix)
-        r = subprocess.run([_hipcc(), *flags, f"-I{CSRC}", str(f), "-o", str(tmp)], capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"jit compile failed:\n{r.stderr[-4000:]}")
+        proc = subprocess.Popen([_hipcc(), *flags, f"-I{CSRC}", str(f), "-o", str(tmp)],
+                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        while True:  # large programs take minutes: keep a heartbeat on stderr
+            try:
+                _, err = proc.communicate(timeout=30)
+                break
+            except subprocess.TimeoutExpired:
+                print(f"[jit] compiling {len(src) // 1024} KiB of HIP for {ARCH}: "
+                      f"{time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+        if proc.returncode != 0:
+            raise RuntimeError(f"jit compile failed:\n{err[-4000:]}")
         os.replace(tmp, out)
     return out, time.perf_counter() - t0
 
@@ -296,3 +316,21 @@ def attach(dev, dps, variants: str = "xe") -> float:
     for dp, name in zip(dps, names):
         dev.attach_kernel(dp, image, name)
     return dt
+
+
+def warm_bench_cache(n_nodes: int = 10000, log=print) -> float:
+    """Pre-compile bench.py's C5 kernel into the in-tree cache (run by build()).
+
+    The C5 witness is planted with the host build of the interpreter
+    (mythril_amd/hostemu.py), which gives bit for bit the values bench.py gets
+    from the device interpreter, so the generated source — and the cache key —
+    are the ones the benchmark computes on the GPU box.
+    """
+    from . import hostemu
+    from .synth import build_c5
+    syn = build_c5(hostemu.term_values, n_nodes=n_nodes)
+    prog = compile_program(syn.conjuncts)
+    t0 = time.perf_counter()
+    _, names, dt = compile_device([prog], "x")
+    log(f"[jit] C5 kernel {names[0]}: {'compiled in %.0f s' % dt if dt else 'cached'}")
+    return time.perf_counter() - t0

@@ -59,6 +59,8 @@ SIGNATURES = {
     "mg_free": (ctypes.c_int, [_P]),
     "mg_prog_load": (ctypes.c_int, [_P, ctypes.POINTER(MgProgDesc), ctypes.POINTER(_P)]),
     "mg_prog_free": (ctypes.c_int, [_P]),
+    "mg_prog_attach_kernel": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
+    "mg_prog_has_kernel": (ctypes.c_int, [_P]),
     "mg_search": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                  ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
                                  ctypes.POINTER(MgStats)]),
@@ -123,6 +125,7 @@ class DeviceProgram:
         self.dev = dev
         self.handle = handle
         self.prog = prog
+        self.kernel: Optional[str] = None   # specialised kernel name, if attached
 
     def free(self):
         if self.handle:
@@ -160,6 +163,15 @@ class Device:
         h = _P()
         _check(self.lib, self.lib.mg_prog_load(self.handle, ctypes.byref(d), ctypes.byref(h)), "mg_prog_load")
         return DeviceProgram(self, h.value, p)
+
+    def attach_kernel(self, dp: DeviceProgram, image: bytes, name: str) -> None:
+        """Bind a specialised code object (mythril_amd.jit) to a loaded program."""
+        _check(self.lib, self.lib.mg_prog_attach_kernel(dp.handle, image, len(image), name.encode()),
+               "mg_prog_attach_kernel")
+        dp.kernel = name
+
+    def has_kernel(self, dp: DeviceProgram) -> bool:
+        return bool(self.lib.mg_prog_has_kernel(dp.handle))
 
     def search(self, progs: Sequence[DeviceProgram], seed: int, begin: int, count: int,
                flags: int = 0) -> Tuple[List[Optional[int]], dict]:

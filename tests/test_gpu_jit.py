@@ -1,0 +1,128 @@
+"""GPU parity of the specialised-kernel tier (mythril_amd/jit.py) through the C-ABI.
+
+A program with an attached specialised kernel must give exactly the
+interpreter's verdicts and witness indices (and the oracle's, spot-checked)
+on the same generated candidates, in exhaustive, early-exit and
+stop-after-hit modes, alone and batched with interpreted programs; a code
+object generated for another program is refused.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from mythril_amd import isa, jit
+from mythril_amd.compiler import compile_program
+from mythril_amd.ir import topo
+from oracle.dag_eval import eval_nodes
+from tests.helpers import oracle_models
+
+
+def small_planted(n_nodes=600, n_conj=8, density_log2=10, seed=0x5EED0005, witness_index=(1 << 17) + 77):
+    from mythril_amd.synth import build_c5
+
+    def ev(terms, index, sd):
+        p = compile_program([], trace=list(terms))
+        m = oracle_models(p, sd, index, 1)[0]
+        vals = eval_nodes(list(terms), m)
+        return [vals[t.id] for t in terms]
+    return build_c5(ev, n_nodes=n_nodes, n_leaves=16, n_conj=n_conj, seed=seed,
+                    witness_index=witness_index, density_log2=density_log2)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from mythril_amd.runtime import Device
+    d = Device(0)
+    yield d
+    d.close()
+
+
+@pytest.fixture(scope="module")
+def planted():
+    return [small_planted(n_nodes=300, n_conj=6, density_log2=8 + k, seed=0x5EED0005 + k) for k in range(3)]
+
+
+@pytest.fixture(scope="module")
+def random_progs():
+    from tests.test_jit import _random_programs
+    return _random_programs(8, 9100)
+
+
+@pytest.fixture(scope="module")
+def images(planted, random_progs):
+    progs = [compile_program(s.conjuncts) for s in planted] + [p for *_, p in random_progs]
+    image, names, _ = jit.compile_device(progs)  # one module, one hipcc run
+    return progs, image, names
+
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(dev, p, image, name):
+    a = dev.load(p)
+    b = dev.load(p)
+    dev.attach_kernel(b, image, name)
+    assert dev.has_kernel(b) and not dev.has_kernel(a)
+    return a, b
+
+
+def test_random_dag_verdicts_match_interpreter_and_oracle(dev, images, random_progs):
+    progs, image, names = images
+    k0 = len(progs) - len(random_progs)
+    seed, begin, n = 0x5EED0009, (1 << 36) + 5, 8192
+    for (dag, conj, extra, nodes, p), name in zip(random_progs, names[k0:]):
+        a, b = _pair(dev, p, image, name)
+        va, _ = dev.eval_generated(a, seed, begin, n, trace=False)
+        vb, _ = dev.eval_generated(b, seed, begin, n, trace=False)
+        assert np.array_equal(va, vb), name
+        rng = random.Random(1)
+        idx = rng.sample(range(n), 64)
+        models = oracle_models(p, seed, begin, n)
+        for j in idx:
+            vals = eval_nodes(conj, models[j])
+            assert int(vb[j]) == int(all(vals[c.id] for c in conj)), f"{name} cand {j}"
+        a.free()
+        b.free()
+
+
+def test_search_modes_match_interpreter(dev, images, planted):
+    progs, image, names = images
+    count = 1 << 18
+    for s, p, name in zip(planted, progs, names):
+        a, b = _pair(dev, p, image, name)
+        for flags in (0, isa.FLAG_EARLY_EXIT, isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT):
+            (fa,), sa = dev.search([a], s.seed, 0, count, flags)
+            (fb,), sb = dev.search([b], s.seed, 0, count, flags)
+            assert fa == fb, (name, flags)
+            if flags == 0:
+                assert sa["evals"] == sb["evals"] == count
+        assert fb is not None and fb <= s.witness_index
+        m = oracle_models(p, s.seed, fb, 1)[0]
+        vals = eval_nodes(s.conjuncts, m)
+        assert all(vals[c.id] for c in s.conjuncts)
+        a.free()
+        b.free()
+
+
+def test_mixed_batch(dev, images, planted):
+    progs, image, names = images
+    dps = []
+    for k, (p, name) in enumerate(zip(progs[:3], names[:3])):
+        dp = dev.load(p)
+        if k != 1:  # programs 0 and 2 specialised, 1 interpreted
+            dev.attach_kernel(dp, image, name)
+        dps.append(dp)
+    count = 1 << 17
+    got, st = dev.search(dps, 0x5EED0005, 0, count, 0)
+    singles = [dev.search([dev.load(p)], 0x5EED0005, 0, count, 0)[0][0] for p in progs[:3]]
+    assert got == singles
+    assert st["launches"] == 3 and st["evals"] == 3 * count
+
+
+def test_signature_mismatch_refused(dev, images):
+    progs, image, names = images
+    dp = dev.load(progs[0])
+    with pytest.raises(Exception):
+        dev.attach_kernel(dp, image, names[1])  # kernel of another program
+    assert not dev.has_kernel(dp)
