@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 NOMINAL_PEAK = 256 * 64 * 2.4e9  # SURVEY.md §8(d) derived INT32 VALU peak (u32 ops/s)
 BENCH_VARIANTS = "x"  # exhaustive kernel only: the bench never exits early
+BENCH_WAVES = 2
 
 
 def parse():
@@ -41,6 +42,8 @@ def parse():
     ap.add_argument("--engine", choices=["jit", "interp"], default="jit",
                     help="jit: the program's specialised straight-line kernel (mythril_amd/jit.py); "
                          "interp: the bytecode interpreter")
+    ap.add_argument("--jit-waves", type=int, default=BENCH_WAVES, choices=[1, 2],
+                    help="waves per SIMD the specialised kernel is built for")
     return ap.parse_args()
 
 
@@ -77,7 +80,7 @@ def main():
         # one-time program preparation, like the upload: outside the timed region
         # (the in-tree cache, warmed by __graft_entry__.build(), usually makes it 0)
         from mythril_amd import jit
-        jit_s = jit.attach(dev, [dp], variants=BENCH_VARIANTS)
+        jit_s = jit.attach(dev, [dp], variants=BENCH_VARIANTS, waves=args.jit_waves)
     batch = 1 << args.batch_log2
 
     def step(k):
@@ -154,7 +157,7 @@ def main():
             "ops_per_eval": prog.ops_per_eval,
             "program_insns": prog.n_insn,
             "spill_slots": prog.n_spill,
-            "engine": args.engine + (f" ({dp.kernel})" if dp.kernel else ""),
+            "engine": args.engine + (f" ({dp.kernel}, {args.jit_waves} wave/SIMD)" if dp.kernel else ""),
             "jit_compile_s": jit_s,
             "parallelism": f"candidate-shard x{world}",
             "witness_found_in_timed_range": found_any,

@@ -141,10 +141,18 @@ MW_HD void mulhi8(const u32 a[8], const u32 b[8], u32 lo[8], u32 hi[8]) {
 }
 
 // ---------------------------------------------------------------- shifts
-// funnel shifts on 32-bit limbs, b in [0,31]
-MW_HD u32 fshr32(u32 hi, u32 lo, u32 b) { return (u32)((((u64)hi << 32) | lo) >> b); }
-MW_HD u32 fshl32(u32 hi, u32 lo, u32 b) { return (u32)((((u64)hi << 32) | lo) >> (32 - b)) ; }
-// note fshl32 with b == 0 shifts the pair right by 32 and returns hi: correct.
+// funnel shifts on 32-bit limbs, b in [0,31]: one v_alignbit_b32 each (no
+// 64-bit register pairs).  fshl32 with b == 0 must return hi, which the
+// alignbit by (32 - b) & 31 == 0 would not: one select covers it.
+MW_HD u32 alignbit(u32 hi, u32 lo, u32 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(hi, lo, b);
+#else
+  return (u32)((((u64)hi << 32) | lo) >> (b & 31u));
+#endif
+}
+MW_HD u32 fshr32(u32 hi, u32 lo, u32 b) { return alignbit(hi, lo, b); }
+MW_HD u32 fshl32(u32 hi, u32 lo, u32 b) { return b ? alignbit(hi, lo, 32u - b) : hi; }
 
 // r = a << s for s in [0,255] (bits shifted past 256 dropped)
 MW_HD void shl8(const u32 a[8], u32 s, u32 r[8]) {
@@ -262,7 +270,8 @@ MW_HD u32 clz256(const u32 y[8]) {
   }
   return n;
 }
-// Moller-Granlund reciprocal of a normalized divisor d (top bit set)
+// Moller-Granlund reciprocal of a normalized divisor d (top bit set):
+// floor((2^64 - 1) / d) - 2^32
 MW_HD u32 recip32(u32 d) { return (u32)(~0ull / (u64)d - (1ull << 32)); }
 // (u1:u0) / d with u1 < d, d normalized, v = recip32(d)  (Moller & Granlund 2011, Alg. 4)
 MW_HD u32 div2by1(u32 u1, u32 u0, u32 d, u32 v) {
@@ -276,49 +285,97 @@ MW_HD u32 div2by1(u32 u1, u32 u0, u32 d, u32 v) {
   q1 = adj2 ? q1 + 1u : q1;
   return q1;
 }
+// reciprocal for 3-by-2 division by (d1:d0), d1 normalized (Moller & Granlund 2011, Alg. 6)
+MW_HD u32 recip3by2(u32 d1, u32 d0) {
+  u32 v = recip32(d1);
+  u32 p = d1 * v + d0;
+  if (p < d0) {
+    v -= 1u;
+    const bool m = p >= d1;
+    p -= d1;
+    v -= m ? 1u : 0u;
+    p -= m ? d1 : 0u;
+  }
+  const u64 t = (u64)v * d0;
+  const u32 t1 = (u32)(t >> 32), t0 = (u32)t;
+  p += t1;
+  if (p < t1) {
+    v -= 1u;
+    if (p > d1 || (p == d1 && t0 >= d0)) v -= 1u;
+  }
+  return v;
+}
+// (u2:u1:u0) / (d1:d0) for (u2:u1) < (d1:d0): quotient digit, remainder (r1:r0)
+// (Moller & Granlund 2011, Alg. 5)
+MW_HD u32 div3by2(u32 u2, u32 u1, u32 u0, u32 d1, u32 d0, u32 v, u32& r1, u32& r0) {
+  const u64 q = (u64)v * u2 + ((((u64)u2) << 32) | u1);
+  u32 q1 = (u32)(q >> 32);
+  const u32 q0 = (u32)q;
+  const u32 r1a = u1 - q1 * d1;
+  const u64 D = (((u64)d1) << 32) | d0;
+  u64 r = ((((u64)r1a) << 32) | u0) - (u64)d0 * q1 - D;
+  q1 += 1u;
+  const bool a1 = (u32)(r >> 32) >= q0;
+  q1 = a1 ? q1 - 1u : q1;
+  r = a1 ? r + D : r;
+  const bool a2 = r >= D;  // unlikely
+  q1 = a2 ? q1 + 1u : q1;
+  r = a2 ? r - D : r;
+  r1 = (u32)(r >> 32);
+  r0 = (u32)r;
+  return q1;
+}
 
-// q = x / y, r = x % y for y != 0 (Knuth Alg. D, base 2^32, fixed 8x8 shape:
-// the divisor is normalized to a full 8-limb value so every index is static).
-// Written to keep the live set small next to the interpreter's register file:
-// y and x are consumed by the normalising shifts, the add-backs are applied
-// limb by limb, and the remainder is de-normalised in place.
+// q = x / y, r = x % y for y != 0: Knuth Alg. D, base 2^32, fixed 8x8 shape
+// (the divisor is normalized to a full 8-limb value so every index is static),
+// with 3-by-2 quotient estimates (Moller-Granlund).  A digit estimate is at
+// most one too large, with probability ~2^-31, so the add-back runs under an
+// exec mask that is almost always empty (the wave skips it with one branch).
+// When the window's top two words equal the divisor's, the estimate B-1 is
+// exact (GMP mpn_sbpi1_div_qr) and the 3-word partial remainder is
+// (d1:d0) + u0: handled with selects, no separate path.
 MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
   const u32 s = clz256(y);
   u32 v[8];
   shl8(y, s, v);
   u32 u[16];
   shl8to16(x, s, u);
-  const u32 d = v[7];
-  const u32 rec = recip32(d);
+  const u32 d1 = v[7], d0 = v[6];
+  const u32 vinv = recip3by2(d1, d0);
 #pragma unroll
   for (int j = 7; j >= 0; --j) {
-    const u32 u1 = u[j + 8], u0 = u[j + 7];
-    const bool sat = (u1 == d);
-    u32 qh = div2by1(sat ? 0u : u1, u0, d, rec);
+    const u32 u2 = u[j + 8], u1 = u[j + 7], u0 = u[j + 6];
+    const bool sat = (u2 == d1) && (u1 == d0);
+    u32 r1, r0;
+    u32 qh = div3by2(u2, u1, u0, d1, d0, vinv, r1, r0);  // meaningless when sat
+    u32 c0 = 0;
+    const u32 s0 = addc(d0, u0, c0);
+    u32 r2 = 0;
+    const u32 s1 = addc(d1, 0u, c0);
     qh = sat ? 0xffffffffu : qh;
-    // u[j..j+8] -= qh * v
+    r0 = sat ? s0 : r0;
+    r1 = sat ? s1 : r1;
+    r2 = sat ? c0 : 0u;
+    // u[j..j+5] -= qh * v[0..5]; the borrow out comes off (r2:r1:r0)
     u32 carry = 0, br = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      u64 p = (u64)qh * v[k] + carry;
+    for (int k = 0; k < 6; ++k) {
+      const u64 p = (u64)qh * v[k] + carry;
       carry = (u32)(p >> 32);
       u[j + k] = subb(u[j + k], (u32)p, br);
     }
-    u[j + 8] = subb(u[j + 8], carry, br);
-    u32 neg = br;
-    // at most two add-backs (Knuth Thm B: qhat - 2 <= q <= qhat), applied in place
-#pragma unroll
-    for (int ab = 0; ab < 2; ++ab) {
+    const u64 R = (((u64)r1) << 32) | r0;
+    const u64 sub = (u64)carry + br;
+    const bool neg = (r2 == 0u) && (R < sub);
+    const u64 Rn = R - sub;
+    u[j + 6] = (u32)Rn;
+    u[j + 7] = (u32)(Rn >> 32);
+    u[j + 8] = 0u;
+    if (neg) {  // estimate one too large: add the divisor back once
       u32 c = 0;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const u32 t = addc(u[j + k], v[k], c);
-        u[j + k] = neg ? t : u[j + k];
-      }
-      const u32 t8 = addc(u[j + 8], 0u, c);
-      u[j + 8] = neg ? t8 : u[j + 8];
-      qh -= neg;
-      neg = neg & (c ^ 1u);
+      for (int k = 0; k < 8; ++k) u[j + k] = addc(u[j + k], v[k], c);
+      qh -= 1u;
     }
     q[j] = qh;
   }

@@ -246,8 +246,14 @@ __device__ __attribute__((always_inline)) inline void search(const u32* __restri
 
 // <name>_x: exhaustive; <name>_e: per-wave early exit after a failing CHECK.
 // <name>_sig: FNV-1a 64 of the program words, checked by mg_prog_attach_kernel.
+// waves per SIMD the kernel is compiled for: 2 (<= 256 registers per lane) by
+// default; jit.py drops to 1 (512 registers, AGPRs as spill space) for
+// programs whose live set does not fit.
+#ifndef MW_JIT_WAVES
+#define MW_JIT_WAVES 2
+#endif
 #define MW_JIT_KERNEL(NAME, SUFFIX, BODY, EARLY)                                                     \
-  extern "C" __global__ __launch_bounds__(256, 2) void NAME##SUFFIX(                                 \
+  extern "C" __global__ __launch_bounds__(256, MW_JIT_WAVES) void NAME##SUFFIX(                                 \
       const mw::u32* __restrict__ pool, mw::u64 seed, mw::u64 begin, mw::u64 count, mw::u64 chunk0,  \
       mw::u32 flags, mw::u64* __restrict__ out_min, mw::u64* __restrict__ counter,                   \
       mw::u32* __restrict__ verdict) {                                                               \

@@ -86,7 +86,8 @@ def _fnv_words(h: int, a: np.ndarray) -> int:
 class _Gen:
     """Emit the body of one program as straight-line HIP."""
 
-    def __init__(self, p: Program, name: str):
+    def __init__(self, p: Program, name: str, fence_first: bool = False):
+        self.fence_first = fence_first  # diagnostics (tools/opbench.py): no folding across nodes
         self.p = p
         self.name = name
         self.wconst: Dict[int, str] = {}
@@ -130,8 +131,11 @@ class _Gen:
         shape = isa.SHAPES[op]
         A = [self.W(s) if c == "W" else self.N(s) for s, c in zip(S, shape[1])]
         out = self.lines.append
-        if getattr(ins, "remat", False):
+        fence = getattr(ins, "remat", False)
+        if fence or (self.fence_first and S and op not in ("CHECK", "STORE_W", "STORE_N")):
             for j, (s, c) in enumerate(zip(S, shape[1])):
+                if not fence and j > 0:
+                    break
                 if isinstance(s, VReg):
                     self.nf += 1
                     if c == "W":
@@ -226,7 +230,8 @@ class _Gen:
                          ["  } while (0);", "  return alive;", "}"])
 
 
-def generate(progs: Sequence[Program], names: Sequence[str], variants: str = "xe") -> str:
+def generate(progs: Sequence[Program], names: Sequence[str], variants: str = "xe",
+             fence_first: bool = False) -> str:
     """HIP source for a module holding one specialised kernel set per program."""
     parts = ["// generated by mythril_amd/jit.py: specialised witness-search kernels",
              '#include "mw_jit.h"', "using namespace mw;", ""]
@@ -234,7 +239,7 @@ def generate(progs: Sequence[Program], names: Sequence[str], variants: str = "xe
         if not p.ssa:
             raise ValueError("program has no SSA machine IR (compiled by an older compiler?)")
         parts.append(f"// program {name}: {p.n_insn} bytecode insns, {p.ops_per_eval} u32 ops/eval")
-        parts.append(_Gen(p, name).body())
+        parts.append(_Gen(p, name, fence_first).body())
         parts.append(f"MW_JIT_SIG({name}, {signature(p):#x}ull)")
         if "x" in variants:
             parts.append(f"MW_JIT_KERNEL({name}, _x, {name}_body, false)")
@@ -292,11 +297,17 @@ def _compile(src: str, flags: Sequence[str], suffix: str, ext: str) -> Tuple[Pat
     return out, time.perf_counter() - t0
 
 
-def compile_device(progs: Sequence[Program], variants: str = "xe") -> Tuple[bytes, List[str], float]:
-    """gfx950 code object for `progs`; returns (image, kernel names, compile seconds; 0 if cached)."""
+def compile_device(progs: Sequence[Program], variants: str = "xe", fence_first: bool = False,
+                   waves: int = 2) -> Tuple[bytes, List[str], float]:
+    """gfx950 code object for `progs`; returns (image, kernel names, compile seconds; 0 if cached).
+
+    waves: waves per SIMD the kernels are built for (launch bounds): 2 gives
+    each lane 256 registers, 1 gives 512 (AGPRs become spill space instead of
+    scratch memory) at half the latency hiding."""
     names = [kernel_name(p) for p in progs]
-    src = generate(progs, names, variants)
-    path, dt = _compile(src, DEVICE_FLAGS, ".hsaco", ".hip")
+    src = generate(progs, names, variants, fence_first)
+    flags = DEVICE_FLAGS + ([f"-DMW_JIT_WAVES={waves}"] if waves != 2 else [])
+    path, dt = _compile(src, flags, ".hsaco", ".hip")
     return path.read_bytes(), names, dt
 
 
@@ -308,17 +319,17 @@ def compile_host(progs: Sequence[Program]) -> Tuple[Path, List[str]]:
     return path, names
 
 
-def attach(dev, dps, variants: str = "xe") -> float:
+def attach(dev, dps, variants: str = "xe", waves: int = 2) -> float:
     """Compile and attach specialised kernels to loaded programs (DevicePrograms); returns
     the compile seconds (0 when every code object came from the cache)."""
     dps = list(dps)
-    image, names, dt = compile_device([dp.prog for dp in dps], variants)
+    image, names, dt = compile_device([dp.prog for dp in dps], variants, waves=waves)
     for dp, name in zip(dps, names):
         dev.attach_kernel(dp, image, name)
     return dt
 
 
-def warm_bench_cache(n_nodes: int = 10000, log=print) -> float:
+def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 2) -> float:
     """Pre-compile bench.py's C5 kernel into the in-tree cache (run by build()).
 
     The C5 witness is planted with the host build of the interpreter
@@ -331,6 +342,6 @@ def warm_bench_cache(n_nodes: int = 10000, log=print) -> float:
     syn = build_c5(hostemu.term_values, n_nodes=n_nodes)
     prog = compile_program(syn.conjuncts)
     t0 = time.perf_counter()
-    _, names, dt = compile_device([prog], "x")
+    _, names, dt = compile_device([prog], "x", waves=waves)
     log(f"[jit] C5 kernel {names[0]}: {'compiled in %.0f s' % dt if dt else 'cached'}")
     return time.perf_counter() - t0

@@ -163,3 +163,45 @@ def random_assignments(vars_: Sequence[Node], n: int, rng: random.Random, dag: R
             m[v.name] = dag.special(w)
         out.append(m)
     return out
+
+
+def division_stress_pairs(n: int, seed: int, w: int = 256):
+    """(x, y) pairs shaped to reach Knuth D's rare corrections: divisors with
+    structured top limbs over all-ones / random low limbs, dividends y*q + r with
+    q near the digit base.  Most sets of a few dozen include quotient estimates
+    that are one too large (add-back) and equal top words (qhat = B-1)."""
+    rng = random.Random(seed)
+    B = 1 << 32
+    m = (1 << w) - 1
+    out = []
+    while len(out) < n:
+        nb = rng.randint(min(33, w), w)
+        top = rng.choice([B - 1, 1 << 31, (1 << 31) | 1, rng.getrandbits(32) | (1 << 31)])
+        lo_bits = max(nb - 32, 0)
+        y = (top << lo_bits) | (((1 << lo_bits) - 1) if rng.random() < 0.5 else rng.getrandbits(lo_bits) if lo_bits else 0)
+        y &= m
+        if y == 0:
+            continue
+        q = rng.choice([B - 1, B - 2, B, rng.getrandbits(32), (1 << 64) - 1])
+        x = (y * q + rng.choice([0, y - 1, rng.getrandbits(max(1, nb - 1))])) & m
+        out.append((x, y))
+    return out
+
+
+def division_check_programs(npairs: int = 256, seed: int = 11):
+    """Programs asserting op(a, b) == e for the five divisions, where candidate i
+    draws (a, b, e) = pair i and its oracle result from bit-field pools (same
+    digit): every verdict over candidates [0, npairs) must be 1."""
+    from mythril_amd.compiler import LeafSpec, compile_program
+    from oracle import bvsem
+    pairs = division_stress_pairs(npairs, seed)
+    k = (npairs - 1).bit_length()
+    progs = []
+    for op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod"):
+        ctx = Ctx()
+        a, b, e = ctx.var("a", 256), ctx.var("b", 256), ctx.var("e", 256)
+        exp = [getattr(bvsem, op)(256, x, y) for x, y in pairs]
+        specs = {nm: LeafSpec(nm, 256, pool=list(vals), shift=0, bits=k)
+                 for nm, vals in (("a", [x for x, _ in pairs]), ("b", [y for _, y in pairs]), ("e", exp))}
+        progs.append(compile_program([ctx.app("=", ctx.app(op, a, b), e)], leaf_specs=specs))
+    return progs

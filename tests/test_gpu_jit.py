@@ -51,12 +51,18 @@ def random_progs():
 
 @pytest.fixture(scope="module")
 def images(planted, random_progs):
-    progs = [compile_program(s.conjuncts) for s in planted] + [p for *_, p in random_progs]
+    from tests.helpers import division_check_programs
+    progs = [compile_program(s.conjuncts) for s in planted] + [p for *_, p in random_progs] + \
+        division_check_programs()
     image, names, _ = jit.compile_device(progs)  # one module, one hipcc run
     return progs, image, names
 
 
 pytestmark = pytest.mark.gpu
+
+
+def planted_names(images):
+    return images[2][:3]
 
 
 def _pair(dev, p, image, name):
@@ -69,7 +75,7 @@ def _pair(dev, p, image, name):
 
 def test_random_dag_verdicts_match_interpreter_and_oracle(dev, images, random_progs):
     progs, image, names = images
-    k0 = len(progs) - len(random_progs)
+    k0 = len(planted_names(images))
     seed, begin, n = 0x5EED0009, (1 << 36) + 5, 8192
     for (dag, conj, extra, nodes, p), name in zip(random_progs, names[k0:]):
         a, b = _pair(dev, p, image, name)
@@ -84,6 +90,16 @@ def test_random_dag_verdicts_match_interpreter_and_oracle(dev, images, random_pr
             assert int(vb[j]) == int(all(vals[c.id] for c in conj)), f"{name} cand {j}"
         a.free()
         b.free()
+
+
+def test_division_rare_paths(dev, images):
+    progs, image, names = images
+    for p, name in zip(progs[-5:], names[-5:]):
+        dp = dev.load(p)
+        dev.attach_kernel(dp, image, name)
+        v, _ = dev.eval_generated(dp, 1, 0, 256, trace=False)
+        assert int(v.sum()) == 256, name
+        dp.free()
 
 
 def test_search_modes_match_interpreter(dev, images, planted):

@@ -180,3 +180,12 @@ def test_invalid_program_rejected(dev):
     p.code[0] = (int(p.code[0]) & 0xFFFFFF00) | 200  # unknown opcode
     with pytest.raises(Exception):
         dev.load(p)
+
+
+def test_division_rare_paths_gpu(dev):
+    from tests.helpers import division_check_programs
+    for p in division_check_programs():
+        dp = dev.load(p)
+        v, _ = dev.eval_generated(dp, 1, 0, 256, trace=False)
+        assert int(v.sum()) == 256
+        dp.free()

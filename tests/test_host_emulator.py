@@ -136,3 +136,20 @@ def test_host_keccak_matches_oracle():
     lib.mwh_keccak256(ctypes.c_char_p(data), off.ctypes.data, ln.ctypes.data, len(msgs), out.ctypes.data)
     for i, m in enumerate(msgs):
         assert out[32 * i:32 * i + 32].tobytes() == keccak256(m)
+
+
+def test_division_rare_correction_paths():
+    """Quotient estimates one too large (add-back) and equal top words (qhat =
+    B-1) are rare on random operands; these pairs reach both (udivrem8)."""
+    from tests.helpers import division_stress_pairs
+    dag = RandDag(1, widths=[256], nvars=2)
+    a, b = dag.ctx.var("a", 256), dag.ctx.var("b", 256)
+    terms = [dag.ctx.app(op, a, b) for op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")]
+    p = compile_program([dag.ctx.true()], trace=terms)
+    pairs = division_stress_pairs(400, 11)
+    models = [{"a": x, "b": y} for x, y in pairs]
+    _, trace = emu_eval(p, pack_inputs(p, models), len(models))
+    for t in terms:
+        got = unpack_trace(p, trace, t)
+        for j, mm in enumerate(models):
+            assert got[j] == eval_nodes([t], mm)[t.id], f"{t.op} a={mm['a']:#x} b={mm['b']:#x}"

@@ -138,3 +138,13 @@ def test_device_code_object(tmp_path):
     sp = [int(x) for x in re.findall(r"\.vgpr_spill_count:\s+(\d+)", notes)]
     assert vg and max(vg) <= 256
     assert sp and max(sp) <= 8, f"VGPR spills {sp}"
+
+
+def test_host_build_division_rare_paths():
+    from tests.helpers import division_check_programs
+    progs = division_check_programs()
+    path, names = jit.compile_host(progs)
+    lib = ctypes.CDLL(str(path))
+    for p, name in zip(progs, names):
+        v, _ = host_run(lib, name, p, 1, 0, 256)
+        assert int(v.sum()) == 256, name

@@ -1,0 +1,13 @@
+set -o pipefail
+export TMPDIR=/tmp
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+echo "== gpu tests"
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?; tail -5 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+echo "== opbench jit"
+timeout -k 10 300 python3 tools/opbench.py jit 2>&1 | tail -16 || exit 1
+for w in 2 1; do
+echo "== bench jit waves=$w"
+timeout -k 10 600 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --jit-waves $w > gpurun_out/bench_w$w.json 2> gpurun_out/bench_w$w.err || { tail -5 gpurun_out/bench_w$w.err; exit 1; }
+cat gpurun_out/bench_w$w.json
+done

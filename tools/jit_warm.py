@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Pre-compile the specialised kernels the GPU tests and tools use into the
+in-tree JIT cache (build/jit), so GPU runs do not spend minutes in hipcc.
+(bench.py's C5 kernel is warmed by __graft_entry__.build().)"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    from mythril_amd import jit
+    from mythril_amd.compiler import compile_program
+    from tests.helpers import division_check_programs
+    from tests.test_gpu_jit import small_planted
+    from tests.test_jit import _random_programs
+    planted = [small_planted(n_nodes=300, n_conj=6, density_log2=8 + k, seed=0x5EED0005 + k) for k in range(3)]
+    progs = [compile_program(s.conjuncts) for s in planted] + [p for *_, p in _random_programs(8, 9100)] + \
+        division_check_programs()
+    print("tests/test_gpu_jit.py module:", jit.compile_device(progs)[2], "s", flush=True)
+    if "--opbench" in sys.argv:
+        from opbench import OPS, chain
+        for op in OPS:
+            c, conj = chain(op, n=50 if op in ("bvudiv", "bvurem") else 400)
+            print(op, jit.compile_device([compile_program(conj)], "x", fence_first=True)[2], "s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

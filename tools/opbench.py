@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Per-op-class throughput of the interpreter on the device (diagnostic).
+"""Per-op-class throughput of the interpreter or the specialised kernels (diagnostic).
+
+Usage: python tools/opbench.py [interp|jit]
 
 For each op class, a program of one long dependent chain over 4 leaves (no
 spills) is searched exhaustively; reports evals/s, algorithmic Tops/s and the
@@ -15,6 +17,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mythril_amd.compiler import compile_program  # noqa: E402
 from mythril_amd.ir import Ctx  # noqa: E402
 from mythril_amd.runtime import Device  # noqa: E402
+
+
+OPS = ["bvadd", "bvsub", "bvxor", "bvand", "bvmul", "bvult", "=", "ite", "bvshl", "bvlshr", "bvashr",
+       "extract", "bvudiv", "bvurem"]
 
 
 def chain(op, w=256, n=400, nleaves=4):
@@ -40,20 +46,25 @@ def chain(op, w=256, n=400, nleaves=4):
 
 
 def main():
+    engine = sys.argv[1] if len(sys.argv) > 1 else "interp"
     dev = Device(0)
-    res = {}
+    res = {"engine": engine}
     for mul in (False, True):
         ops, ms = dev.valu_peak(mul)
         res["peak_mul" if mul else "peak_add"] = {"ops_per_s": ops, "kernel_ms": ms}
         print(f"peak {'v_mul_lo_u32' if mul else 'v_add_u32'}: {ops/1e12:.2f} T/s ({ms:.2f} ms)", flush=True)
     peak = res["peak_add"]["ops_per_s"]
     count = 1 << 20
-    for op in ["bvadd", "bvsub", "bvxor", "bvand", "bvmul", "bvult", "=", "ite", "bvshl", "bvlshr",
-               "bvashr", "extract", "bvudiv", "bvurem"]:
+    for op in OPS:
         n = 50 if op in ("bvudiv", "bvurem") else 400
         c, conj = chain(op, n=n)
         p = compile_program(conj)
         dp = dev.load(p)
+        if engine == "jit":
+            from mythril_amd import jit
+            # chain values pass through an opaque copy: no folding across nodes
+            image, names, _ = jit.compile_device([p], "x", fence_first=True)
+            dev.attach_kernel(dp, image, names[0])
         dev.search([dp], 1, 0, count, 0)
         (_,), st = dev.search([dp], 1, 0, count, 0)
         evs = count / (st["kernel_ms"] / 1e3)
@@ -66,7 +77,7 @@ def main():
               f"insn-rate {evs*p.n_insn/1e9:6.1f} G/s", flush=True)
         dp.free()
     os.makedirs("gpurun_out", exist_ok=True)
-    json.dump(res, open("gpurun_out/opbench.json", "w"), indent=1)
+    json.dump(res, open(f"gpurun_out/opbench_{engine}.json", "w"), indent=1)
 
 
 if __name__ == "__main__":
