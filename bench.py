@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 
 NOMINAL_PEAK = 256 * 64 * 2.4e9  # SURVEY.md §8(d) derived INT32 VALU peak (u32 ops/s)
 BENCH_VARIANTS = "x"  # exhaustive kernel only: the bench never exits early
-BENCH_WAVES = 2
+BENCH_WAVES = 1  # 512 registers per lane, no spills: 70M vs 50M evals/s at 2 waves (profiles/r1_v3_jit)
 
 
 def parse():

@@ -329,7 +329,7 @@ def attach(dev, dps, variants: str = "xe", waves: int = 2) -> float:
     return dt
 
 
-def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 2) -> float:
+def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 1) -> float:
     """Pre-compile bench.py's C5 kernel into the in-tree cache (run by build()).
 
     The C5 witness is planted with the host build of the interpreter
