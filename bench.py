@@ -44,6 +44,8 @@ def parse():
                          "interp: the bytecode interpreter")
     ap.add_argument("--jit-waves", type=int, default=BENCH_WAVES, choices=[1, 2],
                     help="waves per SIMD the specialised kernel is built for")
+    ap.add_argument("--jit-lds-leaves", type=int, default=None,
+                    help="leaves kept in LDS instead of registers (default: 10 at 2 waves/SIMD, 0 at 1)")
     return ap.parse_args()
 
 
@@ -80,7 +82,9 @@ def main():
         # one-time program preparation, like the upload: outside the timed region
         # (the in-tree cache, warmed by __graft_entry__.build(), usually makes it 0)
         from mythril_amd import jit
-        jit_s = jit.attach(dev, [dp], variants=BENCH_VARIANTS, waves=args.jit_waves)
+        if args.jit_lds_leaves is None:
+            args.jit_lds_leaves = 10 if args.jit_waves == 2 else 0
+        jit_s = jit.attach(dev, [dp], variants=BENCH_VARIANTS, waves=args.jit_waves, lds_leaves=args.jit_lds_leaves)
     batch = 1 << args.batch_log2
 
     def step(k):
@@ -157,7 +161,8 @@ def main():
             "ops_per_eval": prog.ops_per_eval,
             "program_insns": prog.n_insn,
             "spill_slots": prog.n_spill,
-            "engine": args.engine + (f" ({dp.kernel}, {args.jit_waves} wave/SIMD)" if dp.kernel else ""),
+            "engine": args.engine + (f" ({dp.kernel}, {args.jit_waves} wave/SIMD, {args.jit_lds_leaves} leaves in LDS)"
+                                     if dp.kernel else ""),
             "jit_compile_s": jit_s,
             "parallelism": f"candidate-shard x{world}",
             "witness_found_in_timed_range": found_any,

@@ -177,6 +177,7 @@ class _Lowerer:
         self.insns: List[MInsn] = []
         self.memo: Dict[int, object] = {}
         self.memo_scope: Dict[int, int] = {}   # node id -> conjunct in which it was computed
+        self.memo_at: Dict[int, int] = {}      # node id -> instruction count when it was computed
         self.scope = 0
         self.nv = 0
         self.leaf_index: Dict[str, int] = {}
@@ -214,21 +215,25 @@ class _Lowerer:
         raise Unsupported("narrowing class change")
 
     # Cheap terms over leaves/constants (e.g. ``bvor(x, 1)``, ``extract(x)``) are
-    # hash-consed across conjuncts; keeping one computed copy live from its first
-    # to its last conjunct costs 8 registers for the whole span.  Such terms are
-    # recomputed once per conjunct instead (REMAT_MAX_COST u32 ops at most).
+    # hash-consed across the whole DAG; keeping one computed copy live from its
+    # first to its last use costs 8 registers for the whole span.  Such a term
+    # is recomputed instead when its last computation is in an earlier conjunct
+    # or more than REMAT_DISTANCE instructions back (REMAT_MAX_COST u32 ops at
+    # most).
     REMAT_MAX_COST = 16
+    REMAT_DISTANCE = 32
 
     def _fresh(self, m: Node) -> bool:
         if m.id not in self.memo:
             return False
-        if self.memo_scope.get(m.id, self.scope) == self.scope:
-            return True
         if m.op in ("var", "const") or not m.args or node_cost(m) > self.REMAT_MAX_COST:
             return True
         if not all(a.op in ("var", "const") for a in m.args):
             return True
-        del self.memo[m.id]  # recompute in this conjunct
+        if (self.memo_scope.get(m.id, self.scope) == self.scope
+                and len(self.insns) - self.memo_at.get(m.id, 0) <= self.REMAT_DISTANCE):
+            return True
+        del self.memo[m.id]  # recompute here
         return False
 
     def lower(self, n: Node):
@@ -260,6 +265,7 @@ class _Lowerer:
                 ins.remat = True
         self.memo[n.id] = v
         self.memo_scope[n.id] = self.scope
+        self.memo_at[n.id] = len(self.insns)
         if n.id in self.trace_req and n.id not in self.trace_emitted:
             self.trace_emitted[n.id] = v
             cls = v.cls
@@ -507,8 +513,10 @@ def _schedule_narrow_early(insns: List[MInsn]) -> List[MInsn]:
     across the rest of the chain (in C5, most of the spill traffic).  A
     narrow result costs one register, so evaluating it as soon as its operands
     exist never raises the wide live set and usually ends a wide operand's
-    life.  Leaves (no operands) stay at their first use; CHECK/STORE/END keep
-    their place, so the conjunct order (and early exit) is unchanged.
+    life.  CHECKs move with their operand too: a conjunct's comparisons are
+    tested (and, with early exit, can stop the wave) as soon as they exist,
+    instead of holding one register each until the conjunct's end.  Leaves (no
+    operands) stay at their first use; STORE/END keep their place.
     """
     anchor: Dict[int, int] = {}           # vreg id -> index of the insn after which it is defined
     after: Dict[int, List[MInsn]] = {}    # original index -> hoisted insns emitted right after it
@@ -516,12 +524,14 @@ def _schedule_narrow_early(insns: List[MInsn]) -> List[MInsn]:
     keep: List[bool] = []
     for i, ins in enumerate(insns):
         srcs = [s for s in ins.srcs if isinstance(s, VReg)]
-        movable = (ins.dst is not None and ins.dst.cls == "N" and srcs
-                   and not ins.op.startswith(("LEAF", "FILL", "MOV")))
+        movable = ((ins.dst is not None and ins.dst.cls == "N" and srcs
+                    and not ins.op.startswith(("LEAF", "FILL", "MOV")))
+                   or (ins.op == "CHECK" and srcs))
         if movable:
             a = max(anchor[s.id] for s in srcs)
             after.setdefault(a, []).append(ins)
-            anchor[ins.dst.id] = a
+            if ins.dst is not None:
+                anchor[ins.dst.id] = a
             keep.append(False)
         else:
             if ins.dst is not None:

@@ -147,6 +147,44 @@ MW_HD u32 nn_lshri(u32 a, u32 imm, u32 w) { return (imm >= 32 ? 0u : (a >> imm))
 MW_HD u32 nn_sext(u32 a, u32 imm, u32 w) { return n_sext(a, imm) & nmask(w); }
 MW_HD u32 nn_addc(u32 a, u32 b, u32 w) { return (u32)((((u64)a + b) >> w) & 1u); }
 
+// ------------------------------------------------------------------ leaves kept in LDS
+// jit.py (lds_leaves > 0) stores the most-used wide leaves of a program in LDS
+// at their definition and reloads them at every use, so they occupy no
+// registers between uses: at 2 waves/SIMD a lane has 256 registers, and C5's
+// 16 leaves alone would take 128.  Layout [slot][half][lane] x 16 B: each
+// ds_read_b128 of a wave reads 1 KiB of consecutive 16-byte lane records
+// (conflict-free).  Volatile accesses: LLVM may not merge the reloads of one
+// leaf into one long-lived copy.  Budget: slots x 8 KiB per 256-thread block.
+#ifndef MW_JIT_LDS_SLOTS
+#define MW_JIT_LDS_SLOTS 0
+#endif
+#if MW_JIT_LDS_SLOTS > 0
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+#if defined(__HIP_DEVICE_COMPILE__)
+__shared__ u32x4 mw_jit_lds[MW_JIT_LDS_SLOTS * 2 * 256];
+MW_HD void lds_put8(u32 slot, const u32 v[8]) {
+  volatile u32x4* p = mw_jit_lds + slot * 512u + threadIdx.x;
+  u32x4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
+  p[0] = a;
+  p[256] = b;
+}
+MW_HD void lds_get8(u32 slot, u32 r[8]) {
+  volatile u32x4* p = mw_jit_lds + slot * 512u + threadIdx.x;
+  const u32x4 a = p[0], b = p[256];
+  r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
+  r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
+}
+#else
+static u32 mw_jit_host_lds[MW_JIT_LDS_SLOTS * 8];  // host build: one candidate at a time
+MW_HD void lds_put8(u32 slot, const u32 v[8]) {
+  for (int k = 0; k < 8; ++k) mw_jit_host_lds[slot * 8 + k] = v[k];
+}
+MW_HD void lds_get8(u32 slot, u32 r[8]) {
+  for (int k = 0; k < 8; ++k) r[k] = mw_jit_host_lds[slot * 8 + k];
+}
+#endif
+#endif
+
 // ------------------------------------------------------------------ control
 // wave-wide "no lane alive" (per candidate in the host build)
 MW_HD bool none(bool alive) {

@@ -86,9 +86,22 @@ def _fnv_words(h: int, a: np.ndarray) -> int:
 class _Gen:
     """Emit the body of one program as straight-line HIP."""
 
-    def __init__(self, p: Program, name: str, fence_first: bool = False):
+    def __init__(self, p: Program, name: str, fence_first: bool = False, lds_leaves: int = 0):
         self.fence_first = fence_first  # diagnostics (tools/opbench.py): no folding across nodes
         self.p = p
+        # the lds_leaves most-used wide leaves live in LDS (mw_jit.h lds_put8/lds_get8)
+        uses: Dict[int, int] = {}
+        defs: Dict[int, int] = {}
+        for ins in p.ssa:
+            if ins.op == "LEAF_W":
+                defs[ins.dst.id] = ins.imm
+            for s_ in ins.srcs:
+                if isinstance(s_, VReg) and s_.id in defs:
+                    uses[s_.id] = uses.get(s_.id, 0) + 1
+        hot = sorted(uses, key=lambda v: -uses[v])[:lds_leaves]
+        self.lds_slot: Dict[int, int] = {v: k for k, v in enumerate(hot)}
+        self.pre: List[str] = []
+        self.nl = 0
         self.name = name
         self.wconst: Dict[int, str] = {}
         self.lines: List[str] = []
@@ -105,6 +118,11 @@ class _Gen:
             return n
         if s.cls != "W":
             raise ValueError("N register in a W operand")
+        slot = self.lds_slot.get(s.id)
+        if slot is not None:
+            self.nl += 1
+            self.pre.append(f"u32 L{self.nl}[8]; jit::lds_get8({slot}u, L{self.nl});")
+            return f"L{self.nl}"
         return f"v{s.id}"
 
     def N(self, s) -> str:
@@ -131,6 +149,9 @@ class _Gen:
         shape = isa.SHAPES[op]
         A = [self.W(s) if c == "W" else self.N(s) for s, c in zip(S, shape[1])]
         out = self.lines.append
+        for x in self.pre:
+            out(x)
+        self.pre = []
         fence = getattr(ins, "remat", False)
         if fence or (self.fence_first and S and op not in ("CHECK", "STORE_W", "STORE_N")):
             for j, (s, c) in enumerate(zip(S, shape[1])):
@@ -150,6 +171,8 @@ class _Gen:
         if op == "CHECK":
             out(f"alive = jit::check(alive, {A[0]}); if (EARLY) {{ if (jit::none(alive)) break; }} else JIT_SPLIT();")
             self.since_split = 0
+        elif op == "LEAF_W" and d.id in self.lds_slot:
+            out(f"{{ u32 t_[8]; {self.leaf(imm, 't_')} jit::lds_put8({self.lds_slot[d.id]}u, t_); }}")
         elif op == "LEAF_W":
             out(f"u32 {dn}[8]; {self.leaf(imm, dn)}")
         elif op == "LEAF_N":
@@ -231,15 +254,17 @@ class _Gen:
 
 
 def generate(progs: Sequence[Program], names: Sequence[str], variants: str = "xe",
-             fence_first: bool = False) -> str:
+             fence_first: bool = False, lds_leaves: int = 0) -> str:
     """HIP source for a module holding one specialised kernel set per program."""
-    parts = ["// generated by mythril_amd/jit.py: specialised witness-search kernels",
-             '#include "mw_jit.h"', "using namespace mw;", ""]
+    parts = ["// generated by mythril_amd/jit.py: specialised witness-search kernels"]
+    if lds_leaves:
+        parts.append(f"#define MW_JIT_LDS_SLOTS {lds_leaves}")
+    parts += ['#include "mw_jit.h"', "using namespace mw;", ""]
     for p, name in zip(progs, names):
         if not p.ssa:
             raise ValueError("program has no SSA machine IR (compiled by an older compiler?)")
         parts.append(f"// program {name}: {p.n_insn} bytecode insns, {p.ops_per_eval} u32 ops/eval")
-        parts.append(_Gen(p, name, fence_first).body())
+        parts.append(_Gen(p, name, fence_first, lds_leaves).body())
         parts.append(f"MW_JIT_SIG({name}, {signature(p):#x}ull)")
         if "x" in variants:
             parts.append(f"MW_JIT_KERNEL({name}, _x, {name}_body, false)")
@@ -298,38 +323,38 @@ def _compile(src: str, flags: Sequence[str], suffix: str, ext: str) -> Tuple[Pat
 
 
 def compile_device(progs: Sequence[Program], variants: str = "xe", fence_first: bool = False,
-                   waves: int = 2) -> Tuple[bytes, List[str], float]:
+                   waves: int = 2, lds_leaves: int = 0) -> Tuple[bytes, List[str], float]:
     """gfx950 code object for `progs`; returns (image, kernel names, compile seconds; 0 if cached).
 
     waves: waves per SIMD the kernels are built for (launch bounds): 2 gives
     each lane 256 registers, 1 gives 512 (AGPRs become spill space instead of
     scratch memory) at half the latency hiding."""
     names = [kernel_name(p) for p in progs]
-    src = generate(progs, names, variants, fence_first)
+    src = generate(progs, names, variants, fence_first, lds_leaves)
     flags = DEVICE_FLAGS + ([f"-DMW_JIT_WAVES={waves}"] if waves != 2 else [])
     path, dt = _compile(src, flags, ".hsaco", ".hip")
     return path.read_bytes(), names, dt
 
 
-def compile_host(progs: Sequence[Program]) -> Tuple[Path, List[str]]:
+def compile_host(progs: Sequence[Program], lds_leaves: int = 0) -> Tuple[Path, List[str]]:
     """TEST ONLY: x86 build of the same generated source (verdicts + trace rows)."""
     names = [kernel_name(p) for p in progs]
-    src = generate(progs, names, "")
+    src = generate(progs, names, "", lds_leaves=lds_leaves)
     path, _ = _compile(src, HOST_FLAGS, ".so", ".cpp")
     return path, names
 
 
-def attach(dev, dps, variants: str = "xe", waves: int = 2) -> float:
+def attach(dev, dps, variants: str = "xe", waves: int = 2, lds_leaves: int = 0) -> float:
     """Compile and attach specialised kernels to loaded programs (DevicePrograms); returns
     the compile seconds (0 when every code object came from the cache)."""
     dps = list(dps)
-    image, names, dt = compile_device([dp.prog for dp in dps], variants, waves=waves)
+    image, names, dt = compile_device([dp.prog for dp in dps], variants, waves=waves, lds_leaves=lds_leaves)
     for dp, name in zip(dps, names):
         dev.attach_kernel(dp, image, name)
     return dt
 
 
-def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 1) -> float:
+def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 1, lds_leaves: int = 0) -> float:
     """Pre-compile bench.py's C5 kernel into the in-tree cache (run by build()).
 
     The C5 witness is planted with the host build of the interpreter
@@ -342,6 +367,6 @@ def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 1) -> float:
     syn = build_c5(hostemu.term_values, n_nodes=n_nodes)
     prog = compile_program(syn.conjuncts)
     t0 = time.perf_counter()
-    _, names, dt = compile_device([prog], "x", waves=waves)
+    _, names, dt = compile_device([prog], "x", waves=waves, lds_leaves=lds_leaves)
     log(f"[jit] C5 kernel {names[0]}: {'compiled in %.0f s' % dt if dt else 'cached'}")
     return time.perf_counter() - t0

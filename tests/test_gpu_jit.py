@@ -142,3 +142,29 @@ def test_signature_mismatch_refused(dev, images):
     with pytest.raises(Exception):
         dev.attach_kernel(dp, image, names[1])  # kernel of another program
     assert not dev.has_kernel(dp)
+
+
+@pytest.fixture(scope="module")
+def images_lds(planted, random_progs):
+    progs = [compile_program(s.conjuncts) for s in planted] + [p for *_, p in random_progs]
+    image, names, _ = jit.compile_device(progs, lds_leaves=4)
+    return progs, image, names
+
+
+def test_lds_leaves_match_interpreter(dev, images_lds, planted):
+    """Specialised kernels that keep leaves in LDS: same verdicts and witnesses."""
+    progs, image, names = images_lds
+    seed, n = 0x5EED0009, 8192
+    for p, name in zip(progs[3:], names[3:]):
+        a, b = _pair(dev, p, image, name)
+        va, _ = dev.eval_generated(a, seed, 5, n, trace=False)
+        vb, _ = dev.eval_generated(b, seed, 5, n, trace=False)
+        assert np.array_equal(va, vb), name
+        a.free()
+        b.free()
+    for s, p, name in zip(planted, progs[:3], names[:3]):
+        a, b = _pair(dev, p, image, name)
+        for flags in (0, isa.FLAG_EARLY_EXIT):
+            assert dev.search([a], s.seed, 0, 1 << 17, flags)[0] == dev.search([b], s.seed, 0, 1 << 17, flags)[0]
+        a.free()
+        b.free()

@@ -148,3 +148,21 @@ def test_host_build_division_rare_paths():
     for p, name in zip(progs, names):
         v, _ = host_run(lib, name, p, 1, 0, 256)
         assert int(v.sum()) == 256, name
+
+
+def test_host_build_lds_leaves_match_oracle():
+    """Leaves kept in LDS (reloaded at every use) give the same values."""
+    progs = _random_programs(6, 7300)
+    path, names = jit.compile_host([p for *_, p in progs], lds_leaves=3)
+    src = jit.generate([p for *_, p in progs], names, "", lds_leaves=3)
+    assert "lds_put8" in src and "lds_get8" in src
+    lib = ctypes.CDLL(str(path))
+    seed, begin, n = 0x5EED0008, 77, 40
+    for (dag, conj, extra, nodes, p), name in zip(progs, names):
+        v, tr = host_run(lib, name, p, seed, begin, n)
+        models = oracle_models(p, seed, begin, n)
+        for j, m in enumerate(models):
+            vals = eval_nodes(conj + extra, m)
+            assert v[j] == int(all(vals[c.id] for c in conj)), f"{name} verdict {j}"
+            for node in nodes:
+                assert unpack_trace(p, tr, node)[j] == vals[node.id], f"{name} {node!r}[{j}]"

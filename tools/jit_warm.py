@@ -19,6 +19,7 @@ def main():
     progs = [compile_program(s.conjuncts) for s in planted] + [p for *_, p in _random_programs(8, 9100)] + \
         division_check_programs()
     print("tests/test_gpu_jit.py module:", jit.compile_device(progs)[2], "s", flush=True)
+    print("tests/test_gpu_jit.py LDS module:", jit.compile_device(progs[:11], lds_leaves=4)[2], "s", flush=True)
     if "--opbench" in sys.argv:
         from opbench import OPS, chain
         for op in OPS:
