@@ -26,8 +26,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 NOMINAL_PEAK = 256 * 64 * 2.4e9  # SURVEY.md §8(d) derived INT32 VALU peak (u32 ops/s)
+# CDNA4 issues a wave64 VALU instruction in 2 cycles on a 32-lane SIMD
+# (MI355X_MICROARCH.md): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
+THEORETICAL_PEAK = 256 * 4 * 32 * 2.4e9
 BENCH_VARIANTS = "x"  # exhaustive kernel only: the bench never exits early
-BENCH_WAVES = 1  # 512 registers per lane, no spills: 70M vs 50M evals/s at 2 waves (profiles/r1_v3_jit)
+BENCH_WAVES = 2  # with 10 leaves in LDS (profiles/r1_v4_jit); 1 wave/SIMD: 512 registers, no LDS
+BENCH_SPLIT = False  # one kernel: 111.7M evals/s; as 5 part kernels (split_ssa): 109.9M, 7x faster to compile
 
 
 def parse():
@@ -44,6 +48,8 @@ def parse():
                          "interp: the bytecode interpreter")
     ap.add_argument("--jit-waves", type=int, default=BENCH_WAVES, choices=[1, 2],
                     help="waves per SIMD the specialised kernel is built for")
+    ap.add_argument("--jit-split", type=int, default=int(BENCH_SPLIT), choices=[0, 1],
+                    help="1: split the program into part kernels at conjunct boundaries")
     ap.add_argument("--jit-lds-leaves", type=int, default=None,
                     help="leaves kept in LDS instead of registers (default: 10 at 2 waves/SIMD, 0 at 1)")
     return ap.parse_args()
@@ -84,7 +90,8 @@ def main():
         from mythril_amd import jit
         if args.jit_lds_leaves is None:
             args.jit_lds_leaves = 10 if args.jit_waves == 2 else 0
-        jit_s = jit.attach(dev, [dp], variants=BENCH_VARIANTS, waves=args.jit_waves, lds_leaves=args.jit_lds_leaves)
+        jit_s = jit.attach(dev, [dp], variants=BENCH_VARIANTS, waves=args.jit_waves, lds_leaves=args.jit_lds_leaves,
+                           split=bool(args.jit_split))
     batch = 1 << args.batch_log2
 
     def step(k):
@@ -176,6 +183,8 @@ def main():
             "traffic": load_traffic(prog, batch),
             "kernel_ms_avg": avg_kernel_s * 1e3,
             "peak_source": peak_info["source"],
+            "peak_theoretical": THEORETICAL_PEAK / 1e12,
+            "frac_theoretical": achieved / THEORETICAL_PEAK,
         },
         "cpu_baseline": cpu,
     }

@@ -522,11 +522,16 @@ def _schedule_narrow_early(insns: List[MInsn]) -> List[MInsn]:
     after: Dict[int, List[MInsn]] = {}    # original index -> hoisted insns emitted right after it
     head: List[MInsn] = []
     keep: List[bool] = []
+    leafv = {ins.dst.id for ins in insns if ins.op.startswith("LEAF") and ins.dst is not None}
     for i, ins in enumerate(insns):
+        # operands that are leaves do not count: leaves are defined at their first
+        # use, often far above, and stay live anyway (hoisting to them would only
+        # stretch the result's live range)
         srcs = [s for s in ins.srcs if isinstance(s, VReg)]
-        movable = ((ins.dst is not None and ins.dst.cls == "N" and srcs
+        nonleaf = any(s.id not in leafv for s in srcs)
+        movable = ((ins.dst is not None and ins.dst.cls == "N" and nonleaf
                     and not ins.op.startswith(("LEAF", "FILL", "MOV")))
-                   or (ins.op == "CHECK" and srcs))
+                   or (ins.op == "CHECK" and nonleaf))
         if movable:
             a = max(anchor[s.id] for s in srcs)
             after.setdefault(a, []).append(ins)

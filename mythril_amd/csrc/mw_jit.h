@@ -251,6 +251,12 @@ MW_HD void tstore(u32* trace, u64 stride, u64 idx, u32 row, const u32* v, int n)
 
 typedef bool (*body_fn)(const u32* __restrict__, u64, u64, bool, u32, u32*, u64, u64);
 
+// stage bits of a launch: a program is one part (FIRST|LAST) or several parts
+// launched in order over the same candidates, passing each candidate's alive
+// bit through a buffer (jit.py split_ssa: parts end at conjunct boundaries)
+#define MW_JIT_FIRST 1u
+#define MW_JIT_LAST 2u
+
 #if !defined(MW_JIT_HOST)
 // One 256-candidate chunk per block (chunk = chunk0 + blockIdx.x), with the
 // interpreter's result protocol (mw_search_kernel): per-wave ballot -> lowest
@@ -258,20 +264,29 @@ typedef bool (*body_fn)(const u32* __restrict__, u64, u64, bool, u32, u32*, u64,
 // per-candidate verdicts (mg_eval_generated).  No grid-stride loop on purpose:
 // inside a loop LLVM hoists every leaf's Philox key schedule (uniform, loop
 // invariant) into SGPRs and spills hundreds of them into VGPR lanes.
+// A part that is not LAST stores alive bits (index cand - begin) instead; a
+// part that is not FIRST starts from them.
 template <body_fn BODY>
 __device__ __attribute__((always_inline)) inline void search(const u32* __restrict__ pool, u64 seed, u64 begin,
                                                              u64 count, u64 chunk0, u32 flags,
                                                              u64* __restrict__ out_min, u64* __restrict__ counter,
-                                                             u32* __restrict__ verdict) {
+                                                             u32* __restrict__ verdict, u32* __restrict__ alivebuf,
+                                                             u32 stage) {
   const u64 base = begin + (chunk0 + blockIdx.x) * 256;
-  if (flags & MW_FLAG_STOP_AFTER_HIT) {
+  if ((flags & MW_FLAG_STOP_AFTER_HIT) && stage == (MW_JIT_FIRST | MW_JIT_LAST)) {
     const u64 m = __hip_atomic_load(out_min, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (m <= base) return;
   }
   const u32 lane = threadIdx.x & 63u;
   const u64 cand = base + threadIdx.x;
   const bool valid = cand < begin + count;
-  const bool ok = BODY(pool, seed, cand, valid, flags, nullptr, 0, 0);
+  bool in = valid;
+  if (!(stage & MW_JIT_FIRST) && valid) in = alivebuf[cand - begin] != 0u;
+  const bool ok = BODY(pool, seed, cand, in, flags, nullptr, 0, 0);
+  if (!(stage & MW_JIT_LAST)) {
+    if (valid) alivebuf[cand - begin] = ok ? 1u : 0u;
+    return;
+  }
   if (verdict && valid) verdict[cand - begin] = ok ? 1u : 0u;
   const u64 hit = __ballot(ok);
   if (hit) {
@@ -283,24 +298,29 @@ __device__ __attribute__((always_inline)) inline void search(const u32* __restri
 }
 
 // <name>_x: exhaustive; <name>_e: per-wave early exit after a failing CHECK.
-// <name>_sig: FNV-1a 64 of the program words, checked by mg_prog_attach_kernel.
+// <name>_sig: FNV-1a 64 of the whole program's words, checked by
+// mg_prog_attach_kernel; <name>_part / <name>_nparts: this module's part.
 // waves per SIMD the kernel is compiled for: 2 (<= 256 registers per lane) by
-// default; jit.py drops to 1 (512 registers, AGPRs as spill space) for
-// programs whose live set does not fit.
+// default, 1 gives 512 registers (AGPRs as spill space).
 #ifndef MW_JIT_WAVES
 #define MW_JIT_WAVES 2
 #endif
 #define MW_JIT_KERNEL(NAME, SUFFIX, BODY, EARLY)                                                     \
-  extern "C" __global__ __launch_bounds__(256, MW_JIT_WAVES) void NAME##SUFFIX(                                 \
+  extern "C" __global__ __launch_bounds__(256, MW_JIT_WAVES) void NAME##SUFFIX(                      \
       const mw::u32* __restrict__ pool, mw::u64 seed, mw::u64 begin, mw::u64 count, mw::u64 chunk0,  \
       mw::u32 flags, mw::u64* __restrict__ out_min, mw::u64* __restrict__ counter,                   \
-      mw::u32* __restrict__ verdict) {                                                               \
-    mw::jit::search<BODY<EARLY>>(pool, seed, begin, count, chunk0, flags, out_min, counter, verdict); \
+      mw::u32* __restrict__ verdict, mw::u32* __restrict__ alivebuf, mw::u32 stage) {                \
+    mw::jit::search<BODY<EARLY>>(pool, seed, begin, count, chunk0, flags, out_min, counter, verdict, \
+                                 alivebuf, stage);                                                   \
   }
 #define MW_JIT_SIG(NAME, SIG) extern "C" __device__ const mw::u64 NAME##_sig = SIG;
+#define MW_JIT_PART(NAME, K, N)                                \
+  extern "C" __device__ const mw::u32 NAME##_part = K;         \
+  extern "C" __device__ const mw::u32 NAME##_nparts = N;
 #else
 #define MW_JIT_KERNEL(NAME, SUFFIX, BODY, EARLY)
 #define MW_JIT_SIG(NAME, SIG)
+#define MW_JIT_PART(NAME, K, N)
 #endif
 
 // host build (tests only): verdicts (+ trace rows) of candidates [begin, begin+count)

@@ -255,6 +255,8 @@ struct mg_ctx {
   u64* d_min = nullptr;
   size_t nmin = 0;
   u64* d_counter = nullptr;
+  u32* d_alive = nullptr;     // per-candidate alive bits between the parts of a split program
+  size_t alive_cap = 0;
   ProgDev* d_progs = nullptr;
   size_t nprogs_cap = 0;
   std::mutex mu;
@@ -267,9 +269,24 @@ struct mg_prog {
   mg_prog_desc desc{};
   u64 ops_per_eval = 0;
   u64 sig = 0;                  // FNV-1a 64 of the program words (mythril_amd/jit.py signature)
-  hipModule_t mod = nullptr;    // specialised kernels (mg_prog_attach_kernel), or none
-  hipFunction_t fx = nullptr;   // exhaustive
-  hipFunction_t fe = nullptr;   // early exit (optional)
+  // specialised kernels (mg_prog_attach_kernel): one per part, launched in order
+  struct Part {
+    hipModule_t mod = nullptr;
+    hipFunction_t fx = nullptr;  // exhaustive
+    hipFunction_t fe = nullptr;  // early exit (optional)
+  };
+  std::vector<Part> parts;
+  bool jit_ready() const {
+    if (parts.empty()) return false;
+    for (const Part& q : parts)
+      if (!q.fx) return false;
+    return true;
+  }
+  void unload() {
+    for (Part& q : parts)
+      if (q.mod) hipModuleUnload(q.mod);
+    parts.clear();
+  }
 };
 
 namespace {
@@ -292,23 +309,52 @@ u64 prog_signature(const mg_prog_desc* d) {
   return h;
 }
 
-// Launch a program's specialised kernel over [begin, begin+count): one block
-// per 256-candidate chunk (mw_jit.h), split into launches of <= 2^30 blocks.
-int launch_jit(mg_ctx* c, const mg_prog* p, u64 seed, u64 begin, u64 count, u32 flags, u64* d_min,
-               u32* d_verdict) {
-  hipFunction_t f = ((flags & MW_FLAG_EARLY_EXIT) && p->fe) ? p->fe : p->fx;
+// Launch a program's specialised kernels over [begin, begin+count): one block
+// per 256-candidate chunk (mw_jit.h), at most 2^30 blocks per launch.  A split
+// program runs its parts in order over slices of kAliveSlice candidates,
+// passing alive bits through c->d_alive.
+constexpr u64 kAliveSlice = 1ull << 24;
+
+int launch_part(mg_ctx* c, const mg_prog* p, size_t k, u64 seed, u64 begin, u64 count, u32 flags, u64* d_min,
+                u32* d_verdict, u32 stage) {
+  const mg_prog::Part& q = p->parts[k];
+  hipFunction_t f = ((flags & MW_FLAG_EARLY_EXIT) && q.fe) ? q.fe : q.fx;
   const u64 nchunks = (count + kBlock - 1) / kBlock;
   const u64 kMaxBlocks = 1ull << 30;
   for (u64 chunk0 = 0; chunk0 < nchunks; chunk0 += kMaxBlocks) {
     const u32 nb = (u32)std::min<u64>(kMaxBlocks, nchunks - chunk0);
     const u32* pool = p->dev.pool;
     u64 sd = seed, bg = begin, ct = count, c0 = chunk0;
-    u32 fl = flags;
+    u32 fl = flags, st = stage;
     u64* mn = d_min;
     u64* ctr = c->d_counter;
     u32* vd = d_verdict;
-    void* args[] = {&pool, &sd, &bg, &ct, &c0, &fl, &mn, &ctr, &vd};
+    u32* al = c->d_alive;
+    void* args[] = {&pool, &sd, &bg, &ct, &c0, &fl, &mn, &ctr, &vd, &al, &st};
     HIPCHK(hipModuleLaunchKernel(f, nb, 1, 1, kBlock, 1, 1, 0, c->stream, args, nullptr));
+  }
+  return 0;
+}
+
+int launch_jit(mg_ctx* c, const mg_prog* p, u64 seed, u64 begin, u64 count, u32 flags, u64* d_min,
+               u32* d_verdict) {
+  const size_t np = p->parts.size();
+  if (np == 1) return launch_part(c, p, 0, seed, begin, count, flags, d_min, d_verdict, 3u);
+  const size_t need = (size_t)std::min<u64>(count, kAliveSlice);
+  if (need > c->alive_cap) {
+    if (c->d_alive) HIPCHK(hipFree(c->d_alive));
+    c->d_alive = nullptr;
+    c->alive_cap = 0;
+    HIPCHK(hipMalloc(&c->d_alive, need * sizeof(u32)));
+    c->alive_cap = need;
+  }
+  for (u64 s0 = 0; s0 < count; s0 += kAliveSlice) {
+    const u64 sc = std::min<u64>(kAliveSlice, count - s0);
+    for (size_t k = 0; k < np; ++k) {
+      const u32 stage = (k == 0 ? 1u : 0u) | (k + 1 == np ? 2u : 0u);
+      int rc = launch_part(c, p, k, seed, begin + s0, sc, flags, d_min, d_verdict ? d_verdict + s0 : nullptr, stage);
+      if (rc) return rc;
+    }
   }
   return 0;
 }
@@ -385,6 +431,7 @@ int mg_free(mg_ctx* c) {
   if (c->d_min) hipFree(c->d_min);
   if (c->d_progs) hipFree(c->d_progs);
   if (c->d_counter) hipFree(c->d_counter);
+  if (c->d_alive) hipFree(c->d_alive);
   if (c->e0) hipEventDestroy(c->e0);
   if (c->e1) hipEventDestroy(c->e1);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -438,7 +485,7 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
 int mg_prog_free(mg_prog* p) {
   if (!p) return 0;
   hipSetDevice(p->ctx->dev);
-  if (p->mod) hipModuleUnload(p->mod);
+  p->unload();
   if (p->d_buf) hipFree(p->d_buf);
   delete p;
   return 0;
@@ -453,6 +500,15 @@ int mg_prog_attach_kernel(mg_prog* p, const void* image, size_t size, const char
   hipModule_t mod = nullptr;
   HIPCHK(hipModuleLoadData(&mod, image));
   const std::string base(name);
+  auto get32 = [&](const std::string& sym, u32* out) -> bool {
+    hipDeviceptr_t d = nullptr;
+    size_t n = 0;
+    if (hipModuleGetGlobal(&d, &n, mod, sym.c_str()) != hipSuccess || n != sizeof(u32)) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return hipMemcpyDtoH(out, d, sizeof(u32)) == hipSuccess;
+  };
   hipDeviceptr_t dsig = nullptr;
   size_t nsig = 0;
   u64 sig = 0;
@@ -466,6 +522,15 @@ int mg_prog_attach_kernel(mg_prog* p, const void* image, size_t size, const char
     hipModuleUnload(mod);
     return fail(MG_E_PROG, "code object was generated for another program (signature mismatch)");
   }
+  u32 part = 0, nparts = 1;
+  if (!get32(base + "_part", &part) || !get32(base + "_nparts", &nparts)) {
+    part = 0;
+    nparts = 1;
+  }
+  if (nparts == 0 || nparts > 1024 || part >= nparts) {
+    hipModuleUnload(mod);
+    return fail(MG_E_PROG, "bad part index in code object");
+  }
   if (hipModuleGetFunction(&fx, mod, (base + "_x").c_str()) != hipSuccess) {
     hipModuleUnload(mod);
     return fail(MG_E_PROG, "code object lacks kernel " + base + "_x");
@@ -474,14 +539,19 @@ int mg_prog_attach_kernel(mg_prog* p, const void* image, size_t size, const char
     (void)hipGetLastError();
     fe = nullptr;  // early exit is an optimisation only: the exhaustive kernel gives the same results
   }
-  if (p->mod) hipModuleUnload(p->mod);
-  p->mod = mod;
-  p->fx = fx;
-  p->fe = fe;
+  if (p->parts.size() != nparts) {  // a new split of this program replaces the old one
+    p->unload();
+    p->parts.resize(nparts);
+  }
+  mg_prog::Part& q = p->parts[part];
+  if (q.mod) hipModuleUnload(q.mod);
+  q.mod = mod;
+  q.fx = fx;
+  q.fe = fe;
   return 0;
 }
 
-int mg_prog_has_kernel(const mg_prog* p) { return p && p->fx ? 1 : 0; }
+int mg_prog_has_kernel(const mg_prog* p) { return p && p->jit_ready() ? 1 : 0; }
 
 int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uint64_t begin,
               uint64_t count, uint32_t flags, uint64_t* out_min_idx, mg_stats* st) {
@@ -501,7 +571,7 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   u64 ops = 0;
   for (size_t i = 0; i < nprog; ++i) {
     if (!progs[i] || progs[i]->ctx != c) return fail(MG_E_ARG, "program from another context");
-    (progs[i]->fx ? special : interp).push_back(i);
+    (progs[i]->jit_ready() ? special : interp).push_back(i);
     ops += progs[i]->ops_per_eval;
   }
   std::vector<ProgDev> hp;
@@ -605,7 +675,7 @@ int mg_eval(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncan
 
 int mg_eval_generated(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, size_t count,
                       uint32_t* verdict, uint32_t* trace) {
-  if (!p || !p->fx || trace) return eval_common(c, p, nullptr, count, seed, begin, verdict, trace);
+  if (!p || !p->jit_ready() || trace) return eval_common(c, p, nullptr, count, seed, begin, verdict, trace);
   // verdicts only, on the program's specialised kernel
   if (!c || !verdict || count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad argument");
   std::lock_guard<std::mutex> lk(c->mu);

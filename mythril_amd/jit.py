@@ -34,7 +34,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import isa
-from .compiler import Const, Program, VReg, compile_program
+from .compiler import Const, MInsn, Program, VReg, compile_program
 
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "mythril_amd" / "csrc"
@@ -86,13 +86,15 @@ def _fnv_words(h: int, a: np.ndarray) -> int:
 class _Gen:
     """Emit the body of one program as straight-line HIP."""
 
-    def __init__(self, p: Program, name: str, fence_first: bool = False, lds_leaves: int = 0):
+    def __init__(self, p: Program, name: str, fence_first: bool = False, lds_leaves: int = 0,
+                 insns: Optional[List[MInsn]] = None):
         self.fence_first = fence_first  # diagnostics (tools/opbench.py): no folding across nodes
         self.p = p
+        self.insns = p.ssa if insns is None else insns
         # the lds_leaves most-used wide leaves live in LDS (mw_jit.h lds_put8/lds_get8)
         uses: Dict[int, int] = {}
         defs: Dict[int, int] = {}
-        for ins in p.ssa:
+        for ins in self.insns:
             if ins.op == "LEAF_W":
                 defs[ins.dst.id] = ins.imm
             for s_ in ins.srcs:
@@ -240,7 +242,7 @@ class _Gen:
             raise ValueError(f"jit: no emitter for {op}")
 
     def body(self) -> str:
-        for ins in self.p.ssa:
+        for ins in self.insns:
             self.emit(ins)
         head = [f"template <bool EARLY>",
                 f"MW_HD bool {self.name}_body(const u32* __restrict__ pool, u64 seed, u64 cand, bool alive,",
@@ -253,26 +255,105 @@ class _Gen:
                          ["  } while (0);", "  return alive;", "}"])
 
 
+# --------------------------------------------------------------------------- program parts
+# Large programs are split at conjunct boundaries into parts of about
+# PART_WEIGHT estimated machine instructions, each its own kernel and code
+# object (compiled in parallel), launched in order over the same candidates
+# with the alive bits passed through a buffer (mw_jit.h MW_JIT_FIRST/LAST).
+# LLVM allocates a part like a small program (C5: 3k-node programs compile
+# without spills at 2 waves/SIMD, the 10k whole program does not) and each
+# part compiles in a fraction of the time.  A part regenerates the leaves it
+# uses (and recomputes any other value live across its boundary; boundaries
+# are chosen where there is none).
+PART_WEIGHT = 110_000
+_WEIGHT = {"W_UDIV": 900, "W_UREM": 900, "W_SDIV": 950, "W_SREM": 950, "W_SMOD": 950, "W_MUL": 110,
+           "W_SHL": 45, "W_LSHR": 45, "W_ASHR": 45, "LEAF_W": 200, "LEAF_N": 100, "N_ULT": 25, "N_ULE": 25,
+           "N_SLT": 30, "N_SLE": 30, "N_EQ": 16, "N_UMULNO": 150, "N_ADDC": 12}
+
+
+def insn_weight(ins: MInsn) -> int:
+    w = _WEIGHT.get(ins.op)
+    if w is not None:
+        return w
+    return 10 if ins.op.startswith("W_") else 3
+
+
+def split_ssa(p: Program, part_weight: int = PART_WEIGHT) -> List[List[MInsn]]:
+    """Instruction lists of the program's parts (one list when it is small)."""
+    ssa = [i for i in p.ssa if i.op != "END"]
+    n = len(ssa)
+    total = sum(insn_weight(i) for i in ssa)
+    if total <= part_weight * 1.25 or n < 2:
+        return [p.ssa]
+    defs: Dict[int, int] = {}
+    last: Dict[int, int] = {}
+    for i, ins in enumerate(ssa):
+        if ins.dst is not None:
+            defs[ins.dst.id] = i
+        for s_ in ins.srcs:
+            if isinstance(s_, VReg):
+                last[s_.id] = i
+    delta = [0] * (n + 2)  # non-leaf values live across boundary b (before insn b)
+    for vid, d in defs.items():
+        if ssa[d].op.startswith("LEAF"):
+            continue
+        l = last.get(vid, d)
+        if l > d:
+            delta[d + 1] += 1
+            delta[l + 1] -= 1
+    cuts, acc, cross = [], 0, 0
+    target = total / max(2, round(total / part_weight))
+    for b in range(1, n):
+        cross += delta[b]
+        acc += insn_weight(ssa[b - 1])
+        if acc >= target and ssa[b - 1].op == "CHECK" and cross == 0:
+            cuts.append(b)
+            acc = 0
+    if not cuts:
+        return [p.ssa]
+    bounds = [0] + cuts + [n]
+    parts = []
+    for a, b in zip(bounds, bounds[1:]):
+        seg = ssa[a:b]
+        inside = {ins.dst.id for ins in seg if ins.dst is not None}
+        need, stack = set(), [s_.id for ins in seg for s_ in ins.srcs if isinstance(s_, VReg)]
+        while stack:  # defining instructions of values from earlier parts (leaves, in practice)
+            v = stack.pop()
+            if v in inside or v in need:
+                continue
+            need.add(v)
+            stack.extend(s_.id for s_ in ssa[defs[v]].srcs if isinstance(s_, VReg))
+        pre = [ssa[defs[v]] for v in sorted(need, key=lambda v: defs[v])]
+        parts.append(pre + seg + [MInsn("END")])
+    return parts
+
+
 def generate(progs: Sequence[Program], names: Sequence[str], variants: str = "xe",
-             fence_first: bool = False, lds_leaves: int = 0) -> str:
-    """HIP source for a module holding one specialised kernel set per program."""
-    parts = ["// generated by mythril_amd/jit.py: specialised witness-search kernels"]
+             fence_first: bool = False, lds_leaves: int = 0,
+             parts: Optional[Sequence[Tuple[List[MInsn], int, int]]] = None) -> str:
+    """HIP source for a module holding one specialised kernel set per program
+    (with `parts`: per program, its (instructions, part index, part count))."""
+    out = ["// generated by mythril_amd/jit.py: specialised witness-search kernels"]
     if lds_leaves:
-        parts.append(f"#define MW_JIT_LDS_SLOTS {lds_leaves}")
-    parts += ['#include "mw_jit.h"', "using namespace mw;", ""]
-    for p, name in zip(progs, names):
+        out.append(f"#define MW_JIT_LDS_SLOTS {lds_leaves}")
+    out += ['#include "mw_jit.h"', "using namespace mw;", ""]
+    for k, (p, name) in enumerate(zip(progs, names)):
         if not p.ssa:
             raise ValueError("program has no SSA machine IR (compiled by an older compiler?)")
-        parts.append(f"// program {name}: {p.n_insn} bytecode insns, {p.ops_per_eval} u32 ops/eval")
-        parts.append(_Gen(p, name, fence_first, lds_leaves).body())
-        parts.append(f"MW_JIT_SIG({name}, {signature(p):#x}ull)")
+        part = parts[k] if parts else None
+        out.append(f"// program {name}: {p.n_insn} bytecode insns, {p.ops_per_eval} u32 ops/eval"
+                   + (f", part {part[1]} of {part[2]}" if part else ""))
+        out.append(_Gen(p, name, fence_first, lds_leaves, part[0] if part else None).body())
+        out.append(f"MW_JIT_SIG({name}, {signature(p):#x}ull)")
+        if part:
+            out.append(f"MW_JIT_PART({name}, {part[1]}u, {part[2]}u)")
         if "x" in variants:
-            parts.append(f"MW_JIT_KERNEL({name}, _x, {name}_body, false)")
+            out.append(f"MW_JIT_KERNEL({name}, _x, {name}_body, false)")
         if "e" in variants:
-            parts.append(f"MW_JIT_KERNEL({name}, _e, {name}_body, true)")
-        parts.append(f"MW_JIT_HOST_ENTRY({name}, {name}_body)")
-        parts.append("")
-    return "\n".join(parts)
+            out.append(f"MW_JIT_KERNEL({name}, _e, {name}_body, true)")
+        out.append(f"MW_JIT_HOST_ENTRY({name}, {name}_body)")
+        out.append("")
+    return "\n".join(out)
 
 
 def kernel_name(p: Program) -> str:
@@ -296,10 +377,26 @@ HOST_FLAGS = ["-O1", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__",
               "-Wno-unused-variable"]
 
 
+_USED: set = set()  # cache files this process produced or read (prune_cache keeps them)
+
+
+def prune_cache(keep: Optional[set] = None) -> int:
+    """Delete cache entries not used by this process (the cache ships with every
+    GPU run); returns the number removed."""
+    keep = _USED if keep is None else keep
+    n = 0
+    for f in _cache_dir().glob("*"):
+        if f not in keep:
+            f.unlink()
+            n += 1
+    return n
+
+
 def _compile(src: str, flags: Sequence[str], suffix: str, ext: str) -> Tuple[Path, float]:
     cache = _cache_dir()
     cache.mkdir(parents=True, exist_ok=True)
     out = cache / f"{_key(src, flags)}{suffix}"
+    _USED.add(out)
     if out.exists():
         return out, 0.0
     t0 = time.perf_counter()
@@ -331,30 +428,80 @@ def compile_device(progs: Sequence[Program], variants: str = "xe", fence_first: 
     scratch memory) at half the latency hiding."""
     names = [kernel_name(p) for p in progs]
     src = generate(progs, names, variants, fence_first, lds_leaves)
-    flags = DEVICE_FLAGS + ([f"-DMW_JIT_WAVES={waves}"] if waves != 2 else [])
-    path, dt = _compile(src, flags, ".hsaco", ".hip")
+    path, dt = _compile(src, _device_flags(waves), ".hsaco", ".hip")
     return path.read_bytes(), names, dt
 
 
-def compile_host(progs: Sequence[Program], lds_leaves: int = 0) -> Tuple[Path, List[str]]:
-    """TEST ONLY: x86 build of the same generated source (verdicts + trace rows)."""
+def compile_host(progs: Sequence[Program], lds_leaves: int = 0,
+                 part_weight: Optional[int] = None) -> Tuple[Path, List[str]]:
+    """TEST ONLY: x86 build of the same generated source (verdicts + trace rows).
+    With part_weight, every part of every program gets a host entry
+    (<name>_p<k>_host; the program's verdict is the AND over its parts)."""
     names = [kernel_name(p) for p in progs]
+    if part_weight is not None:
+        allp, alln, spec = [], [], []
+        for p, name in zip(progs, names):
+            segs = split_ssa(p, part_weight)
+            for k, seg in enumerate(segs):
+                allp.append(p)
+                alln.append(f"{name}_p{k}")
+                spec.append((seg, k, len(segs)))
+        src = generate(allp, alln, "", lds_leaves=lds_leaves, parts=spec)
+        path, _ = _compile(src, HOST_FLAGS, ".so", ".cpp")
+        return path, alln
     src = generate(progs, names, "", lds_leaves=lds_leaves)
     path, _ = _compile(src, HOST_FLAGS, ".so", ".cpp")
     return path, names
 
 
-def attach(dev, dps, variants: str = "xe", waves: int = 2, lds_leaves: int = 0) -> float:
+def _device_flags(waves: int) -> List[str]:
+    return DEVICE_FLAGS + ([f"-DMW_JIT_WAVES={waves}"] if waves != 2 else [])
+
+
+def compile_parts(p: Program, variants: str = "xe", waves: int = 2, lds_leaves: int = 0,
+                  part_weight: int = PART_WEIGHT) -> Tuple[List[Tuple[bytes, str]], float]:
+    """Code objects of a program's parts (split_ssa), compiled in parallel hipcc
+    processes; returns ([(image, kernel name)], wall seconds, 0 if all cached)."""
+    from concurrent.futures import ThreadPoolExecutor
+    segs = split_ssa(p, part_weight)
+    base = kernel_name(p)
+    n = len(segs)
+    jobs = []
+    for k, seg in enumerate(segs):
+        name = base if n == 1 else f"{base}_p{k}"
+        spec = None if n == 1 else [(seg, k, n)]
+        jobs.append((name, generate([p], [name], variants, lds_leaves=lds_leaves, parts=spec)))
+    t0 = time.perf_counter()
+    workers = max(1, min(n, int(os.environ.get("MW_JIT_JOBS", "8"))))
+    with ThreadPoolExecutor(workers) as ex:
+        res = list(ex.map(lambda j: _compile(j[1], _device_flags(waves), ".hsaco", ".hip"), jobs))
+    dt = time.perf_counter() - t0 if any(d for _, d in res) else 0.0
+    return [(path.read_bytes(), name) for (path, _), (name, _) in zip(res, jobs)], dt
+
+
+def attach(dev, dps, variants: str = "xe", waves: int = 2, lds_leaves: int = 0,
+           split: bool = False, part_weight: int = PART_WEIGHT) -> float:
     """Compile and attach specialised kernels to loaded programs (DevicePrograms); returns
-    the compile seconds (0 when every code object came from the cache)."""
+    the compile seconds (0 when every code object came from the cache).  split: large
+    programs become several part kernels (compile_parts) instead of one."""
     dps = list(dps)
+    if split:
+        total = 0.0
+        for dp in dps:
+            objs, dt = compile_parts(dp.prog, variants, waves, lds_leaves, part_weight)
+            for image, name in objs:
+                dev.attach_kernel(dp, image, name)
+            dp.kernel = objs[0][1].rsplit("_p", 1)[0] + (f" ({len(objs)} parts)" if len(objs) > 1 else "")
+            total += dt
+        return total
     image, names, dt = compile_device([dp.prog for dp in dps], variants, waves=waves, lds_leaves=lds_leaves)
     for dp, name in zip(dps, names):
         dev.attach_kernel(dp, image, name)
     return dt
 
 
-def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 1, lds_leaves: int = 0) -> float:
+def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 2, lds_leaves: int = 10,
+                     split: bool = False) -> float:
     """Pre-compile bench.py's C5 kernel into the in-tree cache (run by build()).
 
     The C5 witness is planted with the host build of the interpreter
@@ -367,6 +514,10 @@ def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 1, lds_leaves
     syn = build_c5(hostemu.term_values, n_nodes=n_nodes)
     prog = compile_program(syn.conjuncts)
     t0 = time.perf_counter()
-    _, names, dt = compile_device([prog], "x", waves=waves, lds_leaves=lds_leaves)
-    log(f"[jit] C5 kernel {names[0]}: {'compiled in %.0f s' % dt if dt else 'cached'}")
+    if split:
+        objs, dt = compile_parts(prog, "x", waves=waves, lds_leaves=lds_leaves)
+        names = [n for _, n in objs]
+    else:
+        _, names, dt = compile_device([prog], "x", waves=waves, lds_leaves=lds_leaves)
+    log(f"[jit] C5 kernel {names[0]} ({len(names)} part(s)): {'compiled in %.0f s' % dt if dt else 'cached'}")
     return time.perf_counter() - t0

@@ -168,3 +168,21 @@ def test_lds_leaves_match_interpreter(dev, images_lds, planted):
             assert dev.search([a], s.seed, 0, 1 << 17, flags)[0] == dev.search([b], s.seed, 0, 1 << 17, flags)[0]
         a.free()
         b.free()
+
+
+def test_split_program_parts_match_interpreter(dev, planted):
+    """A program run as several part kernels (alive bits passed between them)
+    gives the interpreter's witnesses and verdicts, in every search mode."""
+    for s in planted[:2]:
+        p = compile_program(s.conjuncts)
+        a = dev.load(p)
+        b = dev.load(p)
+        jit.attach(dev, [b], split=True, part_weight=3000, lds_leaves=2)
+        assert dev.has_kernel(b) and "parts" in b.kernel
+        for flags in (0, isa.FLAG_EARLY_EXIT, isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT):
+            assert dev.search([a], s.seed, 0, 1 << 18, flags)[0] == dev.search([b], s.seed, 0, 1 << 18, flags)[0]
+        va, _ = dev.eval_generated(a, s.seed, s.witness_index - 5000, 6000, trace=False)
+        vb, _ = dev.eval_generated(b, s.seed, s.witness_index - 5000, 6000, trace=False)
+        assert np.array_equal(va, vb) and vb[5000] == 1
+        a.free()
+        b.free()

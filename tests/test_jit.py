@@ -166,3 +166,22 @@ def test_host_build_lds_leaves_match_oracle():
             assert v[j] == int(all(vals[c.id] for c in conj)), f"{name} verdict {j}"
             for node in nodes:
                 assert unpack_trace(p, tr, node)[j] == vals[node.id], f"{name} {node!r}[{j}]"
+
+
+def test_host_build_parts_and_to_whole_program():
+    """A program split into parts (jit.split_ssa) is the AND of its parts."""
+    from tests.test_gpu_jit import small_planted
+    s = small_planted(n_nodes=400, n_conj=8, density_log2=6)
+    p = compile_program(s.conjuncts)
+    segs = jit.split_ssa(p, part_weight=3000)
+    assert len(segs) >= 3
+    path, names = jit.compile_host([p], part_weight=3000)
+    lib = ctypes.CDLL(str(path))
+    n, begin = 512, s.witness_index - 300
+    acc = np.ones(n, dtype=np.uint32)
+    for name in names:
+        v, _ = host_run(lib, name, p, s.seed, begin, n)
+        acc &= v
+    whole, _ = emu_eval(p, None, n, seed=s.seed, begin=begin)
+    assert np.array_equal(acc, whole)
+    assert acc[300] == 1  # the planted witness
