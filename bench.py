@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--engine", choices=["jit", "interp"], default="jit",
                     help="jit: the program's specialised straight-line kernel (mythril_amd/jit.py); "
                          "interp: the bytecode interpreter")
-    ap.add_argument("--jit-waves", type=int, default=BENCH_WAVES, choices=[1, 2],
+    ap.add_argument("--jit-waves", type=int, default=BENCH_WAVES, choices=[1, 2, 3, 4],
                     help="waves per SIMD the specialised kernel is built for")
     ap.add_argument("--jit-split", type=int, default=int(BENCH_SPLIT), choices=[0, 1],
                     help="1: split the program into part kernels at conjunct boundaries")
@@ -88,8 +88,8 @@ def main():
         # one-time program preparation, like the upload: outside the timed region
         # (the in-tree cache, warmed by __graft_entry__.build(), usually makes it 0)
         from mythril_amd import jit
-        if args.jit_lds_leaves is None:
-            args.jit_lds_leaves = 10 if args.jit_waves == 2 else 0
+        if args.jit_lds_leaves is None:  # LDS: waves/SIMD x slots x 8 KiB per CU <= 160 KiB
+            args.jit_lds_leaves = {1: 0, 2: 10, 3: 6, 4: 5}[args.jit_waves]
         jit_s = jit.attach(dev, [dp], variants=BENCH_VARIANTS, waves=args.jit_waves, lds_leaves=args.jit_lds_leaves,
                            split=bool(args.jit_split))
     batch = 1 << args.batch_log2

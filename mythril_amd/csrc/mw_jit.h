@@ -162,14 +162,18 @@ MW_HD u32 nn_addc(u32 a, u32 b, u32 w) { return (u32)((((u64)a + b) >> w) & 1u);
 typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 #if defined(__HIP_DEVICE_COMPILE__)
 __shared__ u32x4 mw_jit_lds[MW_JIT_LDS_SLOTS * 2 * 256];
+// through an LDS (address space 3) pointer: ds_read/ds_write_b128 with 32-bit
+// addresses; a generic pointer would make them flat_load/store (64-bit address
+// registers, and sc0 sc1 for the volatile accesses)
+typedef volatile __attribute__((address_space(3))) u32x4 lds_u32x4;
 MW_HD void lds_put8(u32 slot, const u32 v[8]) {
-  volatile u32x4* p = mw_jit_lds + slot * 512u + threadIdx.x;
+  lds_u32x4* p = (lds_u32x4*)mw_jit_lds + slot * 512u + threadIdx.x;
   u32x4 a = {v[0], v[1], v[2], v[3]}, b = {v[4], v[5], v[6], v[7]};
   p[0] = a;
   p[256] = b;
 }
 MW_HD void lds_get8(u32 slot, u32 r[8]) {
-  volatile u32x4* p = mw_jit_lds + slot * 512u + threadIdx.x;
+  lds_u32x4* p = (lds_u32x4*)mw_jit_lds + slot * 512u + threadIdx.x;
   const u32x4 a = p[0], b = p[256];
   r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
   r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
