@@ -90,8 +90,14 @@ def main():
         from mythril_amd import jit
         if args.jit_lds_leaves is None:  # LDS: waves/SIMD x slots x 8 KiB per CU <= 160 KiB
             args.jit_lds_leaves = {1: 0, 2: 10, 3: 6, 4: 5}[args.jit_waves]
+        split = bool(args.jit_split)
+        if not split and not jit.is_cached([prog], BENCH_VARIANTS, args.jit_waves, args.jit_lds_leaves):
+            # one kernel compiles for ~6 min; its parts in ~1 min (parallel hipcc)
+            print("[bench] single-kernel code object not cached: using the split kernels", file=sys.stderr)
+            split = True
+        args.jit_split = int(split)
         jit_s = jit.attach(dev, [dp], variants=BENCH_VARIANTS, waves=args.jit_waves, lds_leaves=args.jit_lds_leaves,
-                           split=bool(args.jit_split))
+                           split=split)
     batch = 1 << args.batch_log2
 
     def step(k):
@@ -171,6 +177,7 @@ def main():
             "engine": args.engine + (f" ({dp.kernel}, {args.jit_waves} wave/SIMD, {args.jit_lds_leaves} leaves in LDS)"
                                      if dp.kernel else ""),
             "jit_compile_s": jit_s,
+            "jit_split": bool(args.jit_split) if args.engine == "jit" else None,
             "parallelism": f"candidate-shard x{world}",
             "witness_found_in_timed_range": found_any,
         },

@@ -4,6 +4,8 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 echo "== smoke"
 timeout -k 10 240 python3 -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -3 || exit 1
+echo "== gpu tests"
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 echo "== bench"
 timeout -k 10 600 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -5 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
@@ -20,3 +22,6 @@ for set in "SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,
   timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc/p$i -o run -- $B > gpurun_out/pmc/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmc/p$i.log; exit 1; }
 done
 echo pmc done
+echo "== torchrun (1 rank, RCCL path)"
+timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_torchrun.json 2> gpurun_out/bench_torchrun.err || { tail -5 gpurun_out/bench_torchrun.err; exit 1; }
+cat gpurun_out/bench_torchrun.json
