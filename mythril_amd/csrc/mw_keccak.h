@@ -22,7 +22,7 @@ MW_HD void keccak_f1600(u64 A[25]) {
                        27, 41, 56, 8, 25, 43, 62, 18, 39, 61, 20, 44};
   const int PI[24] = {10, 7, 11, 17, 18, 3, 5, 16, 8, 21, 24, 4,
                       15, 23, 19, 13, 12, 2, 20, 14, 22, 9, 6, 1};
-#pragma unroll 1
+#pragma unroll 4
   for (int rnd = 0; rnd < 24; ++rnd) {
     u64 C[5];
 #pragma unroll
@@ -54,27 +54,38 @@ MW_HD void keccak_f1600(u64 A[25]) {
   }
 }
 
-// absorb + squeeze one message; out = 32 digest bytes as 4 little-endian u64 lanes
+// absorb + squeeze one message; out = 32 digest bytes as 4 little-endian u64 lanes.
+// Whole 8-byte state lanes of a 4-byte-aligned message are read as two dwords;
+// only the lane that straddles the end of the message (and unaligned messages)
+// goes byte by byte.  Padding (0x01 ... 0x80, rate 136) is XORed in afterwards.
 MW_HD void keccak256_msg(const uint8_t* __restrict__ msg, u32 len, u64 out[4]) {
   u64 A[25];
 #pragma unroll
   for (int i = 0; i < 25; ++i) A[i] = 0;
+  const bool aligned = (((uintptr_t)msg) & 3u) == 0u;
   const u32 nblk = len / 136u + 1u;
   for (u32 blk = 0; blk < nblk; ++blk) {
     const u32 base = blk * 136u;
-    const bool last = (blk + 1u == nblk);
 #pragma unroll
     for (int lane = 0; lane < 17; ++lane) {
+      const u32 p0 = base + (u32)(lane * 8);
       u64 v = 0;
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        u32 pos = base + (u32)(lane * 8 + b);
-        u32 byte = pos < len ? (u32)msg[pos] : 0u;
-        if (last && pos == len) byte ^= 0x01u;
-        if (last && (lane * 8 + b) == 135) byte ^= 0x80u;
-        v |= (u64)byte << (8 * b);
+      if (aligned && p0 + 8u <= len) {
+        const u32* w = (const u32*)(msg + p0);
+        v = (u64)w[0] | ((u64)w[1] << 32);
+      } else if (p0 < len) {
+        for (u32 b = 0; b < 8u && p0 + b < len; ++b) v |= (u64)msg[p0 + b] << (8 * b);
       }
       A[lane] ^= v;
+    }
+    if (blk + 1u == nblk) {  // pad10*1 with Keccak's domain byte 0x01
+      const u32 r = len - base;  // 0..135 message bytes in this block
+#pragma unroll
+      for (int lane = 0; lane < 17; ++lane) {
+        u64 pad = ((u32)lane == r / 8u) ? (0x01ull << (8u * (r % 8u))) : 0ull;
+        if (lane == 16) pad ^= 0x80ull << 56;
+        A[lane] ^= pad;
+      }
     }
     keccak_f1600(A);
   }
