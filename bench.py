@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--nodes", type=int, default=10000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ttfw", action="store_true", help="skip the time-to-first-witness search")
     ap.add_argument("--engine", choices=["jit", "interp"], default="jit",
                     help="jit: the program's specialised straight-line kernel (mythril_amd/jit.py); "
                          "interp: the bytecode interpreter")
@@ -149,6 +150,8 @@ def main():
             dist.destroy_process_group()
         return
 
+    ttfw = None if args.no_ttfw else time_to_first_witness(dev, dp, syn.seed)
+
     cpu = None
     if not args.no_cpu_baseline:
         cpu = cpu_baseline(syn, prog, args.cpu_seconds)
@@ -180,6 +183,7 @@ def main():
             "jit_split": bool(args.jit_split) if args.engine == "jit" else None,
             "parallelism": f"candidate-shard x{world}",
             "witness_found_in_timed_range": found_any,
+            "time_to_first_witness": ttfw,
         },
         "roofline": {
             "bound": "valu-int32",
@@ -198,6 +202,20 @@ def main():
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def time_to_first_witness(dev, dp, seed, slice_log2=24, max_slices=64):
+    """time until the lowest satisfying index in [0, ...) is
+    known, searching slices of 2^24 candidates in order with stop-after-hit (one
+    rank, outside the timed region).  Reported next to the exhaustive rate."""
+    from mythril_amd import isa
+    flags = isa.FLAG_STOP_AFTER_HIT | isa.FLAG_EARLY_EXIT
+    t0 = time.perf_counter()
+    for k in range(max_slices):
+        (found,), _ = dev.search([dp], seed, k << slice_log2, 1 << slice_log2, flags)
+        if found is not None:
+            return {"seconds": time.perf_counter() - t0, "index": found, "candidates_searched": (k + 1) << slice_log2}
+    return {"seconds": time.perf_counter() - t0, "index": None, "candidates_searched": max_slices << slice_log2}
 
 
 def load_peak():
