@@ -365,25 +365,16 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
     r0 = sat ? s0 : r0;
     r1 = sat ? s1 : r1;
     r2 = sat ? c0 : 0u;
-    // u[j..j+5] -= qh * v[0..5]: the low and high halves of the six products
-    // come off in two independent borrow chains (no carry threaded through
-    // the multiplies), and both borrows and the last high half come off (r2:r1:r0)
-    u32 lo[6], hi[6];
+    // u[j..j+5] -= qh * v[0..5]; the borrow out comes off (r2:r1:r0)
+    u32 carry = 0, br = 0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      const u64 p = (u64)qh * v[k];
-      lo[k] = (u32)p;
-      hi[k] = (u32)(p >> 32);
-    }
-    u32 bl = 0, bh = 0;
-    u[j] = subb(u[j], lo[0], bl);
-#pragma unroll
-    for (int k = 1; k < 6; ++k) {
-      u[j + k] = subb(u[j + k], lo[k], bl);
-      u[j + k] = subb(u[j + k], hi[k - 1], bh);
+      const u64 p = (u64)qh * v[k] + carry;
+      carry = (u32)(p >> 32);
+      u[j + k] = subb(u[j + k], (u32)p, br);
     }
     const u64 R = (((u64)r1) << 32) | r0;
-    const u64 sub = (u64)hi[5] + bl + bh;
+    const u64 sub = (u64)carry + br;
     const bool neg = (r2 == 0u) && (R < sub);
     const u64 Rn = R - sub;
     u[j + 6] = (u32)Rn;
