@@ -44,6 +44,8 @@ _engine_lock = threading.Lock()
 _engine_failed = False
 _memo: Dict[tuple, tuple] = {}          # z3 AST-id key -> (witness, script)
 MEMO_MAX = 1 << 16
+_pending: list = []                     # successor constraint sets deferred by the JUMPI hook
+PENDING_MAX = 64
 
 
 def _env():
@@ -100,6 +102,14 @@ def _gpu_model(constraints, timeout):
     raws = [c.raw for c in constraints]
     key = memo_key(raws)
     hit = _memo.get(key)
+    if hit is None and _pending:
+        # the JUMPI successors LASER is about to prune one by one (svm.py:287-292):
+        # search all of them in one launch, then answer this one from the memo
+        batch = _pending[:]
+        _pending.clear()
+        STATS["batched_prefetches"] = STATS.get("batched_prefetches", 0) + 1
+        prefetch(batch)
+        hit = _memo.get(key)
     if hit is not None:
         STATS["memo_hits"] += 1
         witness, script = hit
@@ -151,6 +161,14 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
             return model
     STATS["fallbacks"] += 1
     return _reference(constraints, minimize, maximize, enforce_execution_time)
+
+
+def defer(constraints) -> None:
+    """Queue a fresh state's constraint set (the plugin's JUMPI post hook, run
+    on each successor before LASER's per-step prune): the next memo miss in
+    get_model searches every queued set in the same launch."""
+    if len(_pending) < PENDING_MAX:
+        _pending.append(constraints)
 
 
 def prefetch(constraint_sets) -> int:

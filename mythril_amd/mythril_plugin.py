@@ -7,9 +7,15 @@ Discovered through the ``mythril.plugins`` entry point
 (``mythril/interfaces/cli.py:37``, ``mythril/plugin/loader.py:71-78``).
 ``__call__`` builds the LASER plugin (``mythril/laser/plugin/builder.py``) whose
 ``initialize(vm)`` (``laser/plugin/interface.py:18``) rebinds ``get_model`` and
-registers a ``stop_sym_trans`` hook (``svm.py:243-245``): right before the next
-transaction's reachability prune over ``open_states`` (``svm.py:216-223``)
-every open state's constraint set is searched in ONE launch, and
+registers two batching hooks:
+
+* ``stop_sym_trans`` (``svm.py:243-245``): right before the next
+  transaction's reachability prune over ``open_states`` (``svm.py:216-223``)
+  every open state's constraint set is searched in ONE launch;
+* a JUMPI post hook (``svm.py:_execute_post_hook``, run on each successor):
+  the successors are queued, and the first per-step ``is_possible``
+  (``svm.py:287-292``) searches the pair in one launch.
+
 ``is_possible`` then finds the confirmed witness in the memo.  Exploration
 order is untouched.
 """
@@ -45,6 +51,16 @@ class WitnessBatchingLaserPlugin(_LaserPlugin):
                 log.warning("witness engine prefetch skipped: %s", e)
 
         symbolic_vm.register_laser_hooks("stop_sym_trans", prefetch_open_states)
+
+        def defer_successor(global_state):
+            # svm.py:_execute_post_hook runs this on each JUMPI successor before
+            # the per-step prune (svm.py:287-292) calls is_possible on them
+            try:
+                model.defer(global_state.world_state.constraints)
+            except Exception as e:  # never disturb the analysis
+                log.debug("witness engine: successor not deferred: %s", e)
+
+        symbolic_vm.register_hooks("post", {"JUMPI": [defer_successor]})
 
         def report():
             log.info("witness engine stats: %s", model.STATS)

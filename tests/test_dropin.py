@@ -208,3 +208,50 @@ def test_prefetch_batches_and_feeds_the_memo(mythril):
     assert dropin.get_model(sets[1]).raw[0][1]["x"] == 77
     assert dropin._engine.stats["searches"] == searches  # answered from the memo
     assert dropin.STATS["memo_hits"] >= 1
+
+
+def test_jumpi_successors_searched_in_one_launch(mythril):
+    """The plugin's JUMPI post hook defers both successors; the first get_model
+    searches them together and the second is answered from the memo."""
+    taken = (fb(CTX.app("bvugt", X, CTX.const(100, 8))),)
+    fallthrough = (fb(CTX.app("bvule", X, CTX.const(100, 8))),)
+    dropin._pending.clear()
+    dropin.defer(taken)
+    dropin.defer(fallthrough)
+    s0 = dropin._engine.stats["searches"]
+    assert dropin.get_model(taken).raw[0][1]["x"] > 100
+    assert dropin._engine.stats["searches"] == s0 + 1
+    assert dropin.get_model(fallthrough).raw[0][1]["x"] <= 100
+    assert dropin._engine.stats["searches"] == s0 + 1  # from the memo
+    assert not dropin._pending
+
+
+def test_plugin_registers_rebinding_and_batching_hooks(mythril):
+    """WitnessBatchingLaserPlugin.initialize (laser/plugin/interface.py:18) with a
+    stand-in LaserEVM: stop_sym_trans prefetch, stop_sym_exec report, JUMPI post
+    hook that defers successors."""
+    from mythril_amd.mythril_plugin import MI355XWitnessEngine, WitnessBatchingLaserPlugin
+
+    class VM:
+        def __init__(self):
+            self.laser, self.post, self.open_states = {}, {}, []
+
+        def register_laser_hooks(self, kind, hook):
+            self.laser.setdefault(kind, []).append(hook)
+
+        def register_hooks(self, kind, hooks):
+            assert kind == "post"
+            for op, fs in hooks.items():
+                self.post.setdefault(op, []).extend(fs)
+
+    vm = VM()
+    plugin = MI355XWitnessEngine()()
+    assert isinstance(plugin, WitnessBatchingLaserPlugin)
+    plugin.initialize(vm)
+    assert set(vm.laser) >= {"stop_sym_trans", "stop_sym_exec"} and "JUMPI" in vm.post
+    dropin._pending.clear()
+    state = types.SimpleNamespace(world_state=types.SimpleNamespace(constraints=SAT))
+    vm.post["JUMPI"][0](state)
+    assert dropin._pending == [SAT]
+    vm.laser["stop_sym_trans"][0]()  # no open states: a no-op
+    dropin._pending.clear()
