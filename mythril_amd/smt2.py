@@ -17,10 +17,10 @@ from __future__ import annotations
 
 import re
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Tuple, Union
+from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 from .compiler import Unsupported
-from .ir import BOOL, BOOL_OPS, BV_OPS, ALIASES, Ctx, Node
+from .ir import BOOL, BOOL_OPS, BV_OPS, ALIASES, Ctx, Node, topo
 
 Sexp = Union[str, list]
 
@@ -247,3 +247,79 @@ def parse_script(text: str, ctx: Optional[Ctx] = None) -> Script:
 def parse_file(path: str, ctx: Optional[Ctx] = None) -> Script:
     with open(path) as f:
         return parse_script(f.read(), ctx)
+
+
+# --------------------------------------------------------------------------- printer
+def _q(name: str) -> str:
+    return f"|{name}|"
+
+
+def _bvsort(w: int) -> str:
+    return "Bool" if w == BOOL else f"(_ BitVec {w})"
+
+
+def to_smt2(asserts: Sequence[Node], minimize: Sequence[Node] = (), maximize: Sequence[Node] = ()) -> str:
+    """SMT-LIB2 text in the shape z3's ``Optimize.sexpr()`` gives ``--solver-log``
+    (mythril/support/model.py:45-56): declarations, one ``assert`` per
+    conjunct with shared subterms ``let``-bound, objectives, ``check-sat``.
+    ``parse_script(to_smt2(...))`` rebuilds the same terms."""
+    roots = list(asserts) + list(minimize) + list(maximize)
+    nodes = topo(roots)
+    out: List[str] = []
+    seen = set()
+    for n in nodes:
+        if n.op == "var" and n.name not in seen:
+            seen.add(n.name)
+            out.append(f"(declare-fun {_q(n.name)} () {_bvsort(n.width)})")
+        elif n.op == "array" and n.name not in seen:
+            seen.add(n.name)
+            out.append(f"(declare-fun {_q(n.name)} () (Array (_ BitVec {n.dom}) (_ BitVec {n.width})))")
+        elif n.op == "apply" and n.name not in seen:
+            seen.add(n.name)
+            doms = " ".join(f"(_ BitVec {w})" for w in n.params)
+            out.append(f"(declare-fun {_q(n.name)} ({doms}) (_ BitVec {n.width}))")
+
+    def atom(n: Node, names: Dict[int, str]) -> str:
+        if n.id in names:
+            return names[n.id]
+        if n.op == "const":
+            if n.width == BOOL:
+                return "true" if n.val else "false"
+            if n.width % 4 == 0:
+                return "#x" + format(n.val, f"0{n.width // 4}x")
+            return "#b" + format(n.val, f"0{n.width}b")
+        if n.op in ("var", "array"):
+            return _q(n.name)
+        args = " ".join(names.get(a.id) or atom(a, names) for a in n.args)
+        if n.op in ("extract", "zero_extend", "sign_extend", "repeat", "rotate_left", "rotate_right"):
+            return f"((_ {n.op} {' '.join(str(p) for p in n.params)}) {args})"
+        if n.op == "const_array":
+            return f"((as const (Array (_ BitVec {n.dom}) (_ BitVec {n.width}))) {args})"
+        if n.op == "apply":
+            return f"({_q(n.name)} {args})"
+        return f"({n.op} {args})"
+
+    def term(root: Node) -> str:
+        # let-bind every non-leaf subterm used more than once within this root
+        sub = topo([root])
+        uses: Dict[int, int] = {}
+        for m in sub:
+            for a in m.args:
+                uses[a.id] = uses.get(a.id, 0) + 1
+        names: Dict[int, str] = {}
+        lets: List[Tuple[str, str]] = []
+        for m in sub:
+            if m is not root and uses.get(m.id, 0) > 1 and m.args:
+                nm = f"a!{len(lets) + 1}"
+                lets.append((nm, atom(m, names)))
+                names[m.id] = nm
+        body = atom(root, names)
+        for nm, t in reversed(lets):
+            body = f"(let (({nm} {t})) {body})"
+        return body
+
+    out += [f"(assert {term(a)})" for a in asserts]
+    out += [f"(minimize {term(m)})" for m in minimize]
+    out += [f"(maximize {term(m)})" for m in maximize]
+    out.append("(check-sat)")
+    return "\n".join(out) + "\n"

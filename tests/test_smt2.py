@@ -87,3 +87,34 @@ def test_numerals_and_indexed_ops():
 """)
     vals = eval_nodes(s.asserts, {"x": 0x0102})
     assert all(vals[a.id] for a in s.asserts)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_printer_round_trip(seed):
+    """to_smt2 -> parse_script rebuilds terms that evaluate identically (random
+    DAGs over every lowered op, plus arrays, UFs and keccak conditions)."""
+    import random
+    from mythril_amd.ir import Ctx
+    from mythril_amd.smt2 import to_smt2
+    from tests.helpers import RandDag, random_assignments
+    from tests.mythril_shapes import KeccakManager, calldata_load
+    rng = random.Random(seed)
+    dag = RandDag(500 + seed)
+    conj = [dag.boolean(4) for _ in range(3)]
+    c = dag.ctx
+    km = KeccakManager(c)
+    idx = c.var("idx", 256)
+    conj.append(c.app("bvult", c.app("zero_extend", calldata_load(c, "1", idx), params=(248,)),
+                      km.create_keccak(c.var("k", 256))))
+    conj.append(km.create_conditions())
+    text = to_smt2(conj, minimize=[c.var("1_calldatasize", 256)])
+    s = parse_script(text, Ctx())
+    assert len(s.asserts) == len(conj) and len(s.minimize) == 1
+    for m in random_assignments(dag.vars + dag.bvars, 20, rng, dag):
+        m = dict(m, idx=rng.choice([0, 3, 40]), k=rng.getrandbits(256), **{"1_calldatasize": 64})
+        m["1_calldata"] = ArrayVal({i: rng.getrandbits(8) for i in range(64)}, 0)
+        for fn in ("keccak256_256", "keccak256_256-1"):
+            m[fn] = ({}, 7)
+        a = eval_nodes(conj, m)
+        b = eval_nodes(s.asserts, m)
+        assert [a[t.id] for t in conj] == [b[t.id] for t in s.asserts]
