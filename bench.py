@@ -204,13 +204,13 @@ def main():
         dist.destroy_process_group()
 
 
-def time_to_first_witness(dev, dp, seed, slice_log2=24, max_slices=16):
+def time_to_first_witness(dev, dp, seed, slice_log2=24, max_slices=128):
     """time until the lowest satisfying index in [0, ...) is
     known, searching slices of 2^24 candidates in order with stop-after-hit (one
-    rank, outside the timed region), at most 2^28 candidates.  Reported next to
+    rank, outside the timed region), at most 2^31 candidates.  Reported next to
     the exhaustive rate.  (C5's planted witness sits at index 0x5EED0005 mod 2^31
-    and its conjunct thresholds leave few others, so this mostly times the
-    2^28-candidate sweep.)"""
+    = 1 592 590 341 and its conjunct thresholds leave few others, so this times
+    a ~1.6 G-candidate sweep with stop-after-hit.)"""
     from mythril_amd import isa
     flags = isa.FLAG_STOP_AFTER_HIT | isa.FLAG_EARLY_EXIT
     t0 = time.perf_counter()

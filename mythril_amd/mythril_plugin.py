@@ -17,7 +17,9 @@ registers two batching hooks:
   (``svm.py:287-292``) searches the pair in one launch.
 
 ``is_possible`` then finds the confirmed witness in the memo.  Exploration
-order is untouched.
+order is untouched.  It also installs the batched Keccak-256 service
+(``keccak_service.install``) behind ``find_concrete_keccak`` and
+``_replace_with_actual_sha``.
 """
 from __future__ import annotations
 
@@ -39,8 +41,9 @@ class WitnessBatchingLaserPlugin(_LaserPlugin):
     """LASER plugin: rebinding + transaction-boundary batching."""
 
     def initialize(self, symbolic_vm) -> None:
-        from . import model
+        from . import keccak_service, model
         model.install()
+        keccak_service.install()
 
         def prefetch_open_states():
             try:
@@ -64,6 +67,8 @@ class WitnessBatchingLaserPlugin(_LaserPlugin):
 
         def report():
             log.info("witness engine stats: %s", model.STATS)
+            if keccak_service.service() is not None:
+                log.info("keccak service stats: %s", keccak_service.service().stats)
 
         symbolic_vm.register_laser_hooks("stop_sym_exec", report)
 

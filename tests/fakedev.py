@@ -43,5 +43,18 @@ class FakeDevice:
     def eval_generated(self, dp, seed, begin, count, trace=True):
         return emu_eval(dp.prog, None, count, seed=seed, begin=begin)
 
+    def keccak256(self, msgs):
+        """Device.keccak256 on the host build of the same Keccak source."""
+        from tests.helpers import host_emu
+        self.keccak_launches = getattr(self, "keccak_launches", 0) + 1
+        data = b"".join(msgs) or b"\0"
+        off = np.zeros(len(msgs), dtype=np.uint64)
+        if len(msgs) > 1:
+            off[1:] = np.cumsum([len(m) for m in msgs[:-1]])
+        ln = np.array([len(m) for m in msgs], dtype=np.uint32)
+        out = np.zeros(32 * len(msgs), dtype=np.uint8)
+        host_emu().mwh_keccak256(data, off.ctypes.data, ln.ctypes.data, len(msgs), out.ctypes.data)
+        return [out[32 * i:32 * i + 32].tobytes() for i in range(len(msgs))], {}
+
     def close(self):
         pass

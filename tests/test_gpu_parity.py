@@ -189,3 +189,31 @@ def test_division_rare_paths_gpu(dev):
         v, _ = dev.eval_generated(dp, 1, 0, 256, trace=False)
         assert int(v.sum()) == 256
         dp.free()
+
+
+def test_keccak_service_on_device(dev):
+    """mythril_amd.keccak_service over mg_keccak256: one launch for a batch of
+    distinct messages, memo answers repeats, replace_with_actual_sha output
+    identical to the per-window reference loop (tests/test_keccak_service.py)."""
+    from mythril_amd.keccak_service import KeccakService, replace_with_actual_sha
+    from tests.test_keccak_service import _placeholder, _reference_replace
+    svc = KeccakService(device=dev, reference=None, min_batch=1)
+    rng = random.Random(17)
+    # mapping-slot preimages of the three LASER actors x 300 slots (512-bit concat(key, slot))
+    actors = [0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE, 0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF,
+              0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA]
+    pre = [(512, (a << 256) | s) for a in actors for s in range(300)]
+    assert svc.prefetch_values(pre) == len(pre)
+    assert svc.stats["launches"] == 1 and svc.stats["gpu_hashes"] == len(pre)
+    for size, v in pre[::37]:
+        assert svc.find_concrete_keccak_int(v, size) == int.from_bytes(keccak256(v.to_bytes(64, "big")), "big")
+    assert svc.stats["launches"] == 1
+    holders = [_placeholder(rng) for _ in range(40)]
+    table = {h: (256, rng.getrandbits(256)) for h in holders[:30]}
+    txs = [{"input": "0x" + "a9059cbb" + "".join("%064x" % rng.choice(holders) for _ in range(6))}
+           for _ in range(8)]
+    ref = [dict(t) for t in txs]
+    replace_with_actual_sha(txs, table.get, svc)
+    _reference_replace(ref, table.get)
+    assert txs == ref
+    assert svc.stats["launches"] == 2
