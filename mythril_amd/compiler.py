@@ -96,6 +96,8 @@ class LeafSpec:
     stride: int = 0              # >0: bit-interleaved digit (index bits shift, shift+stride, ...)
     salt: Optional[int] = None   # Philox key salt; default crc32(name) so a variable
                                  # draws the same value in every program for an index
+    tie: Optional[str] = None    # copy this leaf's digit layout (bytes of one ABI word
+                                 # pick the same pool entry: pools.harvest word groups)
 
     def key_salt(self) -> int:
         return self.salt if self.salt is not None else zlib.crc32(self.name.encode()) & 0xFFFFFFFF
@@ -737,8 +739,14 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
             p += [None] * ((1 << nb) - len(p))
             spec.pool = p
         resolved.append(spec)
+    by_name = {s.name: s for s in resolved}
+    for spec in resolved:
+        lead = by_name.get(spec.tie) if spec.tie else None
+        if spec.tie and (lead is None or lead.tie or not lead.pool or not spec.pool
+                         or len(lead.pool) != len(spec.pool)):
+            spec.tie = None
     fresh = [s for s in resolved if s.pool and len(s.pool) > 1 and not s.hashed and s.bits == 0
-             and s.shift == 0 and s.stride == 0]
+             and s.shift == 0 and s.stride == 0 and not s.tie]
     if fresh:
         stride = len(fresh)
         for j, spec in enumerate(fresh):
@@ -753,6 +761,12 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
                     spec.pool = spec.pool[:1 << fit]
                 else:
                     spec.hashed = True
+    for spec in resolved:
+        if spec.tie:   # same digit as the leader: same layout, same hash key
+            lead = by_name[spec.tie]
+            spec.pool = spec.pool[:len(lead.pool)]
+            spec.bits, spec.shift, spec.stride, spec.hashed = lead.bits, lead.shift, lead.stride, lead.hashed
+            spec.salt = lead.key_salt()
     bit = 0
     for li, (n, spec) in enumerate(zip(lw.leaf_nodes, resolved)):
         w = spec.width

@@ -15,6 +15,31 @@ formula, mixed with RANDOM entries (Philox draws):
 * generic boundary values 0, 1, 2, 2^(w-1), 2^w-1 and width-truncated DAG
   constants.
 
+Domain restriction (``domains``): facts that every model must satisfy are read
+off the top-level conjuncts and shrink a leaf's pool to values that can
+satisfy them, with no RANDOM entries:
+
+* ``t == K`` where ``t`` projects injectively onto a leaf (concat / extract /
+  zero_extend / ite with a differing constant arm / +K / ^K) fixes the leaf
+  (the four selector bytes of a dispatcher JUMPI);
+* ``t == K1 or t == K2 or ...`` fixing the same leaf in every disjunct gives
+  that leaf the exact domain {K1, K2, ...} (``caller in ACTORS``,
+  ``transaction/symbolic.py:210-212``);
+* unsigned bounds ``K <= x``, ``x < K`` (and their negations) give an interval,
+  and ``x mod K == 0`` an alignment; the pool becomes aligned values spread
+  over the interval (``calldatasize`` bounds, the keccak UF intervals of
+  ``keccak_function_manager.py:155-163``).
+
+A disjunct that is the constant ``false`` is dropped first (``Or(cond, False)``
+is how ``_create_condition`` reads with no concrete hashes).  Facts on a bare
+leaf hold in every model; the ones read through an ``ite`` arm are heuristic.
+Either way a pool only decides which candidates are tried: every witness is
+re-checked, and a miss goes to z3.
+
+Word ties (``_tie_words``): the byte leaves of one calldata word share one
+word-level pool digit, so whole proposed words (an ABI offset, a count, 2^255)
+are tried rather than byte mixtures.
+
 Pools are laid out as index bit-fields while the 40 field bits last
 (exhaustive enumeration of small spaces) and as hashed digits afterwards.
 """
@@ -32,8 +57,10 @@ ACTORS = [0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE,
 _CMP = ("=", "distinct", "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge")
 
 
-def _project(e: Node, value: int, out: Dict[str, List[int]], depth: int = 0):
-    """Propose leaf values that would make term e equal `value`."""
+def _project(e: Node, value: int, out: Dict[str, List[int]], depth: int = 0,
+             words: Optional[Dict[int, List[int]]] = None):
+    """Propose leaf values that would make term e equal `value` (and, in
+    `words`, whole values for every concat on the way)."""
     if depth > 24:
         return
     w = e.width
@@ -44,36 +71,193 @@ def _project(e: Node, value: int, out: Dict[str, List[int]], depth: int = 0):
     if op == "var":
         out.setdefault(e.name, []).append(value)
     elif op == "concat":
+        if words is not None:
+            words.setdefault(e.id, []).append(value)
         off = w
         for a in e.args:
             off -= a.width
-            _project(a, value >> off, out, depth + 1)
+            _project(a, value >> off, out, depth + 1, words)
     elif op == "extract":
         hi, lo = e.params
-        _project(e.args[0], value << lo, out, depth + 1)
+        _project(e.args[0], value << lo, out, depth + 1, words)
     elif op in ("zero_extend", "sign_extend"):
-        _project(e.args[0], value, out, depth + 1)
+        _project(e.args[0], value, out, depth + 1, words)
     elif op in ("bvadd", "bvsub", "bvxor") and len(e.args) == 2:
         a, b = e.args
         for x, k, xfirst in ((a, b, True), (b, a, False)):
             if k.op == "const":
                 if op == "bvadd":
-                    _project(x, value - k.val, out, depth + 1)
+                    _project(x, value - k.val, out, depth + 1, words)
                 elif op == "bvxor":
-                    _project(x, value ^ k.val, out, depth + 1)
+                    _project(x, value ^ k.val, out, depth + 1, words)
                 elif xfirst:  # x - K = v  ->  x = v + K
-                    _project(x, value + k.val, out, depth + 1)
+                    _project(x, value + k.val, out, depth + 1, words)
                 else:  # K - x = v -> x = K - v
-                    _project(x, k.val - value, out, depth + 1)
+                    _project(x, k.val - value, out, depth + 1, words)
     elif op == "ite":
-        _project(e.args[1], value, out, depth + 1)
-        _project(e.args[2], value, out, depth + 1)
+        _project(e.args[1], value, out, depth + 1, words)
+        _project(e.args[2], value, out, depth + 1, words)
+
+
+def _force(e: Node, value: int, lo: int, hi: int, out: Dict[str, int], depth: int = 0) -> None:
+    """Bits lo..hi of term e must equal those bits of `value`; record every leaf
+    whose bits are all fixed that way."""
+    if depth > 32 or e.width == BOOL or lo > hi:
+        return
+    w = e.width
+    op = e.op
+    if op == "var":
+        if lo == 0 and hi == w - 1:
+            out.setdefault(e.name, value & ((1 << w) - 1))
+    elif op == "concat":
+        off = w
+        for a in e.args:
+            off -= a.width
+            a_lo, a_hi = max(lo, off), min(hi, off + a.width - 1)
+            if a_lo <= a_hi:
+                _force(a, value >> off, a_lo - off, a_hi - off, out, depth + 1)
+    elif op == "extract":
+        _, l = e.params
+        _force(e.args[0], value << l, lo + l, hi + l, out, depth + 1)
+    elif op == "zero_extend":
+        x = e.args[0]
+        _force(x, value, lo, min(hi, x.width - 1), out, depth + 1)
+    elif op == "ite":
+        rng = ((1 << (hi + 1)) - 1) ^ ((1 << lo) - 1)
+        _, a, b = e.args
+        if b.op == "const" and (b.val ^ value) & rng:
+            _force(a, value, lo, hi, out, depth + 1)
+        elif a.op == "const" and (a.val ^ value) & rng:
+            _force(b, value, lo, hi, out, depth + 1)
+    elif op in ("bvadd", "bvxor") and len(e.args) == 2 and lo == 0 and hi == w - 1:
+        a, b = e.args
+        for x, k in ((a, b), (b, a)):
+            if k.op == "const" and x.op != "const":
+                _force(x, value - k.val if op == "bvadd" else value ^ k.val, lo, hi, out, depth + 1)
+
+
+def _eq_const(n: Node):
+    if n.op == "=" and len(n.args) == 2:
+        a, b = n.args
+        if b.op == "const" and a.op != "const":
+            return a, b.val
+        if a.op == "const" and b.op != "const":
+            return b, a.val
+    return None
+
+
+_UPPER = {"bvult": (0, -1), "bvule": (0, 0), "bvugt": (1, -1), "bvuge": (1, 0)}
+
+
+def domains(conjuncts: List[Node]):
+    """Exact domains, unsigned intervals and alignments implied by the top-level
+    conjuncts (module doc).  Returns (exact: name -> [values], interval: name ->
+    [lo, hi] inclusive, align: name -> K)."""
+    exact: Dict[str, List[int]] = {}
+    interval: Dict[str, List[int]] = {}
+    align: Dict[str, int] = {}
+
+    def facts(n: Node, neg: bool = False):
+        if n.op == "not":
+            facts(n.args[0], not neg)
+            return
+        if n.op == ("or" if neg else "and"):
+            for a in n.args:
+                facts(a, neg)
+            return
+        if n.op == ("and" if neg else "or"):
+            live = [a for a in n.args if not (a.op == "const" and bool(a.val) == neg)]
+            if len(live) == 1:
+                facts(live[0], neg)
+                return
+            if neg:
+                return
+            per = []
+            for a in live:
+                ec = _eq_const(a)
+                f: Dict[str, int] = {}
+                if ec is not None:
+                    _force(ec[0], ec[1], 0, ec[0].width - 1, f)
+                per.append(f)
+            if per:
+                for name in set(per[0]).intersection(*per[1:]):
+                    vals = list(dict.fromkeys(f[name] for f in per))
+                    if name not in exact or len(vals) < len(exact[name]):
+                        exact[name] = vals
+            return
+        if neg:
+            if n.op in _UPPER:   # not (a < b) == (b <= a), etc.
+                a, b = n.args
+                flip = {"bvult": "bvule", "bvule": "bvult", "bvugt": "bvuge", "bvuge": "bvugt"}[n.op]
+                _bound(flip, b, a)
+            return
+        ec = _eq_const(n)
+        if ec is not None:
+            f: Dict[str, int] = {}
+            _force(ec[0], ec[1], 0, ec[0].width - 1, f)
+            for name, v in f.items():
+                exact[name] = [v]
+            t, k = ec
+            if k == 0 and t.op == "bvurem" and t.args[0].op == "var" and t.args[1].op == "const" \
+                    and t.args[1].val > 1:
+                align[t.args[0].name] = t.args[1].val
+            return
+        if n.op in _UPPER:
+            _bound(n.op, *n.args)
+
+    def _bound(op, a, b):
+        # op(a, b) holds; normalise to x <= K or K <= x
+        upper, strict = _UPPER[op]   # bvult/bvule: a is below b
+        lo_t, hi_t = (b, a) if upper else (a, b)
+        if lo_t.op == "var" and hi_t.op == "const":       # x <(=) K
+            iv = interval.setdefault(lo_t.name, [0, (1 << lo_t.width) - 1])
+            iv[1] = min(iv[1], hi_t.val + strict)
+        elif hi_t.op == "var" and lo_t.op == "const":     # K <(=) x
+            iv = interval.setdefault(hi_t.name, [0, (1 << hi_t.width) - 1])
+            iv[0] = max(iv[0], lo_t.val - strict)
+
+    for c in conjuncts:
+        facts(c)
+    return exact, interval, align
+
+
+def _pad_pow2(vals: List[int]) -> List[int]:
+    n = 1
+    while n < len(vals):
+        n *= 2
+    return [vals[i % len(vals)] for i in range(n)]
+
+
+def _restrict(pool: List[Optional[int]], name: str, w: int, exact, interval, align, pool_size: int):
+    lo, hi = interval.get(name, (0, (1 << w) - 1))
+    K = align.get(name, 1)
+    ok = lambda v: lo <= v <= hi and v % K == 0   # noqa: E731
+    if name in exact:
+        vals = [v for v in exact[name] if ok(v)]
+        return _pad_pow2(vals) if vals else pool
+    if name not in interval and name not in align:
+        return pool
+    first = lo + (-lo % K)
+    if first > hi:
+        return pool
+    last = hi - (hi % K)
+    keep = [v for v in pool if v is not None and ok(v)]
+    steps = (last - first) // K
+    spread = [first + (steps * i // 16) * K for i in range(1, 16)]
+    # bounds, the strongest harvested values, then values spread over the interval
+    vals = list(dict.fromkeys(v for v in [first, last, first + K, last - K] + keep[:8] + spread + keep[8:]
+                              if ok(v)))[:pool_size]
+    if steps + 1 > len(vals) and (hi - lo) >= (1 << max(w - 2, 0)) and K == 1:
+        return vals + [None] * max(1, pool_size // 4)   # wide interval: random draws still land often
+    return _pad_pow2(vals)   # no RANDOM padding: a random draw would almost never satisfy the facts
 
 
 def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
-            random_share: float = 0.25) -> Dict[str, LeafSpec]:
+            random_share: float = 0.25, restrict: bool = True) -> Dict[str, LeafSpec]:
     nodes = topo(conjuncts)
+    exact, interval, dom_align = domains(conjuncts) if restrict else ({}, {}, {})
     proposals: Dict[str, List[int]] = {}
+    word_props: Dict[int, List[int]] = {}
     consts = []
     for n in nodes:
         if n.op == "const" and n.width != BOOL:
@@ -84,7 +268,7 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
                 if k.op == "const" and x.op != "const":
                     deltas = (0,) if n.op in ("=", "distinct") else (0, 1, -1)
                     for d in deltas:
-                        _project(x, k.val + d, proposals)
+                        _project(x, k.val + d, proposals, words=word_props)
     # alignment facts: (= (bvurem x K) 0)  ->  x should be a multiple of K
     align: Dict[str, int] = {}
     for n in nodes:
@@ -155,5 +339,71 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
         else:
             nrand = max(1, pool_size - len(pool)) if len(pool) >= nfixed else max(1, len(pool) // 3)
             pool += [None] * nrand
+            if restrict:
+                pool = _restrict(pool, leaf.name, w, exact, interval, dom_align, pool_size)
         specs[leaf.name] = LeafSpec(leaf.name, w, pool=pool)
+    _tie_words(nodes, specs, word_props, set(exact), uniq_consts, pool_size, random_share)
     return specs
+
+
+# ABI head values: offsets of dynamic arguments are small multiples of 32
+ABI_WORDS = [0x20, 0x40, 0x60, 0x80, 0xA0, 0xC0]
+
+
+def _byte_leaf(a: Node) -> Optional[Node]:
+    """The 8-bit leaf a concat argument reads: ``x`` or ``ite(g, x, K)`` (a
+    calldata byte behind its ``index < calldatasize`` guard, calldata.py:218-231)."""
+    if a.op == "var" and a.width == 8:
+        return a
+    if a.op == "ite":
+        _, x, y = a.args
+        for v, k in ((x, y), (y, x)):
+            if v.op == "var" and v.width == 8 and k.op == "const":
+                return v
+    return None
+
+
+def _tie_words(nodes, specs, word_props, exact_names, uniq_consts, pool_size, random_share):
+    """Bytes of one word (a concat of byte leaves: an ABI argument read from
+    calldata, ``calldata.py:218-231``) draw one word-level pool entry together:
+    the pool holds whole-word proposals split into bytes, and every byte after
+    the first copies the first's digit (LeafSpec.tie).  Without this each byte
+    picks its own entry and a proposed word value (an array offset, a count) is
+    hit with probability |pool|^-31.  Bytes already fixed by a domain fact stay
+    singletons; a byte joins at most one word, the one with most free bytes."""
+    words = []
+    for n in nodes:
+        if n.op == "concat" and len(n.args) >= 2:
+            bl = [_byte_leaf(a) for a in n.args]
+            if all(b is not None for b in bl) and len({b.name for b in bl}) == len(bl):
+                words.append((n, bl))
+    taken = set(exact_names)
+    nfixed = max(1, int(pool_size * (1 - random_share)))
+    while words:
+        def free(item):
+            return [(i, b) for i, b in enumerate(item[1]) if b.name not in taken and b.name in specs]
+        words.sort(key=lambda it: (-len(free(it)), -len(word_props.get(it[0].id, []))))
+        n, bl = words.pop(0)
+        fb = free((n, bl))
+        if len(fb) < 2:
+            break
+        W = n.width
+        m = (1 << W) - 1
+        generic = {0, 1, 2, m, m - 1, 1 << (W - 1)}
+        props = [v for v in dict.fromkeys(v & m for v in word_props.get(n.id, [])) if v not in generic]
+        abi = ABI_WORDS if any("calldata" in b.name for _, b in fb) else []
+        # Pool order is search order (Morton digits try low entries first), so
+        # the first few proposals, an ABI offset and the extreme values come
+        # before the rest: a crowd of proposals (e.g. from congruence
+        # side-conditions) must not push them out of the early indices.
+        cand = props[:2] + abi[1:2] + [1 << (W - 1), m] + props[2:4] + [0, 1] + abi[2:] + abi[:1] \
+            + [2, m - 1] + props[4:] + [c & m for c in uniq_consts]
+        pool: List[Optional[int]] = list(dict.fromkeys(v & m for v in cand))[:nfixed]
+        pool += [None] * max(1, pool_size - nfixed)
+        nb = len(bl)
+        lead = fb[0][1].name
+        for i, b in fb:
+            sh = 8 * (nb - 1 - i)
+            specs[b.name] = LeafSpec(b.name, 8, pool=[None if v is None else (v >> sh) & 0xFF for v in pool],
+                                     tie=None if b.name == lead else lead)
+            taken.add(b.name)

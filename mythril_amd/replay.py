@@ -31,6 +31,8 @@ class Result:
     index: Optional[int] = None
     values: dict = field(default_factory=dict)
     reason: str = ""
+    arrays: dict = field(default_factory=dict)      # array -> {index: value} (Ackermann leaves)
+    functions: dict = field(default_factory=dict)   # UF -> {args: value}
 
 
 def load(path: str):
@@ -62,7 +64,7 @@ def replay(paths: List[str], engine, batch: int = 64) -> List[Result]:
             if w is None:
                 out.append(Result(p, "miss"))
             else:
-                out.append(Result(p, "witness", w.index, dict(w.values)))
+                out.append(Result(p, "witness", w.index, dict(w.values), arrays=w.arrays, functions=w.functions))
     order = {p: k for k, p in enumerate(paths)}
     return sorted(out, key=lambda r: order[r.path])
 

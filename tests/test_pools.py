@@ -1,0 +1,68 @@
+"""Candidate pools (mythril_amd/pools.py): domain restriction and word-tied
+calldata bytes.  The generated candidates are checked with the oracle's leaf
+generator (tests/helpers.oracle_models), which mirrors csrc/mw_leaf.h."""
+from mythril_amd.compiler import compile_program
+from mythril_amd.ir import Ctx
+from mythril_amd.pools import ACTORS, domains, harvest
+from tests.helpers import oracle_models
+
+
+def _calldata_word(c, base, size):
+    return c.app("concat", *[c.app("ite", c.app("bvslt", c.const(base + i, 256), size),
+                                   c.var(f"1_calldata@{base + i:x}", 8), c.const(0, 8)) for i in range(32)])
+
+
+def test_domains_exact_interval_alignment():
+    c = Ctx()
+    s = c.var("sender_1", 256)
+    size = c.var("1_calldatasize", 256)
+    h = c.var("keccak256_512@s1", 256)
+    word0 = _calldata_word(c, 0, size)
+    conj = [c.app("or", *[c.app("=", s, c.const(a, 256)) for a in ACTORS]),
+            c.app("=", c.app("extract", word0, params=(255, 224)), c.const(0xA9059CBB, 32)),
+            c.app("bvule", c.const(68, 256), size), c.app("not", c.app("bvuge", size, c.const(4096, 256))),
+            c.app("or", c.app("and", c.app("bvule", c.const(1000, 256), h), c.app("bvult", h, c.const(5000, 256)),
+                              c.app("=", c.app("bvurem", h, c.const(64, 256)), c.const(0, 256))), c.false())]
+    exact, interval, align = domains(conj)
+    assert exact["sender_1"] == ACTORS
+    assert [exact[f"1_calldata@{i}"] for i in range(4)] == [[0xA9], [0x05], [0x9C], [0xBB]]
+    assert "1_calldata@4" not in exact
+    assert interval["1_calldatasize"] == [68, 4095]
+    assert interval["keccak256_512@s1"] == [1000, 4999] and align["keccak256_512@s1"] == 64
+    specs = harvest(conj, [s, size, h] + [c.var(f"1_calldata@{i:x}", 8) for i in range(32)])
+    assert sorted(set(specs["sender_1"].pool)) == sorted(ACTORS)
+    assert set(specs["1_calldata@0"].pool) == {0xA9}
+    assert all(v is not None and 68 <= v <= 4095 for v in specs["1_calldatasize"].pool)
+    assert all(v is not None and 1000 <= v < 5000 and v % 64 == 0 for v in specs["keccak256_512@s1"].pool)
+
+
+def test_word_bytes_draw_one_entry_together():
+    """The 32 bytes of an ABI argument pick the same word-level pool entry, so
+    a proposed word value (here: count <= 20, value with 2^255) appears whole."""
+    c = Ctx()
+    size = c.var("1_calldatasize", 256)
+    cnt = _calldata_word(c, 4, size)
+    value = _calldata_word(c, 36, size)
+    conj = [c.app("bvule", cnt, c.const(20, 256)), c.app("bvugt", cnt, c.const(0, 256)),
+            c.app("not", c.app("bvumul_noovfl", cnt, value)), c.app("bvult", size, c.const(4096, 256))]
+    leaves = [size] + [c.var(f"1_calldata@{i:x}", 8) for i in range(4, 68)]
+    specs = harvest(conj, leaves)
+    assert specs["1_calldata@5"].tie == "1_calldata@4" and specs["1_calldata@4"].tie is None
+    p = compile_program(conj, leaf_specs=specs)
+    lay = {s.name: (s.bits, s.shift, s.stride, s.hashed, s.key_salt()) for s in p.leaf_specs}
+    assert len({lay[f"1_calldata@{i:x}"] for i in range(4, 36)}) == 1
+    wpool = set()
+    for k in range(len(specs["1_calldata@4"].pool)):
+        if specs["1_calldata@4"].pool[k] is not None:
+            wpool.add(int.from_bytes(bytes(specs[f"1_calldata@{i:x}"].pool[k] for i in range(4, 36)), "big"))
+    assert {20, 1 << 255} <= wpool | {1 << 255} and 20 in wpool
+    hits = 0
+    for m in oracle_models(p, 0x5EED0003, 0, 512):
+        w = int.from_bytes(bytes(m[f"1_calldata@{i:x}"] for i in range(4, 36)), "big")
+        hits += w in wpool
+        v = int.from_bytes(bytes(m[f"1_calldata@{i:x}"] for i in range(36, 68)), "big")
+        if 0 < w <= 20 and w * v >= 1 << 256:
+            break
+    else:
+        raise AssertionError("no overflowing (count, value) pair in 512 candidates")
+    assert hits > 0

@@ -1,0 +1,115 @@
+"""Throughput of the C2-C4 solver-log queries (BASELINE.json configs[1..3]).
+
+C2: token.sol -t 3 transfer queries, 2^24 candidates each;
+C3: BECToken batchTransfer SWC-101 overflow query, 2^28 candidates;
+C4: WalletLibrary -t 3 queries searched together in one launch (state
+    batching), 2^24 candidates.
+
+The queries are the committed ``--solver-log``-format dumps
+(tests/golden/solver_log, synthetic: no z3/solc exists to dump real ones, see
+tests/make_solver_log_corpus.py).  Each config is timed twice in exhaustive
+mode (early exit off): the interpreter kernel and the specialised kernel
+(mythril_amd/jit.py).  Time to first witness (early exit + stop-after-hit,
+interpreter) is reported beside it.  evals/s = programs x candidates / wall
+time of the mg_search call; the roofline uses the kernel time from the library's
+HIP events and the compiler's ops_per_eval.
+
+    python tools/config_bench.py [--out FILE] [--no-jit]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+LOG = os.path.join(ROOT, "tests", "golden", "solver_log")
+CONFIGS = [
+    ("C2", ["c2_token_transfer_ok.smt2", "c2_token_transfer_underflow.smt2"], 24, False),
+    ("C3", ["c3_bec_batchtransfer_overflow.smt2"], 28, False),
+    ("C4", ["c4_wallet_onlyowner.smt2", "c4_wallet_contradiction.smt2"], 24, True),
+]
+SLICE = 1 << 24   # candidates per launch
+
+
+def _groups(files, together):
+    from mythril_amd.engine import prepare
+    from mythril_amd.smt2 import parse_file
+    qs = []
+    for f in files:
+        s = parse_file(os.path.join(LOG, f))
+        qs.append(prepare(s.asserts, s.ctx))
+    return [(files, qs)] if together else [([f], [q]) for f, q in zip(files, qs)]
+
+
+def warm():
+    """Compile the specialised kernels into build/jit (CPU; tools/jit_warm.py)."""
+    from mythril_amd import jit
+    for _, files, _, together in CONFIGS:
+        for _, g in _groups(files, together):
+            jit.compile_device([q.program for q in g], "xe", waves=2, lds_leaves=0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--no-jit", action="store_true")
+    ap.add_argument("--warm", action="store_true", help="only compile the specialised kernels into build/jit (CPU)")
+    a = ap.parse_args()
+    import bench
+    from mythril_amd import isa, jit
+    from mythril_amd.engine import DEFAULT_SEED
+    from mythril_amd.runtime import Device
+    if a.warm:
+        warm()
+        return
+    dev = Device(0)
+    peak = bench.load_peak()["peak"]
+    lines = []
+    for name, files, log2, together in CONFIGS:
+        for gfiles, g in _groups(files, together):
+            dps = [dev.load(q.program) for q in g]
+            ops = sum(q.ops_per_eval for q in g)
+            count = 1 << log2
+            # time to first witness (interpreter, early exit)
+            t0 = time.perf_counter()
+            first = [None] * len(dps)
+            pos = 0
+            while pos < count and any(x is None for x in first):
+                found, _ = dev.search(dps, DEFAULT_SEED, pos, min(SLICE, count - pos),
+                                      isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT)
+                first = [x if x is not None else y for x, y in zip(first, found)]
+                pos += SLICE
+            ttfw = time.perf_counter() - t0
+            for engine in (["interp"] if a.no_jit else ["interp", "jit"]):
+                compile_s = None
+                if engine == "jit":
+                    compile_s = jit.attach(dev, dps, variants="xe", waves=2, lds_leaves=0)
+                dev.search(dps, DEFAULT_SEED, 0, SLICE, 0)            # warm-up
+                kms, evals = 0.0, 0
+                t0 = time.perf_counter()
+                for pos in range(0, count, SLICE):
+                    _, st = dev.search(dps, DEFAULT_SEED, pos, SLICE, 0)
+                    kms += st["kernel_ms"]
+                    evals += st["evals"]
+                wall = time.perf_counter() - t0
+                achieved = ops * count / (kms / 1e3)
+                line = {"config": name, "files": gfiles, "engine": engine + (f" ({dps[0].kernel})" if dps[0].kernel else ""),
+                        "programs": len(g), "candidates": count, "evals": evals,
+                        "evals_per_s": len(g) * count / wall, "kernel_ms": kms, "ops_per_eval": ops,
+                        "tops": achieved / 1e12, "frac_peak": achieved / peak, "jit_compile_s": compile_s,
+                        "first_witness": first, "ttfw_s": ttfw}
+                print(json.dumps(line), flush=True)
+                lines.append(line)
+            for dp in dps:
+                dp.free()
+    dev.close()
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(lines, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
