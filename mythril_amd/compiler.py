@@ -506,6 +506,9 @@ def _flatten(conjuncts: Iterable[Node]) -> List[Node]:
 
 
 # --------------------------------------------------------------------------- scheduling
+HOIST_CAP = 16
+
+
 def _schedule_narrow_early(insns: List[MInsn]) -> List[MInsn]:
     """Move every instruction with a narrow (N) result right after the last
     definition of its operands.
@@ -534,6 +537,11 @@ def _schedule_narrow_early(insns: List[MInsn]) -> List[MInsn]:
         movable = ((ins.dst is not None and ins.dst.cls == "N" and nonleaf
                     and not ins.op.startswith(("LEAF", "FILL", "MOV")))
                    or (ins.op == "CHECK" and nonleaf))
+        if movable and ins.op != "CHECK":
+            # at most HOIST_CAP results per definition point: one wide value read
+            # by thousands of comparisons (the congruence premises of a symbolic
+            # calldata offset) would otherwise make them all live at once
+            movable = len(after.get(max(anchor[s.id] for s in srcs), ())) < HOIST_CAP
         if movable:
             a = max(anchor[s.id] for s in srcs)
             after.setdefault(a, []).append(ins)

@@ -242,12 +242,47 @@ class _Rewriter:
                     t, u = reads[i], reads[j]
                     if all(a.op == "const" for a in t.args) and all(a.op == "const" for a in u.args):
                         continue  # distinct concrete cells: nothing to relate
-                    same = [self.eq(x, y) for x, y in zip(t.args, u.args)]
+                    if any(_never_equal(x, y) for x, y in zip(t.args, u.args)):
+                        continue  # e.g. cells base+3 and base+7 of one symbolic offset
+                    same = [self.eq(*_fold_offsets(c, x, y)) for x, y in zip(t.args, u.args)]
                     prem = c.app("and", *same) if len(same) > 1 else same[0]
                     vt = t.value if t.value is not None else self.wide_var(t.name, t.width)
                     vu = u.value if u.value is not None else self.wide_var(u.name, u.width)
                     out.append(c.app("=>", prem, self.eq(vt, vu)))
         return out
+
+
+def _offset(n: Node):
+    """(base, k) with n == base + k (mod 2^w), for a const k; (n, 0) otherwise."""
+    if n.op == "bvadd" and len(n.args) == 2:
+        a, b = n.args
+        if b.op == "const" and a.op != "const":
+            return a, b.val
+        if a.op == "const" and b.op != "const":
+            return b, a.val
+    return n, 0
+
+
+def _fold_offsets(c: Ctx, x: Node, y: Node):
+    """x = y with a constant offset moved across: (b + k = K) -> (b = K - k), so
+    every congruence premise of one symbolic calldata offset compares the SAME
+    base term with constants (one live value instead of one per cell)."""
+    for a, k in ((x, y), (y, x)):
+        if k.op == "const":
+            b, off = _offset(a)
+            if off and b.width == a.width:
+                return b, c.const(k.val - off, a.width)
+    return x, y
+
+
+def _never_equal(x: Node, y: Node) -> bool:
+    """True when x = y is false under every assignment: two distinct constants,
+    or one term plus two different constant offsets (the bytes of one ABI word
+    read at a symbolic calldata offset, calldata.py:218-231)."""
+    if x.op == "const" and y.op == "const":
+        return x.val != y.val
+    (bx, kx), (by, ky) = _offset(x), _offset(y)
+    return bx is by and x.width == y.width and (kx - ky) % (1 << x.width) != 0
 
 
 def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
