@@ -7,7 +7,37 @@
 
 namespace mw {
 
-MW_HD u64 rotl64(u64 x, int n) { return (x << n) | (x >> (64 - n)); }
+// 64-bit rotate by a constant 0 < n < 64 on 32-bit halves: two v_alignbit_b32
+// (LLVM otherwise emits two 64-bit shifts and two ORs)
+MW_HD u64 rotl64(u64 x, int n) {
+  u32 lo = (u32)x, hi = (u32)(x >> 32);
+  if (n >= 32) {
+    const u32 t = lo;
+    lo = hi;
+    hi = t;
+    n -= 32;
+  }
+  if (n == 0) return (u64)lo | ((u64)hi << 32);
+  const u32 nh = alignbit(hi, lo, 32u - (u32)n), nl = alignbit(lo, hi, 32u - (u32)n);
+  return (u64)nl | ((u64)nh << 32);
+}
+
+// gfx950 3-input logic (v_bitop3_b32; truth table over src0=0xF0, src1=0xCC,
+// src2=0xAA): a^b^c = 0x96, a^(~b&c) = 0xD2.  One instruction per 32-bit half
+// where plain C takes two (theta's column parity, chi).
+#if defined(__HIP_DEVICE_COMPILE__)
+template <unsigned TT>
+__device__ __forceinline__ u64 bitop3_64(u64 a, u64 b, u64 c) {
+  const u32 lo = __builtin_amdgcn_bitop3_b32((u32)a, (u32)b, (u32)c, TT);
+  const u32 hi = __builtin_amdgcn_bitop3_b32((u32)(a >> 32), (u32)(b >> 32), (u32)(c >> 32), TT);
+  return (u64)lo | ((u64)hi << 32);
+}
+MW_HD u64 xor3_64(u64 a, u64 b, u64 c) { return bitop3_64<0x96>(a, b, c); }
+MW_HD u64 chi_64(u64 a, u64 b, u64 c) { return bitop3_64<0xD2>(a, b, c); }
+#else
+MW_HD u64 xor3_64(u64 a, u64 b, u64 c) { return a ^ b ^ c; }
+MW_HD u64 chi_64(u64 a, u64 b, u64 c) { return a ^ (~b & c); }
+#endif
 
 MW_HD void keccak_f1600(u64 A[25]) {
   const u64 RC[24] = {
@@ -26,12 +56,12 @@ MW_HD void keccak_f1600(u64 A[25]) {
   for (int rnd = 0; rnd < 24; ++rnd) {
     u64 C[5];
 #pragma unroll
-    for (int x = 0; x < 5; ++x) C[x] = A[x] ^ A[x + 5] ^ A[x + 10] ^ A[x + 15] ^ A[x + 20];
+    for (int x = 0; x < 5; ++x) C[x] = xor3_64(xor3_64(A[x], A[x + 5], A[x + 10]), A[x + 15], A[x + 20]);
 #pragma unroll
     for (int x = 0; x < 5; ++x) {
-      u64 D = C[(x + 4) % 5] ^ rotl64(C[(x + 1) % 5], 1);
+      const u64 c1 = C[(x + 4) % 5], r1 = rotl64(C[(x + 1) % 5], 1);
 #pragma unroll
-      for (int y = 0; y < 25; y += 5) A[y + x] ^= D;
+      for (int y = 0; y < 25; y += 5) A[y + x] = xor3_64(A[y + x], c1, r1);
     }
     u64 t = A[1];
 #pragma unroll
@@ -44,11 +74,11 @@ MW_HD void keccak_f1600(u64 A[25]) {
 #pragma unroll
     for (int y = 0; y < 25; y += 5) {
       u64 r0 = A[y], r1 = A[y + 1], r2 = A[y + 2], r3 = A[y + 3], r4 = A[y + 4];
-      A[y] = r0 ^ (~r1 & r2);
-      A[y + 1] = r1 ^ (~r2 & r3);
-      A[y + 2] = r2 ^ (~r3 & r4);
-      A[y + 3] = r3 ^ (~r4 & r0);
-      A[y + 4] = r4 ^ (~r0 & r1);
+      A[y] = chi_64(r0, r1, r2);
+      A[y + 1] = chi_64(r1, r2, r3);
+      A[y + 2] = chi_64(r2, r3, r4);
+      A[y + 3] = chi_64(r3, r4, r0);
+      A[y + 4] = chi_64(r4, r0, r1);
     }
     A[0] ^= RC[rnd];
   }
