@@ -25,6 +25,11 @@ log = logging.getLogger(__name__)
 
 DEFAULT_SEED = 0x5EED_0001
 DEFAULT_BUDGET = 1 << 22  # candidates per query (early exit + stop-after-hit)
+# u32 ops per launch (sum of the programs' ops_per_eval x candidates): bounds what
+# a miss costs before z3 answers.  2^22 candidates of a 2 000-op query, a few ms
+# on the interpreter; a 14 000-op C3-class query gets ~600 k candidates.
+DEFAULT_OP_BUDGET = (1 << 22) * 2000
+MIN_CANDIDATES = 1 << 16
 
 
 @dataclass
@@ -97,13 +102,15 @@ def _combine_chunks(values: Dict[str, int], name: str, width: int) -> int:
 class WitnessEngine:
     """Owns one device context; everything goes through the C-ABI."""
 
-    def __init__(self, device: int = 0, seed: int = DEFAULT_SEED, budget: int = DEFAULT_BUDGET, dev=None):
+    def __init__(self, device: int = 0, seed: int = DEFAULT_SEED, budget: int = DEFAULT_BUDGET, dev=None,
+                 op_budget: Optional[int] = DEFAULT_OP_BUDGET):
         if dev is None:
             from .runtime import Device  # raises EngineUnavailable without the HIP library / GPU
             dev = Device(device)
         self.dev = dev
         self.seed = seed
         self.budget = budget
+        self.op_budget = op_budget
         self.stats = {"searches": 0, "programs": 0, "hits": 0, "evals": 0, "kernel_ms": 0.0}
 
     def close(self):
@@ -113,7 +120,7 @@ class WitnessEngine:
                flags: int = isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT) -> List[Optional[Witness]]:
         if not queries:
             return []
-        count = count or self.budget
+        count = count or self.launch_count(queries)
         dps = [self.dev.load(q.program) for q in queries]
         try:
             found, st = self.dev.search(dps, self.seed, begin, count, flags)
@@ -131,6 +138,14 @@ class WitnessEngine:
                 self.stats["hits"] += 1
             out.append(w)
         return out
+
+    def launch_count(self, queries: Sequence[Query]) -> int:
+        """Candidates per query for one launch: the candidate budget, cut so the
+        launch stays within op_budget u32 ops (never below MIN_CANDIDATES)."""
+        if not self.op_budget:
+            return self.budget
+        ops = max(1, sum(q.ops_per_eval for q in queries))
+        return max(min(self.budget, MIN_CANDIDATES), min(self.budget, self.op_budget // ops))
 
     def materialize(self, q: Query, index: int) -> Optional[Witness]:
         from .runtime import unpack_trace

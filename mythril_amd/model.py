@@ -68,7 +68,9 @@ def engine():
                     from .engine import WitnessEngine
                     dev = int(os.environ.get("LOCAL_RANK", os.environ.get("MYTHRIL_AMD_DEVICE", "0")))
                     budget = int(os.environ.get("MYTHRIL_AMD_BUDGET", str(1 << 22)))
-                    _engine = WitnessEngine(device=dev, budget=budget)
+                    from .engine import DEFAULT_OP_BUDGET
+                    op_budget = int(os.environ.get("MYTHRIL_AMD_OP_BUDGET", str(DEFAULT_OP_BUDGET)))
+                    _engine = WitnessEngine(device=dev, budget=budget, op_budget=op_budget)
                 except Exception as e:  # EngineUnavailable / EngineError
                     log.warning("MI355X witness engine unavailable (%s); using z3 only", e)
                     _engine_failed = True

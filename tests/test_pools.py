@@ -66,3 +66,19 @@ def test_word_bytes_draw_one_entry_together():
     else:
         raise AssertionError("no overflowing (count, value) pair in 512 candidates")
     assert hits > 0
+
+
+def test_launch_count_bounds_ops_per_launch():
+    """engine.WitnessEngine.launch_count: a miss on an expensive query costs at
+    most op_budget u32 ops before z3 answers."""
+    from types import SimpleNamespace
+    from mythril_amd.engine import MIN_CANDIDATES, WitnessEngine
+    from tests.fakedev import FakeDevice
+    eng = WitnessEngine(dev=FakeDevice(), budget=1 << 22, op_budget=(1 << 22) * 2000)
+    q = lambda ops: SimpleNamespace(ops_per_eval=ops)   # noqa: E731
+    assert eng.launch_count([q(1187)]) == 1 << 22
+    assert eng.launch_count([q(14000)]) == (1 << 22) * 2000 // 14000
+    assert eng.launch_count([q(10 ** 9)]) == MIN_CANDIDATES
+    assert eng.launch_count([q(1000), q(1000), q(1000)]) == (1 << 22) * 2000 // 3000
+    eng.op_budget = None
+    assert eng.launch_count([q(10 ** 9)]) == 1 << 22
