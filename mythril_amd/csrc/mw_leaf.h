@@ -124,6 +124,11 @@ MW_HD void leaf_value(const u32* __restrict__ leaf_, const u32* __restrict__ poo
     const u32* e = pool + leaf[MW_LEAF_POOL] + (u64)digit * MW_POOL_ENTRY_WORDS;
     if (e[0] & 1u) {
       random_leaf(id, w, seed, cand, out);
+    } else if (w <= 32u) {  // narrow leaf (calldata bytes, Bools): one limb of the entry, not eight
+      out[0] = e[1];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) out[k] = 0u;
+      canon(out, w);
     } else {
 #pragma unroll
       for (int k = 0; k < 8; ++k) out[k] = e[1 + k];
