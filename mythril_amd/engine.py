@@ -13,7 +13,7 @@ from __future__ import annotations
 import copy
 import logging
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 from . import isa
 from .compiler import LeafSpec, Program, Unsupported, compile_program
@@ -46,9 +46,19 @@ class Query:
     conjuncts: List[Node]
     lowered: Lowered
     program: Program
-    trace_program: Program
+    trace_build: "Callable[[], Program]"     # the materialisation program, compiled on first use
     arg_terms: List[Node]
     arg_chunks: Dict[str, List[List[Node]]] = field(default_factory=dict)
+    _trace: Optional[Program] = None
+
+    @property
+    def trace_program(self) -> Program:
+        """Same conjuncts and leaf layout as ``program``, tracing every leaf and
+        array index / function argument.  Only a witness needs it, so it is
+        compiled lazily (half of prepare()'s cost on a miss)."""
+        if self._trace is None:
+            self._trace = self.trace_build()
+        return self._trace
 
     @property
     def ops_per_eval(self) -> int:
@@ -82,8 +92,9 @@ def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True) -> Quer
             per.append(parts)
             arg_terms.extend(parts)
         arg_chunks[al.name] = per
-    tprog = compile_program(low.conjuncts, leaf_specs=fixed, trace=list(prog.leaf_nodes) + arg_terms)
-    q = Query(ctx, conj, low, prog, tprog, arg_terms)
+    traced = list(prog.leaf_nodes) + arg_terms
+    q = Query(ctx, conj, low, prog, lambda: compile_program(low.conjuncts, leaf_specs=fixed, trace=traced),
+              arg_terms)
     q.arg_chunks = arg_chunks
     return q
 
