@@ -82,3 +82,28 @@ def test_launch_count_bounds_ops_per_launch():
     assert eng.launch_count([q(1000), q(1000), q(1000)]) == (1 << 22) * 2000 // 3000
     eng.op_budget = None
     assert eng.launch_count([q(10 ** 9)]) == 1 << 22
+
+
+def test_congruence_trimming_is_sound():
+    """lower._never_equal / _fold_offsets: pairs skipped are unequal under every
+    assignment, and folded premises are equivalent (checked with the oracle on
+    random assignments, widths 8 and 256)."""
+    import random
+    from mythril_amd.lower import _fold_offsets, _never_equal
+    from oracle.dag_eval import eval_nodes
+    rng = random.Random(5)
+    for w in (8, 256):
+        c = Ctx()
+        b = c.var("b", w)
+        terms = [b] + [c.app("bvadd", b, c.const(k, w)) for k in (1, 3, (1 << w) - 1, 1 << (w - 1))] + \
+                [c.app("bvadd", c.const(7, w), b), c.const(5, w), c.const(9, w)]
+        for x in terms:
+            for y in terms:
+                fx, fy = _fold_offsets(c, x, y)
+                eq, feq = c.app("=", x, y), c.app("=", fx, fy)
+                for _ in range(40):
+                    v = rng.choice([0, 1, 5, 9, (1 << w) - 1, rng.getrandbits(w)])
+                    vals = eval_nodes([eq, feq], {"b": v})
+                    assert vals[eq.id] == vals[feq.id], (x, y, v)
+                    if _never_equal(x, y):
+                        assert not vals[eq.id], (x, y, v)
