@@ -311,9 +311,8 @@ class _Lowerer:
                 return self._fold("N_XOR", 1, args)
             if op == "not":
                 return self.emit("N_XOR", 1, [args[0], self.k(1, 1)])
-            if op == "=>":
-                na = self.emit("N_XOR", 1, [args[0], self.k(1, 1)])
-                return self.emit("N_OR", 1, [na, args[1]])
+            if op == "=>":   # a => b  ==  a <=u b on Bools: one instruction instead of not + or
+                return self.emit("N_ULEN", 1, [args[0], args[1]])
             if op in ("=", "distinct"):
                 aw = _w(n.args[0])
                 if n.args[0].is_array:
