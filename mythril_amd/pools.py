@@ -380,13 +380,16 @@ def _tie_words(nodes, specs, word_props, exact_names, uniq_consts, pool_size, ra
     taken = set(exact_names)
     nfixed = max(1, int(pool_size * (1 - random_share)))
     while words:
-        def free(item):
-            return [(i, b) for i, b in enumerate(item[1]) if b.name not in taken and b.name in specs]
-        words.sort(key=lambda it: (-len(free(it)), -len(word_props.get(it[0].id, []))))
-        n, bl = words.pop(0)
-        fb = free((n, bl))
-        if len(fb) < 2:
+        scored = []
+        for n, bl in words:
+            f = [(i, b) for i, b in enumerate(bl) if b.name not in taken and b.name in specs]
+            if len(f) >= 2:   # a word with fewer free bytes never regains them
+                scored.append(((len(f), len(word_props.get(n.id, ()))), n, bl, f))
+        if not scored:
             break
+        best = max(scored, key=lambda x: x[0])
+        _, n, bl, fb = best
+        words = [(m, ml) for _, m, ml, _ in scored if m is not n]
         W = n.width
         m = (1 << W) - 1
         generic = {0, 1, 2, m, m - 1, 1 << (W - 1)}
