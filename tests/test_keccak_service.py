@@ -150,3 +150,75 @@ def test_replace_with_actual_sha_identical_to_reference(seed):
     _reference_replace(b, lambda v: pre.get(v), code_bc)
     assert a == b
     assert getattr(dev, "keccak_launches", 0) <= 1
+
+
+def test_install_rebinds_reference_sites(monkeypatch):
+    """keccak_service.install() against stand-ins for the Mythril modules it
+    touches (mythril is not importable here): find_concrete_keccak and
+    _replace_with_actual_sha are rebound and give the reference's results."""
+    import sys
+    import types
+
+    from mythril_amd import keccak_service, model
+    from mythril_amd.engine import WitnessEngine
+
+    class BitVecVal:
+        def __init__(self, v, size):
+            self.value, self._size = v, size
+            self.raw = ("val", v)
+
+        def size(self):
+            return self._size
+
+    sf = types.SimpleNamespace(BitVecVal=BitVecVal)
+
+    class Inverse:
+        def __call__(self, x):
+            return types.SimpleNamespace(raw=("inv", x.value))
+
+    class KFM:
+        @staticmethod
+        def find_concrete_keccak(data):
+            raise AssertionError("reference path must not run")
+
+    manager = KFM()
+    placeholder = 0xFFFFFFFF00000000000000000000000000000000000000000000000000000040
+    preimage = 0xDEADBEEF
+    manager.store_function = {256: (None, Inverse())}
+    manager.get_concrete_hash_data = lambda m: {256: [placeholder]}
+
+    class Z3Model:
+        def eval(self, raw):
+            assert raw == ("inv", placeholder)
+            return types.SimpleNamespace(as_long=lambda: preimage)
+
+    mods = {
+        "mythril": types.ModuleType("mythril"),
+        "mythril.analysis": types.ModuleType("mythril.analysis"),
+        "mythril.analysis.solver": types.SimpleNamespace(_replace_with_actual_sha=None),
+        "mythril.support": types.ModuleType("mythril.support"),
+        "mythril.support.support_utils": types.SimpleNamespace(sha3=keccak256),
+        "mythril.laser": types.ModuleType("mythril.laser"),
+        "mythril.laser.smt": types.SimpleNamespace(symbol_factory=sf),
+        "mythril.laser.ethereum": types.ModuleType("mythril.laser.ethereum"),
+        "mythril.laser.ethereum.function_managers": types.ModuleType("mythril.laser.ethereum.function_managers"),
+        "mythril.laser.ethereum.function_managers.keccak_function_manager":
+            types.SimpleNamespace(KeccakFunctionManager=KFM, keccak_function_manager=manager, sha3=None),
+    }
+    for k, v in mods.items():
+        monkeypatch.setitem(sys.modules, k, v)
+    mods["mythril.laser.ethereum.function_managers"].keccak_function_manager = \
+        mods["mythril.laser.ethereum.function_managers.keccak_function_manager"]
+    monkeypatch.setattr(keccak_service, "_service", None)
+    monkeypatch.setattr(model, "_engine", WitnessEngine(dev=FakeDevice(), budget=1 << 10))
+    monkeypatch.setattr(model, "_engine_failed", False)
+    assert keccak_service.install()
+    svc = keccak_service.service()
+    assert svc is not None and svc.device is model._engine.dev
+    h = KFM.find_concrete_keccak(BitVecVal(5, 256))
+    assert h.value == int.from_bytes(keccak256((5).to_bytes(32, "big")), "big") and h.size() == 256
+    kmod = mods["mythril.laser.ethereum.function_managers.keccak_function_manager"]
+    assert kmod.sha3("0x") .hex() == EMPTY
+    txs = [{"input": "0x" + "a9059cbb" + "%064x" % placeholder + "%064x" % 7}]
+    mods["mythril.analysis.solver"]._replace_with_actual_sha(txs, Z3Model())
+    assert txs[0]["input"] == "0x" + "a9059cbb" + keccak256(preimage.to_bytes(32, "big")).hex() + "%064x" % 7
