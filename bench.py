@@ -153,7 +153,7 @@ def main():
     ttfw = None if args.no_ttfw else time_to_first_witness(dev, dp, syn.seed)
 
     cpu = None
-    if not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline:   # the CPU baseline is an N=1 figure
         cpu = cpu_baseline(syn, prog, args.cpu_seconds)
 
     out = {
