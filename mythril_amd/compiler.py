@@ -508,6 +508,33 @@ def _flatten(conjuncts: Iterable[Node]) -> List[Node]:
 HOIST_CAP = 16
 
 
+def _fuse_checks(insns: List[MInsn]) -> List[MInsn]:
+    """Interpreter bytecode only (``Program.ssa`` keeps the unfused list for
+    jit.py): ``t = a <=u b`` (a Bool implication, see ``=>`` in _lower)
+    immediately followed by ``CHECK t``, with t used nowhere else, becomes one
+    ``CHECK_IMP a, b``.  The interpreter is dispatch-bound, and C3's 2 176
+    congruence conjuncts are exactly this pair."""
+    uses: Dict[int, int] = {}
+    for ins in insns:
+        for s in ins.srcs:
+            if isinstance(s, VReg):
+                uses[s.id] = uses.get(s.id, 0) + 1
+    out: List[MInsn] = []
+    i = 0
+    while i < len(insns):
+        ins = insns[i]
+        nxt = insns[i + 1] if i + 1 < len(insns) else None
+        if (ins.op == "N_ULEN" and ins.width == 1 and ins.dst is not None and nxt is not None
+                and nxt.op == "CHECK" and len(nxt.srcs) == 1 and isinstance(nxt.srcs[0], VReg)
+                and nxt.srcs[0].id == ins.dst.id and uses.get(ins.dst.id, 0) == 1):
+            out.append(MInsn("CHECK_IMP", 1, None, list(ins.srcs)))
+            i += 2
+            continue
+        out.append(ins)
+        i += 1
+    return out
+
+
 def _schedule_narrow_early(insns: List[MInsn]) -> List[MInsn]:
     """Move every instruction with a narrow (N) result right after the last
     definition of its operands.
@@ -684,7 +711,7 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
     lw.emit_void("END", 0, [])
 
     lw.insns = _schedule_narrow_early(lw.insns)
-    insns, n_spill = _allocate(lw.insns)
+    insns, n_spill = _allocate(_fuse_checks(lw.insns))
 
     # constant pool
     consts: List[int] = []

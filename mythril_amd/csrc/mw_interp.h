@@ -101,6 +101,14 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
         break;
       }
+      case MW_CHECK_IMP: {
+        u32 p, q;
+        MW_FETCH_N(oa, p);
+        MW_FETCH_N(ob, q);
+        alive = alive && (p == 0u || q != 0u);
+        if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
+        break;
+      }
       case MW_LEAF_W:
         env.leaf(imm, r);
         wk = 1;

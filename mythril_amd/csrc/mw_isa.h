@@ -51,6 +51,7 @@ enum mw_opcode {
   MW_MOV_N = 9,    // N[dst] = N/K a
   MW_SPILL_N = 10,
   MW_FILL_N = 11,
+  MW_CHECK_IMP = 12,  // alive &= (N[a] == 0) | (N[b] != 0): a congruence conjunct a => b in one dispatch
 
   // wide: W[dst] = f(W/K a, W/K b) at `width`
   MW_W_ADD = 16, MW_W_SUB = 17, MW_W_MUL = 18, MW_W_AND = 19, MW_W_OR = 20,

@@ -34,6 +34,7 @@ bool op_shape(u32 op, OpShape& s) {
   switch (op) {
     case MW_END: return true;
     case MW_CHECK: s.a = 2; return true;
+    case MW_CHECK_IMP: s.a = 2; s.b = 2; return true;
     case MW_LEAF_W: s.dst = 3; return true;
     case MW_LEAF_N: s.dst = 4; return true;
     case MW_STORE_W: s.a = 1; return true;
@@ -110,7 +111,7 @@ int mg_validate_desc(const mg_prog_desc* d) {
       return fail(MG_E_PROG, "operand out of range at instruction " + std::to_string(i));
     if (s.dst == 3 || s.dst == 4 || s.a || s.b) {
       const u32 maxw = (s.wide || s.dst == 3) ? 256u : 32u;
-      if (op != MW_CHECK && op != MW_STORE_W && op != MW_STORE_N && op != MW_SPILL_W &&
+      if (op != MW_CHECK && op != MW_CHECK_IMP && op != MW_STORE_W && op != MW_STORE_N && op != MW_SPILL_W &&
           op != MW_SPILL_N && op != MW_FILL_W && op != MW_FILL_N && op != MW_MOV_W && op != MW_MOV_N &&
           op != MW_LEAF_W && op != MW_LEAF_N && (w < 1 || w > maxw))
         return fail(MG_E_PROG, "bad width " + std::to_string(w) + " at instruction " + std::to_string(i));

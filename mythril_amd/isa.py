@@ -13,7 +13,7 @@ LEAF_WIDTH, LEAF_KIND, LEAF_ID, LEAF_SHIFT, LEAF_BITS, LEAF_POOL, LEAF_INROW = r
 
 OPCODES = {
     "END": 0, "CHECK": 1, "LEAF_W": 2, "LEAF_N": 3, "STORE_W": 4, "STORE_N": 5,
-    "SPILL_W": 6, "FILL_W": 7, "MOV_W": 8, "MOV_N": 9, "SPILL_N": 10, "FILL_N": 11,
+    "SPILL_W": 6, "FILL_W": 7, "MOV_W": 8, "MOV_N": 9, "SPILL_N": 10, "FILL_N": 11, "CHECK_IMP": 12,
     "W_ADD": 16, "W_SUB": 17, "W_MUL": 18, "W_AND": 19, "W_OR": 20, "W_XOR": 21, "W_NOT": 22,
     "W_SHL": 23, "W_LSHR": 24, "W_ASHR": 25,
     "W_UDIV": 26, "W_UREM": 27, "W_SDIV": 28, "W_SREM": 29, "W_SMOD": 30,
@@ -32,7 +32,7 @@ OPCODES = {
 # operand classes: 'W' = W slot or 8-word constant, 'N' = N slot or 1-word constant
 # (dst class, [src classes for a, b, c])
 SHAPES = {
-    "END": (None, []), "CHECK": (None, ["N"]),
+    "END": (None, []), "CHECK": (None, ["N"]), "CHECK_IMP": (None, ["N", "N"]),
     "LEAF_W": ("W", []), "LEAF_N": ("N", []),
     "STORE_W": (None, ["W"]), "STORE_N": (None, ["N"]),
     "SPILL_W": (None, ["W"]), "FILL_W": ("W", []), "SPILL_N": (None, ["N"]), "FILL_N": ("N", []),

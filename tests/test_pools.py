@@ -107,3 +107,19 @@ def test_congruence_trimming_is_sound():
                     assert vals[eq.id] == vals[feq.id], (x, y, v)
                     if _never_equal(x, y):
                         assert not vals[eq.id], (x, y, v)
+
+
+def test_congruence_conjuncts_fuse_to_one_check():
+    """compiler._fuse_checks: C3's congruence conjuncts (a => b) become single
+    CHECK_IMP instructions in the interpreter bytecode; Program.ssa (the
+    specialised-kernel input) keeps the unfused pair."""
+    import os
+    from mythril_amd import isa
+    from mythril_amd.engine import prepare
+    from mythril_amd.smt2 import parse_file
+    s = parse_file(os.path.join(os.path.dirname(__file__), "golden", "solver_log",
+                                "c3_bec_batchtransfer_overflow.smt2"))
+    q = prepare(s.asserts, s.ctx)
+    ops = [int(w) & 0xFF for w in q.program.code.reshape(-1, 4)[:, 0]]
+    assert ops.count(isa.OPCODES["CHECK_IMP"]) >= 2000
+    assert all(i.op != "CHECK_IMP" for i in q.program.ssa)
