@@ -25,7 +25,6 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-NOMINAL_PEAK = 256 * 64 * 2.4e9  # SURVEY.md §8(d) derived INT32 VALU peak (u32 ops/s)
 # CDNA4 issues a wave64 VALU instruction in 2 cycles on a 32-lane SIMD
 # (MI355X_MICROARCH.md): 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 THEORETICAL_PEAK = 256 * 4 * 32 * 2.4e9
@@ -132,18 +131,15 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        w = torch.tensor([found_any if found_any is not None else (1 << 63) - 1], dtype=torch.int64,
-                         device=f"cuda:{local}")
-        dist.all_reduce(w, op=dist.ReduceOp.MIN)  # RCCL MIN of the witness index
-        found_any = None if int(w.item()) == (1 << 63) - 1 else int(w.item())
+        from mythril_amd.distributed import allreduce_min
+        (found_any,) = allreduce_min([found_any], device=f"cuda:{local}")  # RCCL MIN of the witness index
 
     total_evals = world * args.steps * batch
     value = total_evals / elapsed
     avg_kernel_s = sum(kms) / len(kms) / 1e3
     ops_launch = prog.ops_per_eval * batch
     achieved = ops_launch / avg_kernel_s
-    peak_info = load_peak()
-    peak = peak_info["peak"]
+    measured_peak = load_measured_peak()
 
     if rank != 0:
         if dist is not None:
@@ -154,7 +150,7 @@ def main():
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:   # the CPU baseline is an N=1 figure
-        cpu = cpu_baseline(syn, prog, args.cpu_seconds)
+        cpu = cpu_baseline(syn, prog, args.cpu_seconds, dev, dp)
 
     out = {
         "metric": "candidate-assignment evals/sec",
@@ -188,14 +184,15 @@ def main():
         "roofline": {
             "bound": "valu-int32",
             "achieved": achieved / 1e12,
-            "peak": peak / 1e12,
+            "peak": THEORETICAL_PEAK / 1e12,
             "unit": "Tops/s (u32)",
-            "frac": achieved / peak,
-            "traffic": load_traffic(prog, batch),
+            "frac": achieved / THEORETICAL_PEAK,
+            "traffic": load_traffic(prog, batch, dp.kernel),
             "kernel_ms_avg": avg_kernel_s * 1e3,
-            "peak_source": peak_info["source"],
-            "peak_theoretical": THEORETICAL_PEAK / 1e12,
-            "frac_theoretical": achieved / THEORETICAL_PEAK,
+            "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (wave64 VALU op = 2 cycles)",
+            "peak_measured": measured_peak / 1e12 if measured_peak else None,
+            "frac_measured": achieved / measured_peak if measured_peak else None,
+            "peak_measured_source": "v_add_u32 microbenchmark, 8 chains x 8 waves/SIMD (profiles/valu_peak.json)",
         },
         "cpu_baseline": cpu,
     }
@@ -221,39 +218,48 @@ def time_to_first_witness(dev, dp, seed, slice_log2=24, max_slices=128):
     return {"seconds": time.perf_counter() - t0, "index": None, "candidates_searched": max_slices << slice_log2}
 
 
-def load_peak():
-    """INT32 VALU peak: the measured v_add_u32 microbenchmark (profiles/valu_peak.json) when
-    present and above the derived figure, else SURVEY.md §8(d)'s derived 39.3 T u32-ops/s."""
+def load_measured_peak():
+    """The measured v_add_u32 rate (profiles/valu_peak.json), reported beside the
+    guide's peak; None when absent."""
     path = os.path.join(ROOT, "profiles", "valu_peak.json")
-    if os.path.exists(path):
-        try:
-            d = json.load(open(path))
-            m = float(d["measured_ops_per_s"])
-            if m > NOMINAL_PEAK:
-                return {"peak": m, "source": "measured v_add_u32 microbenchmark (profiles/valu_peak.json)"}
-        except Exception:
-            pass
-    return {"peak": NOMINAL_PEAK, "source": "derived 256 CU x 64 lanes x 2.4 GHz (SURVEY.md 8d)"}
-
-
-def load_traffic(prog, batch):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass for this workload, else None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
+    try:
+        return float(json.load(open(path))["measured_ops_per_s"])
+    except Exception:
         return None
+
+
+def load_traffic(prog, batch, kernel):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes for this
+    kernel and batch (profiles/pmc_traffic.json, written by tools/pmc_traffic.py:
+    (2 x FETCH_SIZE + WRITE_SIZE) x 1024, the gfx950 correction of
+    MI355X_MICROARCH.md §HBM), else None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
-        if d.get("ops_per_eval") == prog.ops_per_eval and d.get("batch") == batch:
-            return d.get("hbm_bytes_per_launch")
     except Exception:
-        pass
+        return None
+    if d.get("ops_per_eval") == prog.ops_per_eval and d.get("batch") == batch and \
+            (kernel or "").startswith(d.get("kernel_name", "?")):
+        return d.get("hbm_bytes_per_launch")
     return None
 
 
-def cpu_baseline(syn, prog, budget_s):
-    """Oracle on the host cores over a bounded sample of the same candidate indices."""
+def cpu_baseline(syn, prog, budget_s, dev, dp):
+    """Oracle on the host cores over a bounded sample of the same candidate
+    indices; its verdict vector is compared with the GPU's on those indices
+    (a full-size parity check of the benchmarked kernel)."""
+    import numpy as np
     from oracle import cbaseline
-    return cbaseline.run(syn, prog, budget_s)
+    rec, vo = cbaseline.run(syn, prog, budget_s, verdicts=True)
+    if vo is not None:
+        vg, _ = dev.eval_generated(dp, syn.seed, 0, len(vo), trace=False)
+        bad = int(np.count_nonzero(vg.astype(np.uint8) != vo))
+        rec["verdicts_compared"] = int(len(vo))
+        rec["verdict_mismatches_vs_gpu"] = bad
+        if bad:
+            print(f"[bench] PARITY FAILURE: {bad} of {len(vo)} CPU-baseline verdicts differ from the GPU's",
+                  file=sys.stderr)
+    return rec
 
 
 if __name__ == "__main__":

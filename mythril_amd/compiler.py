@@ -144,6 +144,8 @@ def node_cost(n: Node) -> int:
     Lo = (_w(n) + 31) // 32
     if op in ("bvadd", "bvsub", "bvand", "bvor", "bvxor"):
         return L * max(k - 1, 1)
+    if op == "bvaddc":
+        return L
     if op in ("bvneg", "bvnot"):
         return L
     if op in ("bvnand", "bvnor", "bvxnor"):
@@ -340,6 +342,11 @@ class _Lowerer:
                 if cls_of(aw) == "W":
                     return self.emit("N_" + name, aw, [self.as_cls(a, aw, "W"), self.as_cls(b, aw, "W")])
                 return self.emit("N_" + name + "N", aw, [a, b])
+            if op == "bvaddc":   # carry out of a + b (lower.py wide-arithmetic legalisation)
+                aw = _w(n.args[0])
+                if cls_of(aw) == "W":
+                    return self.emit("N_ADDC", aw, [self.as_cls(args[0], aw, "W"), self.as_cls(args[1], aw, "W")])
+                return self.emit("N_ADDCN", aw, args)
             if op == "bvumul_noovfl":
                 aw = _w(n.args[0])
                 return self._bin("N_UMULNO", "N_UMULNON", aw, *args) if cls_of(aw) == "W" else \

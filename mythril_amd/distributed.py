@@ -14,7 +14,22 @@ from __future__ import annotations
 
 from typing import List, Optional, Sequence, Tuple
 
-NONE = (1 << 63) - 1
+NONE = (1 << 64) - 1   # MG_NONE: no witness (never a candidate index: mg_search rejects ranges past it)
+_BIAS = 1 << 63
+
+
+def _to_i64(v: Optional[int]) -> int:
+    """u64 index -> int64 with the order preserved (x - 2^63), so MIN over the
+    signed tensor is MIN over the unsigned indices; "none" is the largest."""
+    u = NONE if v is None else int(v)
+    if not 0 <= u <= NONE:
+        raise ValueError(f"witness index out of u64 range: {u}")
+    return u - _BIAS
+
+
+def _from_i64(x: int) -> Optional[int]:
+    u = int(x) + _BIAS
+    return None if u == NONE else u
 
 
 def shard_range(begin: int, count: int, rank: int, world: int) -> Tuple[int, int]:
@@ -26,10 +41,9 @@ def shard_range(begin: int, count: int, rank: int, world: int) -> Tuple[int, int
 def allreduce_min(values: Sequence[Optional[int]], device: Optional[str] = None) -> List[Optional[int]]:
     import torch
     import torch.distributed as dist
-    t = torch.tensor([NONE if v is None else int(v) for v in values], dtype=torch.int64,
-                     device=device or "cpu")
+    t = torch.tensor([_to_i64(v) for v in values], dtype=torch.int64, device=device or "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
-    return [None if int(x) == NONE else int(x) for x in t.tolist()]
+    return [_from_i64(x) for x in t.tolist()]
 
 
 def sharded_search(engine, queries, count: int, begin: int = 0, flags: Optional[int] = None,

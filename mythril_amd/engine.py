@@ -132,8 +132,10 @@ class WitnessEngine:
         if not queries:
             return []
         count = count or self.launch_count(queries)
-        dps = [self.dev.load(q.program) for q in queries]
+        dps = []
         try:
+            for q in queries:   # a failed load frees the programs already loaded
+                dps.append(self.dev.load(q.program))
             found, st = self.dev.search(dps, self.seed, begin, count, flags)
         finally:
             for dp in dps:

@@ -28,6 +28,7 @@ BOOL_OPS = frozenset({
     "and", "or", "not", "xor", "=>", "=", "distinct",
     "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge",
     "bvumul_noovfl", "bvsmul_noovfl", "bvsmul_noudfl",
+    "bvaddc",   # internal: carry out of a w-bit add (wide-arithmetic legalisation, lower.py)
 })
 
 # bitvector ops: name -> (min arity, max arity or None for n-ary)
@@ -134,6 +135,12 @@ class Ctx:
     def app(self, op: str, *args: Node, params: Sequence[int] = ()) -> Node:
         op = ALIASES.get(op, op)
         params = tuple(int(p) for p in params)
+        if op == "=>" and len(args) > 2:
+            # SMT-LIB: => is right-associative, (=> a b c) = (=> a (=> b c))
+            acc = args[-1]
+            for a in reversed(args[:-1]):
+                acc = self._mk("=>", BOOL, (a, acc))
+            return acc
         if op in BOOL_OPS:
             return self._mk(op, BOOL, args, params)
         if op == "ite":

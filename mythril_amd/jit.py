@@ -518,15 +518,20 @@ def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 2, lds_leaves
     """
     from . import hostemu
     from .synth import build_c5
-    syn = build_c5(hostemu.term_values, n_nodes=n_nodes)
-    prog = compile_program(syn.conjuncts)
     t0 = time.perf_counter()
-    # the split kernels too: bench.py falls back to them (a minute of parallel
-    # compiles) when the single kernel's code object is missing
-    objs, dts = compile_parts(prog, "x", waves=waves, lds_leaves=lds_leaves)
-    if split:
-        names, dt = [n for _, n in objs], dts
-    else:
-        _, names, dt = compile_device([prog], "x", waves=waves, lds_leaves=lds_leaves)
-    log(f"[jit] C5 kernel {names[0]} ({len(names)} part(s)): {'compiled in %.0f s' % dt if dt else 'cached'}")
+    # density 24: the benchmark's program; density 8: the same DAG with mixed
+    # verdicts, for the full-size parity test (tests/test_gpu_fullsize.py)
+    for dens in (24, 8):
+        syn = build_c5(hostemu.term_values, n_nodes=n_nodes, density_log2=dens)
+        prog = compile_program(syn.conjuncts)
+        if dens == 24:
+            # the split kernels too: bench.py falls back to them (a minute of
+            # parallel compiles) when the single kernel's code object is missing
+            objs, dts = compile_parts(prog, "x", waves=waves, lds_leaves=lds_leaves)
+        if split and dens == 24:
+            names, dt = [n for _, n in objs], dts
+        else:
+            _, names, dt = compile_device([prog], "x", waves=waves, lds_leaves=lds_leaves)
+        log(f"[jit] C5 (density 2^-{dens}) kernel {names[0]} ({len(names)} part(s)): "
+            f"{'compiled in %.0f s' % dt if dt else 'cached'}")
     return time.perf_counter() - t0

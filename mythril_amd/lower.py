@@ -17,11 +17,23 @@
    function whose indices/arguments are not both concrete,
    ``(args_t = args_u) => (val_t = val_u)`` is added as a conjunct, so any
    satisfying assignment of the leaves extends to a model of the arrays/UFs.
-4. **Width legalisation**: equalities over terms wider than 256 bits (512-bit
-   keccak inputs from ``Concat`` in ``instructions.py:1016-1030``,
-   ``bitvec.py:79-85`` zero-padded ``==``) are split into 256-bit chunks, and
-   extracts are pushed through ``concat`` / ``zero_extend`` / ``extract``.
-   Anything that still needs >256-bit arithmetic raises ``Unsupported``.
+4. **Width legalisation** (generic in the width): every term wider than 256
+   bits is decomposed into 256-bit chunks (least significant first) when a
+   narrower term consumes it:
+   * structure (``concat``, ``extract``, ``zero_extend``, ``sign_extend``,
+     ``repeat``, rotates and shifts by constants) regroups bit slices;
+   * ``bvand/bvor/bvxor/bvnot`` and ``ite`` work chunk by chunk;
+   * ``bvadd/bvsub/bvneg`` propagate carries between chunks with the
+     carry-out op ``bvaddc`` (``N_ADDC``), e.g. ``BVAddNoOverflow``'s 257-bit
+     add (``bitvec_helper.py:196-208``, z3 ``Z3_mk_bvadd_no_overflow``:
+     ``extract(256,256, zext1 a + zext1 b) = 0``, SWC-101 ``integer.py:143``)
+     becomes ``not(bvaddc(a, b))``;
+   * ``=``/``distinct`` compare chunks; unsigned/signed orderings compare
+     chunks lexicographically from the top (sign bit flipped for signed);
+   * 512-bit keccak inputs (``instructions.py:1016-1030``) and the
+     zero-padded ``==`` of ``bitvec.py:79-85`` are the same mechanism.
+   Wide ``bvmul``/division/remainder and shifts by a non-constant amount still
+   raise ``Unsupported`` (fail closed to z3).
 
 The result records, per synthesized leaf, which array/function cell it stands
 for (:class:`AckLeaf`) so a witness can be turned back into a model.
@@ -63,6 +75,8 @@ class _Rewriter:
         self.leaf_of_key: Dict[tuple, Node] = {}
         self.inner_apply: Dict[int, tuple] = {}   # leaf id of f(x) -> (f, x)
         self.nsym = 0
+        self.seg_memo: Dict[int, List[Node]] = {}
+        self.chunk_memo: Dict[int, List[Node]] = {}
 
     # -- extract simplification (pushes extracts towards leaves) ------------------
     def extract(self, x: Node, hi: int, lo: int) -> Node:
@@ -95,17 +109,170 @@ class _Rewriter:
                 parts.append(self.extract(a, min(hi, ahi) - aoff, max(lo, aoff) - aoff))
             return parts[0] if len(parts) == 1 else c.app("concat", *parts)
         if x.width > MAXW:
-            raise Unsupported(f"extract from a {x.width}-bit {x.op}")
+            return self._assemble(self._slice(self.segs(x), lo, hi))
         return c.app("extract", x, params=(hi, lo))
 
+    # -- wide terms as 256-bit chunks ------------------------------------------------
     def chunks(self, x: Node) -> List[Node]:
         """x as 256-bit (or narrower, last) chunks, least significant first."""
+        if x.width <= MAXW:
+            return [x]
+        got = self.chunk_memo.get(x.id)
+        if got is None:
+            segs = self.segs(x)
+            got = []
+            lo = 0
+            while lo < x.width:
+                hi = min(x.width, lo + MAXW) - 1
+                got.append(self._assemble(self._slice(segs, lo, hi)))
+                lo = hi + 1
+            self.chunk_memo[x.id] = got
+        return got
+
+    def _slice(self, segs: List[Node], lo: int, hi: int) -> List[Node]:
+        """Bits [lo, hi] of an LSB-first slice list, as LSB-first slices."""
+        c = self.ctx
+        out: List[Node] = []
+        off = 0
+        for t in segs:
+            a, b = max(lo, off), min(hi, off + t.width - 1)
+            if a <= b:
+                if a == off and b == off + t.width - 1:
+                    out.append(t)
+                else:
+                    out.append(self.extract(t, b - off, a - off))
+            off += t.width
+        return out
+
+    def _assemble(self, segs: List[Node]) -> Node:
+        """One term (<= 256 bits) from LSB-first slices."""
+        if len(segs) == 1:
+            return segs[0]
+        if all(t.op == "const" for t in segs):
+            v, off = 0, 0
+            for t in segs:
+                v |= t.val << off
+                off += t.width
+            return self.ctx.const(v, off)
+        return self.ctx.app("concat", *segs[::-1])
+
+    def segs(self, x: Node) -> List[Node]:
+        """x as LSB-first slices of at most 256 bits each (any boundaries)."""
+        if x.width <= MAXW:
+            return [x]
+        got = self.seg_memo.get(x.id)
+        if got is None:
+            got = self._segs(x)
+            assert sum(t.width for t in got) == x.width, (x.op, x.width)
+            self.seg_memo[x.id] = got
+        return got
+
+    def _segs(self, x: Node) -> List[Node]:
+        c = self.ctx
+        op, w = x.op, x.width
+        if op == "const":
+            return [c.const(x.val >> lo, min(MAXW, w - lo)) for lo in range(0, w, MAXW)]
+        if op == "var":
+            return [c.var(f"{x.name}#{k}", min(MAXW, w - lo)) for k, lo in enumerate(range(0, w, MAXW))]
+        if op == "concat":
+            out: List[Node] = []
+            for a in reversed(x.args):
+                out.extend(self.segs(a))
+            return out
+        if op == "zero_extend":
+            return self.segs(x.args[0]) + _zeros(c, x.params[0])
+        if op == "sign_extend":
+            a = x.args[0]
+            sbit = self.extract(a, a.width - 1, a.width - 1)
+            neg = c.app("=", sbit, c.const(1, 1))
+            fill = []
+            n = x.params[0]
+            while n:
+                k = min(MAXW, n)
+                fill.append(c.app("ite", neg, c.const((1 << k) - 1, k), c.const(0, k)))
+                n -= k
+            return self.segs(a) + fill
+        if op == "extract":
+            hi, lo = x.params
+            return self._slice(self.segs(x.args[0]), lo, hi)
+        if op == "repeat":
+            return self.segs(x.args[0]) * x.params[0]
+        if op in ("rotate_left", "rotate_right"):
+            r = x.params[0] % w
+            if op == "rotate_right":
+                r = (w - r) % w
+            if r == 0:
+                return self.segs(x.args[0])
+            sg = self.segs(x.args[0])
+            return self._slice(sg, w - r, w - 1) + self._slice(sg, 0, w - r - 1)   # (x << r) | (x >> (w - r))
+        if op in ("bvshl", "bvlshr", "bvashr"):
+            a, amt = x.args
+            if amt.op != "const":
+                raise Unsupported(f"{w}-bit {op} by a variable amount")
+            k = amt.val
+            sg = self.segs(a)
+            if op == "bvshl":
+                return _zeros(c, w) if k >= w else _zeros(c, k) + self._slice(sg, 0, w - k - 1)
+            if op == "bvlshr":
+                return _zeros(c, w) if k >= w else self._slice(sg, k, w - 1) + _zeros(c, k)
+            k = min(k, w)
+            top = self._slice(sg, w - 1, w - 1)[0]
+            neg = c.app("=", top, c.const(1, 1))
+            fill = []
+            n = k
+            while n:
+                m = min(MAXW, n)
+                fill.append(c.app("ite", neg, c.const((1 << m) - 1, m), c.const(0, m)))
+                n -= m
+            return (self._slice(sg, k, w - 1) if k < w else []) + fill
+        # element-wise and arithmetic ops: on aligned 256-bit chunks
+        if op == "ite":
+            cond, a, b = x.args
+            return [c.app("ite", cond, p, q) for p, q in zip(self.chunks(a), self.chunks(b))]
+        if op in ("bvand", "bvor", "bvxor"):
+            cols = zip(*[self.chunks(a) for a in x.args])
+            return [c.app(op, *col) for col in cols]
+        if op in ("bvnot", "bvnand", "bvnor", "bvxnor"):
+            if op == "bvnot":
+                return [c.app("bvnot", p) for p in self.chunks(x.args[0])]
+            inner = {"bvnand": "bvand", "bvnor": "bvor", "bvxnor": "bvxor"}[op]
+            return [c.app("bvnot", c.app(inner, p, q)) for p, q in zip(self.chunks(x.args[0]), self.chunks(x.args[1]))]
+        if op == "bvadd":
+            acc = self.chunks(x.args[0])
+            for b in x.args[1:]:
+                acc = self._add_chunks(acc, self.chunks(b), None)
+            return acc
+        if op == "bvsub":
+            nb = [c.app("bvnot", q) for q in self.chunks(x.args[1])]
+            return self._add_chunks(self.chunks(x.args[0]), nb, c.true())
+        if op == "bvneg":
+            nb = [c.app("bvnot", q) for q in self.chunks(x.args[0])]
+            return self._add_chunks([c.const(0, q.width) for q in nb], nb, c.true())
+        raise Unsupported(f"{op} on {w} bits")
+
+    def _add_chunks(self, A: List[Node], B: List[Node], cin: Optional[Node]) -> List[Node]:
+        """Chunk-wise a + b (+ cin), carries through bvaddc; folds zero operands."""
+        c = self.ctx
         out = []
-        lo = 0
-        while lo < x.width:
-            hi = min(x.width, lo + MAXW) - 1
-            out.append(self.extract(x, hi, lo))
-            lo = hi + 1
+        carry = cin
+        for a, b in zip(A, B):
+            w = a.width
+            if a.op == "const" and a.val == 0:
+                a, b = b, a
+            if b.op == "const" and b.val == 0:
+                s, co = a, None
+            else:
+                s, co = c.app("bvadd", a, b), c.app("bvaddc", a, b)
+            if carry is not None and not (carry.op == "const" and not carry.val):
+                one = c.const(1, w) if carry.op == "const" else c.app("ite", carry, c.const(1, w), c.const(0, w))
+                if s.op == "const" and s.val == 0:
+                    s2, co2 = one, None
+                else:
+                    s2, co2 = c.app("bvadd", s, one), c.app("bvaddc", s, one)
+                s = s2
+                co = co2 if co is None else (co if co2 is None else c.app("or", co, co2))
+            out.append(s)
+            carry = co
         return out
 
     def eq(self, a: Node, b: Node) -> Node:
@@ -114,6 +281,21 @@ class _Rewriter:
             return c.app("=", a, b)
         parts = [c.app("=", x, y) for x, y in zip(self.chunks(a), self.chunks(b))]
         return c.app("and", *parts) if len(parts) > 1 else parts[0]
+
+    def ult(self, a: Node, b: Node, signed: bool) -> Node:
+        """a < b on chunks, lexicographic from the most significant chunk."""
+        c = self.ctx
+        A, B = self.chunks(a), self.chunks(b)
+        if signed:   # flip the sign bit, compare unsigned
+            tw = A[-1].width
+            m = c.const(1 << (tw - 1), tw)
+            A = A[:-1] + [c.app("bvxor", A[-1], m)]
+            B = B[:-1] + [c.app("bvxor", B[-1], m)]
+        lt = None
+        for p, q in zip(A, B):
+            here = c.app("bvult", p, q)
+            lt = here if lt is None else c.app("or", here, c.app("and", c.app("=", p, q), lt))
+        return lt
 
     # -- leaves for array reads / UF applications ---------------------------------
     def _key_name(self, base: str, args: Tuple[Node, ...]) -> Tuple[tuple, str]:
@@ -219,17 +401,31 @@ class _Rewriter:
             return leaf
         if op in ("=", "distinct") and args and args[0].is_array:
             raise Unsupported("array equality")
-        if op == "=" and args[0].width > MAXW:
+        wide_args = any(a.width > MAXW and not a.is_array for a in args)
+        if op == "=" and wide_args:
             eqs = [self.eq(args[0], b) for b in args[1:]]
             return c.app("and", *eqs) if len(eqs) > 1 else eqs[0]
-        if op == "distinct" and args[0].width > MAXW:
-            if len(args) != 2:
-                raise Unsupported("wide n-ary distinct")
-            return c.app("not", self.eq(args[0], args[1]))
+        if op == "distinct" and wide_args:
+            ne = [c.app("not", self.eq(args[i], args[j]))
+                  for i in range(len(args)) for j in range(i + 1, len(args))]
+            return c.app("and", *ne) if len(ne) > 1 else ne[0]
+        if op == "bvcomp" and wide_args:
+            return c.app("ite", self.eq(args[0], args[1]), c.const(1, 1), c.const(0, 1))
+        if op in _ORDER and wide_args:
+            name, swap, strict = _ORDER[op]
+            a, b = (args[1], args[0]) if swap else (args[0], args[1])
+            signed = name == "s"
+            if strict:
+                return self.ult(a, b, signed)
+            return c.app("not", self.ult(b, a, signed))
         if op == "extract":
             return self.extract(args[0], n.params[0], n.params[1])
-        if op in ("concat", "zero_extend") and n.width > MAXW:
-            # kept only as an operand of a wide =, which chunks it via extract
+        if n.width > MAXW or wide_args:
+            # a wide term is kept as built; whatever narrower term consumes it
+            # decomposes it into chunks (extract / eq / ult above)
+            if op in ("bvmul", "bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod", "bvumul_noovfl",
+                      "bvsmul_noovfl", "bvsmul_noudfl"):
+                raise Unsupported(f"{op} on {max(a.width for a in args)} bits")
             return c._mk(op, n.width, tuple(args), n.params)
         return c.app(op, *args, params=n.params) if op not in ("ite",) else c.app("ite", *args)
 
@@ -248,6 +444,16 @@ class _Rewriter:
                     vu = u.value if u.value is not None else self.wide_var(u.name, u.width)
                     out.append(c.app("=>", prem, self.eq(vt, vu)))
         return out
+
+
+# wide orderings: op -> (signedness, swap operands, strict)
+_ORDER = {"bvult": ("u", False, True), "bvugt": ("u", True, True), "bvule": ("u", False, False),
+          "bvuge": ("u", True, False), "bvslt": ("s", False, True), "bvsgt": ("s", True, True),
+          "bvsle": ("s", False, False), "bvsge": ("s", True, False)}
+
+
+def _zeros(c: Ctx, n: int) -> List[Node]:
+    return [c.const(0, min(MAXW, n - lo)) for lo in range(0, n, MAXW)]
 
 
 def _offset(n: Node):
@@ -307,10 +513,8 @@ def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
     out = [rw.rw(cj) for cj in conjuncts]
     cong = rw.congruence()
     for n in topo(out + cong):
-        if n.width > MAXW and n.op not in ("concat", "zero_extend", "var"):
-            raise Unsupported(f"{n.op} on {n.width} bits")
-        if n.op in ("concat", "zero_extend") and n.width > MAXW:
-            raise Unsupported(f"{n.width}-bit {n.op} outside an equality")
+        if n.width > MAXW:   # every consumer chunks its wide operands; none may remain
+            raise Unsupported(f"{n.width}-bit {n.op} outside the legalised vocabulary")
     return Lowered(out + cong, rw.ack, len(cong))
 
 

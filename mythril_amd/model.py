@@ -42,7 +42,7 @@ _reference: Optional[Callable] = None   # the reference get_model, uncached (__w
 _engine = None
 _engine_lock = threading.Lock()
 _engine_failed = False
-_memo: Dict[tuple, tuple] = {}          # z3 AST-id key -> (witness, script)
+_memo: Dict[tuple, tuple] = {}          # z3 AST-id key -> (raws, witness, script)
 MEMO_MAX = 1 << 16
 _pending: list = []                     # successor constraint sets deferred by the JUMPI hook
 PENDING_MAX = 64
@@ -81,6 +81,20 @@ def memo_key(raws) -> tuple:
     return tuple(r.get_id() for r in raws)
 
 
+def _memo_get(raws, key):
+    """The memo entry for these ASTs.  z3 reuses the ids of collected ASTs, so
+    an id match is confirmed structurally (``eq``) against the ASTs the entry
+    keeps alive; a stale entry is dropped."""
+    hit = _memo.get(key)
+    if hit is None:
+        return None
+    kept = hit[0]
+    if len(kept) == len(raws) and all(a is b or a.eq(b) for a, b in zip(kept, raws)):
+        return hit
+    del _memo[key]
+    return None
+
+
 def _solver_log(constraints, minimize, maximize, args, timeout):
     """Write the .smt2 dump exactly as mythril/support/model.py:45-56 does."""
     from mythril.laser.smt import Optimize
@@ -101,9 +115,10 @@ def _solver_log(constraints, minimize, maximize, args, timeout):
 
 def _gpu_model(constraints, timeout):
     from . import z3bridge
+    from .runtime import EngineError
     raws = [c.raw for c in constraints]
     key = memo_key(raws)
-    hit = _memo.get(key)
+    hit = _memo_get(raws, key)
     if hit is None and _pending:
         # the JUMPI successors LASER is about to prune one by one (svm.py:287-292):
         # search all of them in one launch, then answer this one from the memo
@@ -111,10 +126,10 @@ def _gpu_model(constraints, timeout):
         _pending.clear()
         STATS["batched_prefetches"] = STATS.get("batched_prefetches", 0) + 1
         prefetch(batch)
-        hit = _memo.get(key)
+        hit = _memo_get(raws, key)
     if hit is not None:
         STATS["memo_hits"] += 1
-        witness, script = hit
+        _, witness, script = hit
     else:
         eng = engine()
         if eng is None:
@@ -128,7 +143,14 @@ def _gpu_model(constraints, timeout):
             log.debug("witness engine: unsupported formula (%s)", e)
             return None
         STATS["gpu_attempts"] += 1
-        witness = eng.search([q])[0]
+        try:
+            witness = eng.search([q])[0]
+        except EngineError as e:
+            # a device-side failure (validation, allocation, launch) never escapes:
+            # the reference answers, exactly as without the engine
+            STATS["device_errors"] = STATS.get("device_errors", 0) + 1
+            log.warning("witness engine: device error (%s); z3 answers", e)
+            return None
     if witness is None:
         return None
     STATS["gpu_witnesses"] += 1
@@ -182,27 +204,33 @@ def prefetch(constraint_sets) -> int:
         return 0
     from . import z3bridge
     from .engine import prepare
+    from .runtime import EngineError
     items = []
     for cs in constraint_sets:
         try:
             cl = cs if type(cs) == tuple else cs.get_all_constraints()
             raws = [c.raw for c in cl if type(c) != bool]
             key = memo_key(raws)
-            if key in _memo:
+            if _memo_get(raws, key) is not None:
                 continue
             script = z3bridge.to_ir(raws)
-            items.append((key, script, prepare(script.asserts, script.ctx)))
+            items.append((key, raws, script, prepare(script.asserts, script.ctx)))
         except (Unsupported, RecursionError, ValueError, KeyError):
             STATS["unsupported"] += 1
     if not items:
         return 0
-    found = eng.search([q for _, _, q in items])
+    try:
+        found = eng.search([q for *_, q in items])
+    except EngineError as e:
+        STATS["device_errors"] = STATS.get("device_errors", 0) + 1
+        log.warning("witness engine: device error in batched prefetch (%s)", e)
+        return 0
     n = 0
-    for (key, script, _), w in zip(items, found):
+    for (key, raws, script, _), w in zip(items, found):
         if w is not None:
             if len(_memo) >= MEMO_MAX:
                 _memo.clear()
-            _memo[key] = (w, script)
+            _memo[key] = (raws, w, script)
             n += 1
     return n
 

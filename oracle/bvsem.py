@@ -250,8 +250,15 @@ def bvsmul_noudfl(w, a, b):
     return int(to_signed(a, w) * to_signed(b, w) >= -(1 << (w - 1)))
 
 
+def bvaddc(w, a, b):
+    # internal (mythril_amd/lower.py wide-arithmetic legalisation): carry out of the
+    # w-bit addition a + b, i.e. bit w of the (w+1)-bit sum of the zero-extended operands
+    return int(a + b >= (1 << w))
+
+
 # Table used by dag_eval: op -> callable(width_of_first_arg, *values)
 BINARY_PRED = {
+    "bvaddc": bvaddc,
     "bvult": bvult, "bvule": bvule, "bvugt": bvugt, "bvuge": bvuge,
     "bvslt": bvslt, "bvsle": bvsle, "bvsgt": bvsgt, "bvsge": bvsge,
     "bvumul_noovfl": bvumul_noovfl, "bvsmul_noovfl": bvsmul_noovfl,

@@ -24,7 +24,7 @@ typedef uint64_t u64;
 enum {
   O_CONST = 0, O_VAR, O_ADD, O_SUB, O_MUL, O_UDIV, O_UREM, O_SDIV, O_SREM, O_SMOD,
   O_AND, O_OR, O_XOR, O_NOT, O_NEG, O_SHL, O_LSHR, O_ASHR, O_CONCAT, O_EXTRACT,
-  O_ZEXT, O_SEXT, O_ITE, O_EQ, O_ULT, O_ULE, O_SLT, O_SLE, O_UMULNO, O_ROTL, O_ROTR
+  O_ZEXT, O_SEXT, O_ITE, O_EQ, O_ULT, O_ULE, O_SLT, O_SLE, O_UMULNO, O_ROTL, O_ROTR, O_ADDC
 };
 
 /* node record: op, width, a, b, c, p0, p1, salt (8 x i32) */
@@ -150,6 +150,36 @@ static void leaf(u64 seed, u32 salt, u64 cand, int w, u32* out) {
   mask(out, w);
 }
 
+/* Candidate-leaf spec (oracle/philox.py leaf_value; DESIGN.md "Candidate space"):
+ * kind 0 random, 1 pool digit = index bit-field, 2 hashed digit, 3 bit-interleaved
+ * digit.  Pool entries are 9 words: flags (bit 0 = RANDOM) + 8 limbs. */
+typedef struct { int32_t kind, shift, bits, stride, pool; } ospec;
+
+static u64 fmix64(u64 h) {
+  h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; h ^= h >> 33;
+  return h;
+}
+
+static void spec_leaf(const ospec* sp, const u32* pool, u64 seed, u32 salt, u64 cand, int w, u32* out) {
+  if (sp && sp->kind >= 1 && sp->kind <= 3) {
+    u64 d = 0;
+    u64 m = sp->bits >= 64 ? ~0ull : ((1ull << sp->bits) - 1);
+    if (sp->kind == 1) d = (cand >> sp->shift) & m;
+    else if (sp->kind == 2) d = fmix64(cand ^ ((u64)salt * 0x9E3779B97F4A7C15ull)) & m;
+    else for (int b = 0; b < sp->bits; ++b) d |= ((cand >> (sp->shift + b * sp->stride)) & 1ull) << b;
+    const u32* e = pool + sp->pool + 9 * d;
+    if (!(e[0] & 1u)) {
+      for (int k = 0; k < 8; ++k) out[k] = e[1 + k];
+      mask(out, w);
+      return;
+    }
+  }
+  leaf(seed, salt, cand, w, out);
+}
+
+static const ospec* g_specs;   /* set per call (read-only while the OpenMP region runs) */
+static const u32* g_pool;
+
 static void eval1(const onode* g, const u32* consts, int i, u32* V, u64 seed, u64 cand) {
   const onode* n = &g[i];
   u32* r = V + 8 * (size_t)i;
@@ -161,7 +191,7 @@ static void eval1(const onode* g, const u32* consts, int i, u32* V, u64 seed, u6
   u32 t[8], u[8];
   switch (n->op) {
     case O_CONST: memcpy(r, consts + 8 * (size_t)n->p0, 32); break;
-    case O_VAR: leaf(seed, (u32)n->salt, cand, w, r); break;
+    case O_VAR: spec_leaf(g_specs && n->p0 >= 0 ? &g_specs[n->p0] : 0, g_pool, seed, (u32)n->salt, cand, w, r); break;
     case O_ADD: add(a, b, r); mask(r, w); break;
     case O_SUB: sub(a, b, r); mask(r, w); break;
     case O_MUL: mul(a, b, r); mask(r, w); break;
@@ -211,6 +241,12 @@ static void eval1(const onode* g, const u32* consts, int i, u32* V, u64 seed, u6
       for (int k = 0; k < 8; ++k) r[k] = t[k] | u[k];
       break;
     }
+    case O_ADDC: { /* carry out of the aw-bit sum a + b (operands < 2^aw) */
+      u64 cc = 0;
+      for (int k = 0; k < 8; ++k) { cc += (u64)a[k] + b[k]; t[k] = (u32)cc; cc >>= 32; }
+      int co = aw >= 256 ? (int)cc : (int)((t[aw >> 5] >> (aw & 31)) & 1u);
+      memset(r, 0, 32); r[0] = (u32)co; break;
+    }
     default: memset(r, 0, 32); break;
   }
 }
@@ -245,6 +281,19 @@ long long odag_eval(const int32_t* nodes, int nn, const u32* consts, const int32
   }
   if (first_sat) *first_sat = best;
   return total;
+}
+
+/* As odag_eval, with pool/hashed/interleaved leaves: VAR node p0 indexes specs
+ * (-1 = random leaf); pool holds the 9-word entries the specs point into. */
+long long odag_eval_spec(const int32_t* nodes, int nn, const u32* consts, const int32_t* roots, int nroots,
+                         const int32_t* specs, const u32* pool, u64 seed, u64 begin, u64 n, uint8_t* verdict,
+                         int nthreads, u64* first_sat) {
+  g_specs = (const ospec*)specs;
+  g_pool = pool;
+  long long r = odag_eval(nodes, nn, consts, roots, nroots, seed, begin, n, verdict, nthreads, first_sat);
+  g_specs = 0;
+  g_pool = 0;
+  return r;
 }
 
 int odag_max_threads(void) {

@@ -13,13 +13,17 @@ import os
 import time
 
 
-def run(syn, prog, budget_s: float = 10.0) -> dict:
+def run(syn, prog, budget_s: float = 10.0, verdicts: bool = False):
+    """The baseline record; with verdicts=True also the verdict vector of the
+    evaluated indices 0..n-1 (C restatement only; None from the Python path)."""
     try:
         from . import cdag
         if cdag.available():
-            return cdag.baseline(syn, prog, budget_s)
+            return cdag.baseline(syn, prog, budget_s, verdicts=verdicts)
     except Exception:  # pragma: no cover - fall through to Python
         pass
+    if verdicts:
+        return run(syn, prog, budget_s), None
     from .dag_eval import eval_nodes
     from .philox import random_leaf
     import zlib

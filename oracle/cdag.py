@@ -20,7 +20,7 @@ _lib = None
 
 OPS = ["CONST", "VAR", "ADD", "SUB", "MUL", "UDIV", "UREM", "SDIV", "SREM", "SMOD", "AND", "OR", "XOR",
        "NOT", "NEG", "SHL", "LSHR", "ASHR", "CONCAT", "EXTRACT", "ZEXT", "SEXT", "ITE", "EQ", "ULT", "ULE",
-       "SLT", "SLE", "UMULNO", "ROTL", "ROTR"]
+       "SLT", "SLE", "UMULNO", "ROTL", "ROTR", "ADDC"]
 O = {n: i for i, n in enumerate(OPS)}
 
 
@@ -38,6 +38,11 @@ def lib():
         L.odag_eval.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                 ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_uint64)]
+        L.odag_eval_spec.restype = ctypes.c_longlong
+        L.odag_eval_spec.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                     ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                                     ctypes.POINTER(ctypes.c_uint64)]
         L.odag_max_threads.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -49,11 +54,32 @@ def subprocess_build():
 
 
 class Serialized:
-    def __init__(self):
+    def __init__(self, specs=None):
         self.nodes = []     # [op, w, a, b, c, p0, p1, salt]
         self.consts = []    # 8-limb entries
         self.memo = {}
         self.kmemo = {}
+        self.specs_in = specs or {}   # var name -> candidate spec (oracle/philox.py leaf_value fields)
+        self.spec_rows = []           # [kind, shift, bits, stride, pool word offset]
+        self.pool = []
+
+    def _spec_index(self, name: str) -> int:
+        """Spec row of a leaf: the candidate-space definition of oracle/philox.py
+        (pool digits from index bit-fields, interleaved bits or a hash; RANDOM
+        entries fall back to Philox), restated for the C oracle."""
+        sp = self.specs_in.get(name)
+        if not sp or not sp.get("pool"):
+            return -1
+        pool = list(sp["pool"])
+        kind = 2 if sp.get("hashed") else (3 if sp.get("stride") else 1)
+        off = len(self.pool)
+        for e in pool:
+            if e is None:
+                self.pool.extend([1] + [0] * 8)
+            else:
+                self.pool.extend([0] + [(e >> (32 * k)) & 0xFFFFFFFF for k in range(8)])
+        self.spec_rows.append([kind, sp.get("shift", 0), sp.get("bits", 0), sp.get("stride", 0), off])
+        return len(self.spec_rows) - 1
 
     def _add(self, op, w, a=-1, b=-1, c=-1, p0=0, p1=0, salt=0):
         self.nodes.append([O[op], w, a, b, c, p0, p1, salt - (1 << 32) if salt >= (1 << 31) else salt])
@@ -88,7 +114,9 @@ class Serialized:
         if op == "const":
             return self.const(n.val, w)
         if op == "var":
-            return self._add("VAR", w, salt=zlib.crc32(n.name.encode()) & 0xFFFFFFFF)
+            sp = self.specs_in.get(n.name)
+            salt = sp["id"] if sp and "id" in sp else zlib.crc32(n.name.encode()) & 0xFFFFFFFF
+            return self._add("VAR", w, p0=self._spec_index(n.name), salt=salt)
         a = [self.term(x) for x in n.args]
         aw = (1 if n.args[0].width == 0 else n.args[0].width) if n.args else w
         simple = {"bvsub": "SUB", "bvudiv": "UDIV", "bvurem": "UREM", "bvsdiv": "SDIV", "bvsrem": "SREM",
@@ -145,35 +173,66 @@ class Serialized:
             return self._add(o, 1, x, y)
         if op == "bvumul_noovfl":
             return self._add("UMULNO", 1, a[0], a[1])
+        if op == "bvaddc":
+            return self._add("ADDC", 1, a[0], a[1])
         raise ValueError(f"C oracle: unsupported op {op}")
 
 
-def evaluate(conjuncts, seed: int, begin: int, n: int, nthreads: int = 0, want_verdict: bool = False):
-    s = Serialized()
+def program_specs(prog) -> dict:
+    """Candidate specs of a compiled program's leaves in oracle/philox.py's form
+    (the fields the oracle restates; not the program's encoded leaf table)."""
+    out = {}
+    for node, sp in zip(prog.leaf_nodes, prog.leaf_specs):
+        out[node.name] = {"id": sp.key_salt(), "width": sp.width, "shift": sp.shift, "bits": sp.bits,
+                          "pool": sp.pool, "hashed": sp.hashed, "stride": sp.stride}
+    return out
+
+
+def evaluate(conjuncts, seed: int, begin: int, n: int, nthreads: int = 0, want_verdict: bool = False,
+             specs=None):
+    """Evaluate candidates [begin, begin+n) of the conjunction on all host cores.
+    specs: {var name: oracle/philox.py spec} (e.g. program_specs(prog)) for
+    pool-driven leaves; leaves without one are plain Philox draws."""
+    s = Serialized(specs)
     roots = [s.term(c) for c in conjuncts]
     nodes = np.asarray(s.nodes, dtype=np.int32).reshape(-1)
     consts = np.asarray(s.consts or [[0] * 8], dtype=np.uint32).reshape(-1)
     r = np.asarray(roots or [0], dtype=np.int32)
     v = np.zeros(n, dtype=np.uint8) if want_verdict else None
     first = ctypes.c_uint64(0)
-    total = lib().odag_eval(nodes.ctypes.data, len(s.nodes), consts.ctypes.data, r.ctypes.data, len(roots),
-                            seed, begin, n, v.ctypes.data if v is not None else None, nthreads,
-                            ctypes.byref(first))
+    if s.spec_rows:
+        sp = np.asarray(s.spec_rows, dtype=np.int32).reshape(-1)
+        pool = np.asarray(s.pool, dtype=np.uint32)
+        total = lib().odag_eval_spec(nodes.ctypes.data, len(s.nodes), consts.ctypes.data, r.ctypes.data,
+                                     len(roots), sp.ctypes.data, pool.ctypes.data, seed, begin, n,
+                                     v.ctypes.data if v is not None else None, nthreads, ctypes.byref(first))
+    else:
+        total = lib().odag_eval(nodes.ctypes.data, len(s.nodes), consts.ctypes.data, r.ctypes.data, len(roots),
+                                seed, begin, n, v.ctypes.data if v is not None else None, nthreads,
+                                ctypes.byref(first))
     return total, (None if first.value == (1 << 64) - 1 else first.value), v
 
 
-def baseline(syn, prog, budget_s: float = 10.0) -> dict:
-    """bench.py cpu_baseline: all host cores, candidate indices 0.. in growing batches."""
+def baseline(syn, prog, budget_s: float = 10.0, verdicts: bool = False):
+    """bench.py cpu_baseline: all host cores, candidate indices 0.. in growing
+    batches.  verdicts=True also returns the per-candidate verdict vector (the
+    bench compares it with the GPU's on the same indices)."""
     cores = lib().odag_max_threads()
     n, t0, dt, sat = 0, time.perf_counter(), 0.0, 0
     batch = max(64, cores * 16)
+    parts = []
     while dt < budget_s:
-        tot, _, _ = evaluate(syn.conjuncts, syn.seed, n, batch)
+        tot, _, v = evaluate(syn.conjuncts, syn.seed, n, batch, want_verdict=verdicts)
+        if verdicts:
+            parts.append(v)
         sat += tot
         n += batch
         dt = time.perf_counter() - t0
         if dt < budget_s / 4:
             batch *= 2
-    return {"value": n / dt, "unit": "evals/s", "cores": cores, "kind": "port",
-            "sample": f"candidate indices 0..{n - 1} of the same C5 program ({n} evals, {dt:.1f} s), "
-                      f"C restatement oracle/c/dag_oracle.c, OpenMP x{cores}", "satisfied": int(sat)}
+    out = {"value": n / dt, "unit": "evals/s", "cores": cores, "kind": "port",
+           "sample": f"candidate indices 0..{n - 1} of the same C5 program ({n} evals, {dt:.1f} s), "
+                     f"C restatement oracle/c/dag_oracle.c, OpenMP x{cores}", "satisfied": int(sat)}
+    if verdicts:
+        return out, np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint8)
+    return out

@@ -71,3 +71,16 @@ def test_world_size_2_gloo_matches_single_process():
     single, _ = eng.dev.search([eng.dev.load(qq.program) for qq in queries], 7, 0, 4096, 0)
     assert res[0] == single
     assert res[0][0] is not None and res[0][1] is None
+
+
+def test_u64_indices_survive_the_int64_all_reduce():
+    """indices >= 2^63 (pool digits reach bit 63) and 2^63-1 must not
+    overflow torch.int64 or read as "no witness"; MIN order is the u64 order."""
+    from mythril_amd.distributed import _from_i64, _to_i64
+    vals = [0, 1, (1 << 63) - 1, 1 << 63, (1 << 64) - 2, None]
+    enc = [_to_i64(v) for v in vals]
+    assert all(-(1 << 63) <= e < (1 << 63) for e in enc)
+    assert enc == sorted(enc)
+    assert [_from_i64(e) for e in enc] == vals
+    with pytest.raises(ValueError):
+        _to_i64(1 << 64)

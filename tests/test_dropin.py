@@ -35,6 +35,9 @@ class FakeRaw:
     def get_id(self):
         return self.node.id
 
+    def eq(self, other):   # z3.AstRef.eq: structural identity
+        return isinstance(other, FakeRaw) and other.node is self.node
+
 
 class FakeBool:
     def __init__(self, node):
@@ -255,3 +258,51 @@ def test_plugin_registers_rebinding_and_batching_hooks(mythril):
     assert dropin._pending == [SAT]
     vm.laser["stop_sym_trans"][0]()  # no open states: a no-op
     dropin._pending.clear()
+
+
+def test_device_error_falls_back_to_reference(mythril, monkeypatch):
+    """an EngineError from the device (failed validation, allocation,
+    launch) must never escape get_model; the reference answers instead."""
+    from mythril_amd.runtime import EngineError
+
+    class BrokenDevice(FakeDevice):
+        def search(self, *a, **k):
+            raise EngineError("mg_search failed (-3): out of memory")
+
+    freed = []
+
+    class LeakCheck(FakeDevice):
+        n = 0
+
+        def load(self, p):
+            LeakCheck.n += 1
+            if LeakCheck.n == 2:
+                raise EngineError("mg_prog_load failed (-2): pool digit bits > 24")
+            dp = super().load(p)
+            dp.free = lambda: freed.append(1)
+            return dp
+
+    monkeypatch.setattr(dropin, "_engine", WitnessEngine(dev=BrokenDevice(), budget=1 << 10))
+    assert dropin.get_model(SAT).raw[0] == "ref"
+    assert dropin.STATS["device_errors"] >= 1
+    dropin.get_model.cache_clear()
+    # a load failure inside a batch frees the programs loaded before it
+    monkeypatch.setattr(dropin, "_engine", WitnessEngine(dev=LeakCheck(), budget=1 << 10))
+    sets = [SAT, (fb(CTX.app("=", X, CTX.const(77, 8))),)]
+    assert dropin.prefetch(sets) == 0
+    assert freed == [1]
+
+
+def test_stale_memo_entry_is_not_used(mythril):
+    """z3 reuses the ids of collected ASTs; a memo entry whose ids
+    match but whose ASTs differ must not answer."""
+    assert dropin.prefetch([SAT]) == 1
+    key = dropin.memo_key([c.raw for c in SAT])
+    other = (fb(CTX.app("=", X, CTX.const(9, 8))), fb(CTX.app("bvult", X, CTX.const(10, 8))))
+    raws_other = [c.raw for c in other]
+    # pretend z3 handed the same ids to different ASTs
+    dropin._memo[dropin.memo_key(raws_other)] = dropin._memo[key]
+    assert dropin._memo_get(raws_other, dropin.memo_key(raws_other)) is None
+    assert dropin.memo_key(raws_other) not in dropin._memo
+    res = dropin.get_model(other)
+    assert res.raw[0][1]["x"] == 9

@@ -123,3 +123,37 @@ def test_congruence_conjuncts_fuse_to_one_check():
     ops = [int(w) & 0xFF for w in q.program.code.reshape(-1, 4)[:, 0]]
     assert ops.count(isa.OPCODES["CHECK_IMP"]) >= 2000
     assert all(i.op != "CHECK_IMP" for i in q.program.ssa)
+
+
+def test_check_imp_verdicts_all_input_combinations():
+    """the fused CHECK_IMP against the oracle on every (p, q) row,
+    with Bool and bv1 premises/conclusions and constant operands, including the
+    rejecting row p=1, q=0; the unfused program (as jit.py sees it) agrees."""
+    from mythril_amd import isa
+    from mythril_amd.compiler import compile_program
+    from mythril_amd.runtime import pack_inputs
+    from oracle.dag_eval import eval_nodes
+    from tests.helpers import emu_eval
+    c = Ctx()
+    a, b = c.var("a", 0), c.var("b", 0)
+    u, v = c.var("u", 1), c.var("v", 1)
+    x = c.var("x", 8)
+    t, f = c.true(), c.false()
+    shapes = [
+        [c.app("=>", a, b)],
+        [c.app("=>", c.app("=", u, c.const(1, 1)), c.app("=", v, c.const(1, 1)))],
+        [c.app("=>", c.app("bvule", u, v), b)],
+        [c.app("=>", a, c.app("=", x, c.const(7, 8)))],
+        [c.app("=>", t, b)], [c.app("=>", a, f)], [c.app("=>", f, b)], [c.app("=>", a, t)],
+        [c.app("=>", a, b), c.app("=>", b, a)],
+    ]
+    models = [{"a": p, "b": q, "u": p, "v": q, "x": 7 if q else 3} for p in (0, 1) for q in (0, 1)]
+    for conj in shapes:
+        prog = compile_program(conj)
+        ops = [int(w) & 0xFF for w in prog.code.reshape(-1, 4)[:, 0]]
+        want = [int(all(eval_nodes(conj, m)[k.id] for k in conj)) for m in models]
+        got, _ = emu_eval(prog, pack_inputs(prog, models), len(models))
+        assert list(map(int, got)) == want, conj
+        if not any(k.args[0].op == "const" or k.args[1].op == "const" for k in conj):
+            assert isa.OPCODES["CHECK_IMP"] in ops, conj
+    assert [int(all(eval_nodes(shapes[0], m)[k.id] for k in shapes[0])) for m in models] == [1, 1, 0, 1]

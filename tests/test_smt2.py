@@ -118,3 +118,26 @@ def test_printer_round_trip(seed):
         a = eval_nodes(conj, m)
         b = eval_nodes(s.asserts, m)
         assert [a[t.id] for t in conj] == [b[t.id] for t in s.asserts]
+
+
+def test_nary_implication_is_right_associative():
+    """(=> a b c) is (=> a (=> b c)) in SMT-LIB 2.6; the compiler and
+    the oracle both see the folded binary form."""
+    from mythril_amd.compiler import compile_program
+    from mythril_amd.runtime import pack_inputs
+    from tests.helpers import emu_eval
+    s = parse_script("""
+(declare-fun a () Bool)(declare-fun b () Bool)(declare-fun c () Bool)
+(assert (=> a b c))
+""")
+    (t,) = s.asserts
+    assert t.op == "=>" and len(t.args) == 2 and t.args[1].op == "=>"
+    models = [{"a": (k >> 2) & 1, "b": (k >> 1) & 1, "c": k & 1} for k in range(8)]
+    want = [int((not m["a"]) or (not m["b"]) or bool(m["c"])) for m in models]
+    got = [eval_nodes(s.asserts, m)[t.id] for m in models]
+    assert got == want
+    # a=1, b=1, c=0 is the only falsifying row; (=> a b) would accept it
+    assert want[6] == 0
+    p = compile_program(s.asserts)
+    v, _ = emu_eval(p, pack_inputs(p, models), len(models))
+    assert list(map(int, v)) == want

@@ -1,0 +1,90 @@
+#!/bin/bash
+# One parameterised GPU-box recipe (run under gpurun):
+#
+#   tools/gpu_run.sh TAG STEP [STEP...]
+#
+# Steps (each under its own time limit; the script stops at the first failure):
+#   smoke          __graft_entry__.smoke()
+#   tests[=EXPR]   pytest -m gpu (optionally -k EXPR)
+#   bench          python bench.py (default flags) -> bench.json
+#   bench1         bench.py --steps 5 --no-ttfw --no-cpu-baseline (quick)
+#   prof           rocprofv3 --kernel-trace --stats on a short bench run
+#   pmc            PMC passes on one bench launch (SQ, instruction mix, FETCH_SIZE, WRITE_SIZE)
+#   config         tools/config_bench.py (C2-C4 queries) -> config_bench.json
+#   latency        tools/latency_bench.py (drop-in prepare/search/materialise per query)
+#   replay         python -m mythril_amd.replay tests/golden/solver_log
+#   opbench        tools/opbench.py jit
+#   keccak         tools/keccak_bench.py
+# Outputs land in gpurun_out/TAG/.
+set -o pipefail
+export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+TAG=$1
+shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-ttfw"
+
+run() {  # run LIMIT LOG CMD...: one GPU step, bounded; print the log tail on failure
+  local lim=$1 log=$2
+  shift 2
+  timeout -k 10 "$lim" "$@" > "$log" 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "step failed rc=$rc: $*"
+    tail -30 "$log"
+    exit $rc
+  fi
+}
+
+for step in "$@"; do
+  echo "== $step ($(date +%T))"
+  case $step in
+    smoke)
+      run 240 "$OUT/smoke.log" python3 -c "import __graft_entry__ as g; g.smoke()"
+      tail -2 "$OUT/smoke.log" ;;
+    tests|tests=*)
+      K=()
+      [ "$step" != tests ] && K=(-k "${step#tests=}")
+      run 1000 "$OUT/gpu_tests.log" python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}"
+      tail -3 "$OUT/gpu_tests.log" ;;
+    bench)
+      run 500 "$OUT/bench.err" bash -c "python3 bench.py > $OUT/bench.json"
+      cat "$OUT/bench.json" ;;
+    bench1)
+      run 300 "$OUT/bench1.err" bash -c "$B > $OUT/bench1.json"
+      cat "$OUT/bench1.json" ;;
+    prof)
+      run 400 "$OUT/prof.log" rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- $B
+      find "$OUT/prof" -name "*kernel_stats.csv" -exec head -5 {} \; ;;
+    pmc)
+      i=0
+      for set in "SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_SCA" \
+                 "SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_SMEM,SQ_INSTS_LDS,SQ_INSTS_BRANCH,SQ_INSTS_VMEM,SQ_INST_CYCLES_SALU,SQ_INSTS_FLAT" \
+                 "FETCH_SIZE" "WRITE_SIZE"; do
+        i=$((i + 1))
+        run 150 "$OUT/pmc$i.log" timeout -s KILL 140 rocprofv3 --pmc $set --output-format csv -d "$OUT/pmc/p$i" -o run -- \
+          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ttfw
+      done
+      find "$OUT/pmc" -name "*counter_collection*" ;;
+    config)
+      run 600 "$OUT/config_bench.log" python3 tools/config_bench.py --out "$OUT/config_bench.json"
+      tail -12 "$OUT/config_bench.log" ;;
+    latency)
+      run 600 "$OUT/latency.log" python3 tools/latency_bench.py --out "$OUT/latency.json"
+      tail -20 "$OUT/latency.log" ;;
+    replay)
+      run 300 "$OUT/replay.txt" python3 -m mythril_amd.replay tests/golden/solver_log
+      tail -12 "$OUT/replay.txt" ;;
+    opbench)
+      run 400 "$OUT/opbench.log" python3 tools/opbench.py jit
+      tail -20 "$OUT/opbench.log" ;;
+    keccak)
+      run 300 "$OUT/keccak.log" python3 tools/keccak_bench.py
+      tail -8 "$OUT/keccak.log" ;;
+    *)
+      echo "unknown step $step"
+      exit 2 ;;
+  esac
+done
+echo "== done ($(date +%T))"
