@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 THEORETICAL_PEAK = 256 * 4 * 32 * 2.4e9
 BENCH_VARIANTS = "x"  # exhaustive kernel only: the bench never exits early
 BENCH_WAVES = 2  # with 10 leaves in LDS (profiles/r1_v4_jit); 1 wave/SIMD: 512 registers, no LDS
+BENCH_INTERLEAVE = 1  # conjunct streams merged per basic block (jit.interleave_conjuncts)
 BENCH_SPLIT = False  # one kernel: 111.7M evals/s; as 5 part kernels (split_ssa): 109.9M, 7x faster to compile
 
 
@@ -50,6 +51,8 @@ def parse():
                     help="waves per SIMD the specialised kernel is built for")
     ap.add_argument("--jit-split", type=int, default=int(BENCH_SPLIT), choices=[0, 1],
                     help="1: split the program into part kernels at conjunct boundaries")
+    ap.add_argument("--jit-interleave", type=int, default=BENCH_INTERLEAVE,
+                    help="conjuncts interleaved per instruction stream in the specialised kernel")
     ap.add_argument("--jit-lds-leaves", type=int, default=None,
                     help="leaves kept in LDS instead of registers (default: 10 at 2 waves/SIMD, 0 at 1)")
     return ap.parse_args()
@@ -91,13 +94,14 @@ def main():
         if args.jit_lds_leaves is None:  # LDS: waves/SIMD x slots x 8 KiB per CU <= 160 KiB
             args.jit_lds_leaves = {1: 0, 2: 10, 3: 6, 4: 5}[args.jit_waves]
         split = bool(args.jit_split)
-        if not split and not jit.is_cached([prog], BENCH_VARIANTS, args.jit_waves, args.jit_lds_leaves):
+        if not split and not jit.is_cached([prog], BENCH_VARIANTS, args.jit_waves, args.jit_lds_leaves,
+                                           args.jit_interleave):
             # one kernel compiles for ~6 min; its parts in ~1 min (parallel hipcc)
             print("[bench] single-kernel code object not cached: using the split kernels", file=sys.stderr)
             split = True
         args.jit_split = int(split)
         jit_s = jit.attach(dev, [dp], variants=BENCH_VARIANTS, waves=args.jit_waves, lds_leaves=args.jit_lds_leaves,
-                           split=split)
+                           split=split, interleave=args.jit_interleave)
     batch = 1 << args.batch_log2
 
     def step(k):
@@ -117,11 +121,13 @@ def main():
 
     barrier()
     kms = []
+    dsteps = []
     found_any = None
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
         found, st = step(k)
         kms.append(st["kernel_ms"])
+        dsteps.append(st["lane_div_steps"])
         if found is not None:
             found_any = found if found_any is None else min(found_any, found)
     barrier()
@@ -137,7 +143,9 @@ def main():
     total_evals = world * args.steps * batch
     value = total_evals / elapsed
     avg_kernel_s = sum(kms) / len(kms) / 1e3
-    ops_launch = prog.ops_per_eval * batch
+    # executed algorithmic work per launch: the wide divisions' digit steps are
+    # priced by the steps the kernel ran (zero digits are skipped per wave)
+    ops_launch = prog.executed_ops(batch, sum(dsteps) / len(dsteps))
     achieved = ops_launch / avg_kernel_s
     measured_peak = load_measured_peak()
 
@@ -171,9 +179,12 @@ def main():
             "dag_nodes": len(__import__("mythril_amd.ir", fromlist=["topo"]).topo(syn.conjuncts)),
             "candidates_per_gpu_step": batch,
             "ops_per_eval": prog.ops_per_eval,
+            "ops_per_eval_executed": ops_launch / batch,
+            "division_steps_per_eval": (sum(dsteps) / len(dsteps)) / batch,
             "program_insns": prog.n_insn,
             "spill_slots": prog.n_spill,
-            "engine": args.engine + (f" ({dp.kernel}, {args.jit_waves} wave/SIMD, {args.jit_lds_leaves} leaves in LDS)"
+            "engine": args.engine + (f" ({dp.kernel}, {args.jit_waves} wave/SIMD, {args.jit_lds_leaves} leaves in LDS, "
+                                     f"interleave {args.jit_interleave}, split {jit.SPLIT_KIND})"
                                      if dp.kernel else ""),
             "jit_compile_s": jit_s,
             "jit_split": bool(args.jit_split) if args.engine == "jit" else None,

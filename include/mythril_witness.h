@@ -68,6 +68,10 @@ typedef struct {
   uint64_t evals;        /* program x candidate verdicts determined */
   uint64_t launches;
   double ops;            /* algorithmic u32 ops executed (evals x ops_per_eval) */
+  uint64_t lane_div_steps; /* wide-division digit steps run x lanes running them: the
+                              division zero-digit skip (mw_alu.h udivrem8) makes the
+                              executed share of ops_per_eval data-dependent; bench.py
+                              prices the executed steps from this count */
 } mg_stats;
 
 int mg_device_count(int* n);

@@ -121,6 +121,14 @@ class Program:
     stats: Dict[str, int] = field(default_factory=dict)
     ssa: List[MInsn] = field(default_factory=list)   # machine IR before slot allocation (jit.py)
 
+    def executed_ops(self, evals: int, lane_div_steps: int) -> float:
+        """Algorithmic u32 ops a search of `evals` candidates ran: ops_per_eval
+        with the wide divisions' digit steps priced by the steps the kernel
+        counted (mg_stats.lane_div_steps; zero digits are skipped per wave)."""
+        dso, dsm = self.stats.get("div_step_ops", 0), self.stats.get("div_steps_max", 0)
+        per_step = dso / dsm if dsm else 0.0
+        return evals * (self.ops_per_eval - dso) + lane_div_steps * per_step
+
     def input_rows_for(self, leaf_index: int) -> Tuple[int, int]:
         off = int(self.leaves[leaf_index * isa.LEAF_WORDS + isa.LEAF_INROW])
         return off, (self.leaf_specs[leaf_index].width + 31) // 32
@@ -838,9 +846,20 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
 
     reach = topo(conj + list(trace))
     ops = sum(node_cost(n) for n in reach)
+    # wide divisions: the digit-step part of their cost (all 8 steps of the fixed
+    # shape) and the step count; the kernels skip steps whose digit is 0 in every
+    # lane of a wave and count the steps they ran (mg_stats.lane_div_steps), so
+    # the executed work is ops_per_eval - div_step_ops + steps run x step cost
+    div_step_ops, div_steps_max = 0, 0
+    for n in reach:
+        if n.op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod") and _w(n) > isa.NARROW_MAX:
+            L = (_w(n) + 31) // 32
+            div_step_ops += L * (6 * L + 20)
+            div_steps_max += 8
     arr = lambda x: np.asarray(x if x else [0], dtype=np.uint32)
     stats = {"nodes": len(reach), "insns": len(code) // 4, "spills": sum(1 for i in insns if i.op.startswith("SPILL")),
-             "fills": sum(1 for i in insns if i.op.startswith("FILL"))}
+             "fills": sum(1 for i in insns if i.op.startswith("FILL")),
+             "div_step_ops": div_step_ops, "div_steps_max": div_steps_max}
     return Program(code=np.asarray(code, dtype=np.uint32), consts=arr(consts),
                    leaves=np.asarray(leaf_words, dtype=np.uint32), pool=arr(pool_words),
                    n_spill=n_spill, n_trace_rows=rows, n_input_rows=in_row, ops_per_eval=ops,

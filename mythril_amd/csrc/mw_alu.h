@@ -343,17 +343,43 @@ MW_HD u32 div3by2(u32 u2, u32 u1, u32 u0, u32 d1, u32 d0, u32 v, u32& r1, u32& r
 // When the window's top two words equal the divisor's, the estimate B-1 is
 // exact (GMP mpn_sbpi1_div_qr) and the 3-word partial remainder is
 // (d1:d0) + u0: handled with selects, no separate path.
-MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
+//
+// Zero digits are skipped per wave: when the window's top limb is 0 and the
+// next one is below d1 (the divisor's normalized top limb), the window is
+// below the divisor, so the digit is 0 and the step would change nothing.
+// A wave runs a step only if some lane needs it (the quotient of two random
+// 256-bit values has one digit: one step of eight).  *steps (optional) counts
+// the steps the wave ran, for the executed-work roofline (bench.py).
+MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], u32* steps = nullptr) {
   const u32 s = clz256(y);
+  // Normalisation shifts: with a full-width divisor (top limb nonzero in every
+  // lane of the wave, the common case) s < 32 and the limb-moving stages of
+  // the shifters are identities, so only the funnel shifts run.
+  const bool wide_shift = MW_ANY(s >= 32u);
   u32 v[8];
-  shl8(y, s, v);
   u32 u[16];
-  shl8to16(x, s, u);
+  if (wide_shift) {
+    shl8(y, s, v);
+    shl8to16(x, s, u);
+  } else {
+#pragma unroll
+    for (int k = 7; k >= 1; --k) v[k] = fshl32(y[k], y[k - 1], s);
+    v[0] = y[0] << s;
+    u[8] = fshl32(0u, x[7], s);
+#pragma unroll
+    for (int k = 7; k >= 1; --k) u[k] = fshl32(x[k], x[k - 1], s);
+    u[0] = x[0] << s;
+#pragma unroll
+    for (int k = 9; k < 16; ++k) u[k] = 0u;
+  }
   const u32 d1 = v[7], d0 = v[6];
   const u32 vinv = recip3by2(d1, d0);
 #pragma unroll
   for (int j = 7; j >= 0; --j) {
     const u32 u2 = u[j + 8], u1 = u[j + 7], u0 = u[j + 6];
+    q[j] = 0u;
+    if (!MW_ANY(u2 != 0u || u1 >= d1)) continue;  // digit 0 in every lane: nothing to do
+    if (steps) *steps += 1u;
     const bool sat = (u2 == d1) && (u1 == d0);
     u32 r1, r0;
     u32 qh = div3by2(u2, u1, u0, d1, d0, vinv, r1, r0);  // meaningless when sat
@@ -390,7 +416,13 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
     }
     q[j] = qh;
   }
-  shr8(u, s, 0u, r);
+  if (wide_shift) {
+    shr8(u, s, 0u, r);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) r[k] = fshr32(u[k + 1], u[k], s);
+    r[7] = fshr32(u[8], u[7], s);
+  }
 }
 
 MW_HD void neg8(const u32 a[8], u32 r[8]) {
@@ -409,7 +441,7 @@ MW_HD void cneg8(u32 a[8], bool c, u32 w) {  // a = c ? -a mod 2^w : a
 }
 
 // kind: 0 udiv, 1 urem, 2 sdiv, 3 srem, 4 smod.  x, y are consumed (overwritten).
-MW_HD void wdiv(int kind, u32 x[8], u32 y[8], u32 w, u32 r[8]) {
+MW_HD void wdiv(int kind, u32 x[8], u32 y[8], u32 w, u32 r[8], u32* steps = nullptr) {
   bool sa = false, sb = false;
   if (kind >= 2) {
     sa = signbit8(x, w);
@@ -420,7 +452,7 @@ MW_HD void wdiv(int kind, u32 x[8], u32 y[8], u32 w, u32 r[8]) {
   const bool yz = is_zero8(y);
   y[0] |= yz ? 1u : 0u;  // divide by 1 instead; result replaced below
   u32 q[8];
-  udivrem8(x, y, q, r);  // r = |s| mod |t|
+  udivrem8(x, y, q, r, steps);  // r = |s| mod |t|
   if (yz) {  // SMT-LIB: q = all ones, r = dividend magnitude
 #pragma unroll
     for (int k = 0; k < 8; ++k) {

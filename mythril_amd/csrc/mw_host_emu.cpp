@@ -21,6 +21,7 @@ struct HostEnv {
   u32* trace;
   u64 ncand, idx, seed, cand;
   std::vector<u32>* spillv;
+  u32 dsteps = 0;  // division digit steps (one candidate at a time here)
   void leaf(u32 li, u32 out[8]) {
     const u32* L = leaves + (u64)li * MW_LEAF_WORDS;
     if (in) {

@@ -13,6 +13,7 @@
 //   void store(u32 row, const u32* v, int n);  trace rows (mg_eval)
 //   void spill(u32 slot, const u32* v, int n); void fill(u32 slot, u32* v, int n);
 //   bool none(bool alive);                     wave-wide "no lane alive"
+//   u32 dsteps;                                division digit steps run (mw_alu.h udivrem8)
 #pragma once
 #include "mw_alu.h"
 #include "mw_isa.h"
@@ -226,7 +227,7 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
       case MW_W_SMOD:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
-        wdiv((int)(op - MW_W_UDIV), x, y, w, r);
+        wdiv((int)(op - MW_W_UDIV), x, y, w, r, &env.dsteps);
         wk = 1;
         break;
       case MW_W_ITE: {

@@ -51,12 +51,13 @@ MW_HD void w_not(const u32 x[8], u32 w, u32 r[8]) {
 MW_HD void w_shl(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { wshl(x, y, w, r); canon(r, w); }
 MW_HD void w_lshr(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { wlshr(x, y, w, r); canon(r, w); }
 MW_HD void w_ashr(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { washr(x, y, w, r); canon(r, w); }
-// kind: 0 udiv, 1 urem, 2 sdiv, 3 srem, 4 smod (wdiv consumes its operands)
-MW_HD void w_div(int kind, const u32 x[8], const u32 y[8], u32 w, u32 r[8]) {
+// kind: 0 udiv, 1 urem, 2 sdiv, 3 srem, 4 smod (wdiv consumes its operands);
+// steps counts the digit steps the wave ran (udivrem8 zero-digit skip)
+MW_HD void w_div(int kind, const u32 x[8], const u32 y[8], u32 w, u32 r[8], u32& steps) {
   u32 a[8], b[8];
   copy8(a, x);
   copy8(b, y);
-  wdiv(kind, a, b, w, r);
+  wdiv(kind, a, b, w, r, &steps);
   canon(r, w);
 }
 MW_HD void w_ite(u32 c, const u32 x[8], const u32 y[8], u32 w, u32 r[8]) {
@@ -253,7 +254,7 @@ MW_HD void tstore(u32* trace, u64 stride, u64 idx, u32 row, const u32* v, int n)
 #define JIT_SPLIT() ((void)ctl)
 #endif
 
-typedef bool (*body_fn)(const u32* __restrict__, u64, u64, bool, u32, u32*, u64, u64);
+typedef bool (*body_fn)(const u32* __restrict__, u64, u64, bool, u32, u32*, u64, u64, u32&);
 
 // stage bits of a launch: a program is one part (FIRST|LAST) or several parts
 // launched in order over the same candidates, passing each candidate's alive
@@ -286,7 +287,11 @@ __device__ __attribute__((always_inline)) inline void search(const u32* __restri
   const bool valid = cand < begin + count;
   bool in = valid;
   if (!(stage & MW_JIT_FIRST) && valid) in = alivebuf[cand - begin] != 0u;
-  const bool ok = BODY(pool, seed, cand, in, flags, nullptr, 0, 0);
+  u32 dsteps = 0;
+  const bool ok = BODY(pool, seed, cand, in, flags, nullptr, 0, 0, dsteps);
+  const u64 nvalid = (u64)__popcll(__ballot(valid));
+  if (lane == 0 && dsteps && nvalid)   // division digit steps x lanes (mg_stats.lane_div_steps)
+    atomicAdd((unsigned long long*)(counter + 1), (unsigned long long)(nvalid * dsteps));
   if (!(stage & MW_JIT_LAST)) {
     if (valid) alivebuf[cand - begin] = ok ? 1u : 0u;
     return;
@@ -297,8 +302,7 @@ __device__ __attribute__((always_inline)) inline void search(const u32* __restri
     const u32 first = (u32)__ffsll((unsigned long long)hit) - 1u;
     if (lane == first) atomicMin((unsigned long long*)out_min, (unsigned long long)cand);
   }
-  const u64 evals = (u64)__popcll(__ballot(valid));
-  if (lane == 0 && evals) atomicAdd((unsigned long long*)counter, (unsigned long long)evals);
+  if (lane == 0 && nvalid) atomicAdd((unsigned long long*)counter, (unsigned long long)nvalid);
 }
 
 // <name>_x: exhaustive; <name>_e: per-wave early exit after a failing CHECK.
@@ -332,9 +336,11 @@ __device__ __attribute__((always_inline)) inline void search(const u32* __restri
 #define MW_JIT_HOST_ENTRY(NAME, BODY)                                                                \
   extern "C" int NAME##_host(const mw::u32* pool, mw::u64 seed, mw::u64 begin, mw::u64 count,        \
                              mw::u32 early, mw::u32* verdict, mw::u32* trace) {                      \
-    for (mw::u64 i = 0; i < count; ++i)                                                              \
-      verdict[i] = (early ? BODY<true>(pool, seed, begin + i, true, 0u, trace, count, i)                 \
-                          : BODY<false>(pool, seed, begin + i, true, 0u, trace, count, i)) ? 1u : 0u;    \
+    for (mw::u64 i = 0; i < count; ++i) {                                                            \
+      mw::u32 ds = 0;                                                                                \
+      verdict[i] = (early ? BODY<true>(pool, seed, begin + i, true, 0u, trace, count, i, ds)             \
+                          : BODY<false>(pool, seed, begin + i, true, 0u, trace, count, i, ds)) ? 1u : 0u; \
+    }                                                                                                \
     return 0;                                                                                        \
   }
 #else

@@ -74,6 +74,7 @@ struct SearchEnv {
     }
   }
   __device__ bool none(bool alive) { return __ballot(alive) == 0ull; }
+  u32 dsteps = 0;  // division digit steps this wave ran (wave-uniform)
 };
 
 struct EvalEnv {
@@ -120,6 +121,7 @@ struct EvalEnv {
     }
   }
   __device__ bool none(bool) { return false; }  // eval: never exit early
+  u32 dsteps = 0;
 };
 
 }  // namespace
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __r
   const u64 nthreads = (u64)gridDim.x * gridDim.y * kBlock;
   const u64 gtid = ((u64)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x;
   const u32 lane = threadIdx.x & 63u;
-  u64 evals = 0;
+  u64 evals = 0, lane_steps = 0;
   for (u64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const u64 base = begin + ch * kBlock;
     if (flags & MW_FLAG_STOP_AFTER_HIT) {
@@ -151,9 +153,14 @@ __global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __r
       const u32 first = (u32)__ffsll((unsigned long long)hit) - 1u;
       if (lane == first) atomicMin((unsigned long long*)&out_min[blockIdx.y], (unsigned long long)cand);
     }
-    evals += (u64)__popcll(__ballot(valid));
+    const u64 nvalid = (u64)__popcll(__ballot(valid));
+    evals += nvalid;
+    lane_steps += nvalid * env.dsteps;
   }
-  if (lane == 0 && evals) atomicAdd((unsigned long long*)counter, (unsigned long long)evals);
+  if (lane == 0 && evals) {
+    atomicAdd((unsigned long long*)counter, (unsigned long long)evals);
+    if (lane_steps) atomicAdd((unsigned long long*)(counter + 1), (unsigned long long)lane_steps);
+  }
 }
 
 __global__ __launch_bounds__(kBlock, 2) void mw_eval_kernel(ProgDev P, const u32* __restrict__ in,
@@ -254,7 +261,7 @@ struct mg_ctx {
   size_t spill_bytes = 0;
   u64* d_min = nullptr;
   size_t nmin = 0;
-  u64* d_counter = nullptr;
+  u64* d_counter = nullptr;   // [0] evals, [1] division digit steps x lanes (mg_stats)
   u32* d_alive = nullptr;     // per-candidate alive bits between the parts of a split program
   size_t alive_cap = 0;
   ProgDev* d_progs = nullptr;
@@ -407,7 +414,7 @@ int mg_init(int device, mg_ctx** out) {
     c->ncu = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
-      hipMalloc(&c->d_counter, sizeof(u64)) != hipSuccess) {
+      hipMalloc(&c->d_counter, 2 * sizeof(u64)) != hipSuccess) {
     delete c;
     return fail(MG_E_HIP, "context setup failed");
   }
@@ -596,7 +603,7 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   }
   std::vector<u64> init(nprog, MG_NONE);
   HIPCHK(hipMemcpyAsync(c->d_min, init.data(), nprog * sizeof(u64), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemsetAsync(c->d_counter, 0, sizeof(u64), c->stream));
+  HIPCHK(hipMemsetAsync(c->d_counter, 0, 2 * sizeof(u64), c->stream));
   HIPCHK(hipEventRecord(c->e0, c->stream));
   if (ni) {
     hipLaunchKernelGGL(mw_search_kernel, dim3((u32)gx, (u32)ni), dim3(kBlock), (size_t)nlds * 8 * kBlock * 4,
@@ -608,10 +615,11 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
     if (rc) return rc;
   }
   HIPCHK(hipEventRecord(c->e1, c->stream));
-  u64 evals = 0;
+  u64 ctr[2] = {0, 0};
   std::vector<u64> mins(nprog);
   HIPCHK(hipMemcpyAsync(mins.data(), c->d_min, nprog * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(&evals, c->d_counter, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(ctr, c->d_counter, 2 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  const u64 evals = ctr[0];
   HIPCHK(hipStreamSynchronize(c->stream));
   for (size_t j = 0; j < ni; ++j) out_min_idx[interp[j]] = mins[j];
   for (size_t j = 0; j < special.size(); ++j) out_min_idx[special[j]] = mins[ni + j];
@@ -623,6 +631,7 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
     st->evals = evals;  // summed over every program's blocks
     st->launches = (ni ? 1 : 0) + special.size();
     st->ops = (double)evals / (double)nprog * (double)ops;
+    st->lane_div_steps = ctr[1];
   }
   return 0;
 }
@@ -686,7 +695,7 @@ int mg_eval_generated(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin
   if (hipMalloc(&d_v, count * 4) != hipSuccess) return fail(MG_E_NOMEM, "eval verdict alloc");
   const u64 none = MG_NONE;
   hipError_t e = hipMemcpyAsync(c->d_min, &none, sizeof(u64), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, sizeof(u64), c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, 2 * sizeof(u64), c->stream);
   if (e == hipSuccess) {
     rc = launch_jit(c, p, seed, begin, count, 0u, c->d_min, d_v);
     if (rc) {
@@ -742,6 +751,7 @@ int mg_keccak256_device(mg_ctx* c, const uint8_t* d_data, const uint64_t* d_off,
     st->evals = n;
     st->launches = 1;
     st->ops = 0;
+    st->lane_div_steps = 0;
   }
   return 0;
 }

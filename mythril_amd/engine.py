@@ -65,9 +65,15 @@ class Query:
         return self.program.ops_per_eval
 
 
-def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True) -> Query:
+def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True,
+            timings: Optional[Dict[str, float]] = None) -> Query:
+    """Lower, harvest candidate pools and compile one constraint set.
+    timings (optional) receives the seconds of each phase (tools/latency_bench.py)."""
+    import time
+    t0 = time.perf_counter()
     conj = list(conjuncts)
     low = lower_constraints(conj, ctx) if needs_lowering(conj) else Lowered(conj)
+    t1 = time.perf_counter()
     leaves = []
     seen = set()
     from .ir import topo
@@ -76,7 +82,10 @@ def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True) -> Quer
             seen.add(n.name)
             leaves.append(n)
     specs = harvest(low.conjuncts, leaves) if use_pools else {}
+    t2 = time.perf_counter()
     prog = compile_program(low.conjuncts, leaf_specs=specs)
+    if timings is not None:
+        timings.update(lower=t1 - t0, pools=t2 - t1, compile=time.perf_counter() - t2)
     # identical leaf layout (pool fields already assigned) for the materialisation program
     fixed = {s.name: copy.deepcopy(s) for s in prog.leaf_specs}
     # trace every array index / function argument (wider than 256 bits: as 256-bit chunks)

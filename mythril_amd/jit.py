@@ -46,6 +46,9 @@ M256 = (1 << 256) - 1
 # scheduler interleaves far-apart computations and spills heavily (C5-1k:
 # 1121 VGPR spills in one block, 25 with a block per conjunct).
 SPLIT_EVERY = 48
+# how a region boundary is emitted: "branch" (JIT_SPLIT of mw_jit.h) or
+# "sched_barrier" (MW_JIT_SPLIT env: experiments)
+SPLIT_KIND = os.environ.get("MW_JIT_SPLIT", "branch")
 M32 = 0xFFFFFFFF
 
 _WBIN = {"W_ADD": "w_add", "W_SUB": "w_sub", "W_MUL": "w_mul", "W_AND": "w_and", "W_OR": "w_or",
@@ -83,14 +86,66 @@ def _fnv_words(h: int, a: np.ndarray) -> int:
     return h
 
 
+def interleave_conjuncts(insns: List[MInsn], k: int) -> List[MInsn]:
+    """Merge each run of k consecutive conjuncts (SSA segments ending at a
+    CHECK) into one instruction stream, round-robin, so independent dependency
+    chains sit side by side in every basic block.
+
+    A conjunct alone is one serial chain (C5: every node consumes its
+    predecessor; a 256-bit add is an 8-deep carry chain).  gfx950 needs wait
+    states between a VALU that writes a carry/mask SGPR and the VALU reading
+    it, and LLVM pads a serial chain with s_nop; a second, independent chain in
+    the same block fills those slots and the VALU latency instead.  The merge
+    keeps every operand defined before its use: a segment whose next
+    instruction reads a value another segment of the group has not produced
+    yet (a leaf first generated there) waits while that segment advances."""
+    if k <= 1:
+        return list(insns)
+    segs: List[List[MInsn]] = []
+    cur: List[MInsn] = []
+    tail: List[MInsn] = []
+    for ins in insns:
+        if ins.op == "END":
+            tail.append(ins)
+            continue
+        cur.append(ins)
+        if ins.op == "CHECK":
+            segs.append(cur)
+            cur = []
+    if cur:
+        segs.append(cur)
+    out: List[MInsn] = []
+    defined = set()
+    for g in range(0, len(segs), k):
+        group = segs[g:g + k]
+        pos = [0] * len(group)
+        left = sum(len(sg) for sg in group)
+        while left:
+            # round-robin; a head whose operand is still pending waits.  The
+            # earliest unfinished segment can always issue (the original order
+            # is topological), so every round makes progress.
+            for j, sg in enumerate(group):
+                if pos[j] >= len(sg):
+                    continue
+                ins = sg[pos[j]]
+                if any(isinstance(s_, VReg) and s_.id not in defined for s_ in ins.srcs):
+                    continue
+                out.append(ins)
+                if ins.dst is not None:
+                    defined.add(ins.dst.id)
+                pos[j] += 1
+                left -= 1
+    return out + tail
+
+
 class _Gen:
     """Emit the body of one program as straight-line HIP."""
 
     def __init__(self, p: Program, name: str, fence_first: bool = False, lds_leaves: int = 0,
-                 insns: Optional[List[MInsn]] = None):
+                 insns: Optional[List[MInsn]] = None, interleave: int = 1):
         self.fence_first = fence_first  # diagnostics (tools/opbench.py): no folding across nodes
         self.p = p
-        self.insns = p.ssa if insns is None else insns
+        self.insns = interleave_conjuncts(p.ssa if insns is None else insns, interleave)
         # the lds_leaves most-used wide leaves live in LDS (mw_jit.h lds_put8/lds_get8)
         uses: Dict[int, int] = {}
         defs: Dict[int, int] = {}
@@ -192,7 +247,7 @@ class _Gen:
         elif op in _WBIN:
             out(f"u32 {dn}[8]; jit::{_WBIN[op]}({A[0]}, {A[1]}, {w}u, {dn});")
         elif op.startswith("W_") and op[2:] in _DIV:
-            out(f"u32 {dn}[8]; jit::w_div({_DIV[op[2:]]}, {A[0]}, {A[1]}, {w}u, {dn});")
+            out(f"u32 {dn}[8]; jit::w_div({_DIV[op[2:]]}, {A[0]}, {A[1]}, {w}u, {dn}, dsteps);")
         elif op == "W_NOT":
             out(f"u32 {dn}[8]; jit::w_not({A[0]}, {w}u, {dn});")
         elif op == "W_ITE":
@@ -246,7 +301,8 @@ class _Gen:
             self.emit(ins)
         head = [f"template <bool EARLY>",
                 f"MW_HD bool {self.name}_body(const u32* __restrict__ pool, u64 seed, u64 cand, bool alive,",
-                f"                             u32 ctl, u32* __restrict__ trace, u64 tstride, u64 tidx) {{"]
+                f"                             u32 ctl, u32* __restrict__ trace, u64 tstride, u64 tidx,",
+                f"                             u32& dsteps) {{"]
         consts = []
         for v, n in self.wconst.items():
             limbs = ", ".join(f"{(v >> (32 * k)) & M32:#x}u" for k in range(8))
@@ -330,20 +386,26 @@ def split_ssa(p: Program, part_weight: int = PART_WEIGHT) -> List[List[MInsn]]:
 
 def generate(progs: Sequence[Program], names: Sequence[str], variants: str = "xe",
              fence_first: bool = False, lds_leaves: int = 0,
-             parts: Optional[Sequence[Tuple[List[MInsn], int, int]]] = None) -> str:
+             parts: Optional[Sequence[Tuple[List[MInsn], int, int]]] = None, interleave: int = 1) -> str:
     """HIP source for a module holding one specialised kernel set per program
     (with `parts`: per program, its (instructions, part index, part count))."""
     out = ["// generated by mythril_amd/jit.py: specialised witness-search kernels"]
     if lds_leaves:
         out.append(f"#define MW_JIT_LDS_SLOTS {lds_leaves}")
     out += ['#include "mw_jit.h"', "using namespace mw;", ""]
+    if SPLIT_KIND == "sched_barrier":
+        # region boundaries as scheduling barriers instead of never-taken branches:
+        # no branch (and no long-jump sequence past a cold block at the end of a
+        # multi-MiB body), the scheduler still cannot move code across them
+        out += ["#if defined(__HIP_DEVICE_COMPILE__)", "#undef JIT_SPLIT",
+                "#define JIT_SPLIT() __builtin_amdgcn_sched_barrier(0)", "#endif", ""]
     for k, (p, name) in enumerate(zip(progs, names)):
         if not p.ssa:
             raise ValueError("program has no SSA machine IR (compiled by an older compiler?)")
         part = parts[k] if parts else None
         out.append(f"// program {name}: {p.n_insn} bytecode insns, {p.ops_per_eval} u32 ops/eval"
                    + (f", part {part[1]} of {part[2]}" if part else ""))
-        out.append(_Gen(p, name, fence_first, lds_leaves, part[0] if part else None).body())
+        out.append(_Gen(p, name, fence_first, lds_leaves, part[0] if part else None, interleave).body())
         out.append(f"MW_JIT_SIG({name}, {signature(p):#x}ull)")
         if part:
             out.append(f"MW_JIT_PART({name}, {part[1]}u, {part[2]}u)")
@@ -419,22 +481,23 @@ def _compile(src: str, flags: Sequence[str], suffix: str, ext: str) -> Tuple[Pat
     return out, time.perf_counter() - t0
 
 
-def is_cached(progs: Sequence[Program], variants: str = "xe", waves: int = 2, lds_leaves: int = 0) -> bool:
+def is_cached(progs: Sequence[Program], variants: str = "xe", waves: int = 2, lds_leaves: int = 0,
+              interleave: int = 1) -> bool:
     """Whether compile_device(...) with these arguments would be a cache hit."""
     names = [kernel_name(p) for p in progs]
-    src = generate(progs, names, variants, lds_leaves=lds_leaves)
+    src = generate(progs, names, variants, lds_leaves=lds_leaves, interleave=interleave)
     return (_cache_dir() / f"{_key(src, _device_flags(waves))}.hsaco").exists()
 
 
 def compile_device(progs: Sequence[Program], variants: str = "xe", fence_first: bool = False,
-                   waves: int = 2, lds_leaves: int = 0) -> Tuple[bytes, List[str], float]:
+                   waves: int = 2, lds_leaves: int = 0, interleave: int = 1) -> Tuple[bytes, List[str], float]:
     """gfx950 code object for `progs`; returns (image, kernel names, compile seconds; 0 if cached).
 
     waves: waves per SIMD the kernels are built for (launch bounds): 2 gives
     each lane 256 registers, 1 gives 512 (AGPRs become spill space instead of
     scratch memory) at half the latency hiding."""
     names = [kernel_name(p) for p in progs]
-    src = generate(progs, names, variants, fence_first, lds_leaves)
+    src = generate(progs, names, variants, fence_first, lds_leaves, interleave=interleave)
     path, dt = _compile(src, _device_flags(waves), ".hsaco", ".hip")
     return path.read_bytes(), names, dt
 
@@ -466,7 +529,7 @@ def _device_flags(waves: int) -> List[str]:
 
 
 def compile_parts(p: Program, variants: str = "xe", waves: int = 2, lds_leaves: int = 0,
-                  part_weight: int = PART_WEIGHT) -> Tuple[List[Tuple[bytes, str]], float]:
+                  part_weight: int = PART_WEIGHT, interleave: int = 1) -> Tuple[List[Tuple[bytes, str]], float]:
     """Code objects of a program's parts (split_ssa), compiled in parallel hipcc
     processes; returns ([(image, kernel name)], wall seconds, 0 if all cached)."""
     from concurrent.futures import ThreadPoolExecutor
@@ -477,7 +540,8 @@ def compile_parts(p: Program, variants: str = "xe", waves: int = 2, lds_leaves: 
     for k, seg in enumerate(segs):
         name = base if n == 1 else f"{base}_p{k}"
         spec = None if n == 1 else [(seg, k, n)]
-        jobs.append((name, generate([p], [name], variants, lds_leaves=lds_leaves, parts=spec)))
+        jobs.append((name, generate([p], [name], variants, lds_leaves=lds_leaves, parts=spec,
+                                    interleave=interleave)))
     t0 = time.perf_counter()
     workers = max(1, min(n, int(os.environ.get("MW_JIT_JOBS", "8"))))
     with ThreadPoolExecutor(workers) as ex:
@@ -487,7 +551,7 @@ def compile_parts(p: Program, variants: str = "xe", waves: int = 2, lds_leaves: 
 
 
 def attach(dev, dps, variants: str = "xe", waves: int = 2, lds_leaves: int = 0,
-           split: bool = False, part_weight: int = PART_WEIGHT) -> float:
+           split: bool = False, part_weight: int = PART_WEIGHT, interleave: int = 1) -> float:
     """Compile and attach specialised kernels to loaded programs (DevicePrograms); returns
     the compile seconds (0 when every code object came from the cache).  split: large
     programs become several part kernels (compile_parts) instead of one."""
@@ -495,13 +559,14 @@ def attach(dev, dps, variants: str = "xe", waves: int = 2, lds_leaves: int = 0,
     if split:
         total = 0.0
         for dp in dps:
-            objs, dt = compile_parts(dp.prog, variants, waves, lds_leaves, part_weight)
+            objs, dt = compile_parts(dp.prog, variants, waves, lds_leaves, part_weight, interleave)
             for image, name in objs:
                 dev.attach_kernel(dp, image, name)
             dp.kernel = objs[0][1].rsplit("_p", 1)[0] + (f" ({len(objs)} parts)" if len(objs) > 1 else "")
             total += dt
         return total
-    image, names, dt = compile_device([dp.prog for dp in dps], variants, waves=waves, lds_leaves=lds_leaves)
+    image, names, dt = compile_device([dp.prog for dp in dps], variants, waves=waves, lds_leaves=lds_leaves,
+                                      interleave=interleave)
     for dp, name in zip(dps, names):
         dev.attach_kernel(dp, image, name)
     return dt
@@ -519,10 +584,11 @@ def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 2, lds_leaves
     from . import hostemu
     from .synth import build_c5
     t0 = time.perf_counter()
-    # density 24: the benchmark's program; density 8: the same DAG with mixed
-    # verdicts, for the full-size parity test (tests/test_gpu_fullsize.py)
-    for dens in (24, 8):
-        syn = build_c5(hostemu.term_values, n_nodes=n_nodes, density_log2=dens)
+    # density 24: the benchmark's program; density 1 without the leftover
+    # comparisons: the same chains with mixed verdicts (about half satisfied),
+    # for the full-size parity test (tests/test_gpu_fullsize.py)
+    for dens in (24, 1):
+        syn = build_c5(hostemu.term_values, n_nodes=n_nodes, density_log2=dens, keep_pending=dens == 24)
         prog = compile_program(syn.conjuncts)
         if dens == 24:
             # the split kernels too: bench.py falls back to them (a minute of

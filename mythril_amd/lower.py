@@ -385,6 +385,10 @@ class _Rewriter:
             return c._mk(op, n.width, tuple(args), n.params, n.val, n.name, n.dom)
         if op == "ite" and n.is_array:
             return c._mk("ite", n.width, tuple(args), dom=n.dom)
+        if op in _POW2_OPS and len(args) == 2 and n.width <= MAXW:
+            r = self._pow2(op, args, n.width)
+            if r is not None:
+                return r
         if op == "apply":
             # Mythril's keccak inverse (keccak_function_manager.py:80-81): inv(keccak256_N(x)) is
             # *defined* as x.  Sound: every inverse application sits on a keccak application
@@ -429,6 +433,46 @@ class _Rewriter:
             return c._mk(op, n.width, tuple(args), n.params)
         return c.app(op, *args, params=n.params) if op not in ("ite",) else c.app("ite", *args)
 
+    def _pow2(self, op: str, args: List[Node], w: int) -> Optional[Node]:
+        """z3 ``simplify`` rewrites (bv_rewriter) that turn arithmetic by a power
+        of two into structure: ``x / 2^k``, ``x >> k`` -> ``concat(0, extract)``;
+        ``x % 2^k``, ``x & (2^k - 1)`` -> ``concat(0, extract)``;
+        ``x * 2^k``, ``x << k`` -> ``concat(extract, 0)``.  Solidity's selector
+        dispatch ``div(calldataload(0), 2^224) & 0xffffffff`` then reaches the
+        calldata bytes as an extract, which the candidate pools project through,
+        and the kernels run no division for it."""
+        c = self.ctx
+        x, k = args
+        if op in ("bvmul", "bvand") and x.op == "const" and k.op != "const":
+            x, k = k, x
+        if k.op != "const":
+            return None
+        v = k.val
+        if op == "bvand":
+            if v == 0:
+                return c.const(0, w)
+            if v & (v + 1):        # not of the form 2^j - 1
+                return None
+            j = v.bit_length()
+            return x if j >= w else c.app("concat", c.const(0, w - j), self.extract(x, j - 1, 0))
+        if op in ("bvshl", "bvlshr"):
+            j = v
+        else:
+            if v == 0 or v & (v - 1):
+                return None
+            j = v.bit_length() - 1
+        if op in ("bvudiv", "bvlshr"):
+            if j == 0:
+                return x
+            return c.const(0, w) if j >= w else c.app("concat", c.const(0, j), self.extract(x, w - 1, j))
+        if op == "bvurem":
+            return c.const(0, w) if j == 0 else (x if j >= w else
+                                                 c.app("concat", c.const(0, w - j), self.extract(x, j - 1, 0)))
+        # bvmul, bvshl
+        if j == 0:
+            return x
+        return c.const(0, w) if j >= w else c.app("concat", self.extract(x, w - 1 - j, 0), c.const(0, j))
+
     def congruence(self) -> List[Node]:
         c = self.ctx
         out = []
@@ -445,6 +489,8 @@ class _Rewriter:
                     out.append(c.app("=>", prem, self.eq(vt, vu)))
         return out
 
+
+_POW2_OPS = frozenset({"bvudiv", "bvurem", "bvmul", "bvand", "bvshl", "bvlshr"})
 
 # wide orderings: op -> (signedness, swap operands, strict)
 _ORDER = {"bvult": ("u", False, True), "bvugt": ("u", True, True), "bvule": ("u", False, False),
@@ -521,5 +567,7 @@ def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
 def needs_lowering(conjuncts: List[Node]) -> bool:
     for n in topo(conjuncts):
         if n.op in ("select", "apply", "store", "const_array", "array") or n.width > MAXW:
+            return True
+        if n.op in _POW2_OPS and len(n.args) == 2 and any(a.op == "const" for a in n.args):
             return True
     return False

@@ -136,6 +136,19 @@ def _force(e: Node, value: int, lo: int, hi: int, out: Dict[str, int], depth: in
                 _force(x, value - k.val if op == "bvadd" else value ^ k.val, lo, hi, out, depth + 1)
 
 
+def _align_of(t: Node):
+    """(leaf name, K) when ``t == 0`` says the leaf is a multiple of K: the
+    ``bvurem(x, K)`` form and its power-of-two rewrite ``concat(0, extract(j-1, 0, x))``
+    (lower.py, z3 simplify's shape), or a bare low-bit extract."""
+    if t.op == "bvurem" and t.args[0].op == "var" and t.args[1].op == "const" and t.args[1].val > 1:
+        return t.args[0].name, t.args[1].val
+    if t.op == "concat" and len(t.args) == 2 and t.args[0].op == "const" and t.args[0].val == 0:
+        t = t.args[1]
+    if t.op == "extract" and t.params[1] == 0 and t.args[0].op == "var" and t.params[0] + 1 < t.args[0].width:
+        return t.args[0].name, 1 << (t.params[0] + 1)
+    return None
+
+
 def _eq_const(n: Node):
     if n.op == "=" and len(n.args) == 2:
         a, b = n.args
@@ -198,9 +211,9 @@ def domains(conjuncts: List[Node]):
             for name, v in f.items():
                 exact[name] = [v]
             t, k = ec
-            if k == 0 and t.op == "bvurem" and t.args[0].op == "var" and t.args[1].op == "const" \
-                    and t.args[1].val > 1:
-                align[t.args[0].name] = t.args[1].val
+            al = _align_of(t) if k == 0 else None
+            if al is not None:
+                align[al[0]] = al[1]
             return
         if n.op in _UPPER:
             _bound(n.op, *n.args)
@@ -275,9 +288,9 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
         if n.op == "=" and len(n.args) == 2:
             a, b = n.args
             for x, k in ((a, b), (b, a)):
-                if k.op == "const" and k.val == 0 and x.op == "bvurem" and x.args[1].op == "const" \
-                        and x.args[0].op == "var" and x.args[1].val > 1:
-                    align[x.args[0].name] = x.args[1].val
+                al = _align_of(x) if (k.op == "const" and k.val == 0) else None
+                if al is not None:
+                    align[al[0]] = al[1]
     for name, K in align.items():
         props = proposals.get(name, [])
         aligned = []

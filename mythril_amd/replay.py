@@ -78,7 +78,8 @@ def main(argv=None):
     a = ap.parse_args(argv)
     files = []
     for p in a.paths:
-        files += sorted(glob.glob(os.path.join(p, "*.smt2"))) if os.path.isdir(p) else [p]
+        files += sorted(glob.glob(os.path.join(p, "*.smt2")) + glob.glob(os.path.join(p, "*.smt2.gz"))) \
+            if os.path.isdir(p) else [p]
     from .engine import WitnessEngine
     eng = WitnessEngine(device=a.device, budget=a.budget)
     t0 = time.perf_counter()

@@ -245,6 +245,11 @@ def parse_script(text: str, ctx: Optional[Ctx] = None) -> Script:
 
 
 def parse_file(path: str, ctx: Optional[Ctx] = None) -> Script:
+    """Parse a dump; ``.gz`` files (the committed corpora) are read compressed."""
+    if path.endswith(".gz"):
+        import gzip
+        with gzip.open(path, "rt") as f:
+            return parse_script(f.read(), ctx)
     with open(path) as f:
         return parse_script(f.read(), ctx)
 

@@ -115,8 +115,13 @@ def build_chains(n_nodes: int = 10000, n_leaves: int = 16, n_conj: int = 32, see
 
 def build_c5(evaluate: Callable[[Sequence[Node], int, int], List[int]], n_nodes: int = 10000,
              n_leaves: int = 16, n_conj: int = 32, seed: int = 0x5EED0005,
-             witness_index: int = 0x5EED0005 % (1 << 31), density_log2: int = 24) -> Synthetic:
-    """evaluate(terms, candidate_index, seed) -> values of `terms` at that candidate."""
+             witness_index: int = 0x5EED0005 % (1 << 31), density_log2: int = 24,
+             keep_pending: bool = True) -> Synthetic:
+    """evaluate(terms, candidate_index, seed) -> values of `terms` at that candidate.
+
+    keep_pending=False drops the chains' leftover comparisons (each halves the
+    satisfying density), so density_log2 alone sets it: the mixed-verdict
+    variant of the full-size parity test (tests/test_gpu_fullsize.py)."""
     ctx, leaves, ends, pend, count = build_chains(n_nodes, n_leaves, n_conj, seed)
     vals = evaluate(ends, witness_index, seed)
     pend_vals = evaluate([b for bs in pend for b in bs], witness_index, seed) if any(pend) else []
@@ -131,6 +136,7 @@ def build_c5(evaluate: Callable[[Sequence[Node], int, int], List[int]], n_nodes:
         for b in bs:
             bv = pend_vals[k]
             k += 1
-            c = ctx.app("and", c, b if bv else ctx.app("not", b))
+            if keep_pending:
+                c = ctx.app("and", c, b if bv else ctx.app("not", b))
         conj.append(c)
     return Synthetic(ctx, leaves, ends, conj, witness_index, seed, count + len(conj))

@@ -1,9 +1,9 @@
 """Full-size parity of the benchmarked kernels against the oracle.
 
 The C5 program bench.py measures (10k-node DAG, 16 free 256-bit leaves,
-BASELINE.json configs[4]) and a mixed-verdict variant of it (same DAG, conjunct
-thresholds for a satisfying density of 2^-8) are checked on the device at
-their real size:
+BASELINE.json configs[4]) and a mixed-verdict variant of it (the same chains,
+thresholds for a satisfying density of 1/2, leftover comparisons dropped) are
+checked on the device at their real size:
 
 (a) the specialised kernel's and the interpreter's verdicts on 2^16 candidate
     indices around the planted witness (and at the start of the index space)
@@ -19,6 +19,8 @@ __graft_entry__.build() (compiling the 10k-node kernel takes minutes); a
 missing code object fails the test instead of compiling on the GPU box.
 """
 import os
+import sys
+import time
 
 import numpy as np
 import pytest
@@ -44,17 +46,20 @@ def dev():
 def _c5(density_log2):
     from mythril_amd import hostemu
     from mythril_amd.synth import build_c5
-    syn = build_c5(hostemu.term_values, density_log2=density_log2)
+    syn = build_c5(hostemu.term_values, density_log2=density_log2, keep_pending=density_log2 == 24)
     return syn, compile_program(syn.conjuncts)
 
 
-@pytest.fixture(scope="module", params=[24, 8], ids=["bench-density24", "mixed-density8"])
+@pytest.fixture(scope="module", params=[24, 1], ids=["bench-density24", "mixed-density1"])
 def c5(request, dev):
+    t0 = time.perf_counter()
     syn, prog = _c5(request.param)
+    _log(f"density {request.param}: program built in {time.perf_counter() - t0:.1f} s")
     if not jit.is_cached([prog], "x", BENCH_WAVES, BENCH_LDS):
         pytest.fail("C5 specialised kernel not in build/jit: run __graft_entry__.build() first")
     special = dev.load(prog)
     jit.attach(dev, [special], variants="x", waves=BENCH_WAVES, lds_leaves=BENCH_LDS)
+    _log(f"density {request.param}: kernel {special.kernel} attached")
     interp = dev.load(prog)
     assert dev.has_kernel(special) and not dev.has_kernel(interp)
     yield request.param, syn, prog, special, interp
@@ -62,19 +67,27 @@ def c5(request, dev):
     interp.free()
 
 
+def _log(msg):
+    print(f"[fullsize {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def test_c5_verdicts_match_oracle(c5, dev):
     dens, syn, prog, special, interp = c5
     w = syn.witness_index
-    for begin in (w - SWEEP // 2, 0):
-        vs, _ = dev.eval_generated(special, syn.seed, begin, SWEEP, trace=False)
-        vi, _ = dev.eval_generated(interp, syn.seed, begin, SWEEP, trace=False)
-        tot, _, vo = cdag.evaluate(syn.conjuncts, syn.seed, begin, SWEEP, want_verdict=True)
+    for begin, n in ((w - SWEEP // 2, SWEEP), (0, SWEEP // 4)):
+        t0 = time.perf_counter()
+        vs, _ = dev.eval_generated(special, syn.seed, begin, n, trace=False)
+        vi, _ = dev.eval_generated(interp, syn.seed, begin, n, trace=False)
+        _log(f"density {dens}: device verdicts of [{begin}, +{n}) in {time.perf_counter() - t0:.2f} s")
+        t0 = time.perf_counter()
+        tot, _, vo = cdag.evaluate(syn.conjuncts, syn.seed, begin, n, want_verdict=True)
+        _log(f"density {dens}: oracle/c verdicts in {time.perf_counter() - t0:.2f} s ({tot} satisfied)")
         assert np.array_equal(vs.astype(np.uint8), vo), f"specialised vs oracle, density {dens}, begin {begin}"
         assert np.array_equal(vi.astype(np.uint8), vo), f"interpreter vs oracle, density {dens}, begin {begin}"
         if begin != 0:
             assert vo[w - begin] == 1, "planted witness"
-        if dens == 8:
-            assert 0 < tot < SWEEP, "mixed verdicts expected"
+        if dens == 1:
+            assert n // 64 < tot < n - n // 64, "mixed verdicts expected"
 
 
 def test_c5_search_finds_planted_witness(c5, dev):

@@ -7,7 +7,7 @@
 #   smoke          __graft_entry__.smoke()
 #   tests[=EXPR]   pytest -m gpu (optionally -k EXPR)
 #   bench          python bench.py (default flags) -> bench.json
-#   bench1         bench.py --steps 5 --no-ttfw --no-cpu-baseline (quick)
+#   bench1         bench.py --steps 5 --no-ttfw --no-cpu-baseline $BENCH_ARGS (quick A/B runs)
 #   prof           rocprofv3 --kernel-trace --stats on a short bench run
 #   pmc            PMC passes on one bench launch (SQ, instruction mix, FETCH_SIZE, WRITE_SIZE)
 #   config         tools/config_bench.py (C2-C4 queries) -> config_bench.json
@@ -23,7 +23,7 @@ TAG=$1
 shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-ttfw"
+B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-ttfw ${BENCH_ARGS:-}"
 
 run() {  # run LIMIT LOG CMD...: one GPU step, bounded; print the log tail on failure
   local lim=$1 log=$2
@@ -46,7 +46,7 @@ for step in "$@"; do
     tests|tests=*)
       K=()
       [ "$step" != tests ] && K=(-k "${step#tests=}")
-      run 1000 "$OUT/gpu_tests.log" python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}"
+      run 1000 "$OUT/gpu_tests.log" python3 -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread "${K[@]}"
       tail -3 "$OUT/gpu_tests.log" ;;
     bench)
       run 500 "$OUT/bench.err" bash -c "python3 bench.py > $OUT/bench.json"

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Per-query latency of the drop-in path: what one
+get_model(...) feasibility query costs before z3 would be asked.
+
+For every query of the committed corpora (tests/golden/solver_log: the C2-C4
+shapes; tests/golden/laser: LASER-shaped queries over the reference's own
+bytecode) it reports, in ms:
+  parse      SMT-LIB2 text -> IR (stands in for z3bridge.to_ir; no z3 here)
+  lower      Ackermannisation, congruence, wide legalisation (lower.py)
+  pools      candidate pools / domains (pools.py)
+  compile    bytecode + register allocation (compiler.py)
+  search     one mg_search launch, early exit + stop-after-hit, the engine's
+             default per-query budget (device; wall time of the call)
+  materialise  trace program compile + single-candidate re-evaluation (only
+             on a witness)
+and the medians per corpus.  Without a GPU (--no-device) only the host
+phases are timed.
+
+    python tools/latency_bench.py [--out FILE] [--no-device]
+"""
+import argparse
+import glob
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--no-device", action="store_true")
+    a = ap.parse_args()
+    from mythril_amd.engine import WitnessEngine, prepare
+    from mythril_amd.smt2 import parse_file
+    eng = None if a.no_device else WitnessEngine(device=0)
+    rows = []
+    for corpus in ("solver_log", "laser"):
+        files = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", corpus, "*.smt2*")))
+        for f in files:
+            t0 = time.perf_counter()
+            s = parse_file(f)
+            t_parse = time.perf_counter() - t0
+            tm = {}
+            q = prepare(s.asserts, s.ctx, timings=tm)
+            row = {"corpus": corpus, "file": os.path.basename(f), "conjuncts": q.program.n_conjuncts,
+                   "insns": q.program.n_insn, "parse": t_parse * 1e3,
+                   **{k: v * 1e3 for k, v in tm.items()}}
+            row["prepare"] = row["lower"] + row["pools"] + row["compile"]
+            if eng is not None:
+                t1 = time.perf_counter()
+                dp = eng.dev.load(q.program)
+                (idx,), st = eng.dev.search([dp], eng.seed, 0, eng.launch_count([q]), 3)
+                dp.free()
+                row["search"] = (time.perf_counter() - t1) * 1e3
+                row["kernel"] = st["kernel_ms"]
+                if idx is not None:
+                    t2 = time.perf_counter()
+                    eng.materialize(q, idx)
+                    row["materialise"] = (time.perf_counter() - t2) * 1e3
+                row["witness"] = idx is not None
+            rows.append(row)
+            print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in row.items()}), flush=True)
+    summary = {}
+    for corpus in ("solver_log", "laser"):
+        rs = [r for r in rows if r["corpus"] == corpus]
+        summary[corpus] = {k: statistics.median(r[k] for r in rs if k in r)
+                           for k in ("parse", "lower", "pools", "compile", "prepare", "search", "kernel", "materialise")
+                           if any(k in r for r in rs)}
+        summary[corpus]["queries"] = len(rs)
+    print(json.dumps({"median_ms": summary}), flush=True)
+    if a.out:
+        json.dump({"rows": rows, "median_ms": summary}, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
