@@ -262,10 +262,16 @@ class _Lowerer:
             if self._fresh(m):
                 continue
             stack.append((m, True))
+            if self._lazy_concat(m):
+                continue   # parts are lowered one by one as they are inserted (_concat_lazy)
             for a in reversed(m.args):
                 if not self._fresh(a):
                     stack.append((a, False))
         return self.memo[n.id]
+
+    @staticmethod
+    def _lazy_concat(m: Node) -> bool:
+        return m.op == "concat" and cls_of(_w(m)) == "W" and _w(m) <= isa.MAX_WIDTH
 
     def _lower_one(self, n: Node):
         if n.id in self.memo:
@@ -310,6 +316,8 @@ class _Lowerer:
         if op in ("select", "store", "apply", "const_array"):
             raise Unsupported(f"{op} (Ackermannisation pending)")
 
+        if self._lazy_concat(n):
+            return self._concat_lazy(n)
         args = [self.lower(a) for a in n.args]
         # ---------------- Bool connectives (width-1 N values)
         if n.width == BOOL:
@@ -468,6 +476,32 @@ class _Lowerer:
             return self.emit("N_EQ", aw, [self.as_cls(a, aw, "W"), self.as_cls(b, aw, "W")])
         return self.emit("N_EQN", aw, [a, b])
 
+    def _concat_lazy(self, n: Node):
+        """A wide concat built part by part from the least significant end, each
+        part lowered right before it is inserted: an ABI word of 32 guarded
+        calldata bytes keeps one byte live instead of 32, and every byte is the
+        adjacent ``N_SLT, LEAF_N, N_ITE, W_INSN`` run that _fuse_checks turns
+        into one W_CDINS."""
+        w = _w(n)
+        acc = None
+        off = 0
+        for part in reversed(n.args):
+            pw = _w(part)
+            v = self.lower(part)
+            if acc is None:
+                acc = Const(v.value, "W") if isinstance(v, Const) else (v if v.cls == "W" else
+                                                                       self.emit("W_ZEXTN", w, [v]))
+            elif isinstance(v, Const):
+                if v.value:
+                    acc = self.emit("W_OR", w, [self.as_cls(acc, w, "W"), Const(v.value << off, "W")])
+            elif v.cls == "N":
+                acc = self.emit("W_INSN", w, [self.as_cls(acc, w, "W"), v], imm=off)
+            else:
+                sh = self.emit("W_SHLI", w, [v], imm=off)
+                acc = self.emit("W_OR", w, [self.as_cls(acc, w, "W"), sh])
+            off += pw
+        return acc
+
     def _concat(self, widths: List[int], vals: List[object], w: int):
         # first argument is most significant; build from the least significant part up
         parts = list(zip(widths, vals))[::-1]
@@ -523,27 +557,73 @@ def _flatten(conjuncts: Iterable[Node]) -> List[Node]:
 HOIST_CAP = 16
 
 
-def _fuse_checks(insns: List[MInsn]) -> List[MInsn]:
-    """Interpreter bytecode only (``Program.ssa`` keeps the unfused list for
-    jit.py): ``t = a <=u b`` (a Bool implication, see ``=>`` in _lower)
-    immediately followed by ``CHECK t``, with t used nowhere else, becomes one
-    ``CHECK_IMP a, b``.  The interpreter is dispatch-bound, and C3's 2 176
-    congruence conjuncts are exactly this pair."""
+def _uses(insns: List[MInsn]) -> Dict[int, int]:
     uses: Dict[int, int] = {}
     for ins in insns:
         for s in ins.srcs:
             if isinstance(s, VReg):
                 uses[s.id] = uses.get(s.id, 0) + 1
+    return uses
+
+
+def _is(v, ins: MInsn) -> bool:
+    return isinstance(v, VReg) and ins.dst is not None and v.id == ins.dst.id
+
+
+def _fuse_checks(insns: List[MInsn]) -> List[MInsn]:
+    """Interpreter superinstructions (bytecode only: ``Program.ssa`` keeps the
+    unfused list for jit.py).  The interpreter is dispatch-bound,
+    so the frequent Mythril shapes run as one dispatch each:
+
+    * ``t = a <=u b; CHECK t`` (a Bool implication, ``=>`` in _lower) ->
+      ``CHECK_IMP a, b``;
+    * ``t = (x = y); CHECK_IMP p, t`` -> ``CHECK_IMPEQ p, x, y`` (narrow) or
+      ``CHECK_IMPEQW`` (wide): C3's 2 176 congruence conjuncts
+      ``(i_t = i_u) => (v_t = v_u)`` (lower.py);
+    * ``c = K <s size; l = LEAF_N; b = ite(c, l, 0); acc' = acc | b << off``
+      -> ``W_CDINS``: one guarded calldata byte of an ABI word
+      (``If(i <s size, calldata[i], 0)``, state/calldata.py:218-231), the
+      bulk of C2's program.
+    Temporaries must have no other use."""
+    uses = _uses(insns)
     out: List[MInsn] = []
     i = 0
     while i < len(insns):
         ins = insns[i]
         nxt = insns[i + 1] if i + 1 < len(insns) else None
         if (ins.op == "N_ULEN" and ins.width == 1 and ins.dst is not None and nxt is not None
-                and nxt.op == "CHECK" and len(nxt.srcs) == 1 and isinstance(nxt.srcs[0], VReg)
-                and nxt.srcs[0].id == ins.dst.id and uses.get(ins.dst.id, 0) == 1):
+                and nxt.op == "CHECK" and len(nxt.srcs) == 1 and _is(nxt.srcs[0], ins)
+                and uses.get(ins.dst.id, 0) == 1):
             out.append(MInsn("CHECK_IMP", 1, None, list(ins.srcs)))
             i += 2
+            continue
+        out.append(ins)
+        i += 1
+    insns, out, i = out, [], 0
+    uses = _uses(insns)
+    while i < len(insns):
+        ins = insns[i]
+        nxt = insns[i + 1] if i + 1 < len(insns) else None
+        if (ins.op in ("N_EQN", "N_EQ") and ins.dst is not None and nxt is not None and nxt.op == "CHECK_IMP"
+                and _is(nxt.srcs[1], ins) and uses.get(ins.dst.id, 0) == 1):
+            op = "CHECK_IMPEQ" if ins.op == "N_EQN" else "CHECK_IMPEQW"
+            out.append(MInsn(op, ins.width, None, [nxt.srcs[0], ins.srcs[0], ins.srcs[1]]))
+            i += 2
+            continue
+        q = insns[i:i + 4]
+        if (len(q) == 4 and q[0].op == "N_SLT" and q[0].width == 256 and isinstance(q[0].srcs[0], Const)
+                and isinstance(q[0].srcs[1], VReg) and q[1].op == "LEAF_N"
+                and q[2].op == "N_ITE" and _is(q[2].srcs[0], q[1]) and isinstance(q[2].srcs[1], Const)
+                and q[2].srcs[1].value == 0 and _is(q[2].srcs[2], q[0])
+                and ((q[3].op == "W_INSN" and _is(q[3].srcs[1], q[2]))
+                     or (q[3].op == "W_ZEXTN" and _is(q[3].srcs[0], q[2])))
+                and all(uses.get(x.dst.id, 0) == 1 for x in q[:3])
+                and q[1].imm < (1 << 16)):
+            acc = q[3].srcs[0] if q[3].op == "W_INSN" else Const(0, "W")
+            off = q[3].imm if q[3].op == "W_INSN" else 0
+            out.append(MInsn("W_CDINS", q[3].width, q[3].dst, [acc, q[0].srcs[1], Const(q[0].srcs[0].value, "W")],
+                             imm=q[1].imm | (off << 16)))
+            i += 4
             continue
         out.append(ins)
         i += 1

@@ -32,8 +32,13 @@ typedef const u32* kptr;
 #endif
 #define MW_KPTR(p) ((kptr)(p))
 
-typedef u32 u32x16 __attribute__((ext_vector_type(16)));
-typedef u32 u32x32 __attribute__((ext_vector_type(32)));
+typedef u32 u32xW __attribute__((ext_vector_type(MW_NW)));   // one limb of every W slot
+typedef u32 u32xN __attribute__((ext_vector_type(32)));      // one half of the N file
+// (the N file is two 32-slot halves: a single 64-element vector indexed at run
+// time is lowered through scratch memory, two halves stay in VGPRs)
+// slot numbers are validated on load (mw_validate.cpp); the clamp keeps an
+// index inside its vector regardless (one scalar min on a uniform value)
+#define MW_WSLOT(o) ((o) < (u32)MW_NW ? (o) : 0u)
 
 #define MW_FETCH_W(opnd, x)                                                   \
   do {                                                                        \
@@ -43,7 +48,7 @@ typedef u32 u32x32 __attribute__((ext_vector_type(32)));
       x[0] = _p[0]; x[1] = _p[1]; x[2] = _p[2]; x[3] = _p[3];                 \
       x[4] = _p[4]; x[5] = _p[5]; x[6] = _p[6]; x[7] = _p[7];                 \
     } else {                                                                  \
-      _o &= (MW_NW - 1);                                                      \
+      _o = MW_WSLOT(_o);                                                      \
       x[0] = F0[_o]; x[1] = F1[_o]; x[2] = F2[_o]; x[3] = F3[_o];             \
       x[4] = F4[_o]; x[5] = F5[_o]; x[6] = F6[_o]; x[7] = F7[_o];             \
     }                                                                         \
@@ -53,25 +58,30 @@ typedef u32 u32x32 __attribute__((ext_vector_type(32)));
   do {                                                                        \
     u32 _o = (opnd);                                                          \
     if (_o & MW_KBIT) v = cpool[_o & 0x7fffu];                                \
-    else v = NF[_o & (MW_NN - 1)];                                            \
+    else if (_o & 32u) v = NH[_o & 31u];                                      \
+    else v = NF[_o & 31u];                                                    \
   } while (0)
 
 #define MW_WRITE_W(d, r)                                                      \
   do {                                                                        \
-    u32 _d = (d) & (MW_NW - 1);                                               \
+    u32 _d = MW_WSLOT((u32)(d));                                              \
     F0[_d] = r[0]; F1[_d] = r[1]; F2[_d] = r[2]; F3[_d] = r[3];               \
     F4[_d] = r[4]; F5[_d] = r[5]; F6[_d] = r[6]; F7[_d] = r[7];               \
   } while (0)
 
-#define MW_WRITE_N(d, v) NF[(d) & (MW_NN - 1)] = (v)
+#define MW_WRITE_N(d, v)                                                      \
+  do {                                                                        \
+    if ((d) & 32u) NH[(d) & 31u] = (v);                                       \
+    else NF[(d) & 31u] = (v);                                                 \
+  } while (0)
 
 template <class Env>
 MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_, Env& env,
                   bool alive, u32 flags) {
   const kptr code = MW_KPTR(code_);
   const kptr cpool = MW_KPTR(cpool_);
-  u32x16 F0 = 0, F1 = 0, F2 = 0, F3 = 0, F4 = 0, F5 = 0, F6 = 0, F7 = 0;
-  u32x32 NF = 0;
+  u32xW F0 = 0, F1 = 0, F2 = 0, F3 = 0, F4 = 0, F5 = 0, F6 = 0, F7 = 0;
+  u32xN NF = 0, NH = 0;   // N slots 0..31, 32..63
   // Instruction fetch is software-pipelined: the next instruction's s_load is in
   // flight while the current one executes (the words after END are always
   // readable: the constant pool follows the code in the program buffer).
@@ -108,6 +118,42 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         MW_FETCH_N(ob, q);
         alive = alive && (p == 0u || q != 0u);
         if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
+        break;
+      }
+      case MW_CHECK_IMPEQ: {  // a => (b = c): a congruence conjunct over narrow cells
+        u32 p, b, c;
+        MW_FETCH_N(oa, p);
+        MW_FETCH_N(ob, b);
+        MW_FETCH_N(oc, c);
+        alive = alive && (p == 0u || b == c);
+        if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
+        break;
+      }
+      case MW_CHECK_IMPEQW: {
+        u32 p;
+        MW_FETCH_N(oa, p);
+        MW_FETCH_W(ob, x);
+        MW_FETCH_W(oc, y);
+        alive = alive && (p == 0u || eq8(x, y));
+        if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
+        break;
+      }
+      case MW_W_CDINS: {  // acc | (ite(K[c] <s size, leaf, 0) << off)
+        MW_FETCH_W(oa, x);
+        MW_FETCH_W(ob, y);   // size
+        u32 k[8];
+        MW_FETCH_W(oc, k);   // the constant index
+        k[7] ^= 0x80000000u;
+        y[7] ^= 0x80000000u;
+        const bool in_range = ult8(k, y);   // signed 256-bit k < size
+        env.leaf(imm & 0xffffu, r);
+        u32 t[8];
+        zero8(t);
+        t[0] = in_range ? r[0] : 0u;
+        shl8(t, imm >> 16, r);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) r[q] |= x[q];
+        wk = 1;
         break;
       }
       case MW_LEAF_W:

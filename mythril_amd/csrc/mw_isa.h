@@ -6,6 +6,8 @@
 // assignment per lane.  Values live in two per-lane register files:
 //   W file: MW_NW slots x 8 u32 limbs (widths 33..256, limb 0 least significant)
 //   N file: MW_NN slots x 1 u32       (widths 1..32; Bool = width 1, 0/1)
+// (8 + 64: Mythril's queries are mostly narrow values - calldata bytes, Bools -
+// and the two files together must leave the interpreter within 256 VGPRs)
 // Every value is canonical: bits at and above its width are zero.
 //
 // Instruction = 4 u32 words:
@@ -19,8 +21,8 @@
 #pragma once
 #include <stdint.h>
 
-#define MW_NW 16
-#define MW_NN 32
+#define MW_NW 8
+#define MW_NN 64
 #define MW_KBIT 0x8000u
 #define MW_LEAF_WORDS 8
 #define MW_POOL_ENTRY_WORDS 9
@@ -52,6 +54,8 @@ enum mw_opcode {
   MW_SPILL_N = 10,
   MW_FILL_N = 11,
   MW_CHECK_IMP = 12,  // alive &= (N[a] == 0) | (N[b] != 0): a congruence conjunct a => b in one dispatch
+  MW_CHECK_IMPEQ = 13,   // alive &= (N[a] == 0) | (N/K[b] == N/K[c])   (a => (b = c), narrow)
+  MW_CHECK_IMPEQW = 14,  // alive &= (N[a] == 0) | (W/K[b] == W/K[c])   (a => (b = c), wide)
 
   // wide: W[dst] = f(W/K a, W/K b) at `width`
   MW_W_ADD = 16, MW_W_SUB = 17, MW_W_MUL = 18, MW_W_AND = 19, MW_W_OR = 20,
@@ -65,6 +69,9 @@ enum mw_opcode {
   MW_W_SEXT = 35,  // W[dst] = sign-extend(a from imm bits) to width
   MW_W_SEXTN = 36, // W[dst] = sign-extend(N/K a from imm bits) to width
   MW_W_INSN = 37,  // W[dst] = a | (N/K b << imm)   (concat builder)
+  MW_W_CDINS = 38, // W[dst] = W/K a | ((K[c] <s W[b] (256-bit) ? leaf(imm & 0xffff) : 0) << (imm >> 16)):
+                   // one guarded calldata byte ite(i <s size, cd[i], 0) inserted into a word
+                   // (state/calldata.py:218-231), four dispatches in one
 
   // wide -> narrow
   MW_N_EXTRACTW = 48, // N[dst] = (a >> imm) masked to width (<= 32)

@@ -35,6 +35,9 @@ bool op_shape(u32 op, OpShape& s) {
     case MW_END: return true;
     case MW_CHECK: s.a = 2; return true;
     case MW_CHECK_IMP: s.a = 2; s.b = 2; return true;
+    case MW_CHECK_IMPEQ: s.a = 2; s.b = 2; s.c = 2; return true;
+    case MW_CHECK_IMPEQW: s.a = 2; s.b = 1; s.c = 1; return true;
+    case MW_W_CDINS: s.dst = 3; s.a = 1; s.b = 1; s.c = 1; s.wide = true; return true;
     case MW_LEAF_W: s.dst = 3; return true;
     case MW_LEAF_N: s.dst = 4; return true;
     case MW_STORE_W: s.a = 1; return true;
@@ -111,7 +114,8 @@ int mg_validate_desc(const mg_prog_desc* d) {
       return fail(MG_E_PROG, "operand out of range at instruction " + std::to_string(i));
     if (s.dst == 3 || s.dst == 4 || s.a || s.b) {
       const u32 maxw = (s.wide || s.dst == 3) ? 256u : 32u;
-      if (op != MW_CHECK && op != MW_CHECK_IMP && op != MW_STORE_W && op != MW_STORE_N && op != MW_SPILL_W &&
+      if (op != MW_CHECK && op != MW_CHECK_IMP && op != MW_CHECK_IMPEQ && op != MW_CHECK_IMPEQW &&
+          op != MW_STORE_W && op != MW_STORE_N && op != MW_SPILL_W &&
           op != MW_SPILL_N && op != MW_FILL_W && op != MW_FILL_N && op != MW_MOV_W && op != MW_MOV_N &&
           op != MW_LEAF_W && op != MW_LEAF_N && (w < 1 || w > maxw))
         return fail(MG_E_PROG, "bad width " + std::to_string(w) + " at instruction " + std::to_string(i));
@@ -131,6 +135,11 @@ int mg_validate_desc(const mg_prog_desc* d) {
         break;
       case MW_W_SHLI: case MW_W_LSHRI: case MW_N_EXTRACTW: case MW_W_INSN:
         if (I[3] >= 256) return fail(MG_E_PROG, "immediate shift out of range");
+        break;
+      case MW_W_CDINS:   // leaf index | insert offset << 16; c must be a constant (the byte index)
+        if ((I[3] & 0xffffu) >= d->nleaves) return fail(MG_E_PROG, "leaf index out of range");
+        if ((I[3] >> 16) >= 256) return fail(MG_E_PROG, "immediate shift out of range");
+        if (!(c & MW_KBIT)) return fail(MG_E_PROG, "W_CDINS index must be a constant");
         break;
       case MW_W_SEXT: case MW_W_SEXTN: case MW_N_SEXT:
         if (I[3] < 1 || I[3] > w) return fail(MG_E_PROG, "bad sign-extension source width");

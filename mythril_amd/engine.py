@@ -72,7 +72,7 @@ def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True,
     import time
     t0 = time.perf_counter()
     conj = list(conjuncts)
-    low = lower_constraints(conj, ctx) if needs_lowering(conj) else Lowered(conj)
+    low = lower_constraints(conj, ctx)
     t1 = time.perf_counter()
     leaves = []
     seen = set()

@@ -1,8 +1,8 @@
 """Python mirror of ``csrc/mw_isa.h`` (kept in sync by tests/test_isa_sync.py)."""
 from __future__ import annotations
 
-NW = 16          # W file slots (8 x u32 limbs each)
-NN = 32          # N file slots (1 x u32 each)
+NW = 8           # W file slots (8 x u32 limbs each)
+NN = 64          # N file slots (1 x u32 each)
 KBIT = 0x8000
 LEAF_WORDS = 8
 POOL_ENTRY_WORDS = 9
@@ -14,11 +14,12 @@ LEAF_WIDTH, LEAF_KIND, LEAF_ID, LEAF_SHIFT, LEAF_BITS, LEAF_POOL, LEAF_INROW = r
 OPCODES = {
     "END": 0, "CHECK": 1, "LEAF_W": 2, "LEAF_N": 3, "STORE_W": 4, "STORE_N": 5,
     "SPILL_W": 6, "FILL_W": 7, "MOV_W": 8, "MOV_N": 9, "SPILL_N": 10, "FILL_N": 11, "CHECK_IMP": 12,
+    "CHECK_IMPEQ": 13, "CHECK_IMPEQW": 14,
     "W_ADD": 16, "W_SUB": 17, "W_MUL": 18, "W_AND": 19, "W_OR": 20, "W_XOR": 21, "W_NOT": 22,
     "W_SHL": 23, "W_LSHR": 24, "W_ASHR": 25,
     "W_UDIV": 26, "W_UREM": 27, "W_SDIV": 28, "W_SREM": 29, "W_SMOD": 30,
     "W_ITE": 31, "W_SHLI": 32, "W_LSHRI": 33, "W_ZEXTN": 34, "W_SEXT": 35, "W_SEXTN": 36,
-    "W_INSN": 37,
+    "W_INSN": 37, "W_CDINS": 38,
     "N_EXTRACTW": 48, "N_ULT": 49, "N_ULE": 50, "N_SLT": 51, "N_SLE": 52, "N_EQ": 53,
     "N_UMULNO": 54, "N_ADDC": 55,
     "N_ADD": 64, "N_SUB": 65, "N_MUL": 66, "N_AND": 67, "N_OR": 68, "N_XOR": 69, "N_NOT": 70,
@@ -33,6 +34,8 @@ OPCODES = {
 # (dst class, [src classes for a, b, c])
 SHAPES = {
     "END": (None, []), "CHECK": (None, ["N"]), "CHECK_IMP": (None, ["N", "N"]),
+    "CHECK_IMPEQ": (None, ["N", "N", "N"]), "CHECK_IMPEQW": (None, ["N", "W", "W"]),
+    "W_CDINS": ("W", ["W", "W", "W"]),
     "LEAF_W": ("W", []), "LEAF_N": ("N", []),
     "STORE_W": (None, ["W"]), "STORE_N": (None, ["N"]),
     "SPILL_W": (None, ["W"]), "FILL_W": ("W", []), "SPILL_N": (None, ["N"]), "FILL_N": ("N", []),

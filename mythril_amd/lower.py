@@ -389,6 +389,10 @@ class _Rewriter:
             r = self._pow2(op, args, n.width)
             if r is not None:
                 return r
+        if op in ("=", "not") and n.width == BOOL:
+            r = self._bool_bv(op, args)
+            if r is not None:
+                return r
         if op == "apply":
             # Mythril's keccak inverse (keccak_function_manager.py:80-81): inv(keccak256_N(x)) is
             # *defined* as x.  Sound: every inverse application sits on a keccak application
@@ -472,6 +476,37 @@ class _Rewriter:
         if j == 0:
             return x
         return c.const(0, w) if j >= w else c.app("concat", self.extract(x, w - 1 - j, 0), c.const(0, j))
+
+    def _bool_bv(self, op: str, args: List[Node]) -> Optional[Node]:
+        """z3 ``simplify``'s folding of EVM's Bool-as-word round trips
+        (``util.pop_bitvec``'s ``If(b, 1, 0)``, ISZERO, JUMPI's ``cond != 0``):
+        ``If(c, K1, K2) = K`` -> ``c`` / ``not c`` / a constant, ``not not c`` -> ``c``.
+        The comparison inside then reaches the candidate pools' domains
+        (e.g. ``call_value = 0`` from a non-payable check)."""
+        c = self.ctx
+        if op == "not":
+            x = args[0]
+            if x.op == "not":
+                return x.args[0]
+            if x.op == "const":
+                return c.const(0 if x.val else 1, BOOL)
+            return None
+        if len(args) != 2:
+            return None
+        a, b = args
+        if a.op == "const" and b.op != "const":
+            a, b = b, a
+        if b.op != "const" or a.op != "ite" or a.width == BOOL:
+            return None
+        cond, k1, k2 = a.args
+        if k1.op != "const" or k2.op != "const":
+            return None
+        t1, t2 = k1.val == b.val, k2.val == b.val
+        if t1 and t2:
+            return c.true()
+        if not t1 and not t2:
+            return c.false()
+        return cond if t1 else (cond.args[0] if cond.op == "not" else c.app("not", cond))
 
     def congruence(self) -> List[Node]:
         c = self.ctx

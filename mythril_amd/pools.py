@@ -218,16 +218,37 @@ def domains(conjuncts: List[Node]):
         if n.op in _UPPER:
             _bound(n.op, *n.args)
 
+    def _shifted(t: Node):
+        """(leaf, d) when t is leaf + d (bvadd/bvsub with a constant), else None."""
+        if t.op == "var":
+            return t, 0
+        if t.op in ("bvadd", "bvsub") and len(t.args) == 2:
+            x, k = t.args
+            if x.op == "var" and k.op == "const":
+                return x, (k.val if t.op == "bvadd" else -k.val)
+            if t.op == "bvadd" and k.op == "var" and x.op == "const":
+                return k, x.val
+        return None
+
     def _bound(op, a, b):
-        # op(a, b) holds; normalise to x <= K or K <= x
+        # op(a, b) holds; normalise to x (+ d) <= K or K <= x (+ d).  Offsets move
+        # the bound without modelling wrap-around: the interval only steers the
+        # pools (every candidate is still checked exactly)
         upper, strict = _UPPER[op]   # bvult/bvule: a is below b
         lo_t, hi_t = (b, a) if upper else (a, b)
-        if lo_t.op == "var" and hi_t.op == "const":       # x <(=) K
-            iv = interval.setdefault(lo_t.name, [0, (1 << lo_t.width) - 1])
-            iv[1] = min(iv[1], hi_t.val + strict)
-        elif hi_t.op == "var" and lo_t.op == "const":     # K <(=) x
-            iv = interval.setdefault(hi_t.name, [0, (1 << hi_t.width) - 1])
-            iv[0] = max(iv[0], lo_t.val - strict)
+        sl, sh = _shifted(lo_t), _shifted(hi_t)
+        if sl is not None and hi_t.op == "const":       # x + d <(=) K
+            x, d = sl
+            top = hi_t.val + strict - d
+            if 0 <= top < (1 << x.width):
+                iv = interval.setdefault(x.name, [0, (1 << x.width) - 1])
+                iv[1] = min(iv[1], top)
+        elif sh is not None and lo_t.op == "const":     # K <(=) x + d
+            x, d = sh
+            bot = lo_t.val - strict - d
+            if 0 <= bot < (1 << x.width):
+                iv = interval.setdefault(x.name, [0, (1 << x.width) - 1])
+                iv[0] = max(iv[0], bot)
 
     for c in conjuncts:
         facts(c)

@@ -121,8 +121,11 @@ def test_congruence_conjuncts_fuse_to_one_check():
                                 "c3_bec_batchtransfer_overflow.smt2"))
     q = prepare(s.asserts, s.ctx)
     ops = [int(w) & 0xFF for w in q.program.code.reshape(-1, 4)[:, 0]]
-    assert ops.count(isa.OPCODES["CHECK_IMP"]) >= 2000
-    assert all(i.op != "CHECK_IMP" for i in q.program.ssa)
+    fused = ops.count(isa.OPCODES["CHECK_IMP"]) + ops.count(isa.OPCODES["CHECK_IMPEQ"]) + \
+        ops.count(isa.OPCODES["CHECK_IMPEQW"])
+    assert fused >= 2000
+    assert ops.count(isa.OPCODES["CHECK_IMPEQ"]) >= 2000   # (i = j) => (v = w): one dispatch
+    assert all(not i.op.startswith("CHECK_IMP") for i in q.program.ssa)
 
 
 def test_check_imp_verdicts_all_input_combinations():
@@ -150,10 +153,10 @@ def test_check_imp_verdicts_all_input_combinations():
     models = [{"a": p, "b": q, "u": p, "v": q, "x": 7 if q else 3} for p in (0, 1) for q in (0, 1)]
     for conj in shapes:
         prog = compile_program(conj)
-        ops = [int(w) & 0xFF for w in prog.code.reshape(-1, 4)[:, 0]]
+        ops = {int(w) & 0xFF for w in prog.code.reshape(-1, 4)[:, 0]}
         want = [int(all(eval_nodes(conj, m)[k.id] for k in conj)) for m in models]
         got, _ = emu_eval(prog, pack_inputs(prog, models), len(models))
         assert list(map(int, got)) == want, conj
         if not any(k.args[0].op == "const" or k.args[1].op == "const" for k in conj):
-            assert isa.OPCODES["CHECK_IMP"] in ops, conj
+            assert ops & {isa.OPCODES["CHECK_IMP"], isa.OPCODES["CHECK_IMPEQ"], isa.OPCODES["CHECK_IMPEQW"]}, conj
     assert [int(all(eval_nodes(shapes[0], m)[k.id] for k in shapes[0])) for m in models] == [1, 1, 0, 1]
