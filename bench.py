@@ -51,6 +51,9 @@ def parse():
                     help="waves per SIMD the specialised kernel is built for")
     ap.add_argument("--jit-split", type=int, default=int(BENCH_SPLIT), choices=[0, 1],
                     help="1: split the program into part kernels at conjunct boundaries")
+    ap.add_argument("--devices", type=int, default=1,
+                    help="single-process multi-GPU (mythril_amd/multidev.py): this process drives N devices, "
+                         "each searching its slice of every step (the torchrun path is the default)")
     ap.add_argument("--jit-interleave", type=int, default=BENCH_INTERLEAVE,
                     help="conjuncts interleaved per instruction stream in the specialised kernel")
     ap.add_argument("--jit-lds-leaves", type=int, default=None,
@@ -75,6 +78,10 @@ def main():
     from mythril_amd.synth import build_c5
 
     dev = Device(local)
+    multi = None
+    if args.devices > 1:
+        from mythril_amd.multidev import MultiDevice
+        multi = MultiDevice([dev] + [Device(i) for i in range(1, args.devices)])
 
     def gpu_eval(terms, index, seed):
         p = compile_program([], trace=list(terms))
@@ -86,6 +93,7 @@ def main():
     syn = build_c5(gpu_eval, n_nodes=args.nodes)
     prog = compile_program(syn.conjuncts)
     dp = dev.load(prog)
+    mdp = multi.load(prog) if multi is not None else None
     jit_s = None
     if args.engine == "jit":
         # one-time program preparation, like the upload: outside the timed region
@@ -102,9 +110,19 @@ def main():
         args.jit_split = int(split)
         jit_s = jit.attach(dev, [dp], variants=BENCH_VARIANTS, waves=args.jit_waves, lds_leaves=args.jit_lds_leaves,
                            split=split, interleave=args.jit_interleave)
+        if multi is not None:
+            for d, part in zip(multi.devs[1:], mdp.parts[1:]):
+                jit.attach(d, [part], variants=BENCH_VARIANTS, waves=args.jit_waves,
+                           lds_leaves=args.jit_lds_leaves, split=split, interleave=args.jit_interleave)
+            mdp.parts[0].free()
+            mdp.parts[0] = dp   # device 0's copy is the program the kernel was attached to above
     batch = 1 << args.batch_log2
 
     def step(k):
+        if multi is not None:   # one process: every device searches its slice of the step
+            begin = (k * args.devices * batch) % (1 << 62)
+            (found,), st = multi.search([mdp], syn.seed, begin, batch * args.devices, 0)
+            return found, st
         begin = ((k * world + rank) * batch) % (1 << 62)
         (found,), st = dev.search([dp], syn.seed, begin, batch, 0)
         return found, st
@@ -140,12 +158,12 @@ def main():
         from mythril_amd.distributed import allreduce_min
         (found_any,) = allreduce_min([found_any], device=f"cuda:{local}")  # RCCL MIN of the witness index
 
-    total_evals = world * args.steps * batch
+    total_evals = world * args.steps * batch * max(1, args.devices)
     value = total_evals / elapsed
     avg_kernel_s = sum(kms) / len(kms) / 1e3
     # executed algorithmic work per launch: the wide divisions' digit steps are
     # priced by the steps the kernel ran (zero digits are skipped per wave)
-    ops_launch = prog.executed_ops(batch, sum(dsteps) / len(dsteps))
+    ops_launch = prog.executed_ops(batch, sum(dsteps) / len(dsteps) / max(1, args.devices))
     achieved = ops_launch / avg_kernel_s
     measured_peak = load_measured_peak()
 
@@ -164,7 +182,7 @@ def main():
         "metric": "candidate-assignment evals/sec",
         "value": value,
         "unit": "evals/s",
-        "n_gpus": world,
+        "n_gpus": world * max(1, args.devices),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -188,7 +206,8 @@ def main():
                                      if dp.kernel else ""),
             "jit_compile_s": jit_s,
             "jit_split": bool(args.jit_split) if args.engine == "jit" else None,
-            "parallelism": f"candidate-shard x{world}",
+            "parallelism": f"candidate-shard x{world}" + (f" (one process, {args.devices} devices)"
+                                                          if args.devices > 1 else ""),
             "witness_found_in_timed_range": found_any,
             "time_to_first_witness": ttfw,
         },

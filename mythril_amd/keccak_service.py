@@ -21,6 +21,11 @@ and answers them from a digest memo that batched launches of the Keccak kernel
   because one launch costs tens of microseconds and one pysha3 call about one.
 * ``sha3`` / ``find_concrete_keccak`` / ``get_code_hash``: memo first, else
   the reference function.  The results are unchanged either way.
+* ``prefetch_storage_slots``: at each LaserEVM transaction boundary the
+  plugin hashes the likely concrete preimages of the next transaction's SHA3
+  instructions (mapping entries and array bases of the actors and the
+  contract, low slots) in ONE launch, so LASER's one-at-a-time hashing then
+  hits the memo.
 * ``replace_with_actual_sha``: a restatement of ``solver.py:128-164``.  It first
   collects the preimage of every window of the unmodified inputs and hashes
   them all in one launch, then runs the reference's loop.  A window that only
@@ -117,6 +122,20 @@ class KeccakService:
         self.hash_many(msgs)
         return len(msgs)
 
+    def prefetch_storage_slots(self, keys: Iterable[int], slots: Iterable[int]) -> int:
+        """Speculative batch at a LaserEVM transaction boundary: the preimages
+        Solidity's storage layout hashes with concrete data — mapping entries
+        ``keccak(pad32(key) ++ pad32(slot))`` (``instructions.py:1004-1042``
+        reaching ``find_concrete_keccak``) and dynamic-array bases
+        ``keccak(pad32(slot))`` — for the keys LASER's transactions use
+        (the actor addresses, ``transaction/symbolic.py:29-40``, and the
+        contract's address) and the low slots.  One launch fills the memo; the
+        SHA3 instructions that follow are memo hits, the results unchanged."""
+        keys = list(dict.fromkeys(int(k) for k in keys))
+        slots = list(dict.fromkeys(int(sl) for sl in slots))
+        pre = [(512, (k << 256) | sl) for k in keys for sl in slots] + [(256, sl) for sl in slots]
+        return self.prefetch_values(pre)
+
 
 def replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], preimage: Callable[[int], Optional[tuple]],
                             service: KeccakService, code_bytecode: Optional[str] = None) -> None:
@@ -202,6 +221,16 @@ def install(device=None) -> bool:
 
     kfm_mod.KeccakFunctionManager.find_concrete_keccak = staticmethod(find_concrete_keccak)
     kfm_mod.sha3 = svc.sha3
+    # get_code_hash (support_utils.py:31-47) at its import sites: EXTCODEHASH and
+    # CREATE2 (instructions.py:62,1292-1300,1775-1788), EVMContract (evmcontract.py:9)
+    su.get_code_hash = svc.get_code_hash
+    for site in ("mythril.laser.ethereum.instructions", "mythril.ethereum.evmcontract"):
+        try:
+            mod = __import__(site, fromlist=["get_code_hash"])
+            if hasattr(mod, "get_code_hash"):
+                mod.get_code_hash = svc.get_code_hash
+        except ImportError:
+            pass
     manager = kfm_mod.keccak_function_manager
 
     def _replace(concrete_transactions, model, code=None):

@@ -70,7 +70,12 @@ def engine():
                     budget = int(os.environ.get("MYTHRIL_AMD_BUDGET", str(1 << 22)))
                     from .engine import DEFAULT_OP_BUDGET
                     op_budget = int(os.environ.get("MYTHRIL_AMD_OP_BUDGET", str(DEFAULT_OP_BUDGET)))
-                    _engine = WitnessEngine(device=dev, budget=budget, op_budget=op_budget)
+                    ndev = int(os.environ.get("MYTHRIL_AMD_DEVICES", "1"))
+                    multi = None
+                    if ndev > 1:   # one process over several GPUs (multidev.py)
+                        from .multidev import MultiDevice
+                        multi = MultiDevice.open(range(ndev))
+                    _engine = WitnessEngine(device=dev, budget=budget, op_budget=op_budget, dev=multi)
                 except Exception as e:  # EngineUnavailable / EngineError
                     log.warning("MI355X witness engine unavailable (%s); using z3 only", e)
                     _engine_failed = True

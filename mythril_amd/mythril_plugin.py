@@ -12,6 +12,9 @@ registers two batching hooks:
 * ``stop_sym_trans`` (``svm.py:243-245``): right before the next
   transaction's reachability prune over ``open_states`` (``svm.py:216-223``)
   every open state's constraint set is searched in ONE launch;
+  and the likely concrete Keccak preimages of the next transaction (mapping
+  entries and array bases of the actors and accounts, low slots) are hashed
+  in ONE launch of the Keccak kernel;
 * a JUMPI post hook (``svm.py:_execute_post_hook``, run on each successor):
   the successors are queued, and the first per-step ``is_possible``
   (``svm.py:287-292``) searches the pair in one launch.
@@ -37,6 +40,24 @@ except Exception:  # pragma: no cover - exercised only where mythril is installe
     HAVE_MYTHRIL = False
 
 
+SLOTS = 16   # storage slots whose mapping entries / array bases are prefetched
+
+
+def storage_keys(symbolic_vm) -> list:
+    """Concrete keys the next transaction's mapping lookups use: LASER's three
+    actors (transaction/symbolic.py:29-40) and the open states' concrete
+    account addresses."""
+    keys = [0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE, 0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF,
+            0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA]
+    for ws in getattr(symbolic_vm, "open_states", []):
+        for addr in getattr(ws, "accounts", {}) or {}:
+            try:
+                keys.append(int(getattr(addr, "value", addr)))
+            except (TypeError, ValueError):
+                pass
+    return keys
+
+
 class WitnessBatchingLaserPlugin(_LaserPlugin):
     """LASER plugin: rebinding + transaction-boundary batching."""
 
@@ -52,6 +73,12 @@ class WitnessBatchingLaserPlugin(_LaserPlugin):
                          len(symbolic_vm.open_states))
             except Exception as e:  # never disturb the analysis
                 log.warning("witness engine prefetch skipped: %s", e)
+            try:
+                svc = keccak_service.service()
+                if svc is not None:
+                    svc.prefetch_storage_slots(storage_keys(symbolic_vm), range(SLOTS))
+            except Exception as e:  # never disturb the analysis
+                log.debug("keccak prefetch skipped: %s", e)
 
         symbolic_vm.register_laser_hooks("stop_sym_trans", prefetch_open_states)
 

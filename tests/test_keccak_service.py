@@ -222,3 +222,89 @@ def test_install_rebinds_reference_sites(monkeypatch):
     txs = [{"input": "0x" + "a9059cbb" + "%064x" % placeholder + "%064x" % 7}]
     mods["mythril.analysis.solver"]._replace_with_actual_sha(txs, Z3Model())
     assert txs[0]["input"] == "0x" + "a9059cbb" + keccak256(preimage.to_bytes(32, "big")).hex() + "%064x" % 7
+
+
+def test_transaction_boundary_prefetch_then_memo_hits(monkeypatch):
+    """the plugin's stop_sym_trans hook (svm.py:243-245) hashes
+    the next transaction's likely storage preimages in ONE mg_keccak256 launch;
+    LASER's later one-at-a-time find_concrete_keccak calls for mapping entries
+    of the actors are memo hits (no launch, no reference call), with the
+    reference's digests.  get_code_hash is rebound at its import sites."""
+    import sys
+    import types
+
+    from mythril_amd import keccak_service, model, mythril_plugin
+    from mythril_amd.engine import WitnessEngine
+
+    class BitVecVal:
+        def __init__(self, v, size):
+            self.value, self._size = v, size
+
+        def size(self):
+            return self._size
+
+    class KFM:
+        @staticmethod
+        def find_concrete_keccak(data):
+            raise AssertionError("reference path must not run")
+
+    ref, calls = _reference_counter()
+    instr = types.SimpleNamespace(get_code_hash=None)
+    evmc = types.SimpleNamespace(get_code_hash=None)
+    mods = {
+        "mythril": types.ModuleType("mythril"),
+        "mythril.analysis": types.ModuleType("mythril.analysis"),
+        "mythril.analysis.solver": types.SimpleNamespace(_replace_with_actual_sha=None),
+        "mythril.support": types.ModuleType("mythril.support"),
+        "mythril.support.support_utils": types.SimpleNamespace(sha3=ref, get_code_hash=None),
+        "mythril.laser": types.ModuleType("mythril.laser"),
+        "mythril.laser.smt": types.SimpleNamespace(symbol_factory=types.SimpleNamespace(BitVecVal=BitVecVal)),
+        "mythril.laser.ethereum": types.ModuleType("mythril.laser.ethereum"),
+        "mythril.laser.ethereum.instructions": instr,
+        "mythril.ethereum": types.ModuleType("mythril.ethereum"),
+        "mythril.ethereum.evmcontract": evmc,
+        "mythril.laser.ethereum.function_managers": types.ModuleType("mythril.laser.ethereum.function_managers"),
+        "mythril.laser.ethereum.function_managers.keccak_function_manager":
+            types.SimpleNamespace(KeccakFunctionManager=KFM, keccak_function_manager=KFM(), sha3=None),
+    }
+    for k, v in mods.items():
+        monkeypatch.setitem(sys.modules, k, v)
+    dev = FakeDevice()
+    monkeypatch.setattr(keccak_service, "_service", None)
+    monkeypatch.setattr(model, "_engine", WitnessEngine(dev=dev, budget=1 << 10))
+    monkeypatch.setattr(model, "_engine_failed", False)
+    monkeypatch.setattr(model, "install", lambda: True)
+    assert keccak_service.install()
+    assert instr.get_code_hash("0x6001") == "0x" + keccak256(bytes.fromhex("6001")).hex()
+    assert evmc.get_code_hash == instr.get_code_hash
+
+    class VM:
+        def __init__(self):
+            self.laser, self.post, self.open_states = {}, {}, []
+
+        def register_laser_hooks(self, kind, hook):
+            self.laser.setdefault(kind, []).append(hook)
+
+        def register_hooks(self, kind, hooks):
+            pass
+
+    vm = VM()
+    mythril_plugin.WitnessBatchingLaserPlugin().initialize(vm)
+    n_before = getattr(dev, "keccak_launches", 0)
+    ref_before = calls["n"]
+    vm.laser["stop_sym_trans"][0]()        # transaction boundary
+    assert dev.keccak_launches == n_before + 1
+    svc = keccak_service.service()
+    hashed = svc.stats["gpu_hashes"]
+    assert hashed >= 3 * mythril_plugin.SLOTS
+    # LASER's SHA3 on balances[msg.sender] (slot 0) and allowance-style slot 3
+    for actor in (0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF, 0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE):
+        for slot in (0, 3):
+            v = (actor << 256) | slot
+            h = KFM.find_concrete_keccak(BitVecVal(v, 512))
+            assert h.value == int.from_bytes(keccak256(v.to_bytes(64, "big")), "big")
+    assert dev.keccak_launches == n_before + 1 and calls["n"] == ref_before
+    assert svc.stats["memo_hits"] >= 4
+    # a second boundary re-requests the same preimages: all memo hits, no launch
+    vm.laser["stop_sym_trans"][0]()
+    assert dev.keccak_launches == n_before + 1
