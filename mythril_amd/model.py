@@ -46,6 +46,15 @@ _memo: Dict[tuple, tuple] = {}          # z3 AST-id key -> (raws, witness, scrip
 MEMO_MAX = 1 << 16
 _pending: list = []                     # successor constraint sets deferred by the JUMPI hook
 PENDING_MAX = 64
+# Misses: get_model never caches UNSAT (the reference raises UnsatError, which
+# lru_cache does not keep), so LASER asks the same infeasible set again and
+# again.  A set the device already searched without a witness skips the device
+# the next time (z3 answers, as it would anyway), and so does any extension of
+# such a set by one conjunct (a JUMPI successor of an infeasible-looking state):
+# adding a constraint never creates a witness in the candidate space.
+_misses: Dict[tuple, list] = {}          # z3 AST-id key -> raws (kept alive, eq-confirmed)
+MISS_MAX = 1 << 14
+SKIP_EXTENSIONS_OF_MISSES = os.environ.get("MYTHRIL_AMD_SKIP_MISS_PREFIX", "1") != "0"
 
 
 def _env():
@@ -84,6 +93,22 @@ def engine():
 
 def memo_key(raws) -> tuple:
     return tuple(r.get_id() for r in raws)
+
+
+def _known_miss(raws, key) -> bool:
+    for k, rs in ((key, raws), (key[:-1], raws[:-1]) if SKIP_EXTENSIONS_OF_MISSES and len(raws) > 1 else (None, None)):
+        if k is None:
+            continue
+        kept = _misses.get(k)
+        if kept is not None and len(kept) == len(rs) and all(a is b or a.eq(b) for a, b in zip(kept, rs)):
+            return True
+    return False
+
+
+def _record_miss(raws, key) -> None:
+    if len(_misses) >= MISS_MAX:
+        _misses.clear()
+    _misses[key] = list(raws)
 
 
 def _memo_get(raws, key):
@@ -139,6 +164,9 @@ def _gpu_model(constraints, timeout):
         eng = engine()
         if eng is None:
             return None
+        if _known_miss(raws, key):
+            STATS["miss_skips"] = STATS.get("miss_skips", 0) + 1
+            return None
         try:
             script = z3bridge.to_ir(raws)
             from .engine import prepare
@@ -156,6 +184,8 @@ def _gpu_model(constraints, timeout):
             STATS["device_errors"] = STATS.get("device_errors", 0) + 1
             log.warning("witness engine: device error (%s); z3 answers", e)
             return None
+        if witness is None:
+            _record_miss(raws, key)
     if witness is None:
         return None
     STATS["gpu_witnesses"] += 1

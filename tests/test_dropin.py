@@ -306,3 +306,24 @@ def test_stale_memo_entry_is_not_used(mythril):
     assert dropin.memo_key(raws_other) not in dropin._memo
     res = dropin.get_model(other)
     assert res.raw[0][1]["x"] == 9
+
+
+def test_repeated_miss_skips_the_device(mythril):
+    """UNSAT is never cached by get_model (reference behaviour), so LASER asks an
+    infeasible set again: the second time, and for a one-conjunct extension of
+    it, the device is skipped and z3 answers directly (same results)."""
+    dropin._misses.clear()
+    s0 = dropin._engine.stats["searches"]
+    with pytest.raises(UnsatError):
+        dropin.get_model(UNSAT)
+    assert dropin._engine.stats["searches"] == s0 + 1
+    with pytest.raises(UnsatError):
+        dropin.get_model(UNSAT)
+    ext = UNSAT + (fb(CTX.app("bvugt", X, CTX.const(3, 8))),)
+    with pytest.raises(UnsatError):
+        dropin.get_model(ext)
+    assert dropin._engine.stats["searches"] == s0 + 1
+    assert dropin.STATS["miss_skips"] >= 2
+    assert mythril.calls["reference"] == 3
+    # a satisfiable set is still searched
+    assert dropin.get_model(SAT).raw[0][0] == "z3"
