@@ -175,6 +175,10 @@ def _gpu_model(constraints, timeout):
             STATS["unsupported"] += 1
             log.debug("witness engine: unsupported formula (%s)", e)
             return None
+        except Exception as e:   # z3 printing/parsing trouble: fail closed to the reference
+            STATS["unsupported"] += 1
+            log.warning("witness engine: could not translate the query (%s)", e)
+            return None
         STATS["gpu_attempts"] += 1
         try:
             witness = eng.search([q])[0]
@@ -189,12 +193,67 @@ def _gpu_model(constraints, timeout):
     if witness is None:
         return None
     STATS["gpu_witnesses"] += 1
-    zm = z3bridge.model_from_witness(raws, script, witness, timeout)
+    try:
+        zm = z3bridge.model_from_witness(raws, script, witness, timeout)
+    except Exception as e:   # fail closed: the reference answers
+        STATS["recheck_errors"] = STATS.get("recheck_errors", 0) + 1
+        log.warning("witness engine: z3 re-check failed (%s); z3 answers", e)
+        return None
     if zm is None:
         return None
     STATS["z3_confirmed"] += 1
     from mythril.laser.smt.model import Model
     return Model([zm])
+
+
+MINIMIZE_HINTS = os.environ.get("MYTHRIL_AMD_MINIMIZE_HINTS", "0") == "1"
+
+
+def _minimize_hint(constraints, minimize, timeout):
+    """Minimize assistance (``analysis/solver.py:216-256``),
+    OFF by default (``MYTHRIL_AMD_MINIMIZE_HINTS=1``).
+
+    ``get_transaction_sequence`` asks z3's Optimize for lexicographically
+    minimal ``calldatasize``/``call_value`` per transaction.  A device witness
+    of the same constraints bounds the FIRST objective from above: adding
+    ``obj_0 <= witness(obj_0)`` cannot change the optimum (the optimal model
+    satisfies it), only prune z3's search.  Later objectives get no bound (the
+    witness need not be optimal in obj_0, so its later values bound nothing in
+    the lexicographic order).  The optimum is preserved, but z3 may return a
+    different model with the same objective values, i.e. different transaction
+    data in the issue report: hence opt-in.  Returns the extended constraint
+    collection, or None (no witness, objective not a plain variable, engine
+    unavailable)."""
+    if not minimize:
+        return None
+    cl = constraints if type(constraints) == tuple else constraints.get_all_constraints()
+    cl = [c for c in cl if type(c) != bool]
+    raws = [c.raw for c in cl]
+    eng = engine()
+    if eng is None:
+        return None
+    from . import z3bridge
+    from .runtime import EngineError
+    try:
+        script = z3bridge.to_ir(raws)
+        from .engine import prepare
+        q = prepare(script.asserts, script.ctx)
+        w = eng.search([q])[0]
+    except (Unsupported, RecursionError, ValueError, KeyError, EngineError):
+        return None
+    obj = minimize[0]
+    name = z3bridge.var_name(obj.raw)
+    if w is None or name is None or name not in w.values:
+        return None
+    from mythril.laser.smt import UGE, symbol_factory
+    bound = UGE(symbol_factory.BitVecVal(w.values[name], obj.size()), obj)
+    STATS["minimize_hints"] = STATS.get("minimize_hints", 0) + 1
+    if type(constraints) == tuple:
+        return constraints + (bound,)
+    import copy
+    ext = copy.copy(constraints)
+    ext.append(bound)
+    return ext
 
 
 @lru_cache(maxsize=2 ** 23)
@@ -219,6 +278,10 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
                 _solver_log(cl, minimize, maximize, args, timeout)
             return model
     STATS["fallbacks"] += 1
+    if MINIMIZE_HINTS and minimize and not maximize:
+        hinted = _minimize_hint(constraints, minimize, timeout)
+        if hinted is not None:
+            return _reference(hinted, minimize, maximize, enforce_execution_time)
     return _reference(constraints, minimize, maximize, enforce_execution_time)
 
 

@@ -27,6 +27,16 @@ def _z3():
     return z3
 
 
+def var_name(raw) -> Optional[str]:
+    """The declaration name of a z3 constant (an uninterpreted 0-ary symbol), else None."""
+    try:
+        if raw.num_args() == 0 and raw.decl().kind() == _z3().Z3_OP_UNINTERPRETED:
+            return raw.decl().name()
+    except Exception:
+        return None
+    return None
+
+
 def to_ir(raws: Sequence, ctx: Optional[Ctx] = None) -> Script:
     z3 = _z3()
     s = z3.Solver()

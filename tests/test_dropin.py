@@ -327,3 +327,44 @@ def test_repeated_miss_skips_the_device(mythril):
     assert mythril.calls["reference"] == 3
     # a satisfiable set is still searched
     assert dropin.get_model(SAT).raw[0][0] == "z3"
+
+
+def test_minimize_hint_bounds_only_the_first_objective(mythril, monkeypatch):
+    """Opt-in minimize assistance (analysis/solver.py:216-256): a device witness
+    adds obj_0 <= witness(obj_0) to the set z3's Optimize gets; the objectives
+    themselves are untouched.  Off by default (the report's transaction data
+    could differ), and a minimize query without it goes to z3 unchanged."""
+    seen = []
+    ref = dropin._reference
+
+    def recording(constraints, minimize=(), maximize=(), enforce_execution_time=True):
+        seen.append((constraints, minimize))
+        return Model(["ref"])
+    monkeypatch.setattr(dropin, "_reference", recording)
+    Y = CTX.var("y", 8)
+
+    class BV:
+        def __init__(self, node):
+            self.raw = FakeRaw(node)
+            self.node = node
+
+        def size(self):
+            return self.node.width
+
+    def uge(a, b):
+        return fb(CTX.app("bvuge", CTX.const(a, 8), b.node))
+    mythril.mods["mythril.laser.smt"].UGE = uge
+    mythril.mods["mythril.laser.smt"].symbol_factory = types.SimpleNamespace(BitVecVal=lambda v, w: v)
+    monkeypatch.setattr(z3bridge, "var_name", lambda raw: raw.node.name)
+    objs = (BV(X), BV(Y))
+    dropin.get_model(SAT, minimize=objs)
+    assert seen[-1][0] == SAT                        # default: unchanged
+    monkeypatch.setattr(dropin, "MINIMIZE_HINTS", True)
+    dropin.get_model.cache_clear()
+    dropin.get_model(SAT, minimize=objs)
+    hinted, mins = seen[-1]
+    assert mins == objs and len(hinted) == len(SAT) + 1
+    bound = hinted[-1].raw.node
+    assert bound.op == "bvuge" and bound.args[1] is X and 200 < bound.args[0].val < 203
+    assert dropin.STATS["minimize_hints"] >= 1
+    monkeypatch.setattr(dropin, "_reference", ref)
