@@ -568,6 +568,7 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   std::lock_guard<std::mutex> lk(c->mu);
   const double t0 = now_ms();
   HIPCHK(hipSetDevice(c->dev));
+  (void)hipGetLastError();  // start from a clean error state: launch errors are read back below
   int rc = ensure_min(c, nprog);
   if (rc) return rc;
   // Programs with a specialised kernel (mg_prog_attach_kernel) get one launch
@@ -641,6 +642,7 @@ static int eval_common(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, 
   if (!c || !p || !verdict || ncand == 0) return fail(MG_E_ARG, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
+  (void)hipGetLastError();  // clean error state before the launch below
   const u64 nchunks = (ncand + kBlock - 1) / kBlock;
   const u64 gx = std::min<u64>(nchunks, (u64)c->ncu * 8);
   const u64 nthreads = gx * kBlock;

@@ -11,6 +11,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -129,9 +130,12 @@ class DeviceProgram:
         self.kernel: Optional[str] = None   # specialised kernel name, if attached
 
     def free(self):
-        if self.handle:
+        # a program never outlives its context: Device.close() frees the
+        # programs still loaded, and a freed context is never touched again
+        if self.handle and self.dev.handle:
             self.dev.lib.mg_prog_free(self.handle)
-            self.handle = None
+            self.dev._live.discard(self)
+        self.handle = None
 
     def __del__(self):  # pragma: no cover - best effort
         try:
@@ -153,17 +157,24 @@ class Device:
         _check(self.lib, self.lib.mg_init(device, ctypes.byref(h)), "mg_init")
         self.handle = h.value
         self.device = device
+        self._live = weakref.WeakSet()   # programs loaded and not yet freed
 
     def close(self):
         if self.handle:
+            for dp in list(self._live):
+                dp.free()
             self.lib.mg_free(self.handle)
             self.handle = None
 
     def load(self, p: Program) -> DeviceProgram:
+        if not self.handle:
+            raise EngineError("device context is closed")
         d, keep = make_desc(p)
         h = _P()
         _check(self.lib, self.lib.mg_prog_load(self.handle, ctypes.byref(d), ctypes.byref(h)), "mg_prog_load")
-        return DeviceProgram(self, h.value, p)
+        dp = DeviceProgram(self, h.value, p)
+        self._live.add(dp)
+        return dp
 
     def attach_kernel(self, dp: DeviceProgram, image: bytes, name: str) -> None:
         """Bind a specialised code object (mythril_amd.jit) to a loaded program."""

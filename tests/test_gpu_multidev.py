@@ -27,16 +27,19 @@ def test_two_contexts_match_one():
     md = MultiDevice([Device(0), Device(0)], round_size=1 << 16)
     try:
         flags = isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT
-        want, _ = one.search([one.load(q.program) for q in qs], DEFAULT_SEED, 0, 1 << 20, flags)
+        ones = [one.load(q.program) for q in qs]
+        want, _ = one.search(ones, DEFAULT_SEED, 0, 1 << 20, flags)
         mps = [md.load(q.program) for q in qs]
         got, st = md.search(mps, DEFAULT_SEED, 0, 1 << 20, flags)
         assert got == want and any(w is not None for w in want) and any(w is None for w in want)
-        ex_want, _ = one.search([one.load(q.program) for q in qs], DEFAULT_SEED, 0, 1 << 18, 0)
+        ex_want, _ = one.search(ones, DEFAULT_SEED, 0, 1 << 18, 0)
         ex_got, st = md.search(mps, DEFAULT_SEED, 0, 1 << 18, 0)
         assert ex_got == ex_want and st["evals"] == len(qs) * (1 << 18)
-        v1, _ = one.eval_generated(one.load(qs[0].program), DEFAULT_SEED, 0, 1 << 14, trace=False)
+        v1, _ = one.eval_generated(ones[0], DEFAULT_SEED, 0, 1 << 14, trace=False)
         v2, _ = md.eval_generated(mps[0], DEFAULT_SEED, 0, 1 << 14, trace=False)
         assert np.array_equal(v1, v2)
+        for mp in mps:
+            mp.free()
     finally:
-        md.close()
+        md.close()   # frees any program still loaded before the context
         one.close()
