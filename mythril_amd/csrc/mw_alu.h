@@ -280,8 +280,31 @@ MW_HD u32 clz256(const u32 y[8]) {
   return n;
 }
 // Moller-Granlund reciprocal of a normalized divisor d (top bit set):
-// floor((2^64 - 1) / d) - 2^32
-MW_HD u32 recip32(u32 d) { return (u32)(~0ull / (u64)d - (1ull << 32)); }
+// floor((2^64 - 1) / d) - 2^32, i.e. the 2-by-1 quotient (~d : 0xffffffff) / d.
+// On the device an f64 reciprocal (two Newton steps) gives the quotient to
+// within one, and one integer correction makes it exact (tools/exp/recip_check.hip
+// checks it against the u64 division on 2^31 divisors): ~20 instructions where
+// LLVM's generic u64 division expands to ~350 (about 100 executed).
+MW_HD u32 recip32(u32 d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const u32 nh = ~d;
+  const double dd = (double)d;
+  double r = __builtin_amdgcn_rcp(dd);
+  double e = __builtin_fma(-dd, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-dd, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  const double n = __builtin_fma((double)nh, 4294967296.0, 4294967295.0);
+  u32 v = (u32)(n * r);
+  const u64 nx = ((u64)nh << 32) | 0xffffffffu;
+  const u64 p = (u64)v * d;
+  if (p > nx) v -= 1u;
+  else if (nx - p >= d) v += 1u;
+  return v;
+#else
+  return (u32)(~0ull / (u64)d - (1ull << 32));
+#endif
+}
 // (u1:u0) / d with u1 < d, d normalized, v = recip32(d)  (Moller & Granlund 2011, Alg. 4)
 MW_HD u32 div2by1(u32 u1, u32 u0, u32 d, u32 v) {
   u64 q = (u64)v * u1 + ((((u64)u1) << 32) | u0);

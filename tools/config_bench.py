@@ -3,7 +3,10 @@
 C2: token.sol -t 3 transfer queries, 2^24 candidates each;
 C3: BECToken batchTransfer SWC-101 overflow query, 2^28 candidates;
 C4: WalletLibrary -t 3 queries searched together in one launch (state
-    batching), 2^24 candidates.
+    batching), 2^24 candidates;
+C2L: the LASER-shaped queries of token.sol's runtime bytecode
+    (tests/golden/laser/underflow_*, from the reference's underflow.sol.o),
+    all in one launch, 2^24 candidates each.
 
 The queries are the committed ``--solver-log``-format dumps
 (tests/golden/solver_log, synthetic: no z3/solc exists to dump real ones, see
@@ -26,8 +29,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 LOG = os.path.join(ROOT, "tests", "golden", "solver_log")
+LASER = os.path.join(ROOT, "tests", "golden", "laser")
 CONFIGS = [
     ("C2", ["c2_token_transfer_ok.smt2", "c2_token_transfer_underflow.smt2"], 24, False),
+    # C2 on queries derived from the reference's own bytecode: every JUMPI
+    # successor set of a 2-3 transaction token.sol run (underflow.sol.o),
+    # searched together in one launch (LaserEVM batching)
+    ("C2L", sorted(f for f in os.listdir(LASER) if f.startswith("underflow_") and f.endswith(".smt2.gz")), 24, True),
     ("C3", ["c3_bec_batchtransfer_overflow.smt2"], 28, False),
     ("C4", ["c4_wallet_onlyowner.smt2", "c4_wallet_contradiction.smt2"], 24, True),
 ]
@@ -39,7 +47,7 @@ def _groups(files, together):
     from mythril_amd.smt2 import parse_file
     qs = []
     for f in files:
-        s = parse_file(os.path.join(LOG, f))
+        s = parse_file(os.path.join(LASER if f.endswith(".gz") else LOG, f))
         qs.append(prepare(s.asserts, s.ctx))
     return [(files, qs)] if together else [([f], [q]) for f, q in zip(files, qs)]
 
@@ -66,7 +74,7 @@ def main():
         warm()
         return
     dev = Device(0)
-    peak = bench.load_peak()["peak"]
+    peak = bench.THEORETICAL_PEAK
     lines = []
     for name, files, log2, together in CONFIGS:
         for gfiles, g in _groups(files, together):
