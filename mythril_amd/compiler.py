@@ -783,6 +783,95 @@ def _limbs(v: int) -> List[int]:
     return [(v >> (32 * k)) & 0xFFFFFFFF for k in range(8)]
 
 
+def layout_leaves(leaf_nodes: Sequence[Node], leaf_specs: Optional[Dict[str, LeafSpec]] = None,
+                  pools: Optional[Dict[str, List[Optional[int]]]] = None):
+    """Leaf table + pool words for `leaf_nodes` (in leaf-index order).
+
+    Default layout: bit-interleaved (Morton) digits over the first
+    INDEX_FIELD_BITS index bits, so every pool varies at small indices and the
+    best proposals of all leaves are tried together first; leaves that do not
+    fit are sampled with hashed digits.  Returns (specs, leaf words, pool
+    words, input rows).  The code refers to leaves by index only, so a program
+    whose leaf set grows (incremental.py) re-lays its table with this."""
+    specs: List[LeafSpec] = []
+    leaf_words: List[int] = []
+    pool_words: List[int] = []
+    in_row = 0
+    user = dict(leaf_specs or {})
+    resolved: List[LeafSpec] = []
+    for n in leaf_nodes:
+        w = _w(n)
+        spec = user.get(n.name)
+        if spec is None and pools and n.name in pools:
+            spec = LeafSpec(n.name, w, pool=list(pools[n.name]))
+        if spec is None:
+            spec = LeafSpec(n.name, w)
+        spec.width = w
+        if spec.pool:
+            p = list(spec.pool)
+            nb = max(0, math.ceil(math.log2(len(p)))) if len(p) > 1 else 0
+            p += [None] * ((1 << nb) - len(p))
+            spec.pool = p
+        resolved.append(spec)
+    by_name = {s.name: s for s in resolved}
+    for spec in resolved:
+        lead = by_name.get(spec.tie) if spec.tie else None
+        if spec.tie and (lead is None or lead.tie or not lead.pool or not spec.pool
+                         or len(lead.pool) != len(spec.pool)):
+            spec.tie = None
+    fresh = [s for s in resolved if s.pool and len(s.pool) > 1 and not s.hashed and s.bits == 0
+             and s.shift == 0 and s.stride == 0 and not s.tie]
+    if fresh:
+        stride = len(fresh)
+        for j, spec in enumerate(fresh):
+            nb = int(math.log2(len(spec.pool)))
+            top = j + (nb - 1) * stride
+            if top < INDEX_FIELD_BITS:
+                spec.bits, spec.shift, spec.stride = nb, j, stride
+            else:
+                fit = max(0, (INDEX_FIELD_BITS - 1 - j) // stride + 1)
+                if fit >= 2:  # interleave the first 2^fit entries, hash nothing
+                    spec.bits, spec.shift, spec.stride = fit, j, stride
+                    spec.pool = spec.pool[:1 << fit]
+                else:
+                    spec.hashed = True
+    for spec in resolved:
+        if spec.tie:   # same digit as the leader: same layout, same hash key
+            lead = by_name[spec.tie]
+            spec.pool = spec.pool[:len(lead.pool)]
+            spec.bits, spec.shift, spec.stride, spec.hashed = lead.bits, lead.shift, lead.stride, lead.hashed
+            spec.salt = lead.key_salt()
+    bit = 0
+    for li, (n, spec) in enumerate(zip(leaf_nodes, resolved)):
+        w = spec.width
+        kind, pshift, pbits, poff, pstride = 0, 0, 0, 0, 0
+        if spec.pool:
+            nb = int(math.log2(len(spec.pool))) if len(spec.pool) > 1 else 0
+            if spec.hashed:
+                spec.bits, spec.shift, spec.stride = nb, 0, 0
+                kind = 2
+            elif spec.stride:
+                kind = 3
+            else:
+                kind = 1
+                if spec.bits == 0 and spec.shift == 0:
+                    spec.bits = nb
+            pshift, pbits, poff, pstride = spec.shift, spec.bits, len(pool_words), spec.stride
+            bit = max(bit, spec.shift + (spec.bits - 1) * max(spec.stride, 1) + 1 if spec.bits else 0)
+            for e in spec.pool:
+                if e is None:
+                    pool_words.extend([1] + [0] * 8)
+                else:
+                    pool_words.extend([0] + _limbs(e & ((1 << w) - 1)))
+        leaf_words.extend([w, kind, spec.key_salt(), pshift, pbits, poff, in_row, pstride])
+        in_row += (w + 31) // 32
+        specs.append(spec)
+    if bit > 63:
+        raise Unsupported("pool digit fields exceed the 64-bit candidate index")
+
+    return specs, leaf_words, pool_words, in_row
+
+
 def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, LeafSpec]] = None,
                     trace: Sequence[Node] = (), pools: Optional[Dict[str, List[Optional[int]]]] = None
                     ) -> Program:
@@ -844,85 +933,7 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
     if len(consts) > 0x7FFF:
         raise Unsupported("constant pool overflow")
 
-    # leaf table + pools.  Default layout: bit-interleaved (Morton) digits over the
-    # first INDEX_FIELD_BITS index bits, so every pool varies at small indices and
-    # the best proposals of all leaves are tried together first; leaves that do
-    # not fit are sampled with hashed digits.
-    specs: List[LeafSpec] = []
-    leaf_words: List[int] = []
-    pool_words: List[int] = []
-    in_row = 0
-    user = dict(leaf_specs or {})
-    resolved: List[LeafSpec] = []
-    for n in lw.leaf_nodes:
-        w = _w(n)
-        spec = user.get(n.name)
-        if spec is None and pools and n.name in pools:
-            spec = LeafSpec(n.name, w, pool=list(pools[n.name]))
-        if spec is None:
-            spec = LeafSpec(n.name, w)
-        spec.width = w
-        if spec.pool:
-            p = list(spec.pool)
-            nb = max(0, math.ceil(math.log2(len(p)))) if len(p) > 1 else 0
-            p += [None] * ((1 << nb) - len(p))
-            spec.pool = p
-        resolved.append(spec)
-    by_name = {s.name: s for s in resolved}
-    for spec in resolved:
-        lead = by_name.get(spec.tie) if spec.tie else None
-        if spec.tie and (lead is None or lead.tie or not lead.pool or not spec.pool
-                         or len(lead.pool) != len(spec.pool)):
-            spec.tie = None
-    fresh = [s for s in resolved if s.pool and len(s.pool) > 1 and not s.hashed and s.bits == 0
-             and s.shift == 0 and s.stride == 0 and not s.tie]
-    if fresh:
-        stride = len(fresh)
-        for j, spec in enumerate(fresh):
-            nb = int(math.log2(len(spec.pool)))
-            top = j + (nb - 1) * stride
-            if top < INDEX_FIELD_BITS:
-                spec.bits, spec.shift, spec.stride = nb, j, stride
-            else:
-                fit = max(0, (INDEX_FIELD_BITS - 1 - j) // stride + 1)
-                if fit >= 2:  # interleave the first 2^fit entries, hash nothing
-                    spec.bits, spec.shift, spec.stride = fit, j, stride
-                    spec.pool = spec.pool[:1 << fit]
-                else:
-                    spec.hashed = True
-    for spec in resolved:
-        if spec.tie:   # same digit as the leader: same layout, same hash key
-            lead = by_name[spec.tie]
-            spec.pool = spec.pool[:len(lead.pool)]
-            spec.bits, spec.shift, spec.stride, spec.hashed = lead.bits, lead.shift, lead.stride, lead.hashed
-            spec.salt = lead.key_salt()
-    bit = 0
-    for li, (n, spec) in enumerate(zip(lw.leaf_nodes, resolved)):
-        w = spec.width
-        kind, pshift, pbits, poff, pstride = 0, 0, 0, 0, 0
-        if spec.pool:
-            nb = int(math.log2(len(spec.pool))) if len(spec.pool) > 1 else 0
-            if spec.hashed:
-                spec.bits, spec.shift, spec.stride = nb, 0, 0
-                kind = 2
-            elif spec.stride:
-                kind = 3
-            else:
-                kind = 1
-                if spec.bits == 0 and spec.shift == 0:
-                    spec.bits = nb
-            pshift, pbits, poff, pstride = spec.shift, spec.bits, len(pool_words), spec.stride
-            bit = max(bit, spec.shift + (spec.bits - 1) * max(spec.stride, 1) + 1 if spec.bits else 0)
-            for e in spec.pool:
-                if e is None:
-                    pool_words.extend([1] + [0] * 8)
-                else:
-                    pool_words.extend([0] + _limbs(e & ((1 << w) - 1)))
-        leaf_words.extend([w, kind, spec.key_salt(), pshift, pbits, poff, in_row, pstride])
-        in_row += (w + 31) // 32
-        specs.append(spec)
-    if bit > 63:
-        raise Unsupported("pool digit fields exceed the 64-bit candidate index")
+    specs, leaf_words, pool_words, in_row = layout_leaves(lw.leaf_nodes, leaf_specs, pools)
 
     reach = topo(conj + list(trace))
     ops = sum(node_cost(n) for n in reach)
