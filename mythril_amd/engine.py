@@ -10,7 +10,7 @@ into a :class:`Witness` by re-evaluating that single candidate on the device.
 """
 from __future__ import annotations
 
-import copy
+import dataclasses
 import logging
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -87,7 +87,8 @@ def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True,
     if timings is not None:
         timings.update(lower=t1 - t0, pools=t2 - t1, compile=time.perf_counter() - t2)
     # identical leaf layout (pool fields already assigned) for the materialisation program
-    fixed = {s.name: copy.deepcopy(s) for s in prog.leaf_specs}
+    fixed = {s.name: dataclasses.replace(s, pool=None if s.pool is None else list(s.pool))
+             for s in prog.leaf_specs}
     # trace every array index / function argument (wider than 256 bits: as 256-bit chunks)
     from .lower import _Rewriter
     chunker = _Rewriter(ctx)

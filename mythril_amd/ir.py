@@ -60,7 +60,7 @@ class Node:
 
     __slots__ = ("op", "width", "args", "params", "val", "name", "dom", "id", "_h")
 
-    def __init__(self, op, width, args, params, val, name, dom, nid):
+    def __init__(self, op, width, args, params, val, name, dom, nid, h=None):
         self.op = op
         self.width = width
         self.args = args
@@ -69,7 +69,7 @@ class Node:
         self.name = name
         self.dom = dom
         self.id = nid
-        self._h = hash((op, width, tuple(a.id for a in args), params, val, name, dom))
+        self._h = hash((op, width, tuple(a.id for a in args), params, val, name, dom)) if h is None else h
 
     # -- sort helpers -------------------------------------------------
     @property
@@ -102,10 +102,11 @@ class Ctx:
         self.nodes: List[Node] = []
 
     def _mk(self, op, width, args=(), params=(), val=None, name=None, dom=None) -> Node:
-        key = (op, width, tuple(a.id for a in args), tuple(params), val, name, dom)
+        params = tuple(params)
+        key = (op, width, tuple([a.id for a in args]), params, val, name, dom)
         n = self._tab.get(key)
         if n is None:
-            n = Node(op, width, tuple(args), tuple(params), val, name, dom, len(self.nodes))
+            n = Node(op, width, tuple(args), params, val, name, dom, len(self.nodes), hash(key))
             self._tab[key] = n
             self.nodes.append(n)
         return n
@@ -185,25 +186,33 @@ def bv_result_width(op: str, ws: Sequence[int], params: Sequence[int]) -> int:
     return w
 
 
-def topo(roots: Iterable[Node]) -> List[Node]:
-    """Post-order (operands first) list of every node reachable from roots."""
+def topo(roots: Iterable[Node], seen: Optional[set] = None) -> List[Node]:
+    """Post-order (operands first) list of every node reachable from roots.
+    `seen` (optional, updated in place): ids already visited by an earlier
+    call; those nodes and everything under them are skipped."""
     out: List[Node] = []
-    seen = set()
+    if seen is None:
+        seen = set()
+    emit, mark = out.append, seen.add
     for r in roots:
         if r.id in seen:
             continue
-        stack: List[Tuple[Node, int]] = [(r, 0)]
+        stack: List[Node] = [r]
+        push, pop = stack.append, stack.pop
         while stack:
-            n, i = stack.pop()
-            if i < len(n.args):
-                stack.append((n, i + 1))
-                a = n.args[i]
+            n = stack[-1]
+            if n.id in seen:
+                pop()
+                continue
+            pending = False
+            for a in reversed(n.args):   # first operand on top: the same order as a recursive walk
                 if a.id not in seen:
-                    stack.append((a, 0))
-            else:
-                if n.id not in seen:
-                    seen.add(n.id)
-                    out.append(n)
+                    push(a)
+                    pending = True
+            if not pending:
+                pop()
+                mark(n.id)
+                emit(n)
     return out
 
 

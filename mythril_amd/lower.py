@@ -70,6 +70,7 @@ class _Rewriter:
     def __init__(self, ctx: Ctx):
         self.ctx = ctx
         self.memo: Dict[int, Node] = {}
+        self._visited: set = set()   # node ids rw() has walked (topo skips them)
         self.ack: Dict[str, AckLeaf] = {}
         self.by_base: Dict[str, List[AckLeaf]] = {}
         self.leaf_of_key: Dict[tuple, Node] = {}
@@ -363,7 +364,7 @@ class _Rewriter:
 
     # -- main rewrite --------------------------------------------------------------
     def rw(self, root: Node) -> Node:
-        for n in topo([root]):
+        for n in topo([root], self._visited):
             if n.id in self.memo:
                 continue
             self.memo[n.id] = self._rw1(n)

@@ -45,6 +45,7 @@ Pools are laid out as index bit-fields while the 40 field bits last
 """
 from __future__ import annotations
 
+import itertools
 from typing import Dict, List, Optional
 
 from .compiler import LeafSpec
@@ -286,6 +287,14 @@ def _restrict(pool: List[Optional[int]], name: str, w: int, exact, interval, ali
     return _pad_pow2(vals)   # no RANDOM padding: a random draw would almost never satisfy the facts
 
 
+def _const_props(consts, m: int, split_bytes: bool):
+    for c in consts:
+        yield c & m
+        if split_bytes:
+            for i in range(min(32, (c.bit_length() + 7) // 8)):
+                yield (c >> (8 * i)) & 0xFF
+
+
 def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
             random_share: float = 0.25, restrict: bool = True) -> Dict[str, LeafSpec]:
     nodes = topo(conjuncts)
@@ -343,21 +352,21 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
             proposals[name] = list(dict.fromkeys(proposals.get(name, []) + merged))
     specs: Dict[str, LeafSpec] = {}
     uniq_consts = list(dict.fromkeys(consts))[:256]
+    tails: Dict[int, List[int]] = {}   # width -> the constants' proposals, deduplicated
     for leaf in leaves:
         if leaf.op != "var":
             continue
         w = 1 if leaf.width == BOOL else leaf.width
         m = (1 << w) - 1
-        cand: List[int] = []
-        cand += proposals.get(leaf.name, [])
         lname = leaf.name.lower()
-        if w >= 160 and any(t in lname for t in ("sender", "caller", "origin", "creator", "address")):
-            cand += ACTORS
-        cand += [0, 1, 2, m, 1 << (w - 1), m - 1]
-        for c in uniq_consts:
-            cand.append(c & m)
-            if w == 8:
-                cand.extend((c >> (8 * i)) & 0xFF for i in range(min(32, (c.bit_length() + 7) // 8)))
+        actors = ACTORS if w >= 160 and any(t in lname for t in ("sender", "caller", "origin", "creator",
+                                                                  "address")) else ()
+        # lazily: the pool fills after a few dozen values, and the byte split of
+        # 256 constants for every calldata byte leaf was most of prepare()'s time
+        tail = tails.get(w)
+        if tail is None:
+            tail = tails[w] = list(dict.fromkeys(_const_props(uniq_consts, m, w == 8)))
+        cand = itertools.chain(proposals.get(leaf.name, ()), actors, (0, 1, 2, m, 1 << (w - 1), m - 1), tail)
         pool: List[Optional[int]] = []
         seen = set()
         nfixed = max(1, int(pool_size * (1 - random_share)))

@@ -24,37 +24,27 @@ from .ir import BOOL, BOOL_OPS, BV_OPS, ALIASES, Ctx, Node, topo
 
 Sexp = Union[str, list]
 
-_TOKEN = re.compile(r"""\s*(?:
-      (?P<comment>;[^\n]*)
-    | (?P<lp>\()
-    | (?P<rp>\))
-    | (?P<quoted>\|[^|]*\|)
-    | (?P<string>"(?:[^"]|"")*")
-    | (?P<atom>[^\s()|";]+)
-    )""", re.X)
+# one findall over the whole text; the last alternative catches what no token
+# matches (an unterminated |symbol| or "string") so it fails loudly below
+_TOKEN = re.compile(r''';[^\n]*|\(|\)|\|[^|]*\||"(?:[^"]|"")*"|[^\s()|";]+|\S''')
 
 
-def tokenize(text: str):
-    pos = 0
-    n = len(text)
-    while pos < n:
-        m = _TOKEN.match(text, pos)
-        if not m or m.end() == pos:
-            if text[pos:].strip() == "":
-                return
-            raise Unsupported(f"smt2: cannot tokenize at {text[pos:pos + 30]!r}")
-        pos = m.end()
-        kind = m.lastgroup
-        if kind == "comment":
+def tokenize(text: str) -> List[Union[str, tuple]]:
+    out: List[Union[str, tuple]] = []
+    emit = out.append
+    for t in _TOKEN.findall(text):
+        c = t[0]
+        if c == ";":
             continue
-        if kind == "lp":
-            yield "("
-        elif kind == "rp":
-            yield ")"
-        elif kind == "quoted":
-            yield ("Q", m.group(kind)[1:-1])
+        if c == "|":
+            if len(t) < 2 or t[-1] != "|":
+                raise Unsupported(f"smt2: cannot tokenize at {t!r}")
+            emit(("Q", t[1:-1]))
+        elif c == '"' and (len(t) < 2 or t[-1] != '"'):
+            raise Unsupported(f"smt2: cannot tokenize at {t!r}")
         else:
-            yield m.group(kind)
+            emit(t)
+    return out
 
 
 def parse_sexps(text: str) -> List[Sexp]:
@@ -123,6 +113,7 @@ class _Builder:
         self.s = script
         self.ctx = script.ctx
         self.defs: Dict[str, Node] = {}
+        self.lits: Dict[str, Node] = {}   # #x / #b literal -> const node
 
     def leaf(self, name: str) -> Node:
         if name in self.defs:
@@ -151,10 +142,15 @@ class _Builder:
                 return self.ctx.true()
             if e == "false":
                 return self.ctx.false()
+            k = self.lits.get(e)
+            if k is not None:
+                return k
             if e.startswith("#x"):
-                return self.ctx.const(int(e[2:], 16), 4 * (len(e) - 2))
+                k = self.lits[e] = self.ctx.const(int(e[2:], 16), 4 * (len(e) - 2))
+                return k
             if e.startswith("#b"):
-                return self.ctx.const(int(e[2:], 2), len(e) - 2)
+                k = self.lits[e] = self.ctx.const(int(e[2:], 2), len(e) - 2)
+                return k
             if re.fullmatch(r"\d+", e):
                 raise Unsupported("smt2: Int numerals are outside QF_ABV")
             return self.leaf(e)
