@@ -399,7 +399,11 @@ def generate(progs: Sequence[Program], names: Sequence[str], variants: str = "xe
         # multi-MiB body), the scheduler still cannot move code across them
         out += ["#if defined(__HIP_DEVICE_COMPILE__)", "#undef JIT_SPLIT",
                 "#define JIT_SPLIT() __builtin_amdgcn_sched_barrier(0)", "#endif", ""]
+    done = set()
     for k, (p, name) in enumerate(zip(progs, names)):
+        if name in done:   # two queries that compile to the same program share one kernel
+            continue
+        done.add(name)
         if not p.ssa:
             raise ValueError("program has no SSA machine IR (compiled by an older compiler?)")
         part = parts[k] if parts else None

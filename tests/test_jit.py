@@ -113,6 +113,17 @@ def test_signature_matches_library_definition():
     assert jit.kernel_name(p) == f"mwj_{h:016x}"
 
 
+def test_identical_programs_share_one_kernel():
+    # two queries of one launch group that compile to the same program
+    # (config_bench's LASER groups have such pairs) must not define it twice
+    p = compile_program([RandDag(5).boolean(3)])
+    q = compile_program([RandDag(5).boolean(3)])
+    assert jit.kernel_name(p) == jit.kernel_name(q)
+    src = jit.generate([p, q], [jit.kernel_name(p)] * 2)
+    assert src.count("MW_JIT_SIG(") == 1
+    assert src.count(f"MW_JIT_KERNEL({jit.kernel_name(p)}, _x") == 1
+
+
 def _unbundle(hsaco_bytes, tmp_path):
     src = tmp_path / "k.hsaco"
     src.write_bytes(hsaco_bytes)

@@ -15,6 +15,7 @@
 #   replay         python -m mythril_amd.replay tests/golden/solver_log
 #   opbench        tools/opbench.py jit
 #   keccak         tools/keccak_bench.py
+#   recip          tools/exp/recip_check (device reciprocal vs u64 division; built by hand)
 # Outputs land in gpurun_out/TAG/.
 set -o pipefail
 export TMPDIR=/tmp
@@ -82,6 +83,9 @@ for step in "$@"; do
     keccak)
       run 300 "$OUT/keccak.log" python3 tools/keccak_bench.py
       tail -8 "$OUT/keccak.log" ;;
+    recip)
+      run 120 "$OUT/recip.txt" ./tools/exp/recip_check
+      tail -4 "$OUT/recip.txt" ;;
     *)
       echo "unknown step $step"
       exit 2 ;;
