@@ -32,7 +32,12 @@ typedef const u32* kptr;
 #endif
 #define MW_KPTR(p) ((kptr)(p))
 
-typedef u32 u32xW __attribute__((ext_vector_type(MW_NW)));   // one limb of every W slot
+// W file: four vectors, F<k> holding limb k of every slot (elements 0..NW-1)
+// and limb k+4 (elements NW..2NW-1).  A 16-element vector read or written at a
+// uniform index is lowered to s_set_gpr_idx + v_mov; an 8-element one (one
+// vector per limb) was expanded into compare + v_cndmask chains, ~16
+// instructions per limb and ~250 per W operand fetch + write-back.
+typedef u32 u32xW __attribute__((ext_vector_type(2 * MW_NW)));
 typedef u32 u32xN __attribute__((ext_vector_type(32)));      // one half of the N file
 // (the N file is two 32-slot halves: a single 64-element vector indexed at run
 // time is lowered through scratch memory, two halves stay in VGPRs)
@@ -50,7 +55,8 @@ typedef u32 u32xN __attribute__((ext_vector_type(32)));      // one half of the 
     } else {                                                                  \
       _o = MW_WSLOT(_o);                                                      \
       x[0] = F0[_o]; x[1] = F1[_o]; x[2] = F2[_o]; x[3] = F3[_o];             \
-      x[4] = F4[_o]; x[5] = F5[_o]; x[6] = F6[_o]; x[7] = F7[_o];             \
+      x[4] = F0[_o + MW_NW]; x[5] = F1[_o + MW_NW];                           \
+      x[6] = F2[_o + MW_NW]; x[7] = F3[_o + MW_NW];                           \
     }                                                                         \
   } while (0)
 
@@ -62,11 +68,18 @@ typedef u32 u32xN __attribute__((ext_vector_type(32)));      // one half of the 
     else v = NF[_o & 31u];                                                    \
   } while (0)
 
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MW_OPAQUE(v) asm volatile("" : "+v"(v))
+#else
+#define MW_OPAQUE(v) ((void)0)
+#endif
+
 #define MW_WRITE_W(d, r)                                                      \
   do {                                                                        \
     u32 _d = MW_WSLOT((u32)(d));                                              \
     F0[_d] = r[0]; F1[_d] = r[1]; F2[_d] = r[2]; F3[_d] = r[3];               \
-    F4[_d] = r[4]; F5[_d] = r[5]; F6[_d] = r[6]; F7[_d] = r[7];               \
+    F0[_d + MW_NW] = r[4]; F1[_d + MW_NW] = r[5];                             \
+    F2[_d + MW_NW] = r[6]; F3[_d + MW_NW] = r[7];                             \
   } while (0)
 
 #define MW_WRITE_N(d, v)                                                      \
@@ -80,7 +93,7 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
                   bool alive, u32 flags) {
   const kptr code = MW_KPTR(code_);
   const kptr cpool = MW_KPTR(cpool_);
-  u32xW F0 = 0, F1 = 0, F2 = 0, F3 = 0, F4 = 0, F5 = 0, F6 = 0, F7 = 0;
+  u32xW F0 = 0, F1 = 0, F2 = 0, F3 = 0;
   u32xN NF = 0, NH = 0;   // N slots 0..31, 32..63
   // Instruction fetch is software-pipelined: the next instruction's s_load is in
   // flight while the current one executes (the words after END are always
@@ -454,13 +467,30 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         break;
       }
     }
-    // single write-back point: keeps one SSA version of each register-file
-    // vector live across the dispatch (otherwise hipcc duplicates the files)
-    if (wk == 1) {
-      if (w - 1u < 255u) canon(r, w);  // results of width 1..255: clear bits >= w (FILL/MOV carry 0)
-      MW_WRITE_W(dst, r);
-    } else if (wk == 2) {
-      MW_WRITE_N(dst, r[0]);
+    // Single, UNCONDITIONAL write-back: every dispatch rewrites W[dst] and
+    // N[dst] (with their old values when the op writes elsewhere or nothing).
+    // A conditional indexed write leaves two versions of a file live at the
+    // loop latch (written / not written), and the register allocator resolves
+    // that with a whole-file copy per dispatch (32 v_mov_b64 for the N file:
+    // most of the interpreter's VALU work before this).  The asm barriers stop
+    // the compiler turning "write back the old value" into a branch again.
+    if (wk == 1 && w - 1u < 255u) canon(r, w);  // results of width 1..255: clear bits >= w
+    {
+      const u32 dw = MW_WSLOT(dst);
+      const bool ww = wk == 1;
+      u32 v0 = ww ? r[0] : F0[dw], v1 = ww ? r[1] : F1[dw], v2 = ww ? r[2] : F2[dw], v3 = ww ? r[3] : F3[dw];
+      u32 v4 = ww ? r[4] : F0[dw + MW_NW], v5 = ww ? r[5] : F1[dw + MW_NW];
+      u32 v6 = ww ? r[6] : F2[dw + MW_NW], v7 = ww ? r[7] : F3[dw + MW_NW];
+      MW_OPAQUE(v0); MW_OPAQUE(v1); MW_OPAQUE(v2); MW_OPAQUE(v3);
+      MW_OPAQUE(v4); MW_OPAQUE(v5); MW_OPAQUE(v6); MW_OPAQUE(v7);
+      F0[dw] = v0; F1[dw] = v1; F2[dw] = v2; F3[dw] = v3;
+      F0[dw + MW_NW] = v4; F1[dw + MW_NW] = v5; F2[dw + MW_NW] = v6; F3[dw + MW_NW] = v7;
+      const u32 dn = dst & 31u;
+      const bool wlo = wk == 2 && (dst & 32u) == 0u, whi = wk == 2 && (dst & 32u) != 0u;
+      u32 lo = wlo ? r[0] : NF[dn], hi = whi ? r[0] : NH[dn];
+      MW_OPAQUE(lo); MW_OPAQUE(hi);
+      NF[dn] = lo;
+      NH[dn] = hi;
     }
     w0 = n0;
     w1 = n1;

@@ -15,6 +15,8 @@
 #   replay         python -m mythril_amd.replay tests/golden/solver_log
 #   opbench        tools/opbench.py jit
 #   keccak         tools/keccak_bench.py
+#   ipmc=FILE      PMC passes on one exhaustive interpreter launch of FILE (tools/interp_once.py)
+#   opcost         tools/interp_opcost.py (+ one PMC pass: instructions per bytecode op)
 #   recip          tools/exp/recip_check (device reciprocal vs u64 division; built by hand)
 # Outputs land in gpurun_out/TAG/.
 set -o pipefail
@@ -83,6 +85,23 @@ for step in "$@"; do
     keccak)
       run 300 "$OUT/keccak.log" python3 tools/keccak_bench.py
       tail -8 "$OUT/keccak.log" ;;
+    ipmc=*)
+      F=${step#ipmc=}
+      i=0
+      for set in "SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_SCA" \
+                 "SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_SMEM,SQ_INSTS_LDS,SQ_INSTS_BRANCH,SQ_INSTS_VMEM,SQ_INST_CYCLES_SALU,SQ_INSTS_FLAT" \
+                 "SQ_WAIT_INST_LDS,SQ_ACTIVE_INST_LDS,SQ_ACTIVE_INST_VMEM,SQ_LDS_BANK_CONFLICT"; do
+        i=$((i + 1))
+        run 150 "$OUT/ipmc$i.log" timeout -s KILL 140 rocprofv3 --pmc $set --output-format csv -d "$OUT/ipmc/p$i" -o run -- \
+          python3 tools/interp_once.py "$F" 22
+      done
+      find "$OUT/ipmc" -name "*counter_collection*" ;;
+    opcost)
+      run 300 "$OUT/opcost.log" python3 tools/interp_opcost.py
+      cat "$OUT/opcost.log"
+      run 200 "$OUT/opcost_pmc.log" timeout -s KILL 190 rocprofv3 --pmc SQ_WAVES,SQ_WAVE_CYCLES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_SMEM,SQ_INSTS_BRANCH,SQ_WAIT_INST_ANY,SQ_WAIT_ANY \
+        --output-format csv -d "$OUT/opcost_pmc" -o run -- python3 tools/interp_opcost.py --log2 18
+      find "$OUT/opcost_pmc" -name "*counter_collection*" ;;
     recip)
       run 120 "$OUT/recip.txt" ./tools/exp/recip_check
       tail -4 "$OUT/recip.txt" ;;
