@@ -55,7 +55,7 @@ typedef struct {
   size_t nleaves;
   const uint32_t* pool;   /* candidate pools, MW_POOL_ENTRY_WORDS per entry */
   size_t npool_words;
-  uint32_t n_spill;       /* spill slots (8 limbs each) the program uses */
+  uint32_t n_spill;       /* spill-area words per lane (SPILL_W/FILL_W imm: 8-word slot offset, _N: 1 word) */
   uint32_t n_trace_rows;  /* rows written by MW_STORE_* (mg_eval trace) */
   uint32_t n_input_rows;  /* SoA leaf rows mg_eval reads */
   uint32_t reserved;

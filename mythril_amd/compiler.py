@@ -702,20 +702,23 @@ def _allocate(insns: List[MInsn]):
         return lst[p] if p < len(lst) else 1 << 60
 
     cap = {"W": isa.NW, "N": isa.NN}
-    free = {"W": list(range(isa.NW - 1, -1, -1)), "N": list(range(isa.NN - 1, -1, -1))}
+    # the interpreter's write-back scratch slots are never allocated (mw_isa.h)
+    free = {"W": [k for k in range(isa.NW - 1, -1, -1) if k != isa.W_RESERVED],
+            "N": [k for k in range(isa.NN - 1, -1, -1) if k & 31 != isa.N_RESERVED]}
     reg_of: Dict[int, int] = {}
     resident: Dict[str, Dict[int, VReg]] = {"W": {}, "N": {}}
+    # spill slots: per class (a W slot is 8 words of the per-lane spill area,
+    # an N slot 1 word); numbered here, laid out by _layout_spills
     spill_of: Dict[int, int] = {}
-    spill_free: List[int] = []
-    n_spill = 0
+    spill_free: Dict[str, List[int]] = {"W": [], "N": []}
+    slot_cls: List[str] = []
     out: List[MInsn] = []
 
-    def get_spill_slot() -> int:
-        nonlocal n_spill
-        if spill_free:
-            return spill_free.pop()
-        n_spill += 1
-        return n_spill - 1
+    def get_spill_slot(cls: str) -> int:
+        if spill_free[cls]:
+            return spill_free[cls].pop()
+        slot_cls.append(cls)
+        return len(slot_cls) - 1
 
     def evict(cls: str, i: int, pinned: set):
         best, best_nu = None, -1
@@ -730,7 +733,7 @@ def _allocate(insns: List[MInsn]):
         slot = reg_of.pop(best.id)
         del resident[cls][best.id]
         if best_nu < (1 << 60) and best.id not in spill_of:
-            sp = get_spill_slot()
+            sp = get_spill_slot(cls)
             spill_of[best.id] = sp
             m = MInsn("SPILL_W" if cls == "W" else "SPILL_N", 0, None, [("phys", slot)], imm=sp)
             out.append(m)
@@ -763,7 +766,7 @@ def _allocate(insns: List[MInsn]):
                 resident[s.cls].pop(s.id, None)
                 free[s.cls].append(slot)
                 if s.id in spill_of:
-                    spill_free.append(spill_of.pop(s.id))
+                    spill_free[s.cls].append(spill_of.pop(s.id))
         dst = None
         if ins.dst is not None:
             d = ins.dst
@@ -775,7 +778,35 @@ def _allocate(insns: List[MInsn]):
                 free[d.cls].append(slot)  # dead result (e.g. traced only) - slot reused
             dst = ("phys", slot)
         out.append(MInsn(ins.op, ins.width, dst, phys_srcs, ins.imm))
-    return out, n_spill
+    return _layout_spills(out, slot_cls)
+
+
+def _layout_spills(insns: List[MInsn], slot_cls: List[str]):
+    """Word offsets for the spill slots; returns (insns, spill words per lane).
+
+    The first LDS_SPILL_WORDS words of a lane's spill area live in LDS and the
+    rest in global memory (mw_kernels.hip), so slots are placed by traffic:
+    most SPILL/FILL accesses per word first.  C3 (129 narrow slots) keeps its
+    hottest 80 in LDS instead of the first 10 W-sized slots."""
+    if not slot_cls:
+        return insns, 0
+    hits = [0] * len(slot_cls)
+    for ins in insns:
+        if ins.op in ("SPILL_W", "SPILL_N", "FILL_W", "FILL_N"):
+            hits[ins.imm] += 1
+    size = [8 if c == "W" else 1 for c in slot_cls]
+    order = sorted(range(len(slot_cls)), key=lambda k: (-hits[k] / size[k], k))
+    off, words = {}, 0
+    for k in order:
+        off[k] = words
+        words += size[k]
+    for ins in insns:
+        if ins.op in ("SPILL_W", "SPILL_N", "FILL_W", "FILL_N"):
+            ins.imm = off[ins.imm]
+    return insns, words
+
+
+LDS_SPILL_WORDS = 80   # mw_kernels.hip kLdsSpillWords
 
 
 # --------------------------------------------------------------------------- encode

@@ -37,13 +37,13 @@ struct HostEnv {
     if (trace)
       for (int k = 0; k < n; ++k) trace[((u64)row + k) * ncand + idx] = v[k];
   }
-  void spill(u32 slot, const u32* v, int n) {
-    if (spillv->size() < (slot + 1) * 8) spillv->resize((slot + 1) * 8, 0u);
-    for (int k = 0; k < n; ++k) (*spillv)[slot * 8 + k] = v[k];
+  void spill(u32 off, const u32* v, int n) {   // spill area in words (mw_kernels.hip)
+    if (spillv->size() < off + 8) spillv->resize(off + 8, 0u);
+    for (int k = 0; k < n; ++k) (*spillv)[off + k] = v[k];
   }
-  void fill(u32 slot, u32* v, int n) {
-    if (spillv->size() < (slot + 1) * 8) spillv->resize((slot + 1) * 8, 0u);
-    for (int k = 0; k < 8; ++k) v[k] = k < n ? (*spillv)[slot * 8 + k] : 0u;
+  void fill(u32 off, u32* v, int n) {
+    if (spillv->size() < off + 8) spillv->resize(off + 8, 0u);
+    for (int k = 0; k < 8; ++k) v[k] = k < n ? (*spillv)[off + k] : 0u;
   }
   bool none(bool alive) { return !alive; }
 };
@@ -59,9 +59,9 @@ int mwh_eval(const mg_prog_desc* d, const uint32_t* leaves_soa, uint64_t seed, u
              uint32_t flags, uint32_t* verdict, uint32_t* trace) {
   int rc = mg_validate_desc(d);
   if (rc) return rc;
-  std::vector<u32> consts(d->nconst_words + 8, 0u);
+  std::vector<u32> consts(d->nconst_words + MW_KPAD, 0u);   // see mg_prog_load
   if (d->nconst_words) std::memcpy(consts.data(), d->consts, d->nconst_words * 4);
-  std::vector<u32> code(d->ncode_words + 8, 0u);  // padded: the interpreter prefetches past END
+  std::vector<u32> code(d->ncode_words + 32, 0u);  // padded: the interpreter reads up to 20 words past END
   std::memcpy(code.data(), d->code, d->ncode_words * 4);
   std::vector<u32> spill;
   for (size_t i = 0; i < ncand; ++i) {

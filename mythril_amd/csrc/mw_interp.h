@@ -31,6 +31,7 @@ typedef const __attribute__((address_space(4))) u32* kptr;
 typedef const u32* kptr;
 #endif
 #define MW_KPTR(p) ((kptr)(p))
+#define MW_KPAD 72   // minimum constant-region words (>= MW_NN + 8, see MW_FETCH_N)
 
 // W file: four vectors, F<k> holding limb k of every slot (elements 0..NW-1)
 // and limb k+4 (elements NW..2NW-1).  A 16-element vector read or written at a
@@ -60,19 +61,17 @@ typedef u32 u32xN __attribute__((ext_vector_type(32)));      // one half of the 
     }                                                                         \
   } while (0)
 
+// Both N halves are read and one is selected (a uniform branch here costs
+// ~10 scalar instructions of structurizer flow); the constant-pool load stays
+// behind a branch, so register operands issue no scalar load (which would wait
+// out the next instruction's prefetch).
 #define MW_FETCH_N(opnd, v)                                                   \
   do {                                                                        \
-    u32 _o = (opnd);                                                          \
+    const u32 _o = (opnd);                                                    \
+    const u32 _h = NH[_o & 31u], _f = NF[_o & 31u];                           \
+    v = (_o & 32u) ? _h : _f;                                                 \
     if (_o & MW_KBIT) v = cpool[_o & 0x7fffu];                                \
-    else if (_o & 32u) v = NH[_o & 31u];                                      \
-    else v = NF[_o & 31u];                                                    \
   } while (0)
-
-#if defined(__HIP_DEVICE_COMPILE__)
-#define MW_OPAQUE(v) asm volatile("" : "+v"(v))
-#else
-#define MW_OPAQUE(v) ((void)0)
-#endif
 
 #define MW_WRITE_W(d, r)                                                      \
   do {                                                                        \
@@ -113,14 +112,22 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
     // lgkmcnt(0) guarding this instruction's words must not also cover the
     // next instruction's load (the barrier stops the load being hoisted).
     asm volatile("" ::: "memory");
-    const u32 n0 = code[pc], n1 = code[pc + 1], n2 = code[pc + 2], n3 = code[pc + 3];
+    u32 n0 = code[pc], n1 = code[pc + 1], n2 = code[pc + 2], n3 = code[pc + 3];
     u32 x[8], y[8], r[8];
     u32 wk = 0;  // 1: write W[dst] = r, 2: write N[dst] = r[0]
     switch (op) {
-      case MW_CHECK: {
-        u32 v;
-        MW_FETCH_N(oa, v);
-        alive = alive && (v != 0);
+      case MW_CHECK: {  // runs of CHECKs as above
+        u32 fa = oa;
+        for (;;) {
+          u32 v;
+          MW_FETCH_N(fa, v);
+          alive = alive && (v != 0);
+          if ((n0 & 0xffu) != MW_CHECK) break;
+          fa = n1 >> 16;
+          pc += 4;
+          asm volatile("" ::: "memory");
+          n0 = code[pc]; n1 = code[pc + 1]; n2 = code[pc + 2]; n3 = code[pc + 3];
+        }
         // wave-uniform: stop at the next loop top (keeps one loop exit)
         if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
         break;
@@ -134,11 +141,38 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         break;
       }
       case MW_CHECK_IMPEQ: {  // a => (b = c): a congruence conjunct over narrow cells
-        u32 p, b, c;
-        MW_FETCH_N(oa, p);
-        MW_FETCH_N(ob, b);
-        MW_FETCH_N(oc, c);
-        alive = alive && (p == 0u || b == c);
+        // Runs of CHECK_IMPEQ (C3: 2 176 congruence conjuncts in a row) stay in
+        // this case, four instructions per scalar load (s_load_dwordx16),
+        // without the dispatch tree and write-back (~150 scalar and vector
+        // instructions per dispatch).  pc keeps indexing the next instruction.
+#define MW_IMPEQ_STEP(fa, fb, fc)                                             \
+  do {                                                                        \
+    u32 _p, _b, _c;                                                           \
+    MW_FETCH_N(fa, _p);                                                       \
+    MW_FETCH_N(fb, _b);                                                       \
+    MW_FETCH_N(fc, _c);                                                       \
+    alive = alive && (_p == 0u || _b == _c);                                  \
+  } while (0)
+        MW_IMPEQ_STEP(oa, ob & 0xffffu, oc);
+        while ((n0 & 0xffu) == MW_CHECK_IMPEQ) {
+          asm volatile("" ::: "memory");
+          u32 q[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) q[k] = code[pc + 4 + k];  // the four instructions after n
+          MW_IMPEQ_STEP(n1 >> 16, n2 & 0xffffu, n2 >> 16);
+          pc += 4;
+          if ((q[0] & 0xffu) != MW_CHECK_IMPEQ) { n0 = q[0]; n1 = q[1]; n2 = q[2]; n3 = q[3]; break; }
+          MW_IMPEQ_STEP(q[1] >> 16, q[2] & 0xffffu, q[2] >> 16);
+          pc += 4;
+          if ((q[4] & 0xffu) != MW_CHECK_IMPEQ) { n0 = q[4]; n1 = q[5]; n2 = q[6]; n3 = q[7]; break; }
+          MW_IMPEQ_STEP(q[5] >> 16, q[6] & 0xffffu, q[6] >> 16);
+          pc += 4;
+          if ((q[8] & 0xffu) != MW_CHECK_IMPEQ) { n0 = q[8]; n1 = q[9]; n2 = q[10]; n3 = q[11]; break; }
+          MW_IMPEQ_STEP(q[9] >> 16, q[10] & 0xffffu, q[10] >> 16);
+          pc += 4;
+          n0 = q[12]; n1 = q[13]; n2 = q[14]; n3 = q[15];
+        }
+#undef MW_IMPEQ_STEP
         if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
         break;
       }
@@ -467,30 +501,24 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         break;
       }
     }
-    // Single, UNCONDITIONAL write-back: every dispatch rewrites W[dst] and
-    // N[dst] (with their old values when the op writes elsewhere or nothing).
-    // A conditional indexed write leaves two versions of a file live at the
-    // loop latch (written / not written), and the register allocator resolves
-    // that with a whole-file copy per dispatch (32 v_mov_b64 for the N file:
-    // most of the interpreter's VALU work before this).  The asm barriers stop
-    // the compiler turning "write back the old value" into a branch again.
+    // Single, UNCONDITIONAL write-back: every dispatch writes r into one W
+    // slot and r[0] into one slot of each N half; an op that does not write
+    // that file writes its reserved scratch slot (MW_W_RESERVED, MW_N_RESERVED:
+    // the compiler never allocates them).  A conditional indexed write leaves
+    // two versions of a file live at the loop latch and the register
+    // allocator resolves that with a whole-file copy per dispatch (32
+    // v_mov_b64 for the N file); reading the old value back instead cost a
+    // read + select per element.  Here: 8 + 2 indexed moves, no reads.
     if (wk == 1 && w - 1u < 255u) canon(r, w);  // results of width 1..255: clear bits >= w
     {
-      const u32 dw = MW_WSLOT(dst);
-      const bool ww = wk == 1;
-      u32 v0 = ww ? r[0] : F0[dw], v1 = ww ? r[1] : F1[dw], v2 = ww ? r[2] : F2[dw], v3 = ww ? r[3] : F3[dw];
-      u32 v4 = ww ? r[4] : F0[dw + MW_NW], v5 = ww ? r[5] : F1[dw + MW_NW];
-      u32 v6 = ww ? r[6] : F2[dw + MW_NW], v7 = ww ? r[7] : F3[dw + MW_NW];
-      MW_OPAQUE(v0); MW_OPAQUE(v1); MW_OPAQUE(v2); MW_OPAQUE(v3);
-      MW_OPAQUE(v4); MW_OPAQUE(v5); MW_OPAQUE(v6); MW_OPAQUE(v7);
-      F0[dw] = v0; F1[dw] = v1; F2[dw] = v2; F3[dw] = v3;
-      F0[dw + MW_NW] = v4; F1[dw + MW_NW] = v5; F2[dw + MW_NW] = v6; F3[dw + MW_NW] = v7;
-      const u32 dn = dst & 31u;
-      const bool wlo = wk == 2 && (dst & 32u) == 0u, whi = wk == 2 && (dst & 32u) != 0u;
-      u32 lo = wlo ? r[0] : NF[dn], hi = whi ? r[0] : NH[dn];
-      MW_OPAQUE(lo); MW_OPAQUE(hi);
-      NF[dn] = lo;
-      NH[dn] = hi;
+      const u32 dw = wk == 1u ? MW_WSLOT(dst) : (u32)MW_W_RESERVED;
+      F0[dw] = r[0]; F1[dw] = r[1]; F2[dw] = r[2]; F3[dw] = r[3];
+      F0[dw + MW_NW] = r[4]; F1[dw + MW_NW] = r[5]; F2[dw + MW_NW] = r[6]; F3[dw + MW_NW] = r[7];
+      const bool wn = wk == 2u;
+      const u32 dlo = (wn && !(dst & 32u)) ? (dst & 31u) : (u32)MW_N_RESERVED;
+      const u32 dhi = (wn && (dst & 32u)) ? (dst & 31u) : (u32)MW_N_RESERVED;
+      NF[dlo] = r[0];
+      NH[dhi] = r[0];
     }
     w0 = n0;
     w1 = n1;

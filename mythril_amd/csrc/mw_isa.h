@@ -23,6 +23,10 @@
 
 #define MW_NW 8
 #define MW_NN 64
+// scratch slots the interpreter's write-back targets when an op writes the
+// other file or nothing (mw_interp.h); never allocated, rejected as operands
+#define MW_W_RESERVED (MW_NW - 1)
+#define MW_N_RESERVED 31   // in each 32-slot half: N slots 31 and 63
 #define MW_KBIT 0x8000u
 #define MW_LEAF_WORDS 8
 #define MW_POOL_ENTRY_WORDS 9

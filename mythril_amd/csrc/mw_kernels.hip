@@ -40,10 +40,13 @@ struct ProgDev {
 };
 
 constexpr int kBlock = 256;
-// LDS spill area: up to kLdsSpillSlots W-sized slots per lane, [slot][limb][lane]
-// (consecutive lanes -> consecutive banks).  10 slots = 80 KiB per 256-lane
-// block, so two blocks (8 waves) still fit a CU's 160 KiB.
-constexpr u32 kLdsSpillSlots = 10;
+// Spill area: n_spill words per lane (a W spill slot is 8 consecutive words, an
+// N slot one; the compiler puts the most-used words first).  Words
+// [0, kLdsSpillWords) live in LDS as [word][lane] (consecutive lanes ->
+// consecutive banks): 80 words = 80 KiB per 256-lane block, so two blocks (8
+// waves) still fit a CU's 160 KiB; the rest in the global spill buffer,
+// [word][thread].
+constexpr u32 kLdsSpillWords = 80;
 extern __shared__ u32 lds_spill[];
 
 struct SearchEnv {
@@ -58,19 +61,18 @@ struct SearchEnv {
     leaf_value(leaves + (u64)idx * MW_LEAF_WORDS, pool, seed, cand, out);
   }
   __device__ void store(u32, const u32*, int) {}
-  u32 nlds;  // spill slots [0, nlds) live in LDS, the rest in the global spill buffer
-  __device__ void spill(u32 slot, const u32* v, int n) {
-    if (slot < nlds) {
-      for (int k = 0; k < n; ++k) lds_spill[(slot * 8 + k) * kBlock + threadIdx.x] = v[k];
-    } else {
-      for (int k = 0; k < n; ++k) spillbuf[((u64)(slot - nlds) * 8 + k) * nthreads + gtid] = v[k];
+  u32 nlds;  // spill words [0, nlds) live in LDS, the rest in the global spill buffer
+  __device__ void spill(u32 off, const u32* v, int n) {
+    for (int k = 0; k < n; ++k) {
+      const u32 wd = off + (u32)k;   // uniform
+      if (wd < nlds) lds_spill[wd * kBlock + threadIdx.x] = v[k];
+      else spillbuf[(u64)(wd - nlds) * nthreads + gtid] = v[k];
     }
   }
-  __device__ void fill(u32 slot, u32* v, int n) {
-    if (slot < nlds) {
-      for (int k = 0; k < 8; ++k) v[k] = k < n ? lds_spill[(slot * 8 + k) * kBlock + threadIdx.x] : 0u;
-    } else {
-      for (int k = 0; k < 8; ++k) v[k] = k < n ? spillbuf[((u64)(slot - nlds) * 8 + k) * nthreads + gtid] : 0u;
+  __device__ void fill(u32 off, u32* v, int n) {
+    for (int k = 0; k < 8; ++k) {
+      const u32 wd = off + (u32)k;
+      v[k] = k >= n ? 0u : wd < nlds ? lds_spill[wd * kBlock + threadIdx.x] : spillbuf[(u64)(wd - nlds) * nthreads + gtid];
     }
   }
   __device__ bool none(bool alive) { return __ballot(alive) == 0ull; }
@@ -105,19 +107,18 @@ struct EvalEnv {
     if (trace)
       for (int k = 0; k < n; ++k) trace[((u64)row + k) * ncand + idx] = v[k];
   }
-  u32 nlds;  // spill slots [0, nlds) live in LDS, the rest in the global spill buffer
-  __device__ void spill(u32 slot, const u32* v, int n) {
-    if (slot < nlds) {
-      for (int k = 0; k < n; ++k) lds_spill[(slot * 8 + k) * kBlock + threadIdx.x] = v[k];
-    } else {
-      for (int k = 0; k < n; ++k) spillbuf[((u64)(slot - nlds) * 8 + k) * nthreads + gtid] = v[k];
+  u32 nlds;  // spill words [0, nlds) live in LDS, the rest in the global spill buffer
+  __device__ void spill(u32 off, const u32* v, int n) {
+    for (int k = 0; k < n; ++k) {
+      const u32 wd = off + (u32)k;   // uniform
+      if (wd < nlds) lds_spill[wd * kBlock + threadIdx.x] = v[k];
+      else spillbuf[(u64)(wd - nlds) * nthreads + gtid] = v[k];
     }
   }
-  __device__ void fill(u32 slot, u32* v, int n) {
-    if (slot < nlds) {
-      for (int k = 0; k < 8; ++k) v[k] = k < n ? lds_spill[(slot * 8 + k) * kBlock + threadIdx.x] : 0u;
-    } else {
-      for (int k = 0; k < 8; ++k) v[k] = k < n ? spillbuf[((u64)(slot - nlds) * 8 + k) * nthreads + gtid] : 0u;
+  __device__ void fill(u32 off, u32* v, int n) {
+    for (int k = 0; k < 8; ++k) {
+      const u32 wd = off + (u32)k;
+      v[k] = k >= n ? 0u : wd < nlds ? lds_spill[wd * kBlock + threadIdx.x] : spillbuf[(u64)(wd - nlds) * nthreads + gtid];
     }
   }
   __device__ bool none(bool) { return false; }  // eval: never exit early
@@ -418,8 +419,8 @@ int mg_init(int device, mg_ctx** out) {
     delete c;
     return fail(MG_E_HIP, "context setup failed");
   }
-  // allow the LDS spill area (up to kLdsSpillSlots x 8 KiB) beyond the 64 KiB default
-  const int lds_max = (int)(kLdsSpillSlots * 8 * kBlock * sizeof(u32));
+  // allow the LDS spill area (up to kLdsSpillWords x 1 KiB) beyond the 64 KiB default
+  const int lds_max = (int)(kLdsSpillWords * kBlock * sizeof(u32));
   if (hipFuncSetAttribute((const void*)mw_search_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
           hipSuccess ||
       hipFuncSetAttribute((const void*)mw_eval_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
@@ -453,7 +454,9 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
-  const size_t nc = d->ncode_words, nk = d->nconst_words + 8, nl = d->nleaves * MW_LEAF_WORDS + 8,
+  // constants padded to >= MW_KPAD words: the interpreter's branch-free narrow
+  // operand fetch reads cpool[slot] (slot < 64) before selecting the register
+  const size_t nc = d->ncode_words, nk = (d->nconst_words + 8 > MW_KPAD ? d->nconst_words + 8 : MW_KPAD), nl = d->nleaves * MW_LEAF_WORDS + 8,
                np = d->npool_words + 8;
   const size_t total = nc + nk + nl + np;
   mg_prog* p = new mg_prog();
@@ -596,9 +599,9 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
     gx = std::max<u64>(1, (u64)c->ncu * 8 / ni);
     gx = std::min<u64>(gx, nchunks);
     const u64 nthreads = gx * ni * kBlock;
-    nlds = std::min(max_spill, kLdsSpillSlots);
+    nlds = std::min(max_spill, kLdsSpillWords);
     const u32 nglob = max_spill - nlds;
-    rc = ensure_spill(c, std::max<size_t>(4, (size_t)nglob * 8 * nthreads * sizeof(u32)));
+    rc = ensure_spill(c, std::max<size_t>(4, (size_t)nglob * nthreads * sizeof(u32)));
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(c->d_progs, hp.data(), ni * sizeof(ProgDev), hipMemcpyHostToDevice, c->stream));
   }
@@ -607,7 +610,7 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   HIPCHK(hipMemsetAsync(c->d_counter, 0, 2 * sizeof(u64), c->stream));
   HIPCHK(hipEventRecord(c->e0, c->stream));
   if (ni) {
-    hipLaunchKernelGGL(mw_search_kernel, dim3((u32)gx, (u32)ni), dim3(kBlock), (size_t)nlds * 8 * kBlock * 4,
+    hipLaunchKernelGGL(mw_search_kernel, dim3((u32)gx, (u32)ni), dim3(kBlock), (size_t)nlds * kBlock * 4,
                        c->stream, c->d_progs, seed, begin, count, flags, c->d_min, c->d_counter, c->d_spill, nlds);
     HIPCHK(hipGetLastError());
   }
@@ -646,8 +649,8 @@ static int eval_common(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, 
   const u64 nchunks = (ncand + kBlock - 1) / kBlock;
   const u64 gx = std::min<u64>(nchunks, (u64)c->ncu * 8);
   const u64 nthreads = gx * kBlock;
-  const u32 nlds = std::min(p->dev.n_spill, kLdsSpillSlots);
-  int rc = ensure_spill(c, std::max<size_t>(4, (size_t)(p->dev.n_spill - nlds) * 8 * nthreads * sizeof(u32)));
+  const u32 nlds = std::min(p->dev.n_spill, kLdsSpillWords);
+  int rc = ensure_spill(c, std::max<size_t>(4, (size_t)(p->dev.n_spill - nlds) * nthreads * sizeof(u32)));
   if (rc) return rc;
   u32 *d_in = nullptr, *d_v = nullptr, *d_t = nullptr;
   const size_t nin = leaves_soa ? (size_t)p->desc.n_input_rows * ncand : 0;
@@ -664,7 +667,7 @@ static int eval_common(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, 
     cleanup(); return fail(MG_E_HIP, "eval input copy");
   }
   if (ntr) hipMemsetAsync(d_t, 0, ntr * 4, c->stream);
-  hipLaunchKernelGGL(mw_eval_kernel, dim3((u32)gx), dim3(kBlock), (size_t)nlds * 8 * kBlock * 4, c->stream,
+  hipLaunchKernelGGL(mw_eval_kernel, dim3((u32)gx), dim3(kBlock), (size_t)nlds * kBlock * 4, c->stream,
                      p->dev, (const u32*)d_in, (u64)ncand, seed, begin, d_v, d_t, c->d_spill, nlds);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, ncand * 4, hipMemcpyDeviceToHost, c->stream);

@@ -73,15 +73,18 @@ bool op_shape(u32 op, OpShape& s) {
   }
 }
 
+bool w_slot_ok(u32 f) { return f < MW_NW && f != MW_W_RESERVED; }
+bool n_slot_ok(u32 f) { return f < MW_NN && (f & 31u) != MW_N_RESERVED; }
+
 bool check_operand(int kind, u32 f, size_t nconst) {
   if (kind == 0) return true;
-  if (kind == 3) return f < MW_NW;
-  if (kind == 4) return f < MW_NN;
+  if (kind == 3) return w_slot_ok(f);
+  if (kind == 4) return n_slot_ok(f);
   if (f & MW_KBIT) {
     size_t o = f & 0x7fffu;
     return o + (kind == 1 ? 8 : 1) <= nconst;
   }
-  return kind == 1 ? f < MW_NW : f < MW_NN;
+  return kind == 1 ? w_slot_ok(f) : n_slot_ok(f);
 }
 
 }  // namespace
@@ -130,7 +133,10 @@ int mg_validate_desc(const mg_prog_desc* d) {
       case MW_STORE_N:
         if ((u64)I[3] + 1 > d->n_trace_rows) return fail(MG_E_PROG, "trace row out of range");
         break;
-      case MW_SPILL_W: case MW_FILL_W: case MW_SPILL_N: case MW_FILL_N:
+      case MW_SPILL_W: case MW_FILL_W:   // imm = word offset of an 8-word slot in the spill area
+        if ((u64)I[3] + 8 > d->n_spill) return fail(MG_E_PROG, "spill slot out of range");
+        break;
+      case MW_SPILL_N: case MW_FILL_N:
         if (I[3] >= d->n_spill) return fail(MG_E_PROG, "spill slot out of range");
         break;
       case MW_W_SHLI: case MW_W_LSHRI: case MW_N_EXTRACTW: case MW_W_INSN:

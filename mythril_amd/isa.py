@@ -3,6 +3,8 @@ from __future__ import annotations
 
 NW = 8           # W file slots (8 x u32 limbs each)
 NN = 64          # N file slots (1 x u32 each)
+W_RESERVED = NW - 1   # interpreter write-back scratch slots, never allocated (mw_isa.h)
+N_RESERVED = 31       # N slots 31 and 63
 KBIT = 0x8000
 LEAF_WORDS = 8
 POOL_ENTRY_WORDS = 9

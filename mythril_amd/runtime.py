@@ -18,7 +18,9 @@ import numpy as np
 
 from .compiler import Program
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmythril_witness.so")
+# MYTHRIL_AMD_LIB: load another build of the library (A/B measurements)
+LIB_PATH = os.environ.get("MYTHRIL_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                             "libmythril_witness.so")
 MG_NONE = (1 << 64) - 1
 
 

@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-jit", action="store_true")
     ap.add_argument("--warm", action="store_true", help="only compile the specialised kernels into build/jit (CPU)")
+    ap.add_argument("--only", default=None, help="comma-separated config names (default: all)")
     a = ap.parse_args()
     import bench
     from mythril_amd import isa, jit
@@ -77,6 +78,8 @@ def main():
     peak = bench.THEORETICAL_PEAK
     lines = []
     for name, files, log2, together in CONFIGS:
+        if a.only and name not in a.only.split(","):
+            continue
         for gfiles, g in _groups(files, together):
             dps = [dev.load(q.program) for q in g]
             ops = sum(q.ops_per_eval for q in g)
