@@ -142,7 +142,7 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
       }
       case MW_CHECK_IMPEQ: {  // a => (b = c): a congruence conjunct over narrow cells
         // Runs of CHECK_IMPEQ (C3: 2 176 congruence conjuncts in a row) stay in
-        // this case, four instructions per scalar load (s_load_dwordx16),
+        // this case, two instructions per scalar load (s_load_dwordx8),
         // without the dispatch tree and write-back (~150 scalar and vector
         // instructions per dispatch).  pc keeps indexing the next instruction.
 #define MW_IMPEQ_STEP(fa, fb, fc)                                             \
@@ -156,21 +156,15 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         MW_IMPEQ_STEP(oa, ob & 0xffffu, oc);
         while ((n0 & 0xffu) == MW_CHECK_IMPEQ) {
           asm volatile("" ::: "memory");
-          u32 q[16];
+          u32 q[8];
 #pragma unroll
-          for (int k = 0; k < 16; ++k) q[k] = code[pc + 4 + k];  // the four instructions after n
+          for (int k = 0; k < 8; ++k) q[k] = code[pc + 4 + k];  // the two instructions after n
           MW_IMPEQ_STEP(n1 >> 16, n2 & 0xffffu, n2 >> 16);
           pc += 4;
           if ((q[0] & 0xffu) != MW_CHECK_IMPEQ) { n0 = q[0]; n1 = q[1]; n2 = q[2]; n3 = q[3]; break; }
           MW_IMPEQ_STEP(q[1] >> 16, q[2] & 0xffffu, q[2] >> 16);
           pc += 4;
-          if ((q[4] & 0xffu) != MW_CHECK_IMPEQ) { n0 = q[4]; n1 = q[5]; n2 = q[6]; n3 = q[7]; break; }
-          MW_IMPEQ_STEP(q[5] >> 16, q[6] & 0xffffu, q[6] >> 16);
-          pc += 4;
-          if ((q[8] & 0xffu) != MW_CHECK_IMPEQ) { n0 = q[8]; n1 = q[9]; n2 = q[10]; n3 = q[11]; break; }
-          MW_IMPEQ_STEP(q[9] >> 16, q[10] & 0xffffu, q[10] >> 16);
-          pc += 4;
-          n0 = q[12]; n1 = q[13]; n2 = q[14]; n3 = q[15];
+          n0 = q[4]; n1 = q[5]; n2 = q[6]; n3 = q[7];
         }
 #undef MW_IMPEQ_STEP
         if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);

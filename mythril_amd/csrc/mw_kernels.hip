@@ -36,7 +36,7 @@ struct ProgDev {
   const u32* leaves;
   const u32* pool;
   u32 n_spill;
-  u32 pad;
+  u32 npool;   // pool words (LDS staging, mw_search_kernel)
 };
 
 constexpr int kBlock = 256;
@@ -49,6 +49,45 @@ constexpr int kBlock = 256;
 constexpr u32 kLdsSpillWords = 80;
 extern __shared__ u32 lds_spill[];
 
+typedef const __attribute__((address_space(3))) u32* lptr;
+
+// leaf_value (mw_leaf.h) with the pool staged in LDS: the per-lane pool gather
+// is a ds_read (~100 cycles) instead of a global load (~2 000): a leaf cost
+// ~2 800 cycles per wave with the pool in HBM (tools/c3_ablate.py).
+__device__ __forceinline__ void leaf_value_lds(const u32* __restrict__ leaf_, lptr pool, u64 seed, u64 cand,
+                                               u32 out[8]) {
+  const __attribute__((address_space(4))) u32* leaf = (const __attribute__((address_space(4))) u32*)leaf_;
+  const u32 w = leaf[MW_LEAF_WIDTH], id = leaf[MW_LEAF_ID], kind = leaf[MW_LEAF_KIND];
+  if (kind >= 1u && kind <= 3u) {
+    const u32 bits = leaf[MW_LEAF_BITS];
+    u32 digit;
+    if (kind == 3u) {
+      const u32 sh = leaf[MW_LEAF_SHIFT], st = leaf[MW_LEAF_STRIDE];
+      digit = 0;
+      for (u32 b = 0; b < bits; ++b) digit |= (u32)((cand >> (sh + b * st)) & 1u) << b;
+    } else {
+      const u64 src = kind == 1u ? (cand >> leaf[MW_LEAF_SHIFT]) : fmix64(cand ^ ((u64)id * 0x9E3779B97F4A7C15ull));
+      digit = (u32)src & ((bits >= 32) ? 0xffffffffu : ((1u << bits) - 1u));
+    }
+    lptr e = pool + leaf[MW_LEAF_POOL] + digit * MW_POOL_ENTRY_WORDS;
+    if (e[0] & 1u) {
+      random_leaf(id, w, seed, cand, out);
+    } else if (w <= 32u) {
+      out[0] = e[1];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) out[k] = 0u;
+      canon(out, w);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) out[k] = e[1 + k];
+      canon(out, w);
+    }
+  } else {
+    random_leaf(id, w, seed, cand, out);
+  }
+}
+
+template <bool POOL_LDS>
 struct SearchEnv {
   const u32* __restrict__ leaves;
   const u32* __restrict__ pool;
@@ -58,7 +97,10 @@ struct SearchEnv {
   u64 nthreads;
   u64 gtid;
   __device__ void leaf(u32 idx, u32 out[8]) {
-    leaf_value(leaves + (u64)idx * MW_LEAF_WORDS, pool, seed, cand, out);
+    if (POOL_LDS)
+      leaf_value_lds(leaves + (u64)idx * MW_LEAF_WORDS, (lptr)(lds_spill + nlds * kBlock), seed, cand, out);
+    else
+      leaf_value(leaves + (u64)idx * MW_LEAF_WORDS, pool, seed, cand, out);
   }
   __device__ void store(u32, const u32*, int) {}
   u32 nlds;  // spill words [0, nlds) live in LDS, the rest in the global spill buffer
@@ -127,12 +169,20 @@ struct EvalEnv {
 
 }  // namespace
 
+// POOL_LDS: the program's pool is copied into LDS after the spill words once
+// per block (the launch sizes LDS for the largest pool of the launch).
+template <bool POOL_LDS>
 __global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __restrict__ progs, u64 seed,
                                                            u64 begin, u64 count, u32 flags,
                                                            u64* __restrict__ out_min,
                                                            u64* __restrict__ counter,
                                                            u32* __restrict__ spillbuf, u32 nlds) {
   const ProgDev P = progs[blockIdx.y];
+  if (POOL_LDS) {
+    u32* dst = lds_spill + nlds * kBlock;
+    for (u32 i = threadIdx.x; i < P.npool; i += kBlock) dst[i] = P.pool[i];
+    __syncthreads();
+  }
   const u64 nchunks = (count + kBlock - 1) / kBlock;
   const u64 end = begin + count;
   const u64 nthreads = (u64)gridDim.x * gridDim.y * kBlock;
@@ -147,7 +197,7 @@ __global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __r
     }
     const u64 cand = base + threadIdx.x;
     const bool valid = cand < end;
-    SearchEnv env{P.leaves, P.pool, seed, cand, spillbuf, nthreads, gtid, nlds};
+    SearchEnv<POOL_LDS> env{P.leaves, P.pool, seed, cand, spillbuf, nthreads, gtid, nlds};
     const bool ok = mw_run(P.code, P.consts, env, valid, flags);
     const u64 hit = __ballot(ok);
     if (hit) {
@@ -421,7 +471,9 @@ int mg_init(int device, mg_ctx** out) {
   }
   // allow the LDS spill area (up to kLdsSpillWords x 1 KiB) beyond the 64 KiB default
   const int lds_max = (int)(kLdsSpillWords * kBlock * sizeof(u32));
-  if (hipFuncSetAttribute((const void*)mw_search_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
+  if (hipFuncSetAttribute((const void*)mw_search_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
+          hipSuccess ||
+      hipFuncSetAttribute((const void*)mw_search_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
           hipSuccess ||
       hipFuncSetAttribute((const void*)mw_eval_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
           hipSuccess) {
@@ -483,6 +535,7 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
   p->dev.leaves = p->d_buf + nc + nk;
   p->dev.pool = p->d_buf + nc + nk + nl;
   p->dev.n_spill = d->n_spill;
+  p->dev.npool = (u32)d->npool_words;
   // the desc's host pointers are not retained
   p->desc.code = nullptr;
   p->desc.consts = nullptr;
@@ -586,9 +639,11 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
     ops += progs[i]->ops_per_eval;
   }
   std::vector<ProgDev> hp;
+  u32 max_pool = 0;
   for (size_t i : interp) {
     hp.push_back(progs[i]->dev);
     max_spill = std::max(max_spill, progs[i]->dev.n_spill);
+    max_pool = std::max(max_pool, progs[i]->dev.npool);
   }
   const u64 nchunks = (count + kBlock - 1) / kBlock;
   const size_t ni = interp.size();
@@ -610,8 +665,19 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   HIPCHK(hipMemsetAsync(c->d_counter, 0, 2 * sizeof(u64), c->stream));
   HIPCHK(hipEventRecord(c->e0, c->stream));
   if (ni) {
-    hipLaunchKernelGGL(mw_search_kernel, dim3((u32)gx, (u32)ni), dim3(kBlock), (size_t)nlds * kBlock * 4,
-                       c->stream, c->d_progs, seed, begin, count, flags, c->d_min, c->d_counter, c->d_spill, nlds);
+    // stage the pools in LDS when they fit beside the spill words (80 KiB per
+    // block keeps two blocks per CU)
+    const size_t spill_bytes = (size_t)nlds * kBlock * 4, pool_bytes = (size_t)max_pool * 4;
+#ifdef MW_NO_POOL_LDS   // A/B builds only
+    if (false)
+#else
+    if (max_pool && spill_bytes + pool_bytes <= (size_t)kLdsSpillWords * kBlock * 4)
+#endif
+      hipLaunchKernelGGL(mw_search_kernel<true>, dim3((u32)gx, (u32)ni), dim3(kBlock), spill_bytes + pool_bytes,
+                         c->stream, c->d_progs, seed, begin, count, flags, c->d_min, c->d_counter, c->d_spill, nlds);
+    else
+      hipLaunchKernelGGL(mw_search_kernel<false>, dim3((u32)gx, (u32)ni), dim3(kBlock), spill_bytes,
+                         c->stream, c->d_progs, seed, begin, count, flags, c->d_min, c->d_counter, c->d_spill, nlds);
     HIPCHK(hipGetLastError());
   }
   for (size_t j = 0; j < special.size(); ++j) {
