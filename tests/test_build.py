@@ -79,3 +79,47 @@ def test_validation_accepts_compiled_and_rejects_malformed():
         q.leaves = q.leaves.copy()
         f(q)
         assert _validate(q) != 0
+
+
+def test_reserved_write_back_slots():
+    """W7 and N31/N63 are the interpreter's write-back scratch slots: the
+    allocator never hands them out and the validator rejects them."""
+    c = Ctx()
+    # enough live values to use every allocatable slot of both files
+    ws = [c.var(f"w{i}", 256) for i in range(20)]
+    ns = [c.var(f"n{i}", 8) for i in range(90)]
+    conj = [c.app("bvult", c.app("bvadd", *ws), c.app("bvxor", *ws)),
+            c.app("=", c.app("bvadd", *ns), c.app("bvxor", *ns))]
+    p = compile_program(conj)
+    assert _validate(p) == 0
+    from mythril_amd.isa import SHAPES
+    inv = {v: k for k, v in isa.OPCODES.items()}
+    used_w, used_n = set(), set()
+    for w0, w1, w2, _ in p.code.reshape(-1, 4):
+        op = inv[int(w0) & 0xFF]
+        dcls, srcs = SHAPES[op]
+        fields = [int(w1) & 0xFFFF, int(w1) >> 16, int(w2) & 0xFFFF, int(w2) >> 16]
+        for cls, f in zip([dcls] + srcs, fields):
+            if cls and not f & isa.KBIT:
+                (used_w if cls == "W" else used_n).add(f)
+    assert isa.W_RESERVED not in used_w and len(used_w) == isa.NW - 1
+    assert isa.N_RESERVED not in used_n and 63 not in used_n and len(used_n) > 32
+    for bad_dst in (isa.W_RESERVED,):
+        q = compile_program([c.app("bvult", c.var("a", 256), c.const(5, 256))])
+        q.code = q.code.copy()
+        k = next(i for i in range(0, q.code.size, 4) if inv[int(q.code[i]) & 0xFF] == "LEAF_W")
+        q.code[k + 1] = (int(q.code[k + 1]) & 0xFFFF0000) | bad_dst
+        assert _validate(q) != 0
+
+
+def test_spill_words_hottest_first():
+    """Spill slots are word offsets (W: 8 words, N: 1), most-accessed first, so
+    the LDS-resident prefix of the spill area holds the hot ones."""
+    from mythril_amd.compiler import _layout_spills, MInsn
+    insns = ([MInsn("SPILL_W", 0, None, [], imm=0)] + [MInsn("FILL_N", 0, None, [], imm=1)] * 5
+             + [MInsn("SPILL_N", 0, None, [], imm=2)] + [MInsn("FILL_W", 0, None, [], imm=0)] * 3)
+    out, words = _layout_spills([MInsn(i.op, 0, None, [], imm=i.imm) for i in insns], ["W", "N", "N"])
+    assert words == 10
+    offs = {(i.op, i.imm) for i in out}
+    # N slot 1 (6 accesses / 1 word) first, then N slot 2 (1/1), then W slot 0 (4/8)
+    assert ("FILL_N", 0) in offs and ("SPILL_N", 1) in offs and ("SPILL_W", 2) in offs and ("FILL_W", 2) in offs
