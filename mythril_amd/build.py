@@ -21,7 +21,7 @@ ARCH = os.environ.get("MW_OFFLOAD_ARCH", "gfx950")
 
 DEVICE_SRCS = ["mw_kernels.hip", "mw_validate.cpp"]
 HOST_SRCS = ["mw_host_emu.cpp", "mw_validate.cpp"]
-HEADERS = ["mw_isa.h", "mw_alu.h", "mw_interp.h", "mw_leaf.h", "mw_keccak.h"]
+HEADERS = ["mw_isa.h", "mw_prog.h", "mw_alu.h", "mw_interp.h", "mw_leaf.h", "mw_keccak.h"]
 
 
 def _hipcc() -> str:

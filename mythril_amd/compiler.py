@@ -72,6 +72,7 @@ class MInsn:
     srcs: List[object] = field(default_factory=list)
     imm: int = 0
     remat: bool = False   # recomputation of a term from an earlier conjunct (jit.py fences its inputs)
+    chain: bool = False   # W_CDINS whose result's only use is the next W_CDINS's acc (MW_FLAG_CHAIN)
 
 
 def cls_of(width: int) -> str:
@@ -627,6 +628,11 @@ def _fuse_checks(insns: List[MInsn]) -> List[MInsn]:
             continue
         out.append(ins)
         i += 1
+    uses = _uses(out)
+    for a, b in zip(out, out[1:]):
+        if (a.op == "W_CDINS" and b.op == "W_CDINS" and a.dst is not None and uses.get(a.dst.id, 0) == 1
+                and _is(b.srcs[0], a)):
+            a.chain = True
     return out
 
 
@@ -777,7 +783,7 @@ def _allocate(insns: List[MInsn]):
             else:
                 free[d.cls].append(slot)  # dead result (e.g. traced only) - slot reused
             dst = ("phys", slot)
-        out.append(MInsn(ins.op, ins.width, dst, phys_srcs, ins.imm))
+        out.append(MInsn(ins.op, ins.width, dst, phys_srcs, ins.imm, chain=ins.chain))
     return _layout_spills(out, slot_cls)
 
 
@@ -943,7 +949,7 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
     trace_map: Dict[int, Tuple[int, str]] = {}
     rows = 0
     code: List[int] = []
-    for ins in insns:
+    for k, ins in enumerate(insns):
         fields = []
         for s in ins.srcs:
             if isinstance(s, Const):
@@ -960,7 +966,11 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
             imm = rows
             rows += 8 if cls == "W" else 1
         dst = ins.dst[1] if ins.dst is not None else 0
-        code.extend(isa.encode(ins.op, ins.width, dst, fields[0], fields[1], fields[2], imm))
+        # the chain holds only if the consumer still follows directly (no FILL/SPILL/STORE between)
+        nxt = insns[k + 1] if k + 1 < len(insns) else None
+        flags = isa.FLAG_CHAIN if (ins.chain and nxt is not None and nxt.op == "W_CDINS" and nxt.srcs
+                                   and nxt.srcs[0] == ins.dst) else 0
+        code.extend(isa.encode(ins.op, ins.width, dst, fields[0], fields[1], fields[2], imm, flags))
     if len(consts) > 0x7FFF:
         raise Unsupported("constant pool overflow")
 

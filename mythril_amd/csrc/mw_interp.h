@@ -17,6 +17,7 @@
 #pragma once
 #include "mw_alu.h"
 #include "mw_isa.h"
+#include "mw_prog.h"
 
 namespace mw {
 
@@ -105,9 +106,10 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
   for (u32 pc = 4;; pc += 4) {
     const u32 op = w0 & 0xffu;
     if (op == MW_END || stop) break;
-    const u32 w = w0 >> 16;
-    const u32 dst = w1 & 0xffffu, oa = w1 >> 16, ob = w2 & 0xffffu, oc = w2 >> 16;
-    const u32 imm = w3;
+    u32 w = w0 >> 16;   // w, dst, imm: a W_CDINS chain leaves its last instruction's here
+    u32 dst = w1 & 0xffffu;
+    const u32 oa = w1 >> 16, ob = w2 & 0xffffu, oc = w2 >> 16;
+    u32 imm = w3;
     // decode above, prefetch below: scalar loads return out of order, so the
     // lgkmcnt(0) guarding this instruction's words must not also cover the
     // next instruction's load (the barrier stops the load being hoisted).
@@ -180,20 +182,42 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         break;
       }
       case MW_W_CDINS: {  // acc | (ite(K[c] <s size, leaf, 0) << off)
+        // A calldata word is built by a chain of these (32 per ABI word: 22 %
+        // of the LASER corpus's instructions).  MW_FLAG_CHAIN (set by the
+        // compiler, checked by the validator) says the next instruction is a
+        // W_CDINS whose only input from here is this result as its acc: the
+        // chain runs inside this case with the word kept in registers, and the
+        // last result goes through the common write-back (w, dst, imm are the
+        // last instruction's).
+        u32 fb = ob, fc = oc, fl = w0;
         MW_FETCH_W(oa, x);
-        MW_FETCH_W(ob, y);   // size
-        u32 k[8];
-        MW_FETCH_W(oc, k);   // the constant index
-        k[7] ^= 0x80000000u;
-        y[7] ^= 0x80000000u;
-        const bool in_range = ult8(k, y);   // signed 256-bit k < size
-        env.leaf(imm & 0xffffu, r);
-        u32 t[8];
-        zero8(t);
-        t[0] = in_range ? r[0] : 0u;
-        shl8(t, imm >> 16, r);
+        for (;;) {
+          MW_FETCH_W(fb, y);   // size
+          u32 k[8];
+          MW_FETCH_W(fc, k);   // the constant index
+          k[7] ^= 0x80000000u;
+          y[7] ^= 0x80000000u;
+          const bool in_range = ult8(k, y);   // signed 256-bit k < size
+          env.leaf(imm & 0xffffu, r);
+          u32 t[8];
+          zero8(t);
+          t[0] = in_range ? r[0] : 0u;
+          shl8(t, imm >> 16, r);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) r[q] |= x[q];
+          for (int q = 0; q < 8; ++q) r[q] |= x[q];
+          if (!(fl & (MW_FLAG_CHAIN << 8))) break;
+          if (w - 1u < 255u) canon(r, w);
+          copy8(x, r);
+          fl = n0;
+          w = n0 >> 16;
+          dst = n1 & 0xffffu;
+          fb = n2 & 0xffffu;
+          fc = n2 >> 16;
+          imm = n3;
+          pc += 4;
+          asm volatile("" ::: "memory");
+          n0 = code[pc]; n1 = code[pc + 1]; n2 = code[pc + 2]; n3 = code[pc + 3];
+        }
         wk = 1;
         break;
       }

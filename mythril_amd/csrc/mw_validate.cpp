@@ -10,6 +10,7 @@
 
 #include "../../include/mythril_witness.h"
 #include "mw_isa.h"
+#include "mw_prog.h"
 
 typedef uint32_t u32;
 typedef uint64_t u64;
@@ -112,6 +113,13 @@ int mg_validate_desc(const mg_prog_desc* d) {
     if (!op_shape(op, s)) return fail(MG_E_PROG, "unknown opcode " + std::to_string(op) + " at " + std::to_string(i));
     if (op == MW_END && i != n - 1) return fail(MG_E_PROG, "END before the last instruction");
     const u32 dst = I[1] & 0xffffu, a = I[1] >> 16, b = I[2] & 0xffffu, c = I[2] >> 16;
+    const u32 iflags = (I[0] >> 8) & 0xffu;
+    if (iflags) {   // only a W_CDINS chain link, followed by the W_CDINS that reads it as its acc
+      const u32* N = I + 4;
+      if (iflags != MW_FLAG_CHAIN || op != MW_W_CDINS || i + 1 >= n || (N[0] & 0xffu) != MW_W_CDINS ||
+          (N[1] >> 16) != dst)
+        return fail(MG_E_PROG, "bad instruction flags at " + std::to_string(i));
+    }
     if (!check_operand(s.dst, dst, d->nconst_words) || !check_operand(s.a, a, d->nconst_words) ||
         !check_operand(s.b, b, d->nconst_words) || !check_operand(s.c, c, d->nconst_words))
       return fail(MG_E_PROG, "operand out of range at instruction " + std::to_string(i));

@@ -63,9 +63,14 @@ FLAG_EARLY_EXIT = 1
 FLAG_STOP_AFTER_HIT = 2
 
 
-def encode(op: str, width: int = 0, dst: int = 0, a: int = 0, b: int = 0, c: int = 0, imm: int = 0):
+# instruction flags, w0 bits [15:8] (csrc/mw_prog.h)
+FLAG_CHAIN = 1   # W_CDINS: result consumed only by the next W_CDINS's acc (kept in registers)
+
+
+def encode(op: str, width: int = 0, dst: int = 0, a: int = 0, b: int = 0, c: int = 0, imm: int = 0,
+           flags: int = 0):
     code = OPCODES[op]
-    return [(code & 0xFF) | ((width & 0xFFFF) << 16),
+    return [(code & 0xFF) | ((flags & 0xFF) << 8) | ((width & 0xFFFF) << 16),
             (dst & 0xFFFF) | ((a & 0xFFFF) << 16),
             (b & 0xFFFF) | ((c & 0xFFFF) << 16),
             imm & 0xFFFFFFFF]
