@@ -32,6 +32,22 @@ typedef const __attribute__((address_space(4))) u32* kptr;
 typedef const u32* kptr;
 #endif
 #define MW_KPTR(p) ((kptr)(p))
+typedef u32 u32x4v __attribute__((ext_vector_type(4), aligned(4)));   // SMEM needs only dword alignment
+typedef u32 u32x8v __attribute__((ext_vector_type(8), aligned(4)));
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) u32x4v* kptr4;
+typedef const __attribute__((address_space(4))) u32x8v* kptr8;
+#else
+typedef const u32x4v* kptr4;
+typedef const u32x8v* kptr8;
+#endif
+// one instruction (4 words at a 16-byte-aligned word index) as ONE scalar load:
+// with pc advanced on several paths, element-wise reads became four s_load_dword
+#define MW_LOAD_INSN(at, a, b, c, d)                                          \
+  do {                                                                        \
+    const u32x4v _v = *(kptr4)(code + (at));                                  \
+    a = _v.x; b = _v.y; c = _v.z; d = _v.w;                                   \
+  } while (0)
 #define MW_KPAD 72   // minimum constant-region words (>= MW_NN + 8, see MW_FETCH_N)
 
 // W file: four vectors, F<k> holding limb k of every slot (elements 0..NW-1)
@@ -114,7 +130,8 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
     // lgkmcnt(0) guarding this instruction's words must not also cover the
     // next instruction's load (the barrier stops the load being hoisted).
     asm volatile("" ::: "memory");
-    u32 n0 = code[pc], n1 = code[pc + 1], n2 = code[pc + 2], n3 = code[pc + 3];
+    u32 n0, n1, n2, n3;
+    MW_LOAD_INSN(pc, n0, n1, n2, n3);
     u32 x[8], y[8], r[8];
     u32 wk = 0;  // 1: write W[dst] = r, 2: write N[dst] = r[0]
     switch (op) {
@@ -128,7 +145,7 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
           fa = n1 >> 16;
           pc += 4;
           asm volatile("" ::: "memory");
-          n0 = code[pc]; n1 = code[pc + 1]; n2 = code[pc + 2]; n3 = code[pc + 3];
+          MW_LOAD_INSN(pc, n0, n1, n2, n3);
         }
         // wave-uniform: stop at the next loop top (keeps one loop exit)
         if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
@@ -158,9 +175,7 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         MW_IMPEQ_STEP(oa, ob & 0xffffu, oc);
         while ((n0 & 0xffu) == MW_CHECK_IMPEQ) {
           asm volatile("" ::: "memory");
-          u32 q[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) q[k] = code[pc + 4 + k];  // the two instructions after n
+          const u32x8v q = *(kptr8)(code + pc + 4);  // the two instructions after n
           MW_IMPEQ_STEP(n1 >> 16, n2 & 0xffffu, n2 >> 16);
           pc += 4;
           if ((q[0] & 0xffu) != MW_CHECK_IMPEQ) { n0 = q[0]; n1 = q[1]; n2 = q[2]; n3 = q[3]; break; }
@@ -216,7 +231,7 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
           imm = n3;
           pc += 4;
           asm volatile("" ::: "memory");
-          n0 = code[pc]; n1 = code[pc + 1]; n2 = code[pc + 2]; n3 = code[pc + 3];
+          MW_LOAD_INSN(pc, n0, n1, n2, n3);
         }
         wk = 1;
         break;
