@@ -965,7 +965,8 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
             trace_map[nid] = (rows, cls)
             imm = rows
             rows += 8 if cls == "W" else 1
-        dst = ins.dst[1] if ins.dst is not None else 0
+        dcls = isa.SHAPES[ins.op][0] if ins.dst is not None else None
+        dst = isa.encode_dst(dcls, ins.dst[1] if ins.dst is not None else 0)
         # the chain holds only if the consumer still follows directly (no FILL/SPILL/STORE between)
         nxt = insns[k + 1] if k + 1 < len(insns) else None
         flags = isa.FLAG_CHAIN if (ins.chain and nxt is not None and nxt.op == "W_CDINS" and nxt.srcs

@@ -132,8 +132,8 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
     asm volatile("" ::: "memory");
     u32 n0, n1, n2, n3;
     MW_LOAD_INSN(pc, n0, n1, n2, n3);
-    u32 x[8], y[8], r[8];
-    u32 wk = 0;  // 1: write W[dst] = r, 2: write N[dst] = r[0]
+    u32 x[8], y[8];
+    u32 r[8];   // the op's result; limbs an op does not set go to scratch slots only
     switch (op) {
       case MW_CHECK: {  // runs of CHECKs as above
         u32 fa = oa;
@@ -233,16 +233,13 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
           asm volatile("" ::: "memory");
           MW_LOAD_INSN(pc, n0, n1, n2, n3);
         }
-        wk = 1;
         break;
       }
       case MW_LEAF_W:
         env.leaf(imm, r);
-        wk = 1;
         break;
       case MW_LEAF_N:
         env.leaf(imm, r);
-        wk = 2;
         break;
       case MW_STORE_W:
         MW_FETCH_W(oa, x);
@@ -259,7 +256,6 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         break;
       case MW_FILL_W:
         env.fill(imm, r, 8);
-        wk = 1;
         break;
       case MW_SPILL_N:
         MW_FETCH_N(oa, x[0]);
@@ -267,18 +263,15 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         break;
       case MW_FILL_N:
         env.fill(imm, r, 1);
-        wk = 2;
         break;
       case MW_MOV_W:
         MW_FETCH_W(oa, x);
         copy8(r, x);
-        wk = 1;
         break;
       case MW_MOV_N: {
         u32 v;
         MW_FETCH_N(oa, v);
         r[0] = v;
-        wk = 2;
         break;
       }
 
@@ -287,64 +280,54 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         add8(x, y, r);
-        wk = 1;
         break;
       case MW_W_SUB:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         sub8(x, y, r);
-        wk = 1;
         break;
       case MW_W_MUL:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         mul8(x, y, r);
-        wk = 1;
         break;
       case MW_W_AND:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
 #pragma unroll
         for (int k = 0; k < 8; ++k) r[k] = x[k] & y[k];
-        wk = 1;
         break;
       case MW_W_OR:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
 #pragma unroll
         for (int k = 0; k < 8; ++k) r[k] = x[k] | y[k];
-        wk = 1;
         break;
       case MW_W_XOR:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
 #pragma unroll
         for (int k = 0; k < 8; ++k) r[k] = x[k] ^ y[k];
-        wk = 1;
         break;
       case MW_W_NOT:
         MW_FETCH_W(oa, x);
 #pragma unroll
         for (int k = 0; k < 8; ++k) r[k] = ~x[k];
-        wk = 1;
         break;
       case MW_W_SHL:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         wshl(x, y, w, r);
-        wk = 1;
         break;
       case MW_W_LSHR:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         wlshr(x, y, w, r);
-        wk = 1;
         break;
       case MW_W_ASHR:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         washr(x, y, w, r);
-        wk = 1;
         break;
       case MW_W_UDIV:
       case MW_W_UREM:
@@ -354,7 +337,6 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         wdiv((int)(op - MW_W_UDIV), x, y, w, r, &env.dsteps);
-        wk = 1;
         break;
       case MW_W_ITE: {
         u32 c;
@@ -363,32 +345,27 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         MW_FETCH_W(ob, y);
 #pragma unroll
         for (int k = 0; k < 8; ++k) r[k] = c ? x[k] : y[k];
-        wk = 1;
         break;
       }
       case MW_W_SHLI:
         MW_FETCH_W(oa, x);
         shl8(x, imm, r);
-        wk = 1;
         break;
       case MW_W_LSHRI:
         MW_FETCH_W(oa, x);
         shr8(x, imm, 0u, r);
-        wk = 1;
         break;
       case MW_W_ZEXTN: {
         u32 v;
         MW_FETCH_N(oa, v);
         zero8(r);
         r[0] = v;
-        wk = 1;
         break;
       }
       case MW_W_SEXT:
         MW_FETCH_W(oa, x);
         sext8(x, imm);
         copy8(r, x);
-        wk = 1;
         break;
       case MW_W_SEXTN: {
         u32 v;
@@ -396,7 +373,6 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         zero8(r);
         r[0] = v;
         sext8(r, imm);
-        wk = 1;
         break;
       }
       case MW_W_INSN: {
@@ -408,7 +384,6 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         shl8(y, imm, r);
 #pragma unroll
         for (int k = 0; k < 8; ++k) r[k] |= x[k];
-        wk = 1;
         break;
       }
 
@@ -417,20 +392,17 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         MW_FETCH_W(oa, x);
         shr8(x, imm, 0u, r);
         r[0] = r[0] & nmask(w);
-        wk = 2;
         break;
       }
       case MW_N_ULT:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         r[0] = ult8(x, y) ? 1u : 0u;
-        wk = 2;
         break;
       case MW_N_ULE:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         r[0] = ult8(y, x) ? 0u : 1u;
-        wk = 2;
         break;
       case MW_N_SLT:
       case MW_N_SLE: {
@@ -446,14 +418,12 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         }
         bool lt = (op == MW_N_SLT) ? ult8(x, y) : !ult8(y, x);
         r[0] = lt ? 1u : 0u;
-        wk = 2;
         break;
       }
       case MW_N_EQ:
         MW_FETCH_W(oa, x);
         MW_FETCH_W(ob, y);
         r[0] = eq8(x, y) ? 1u : 0u;
-        wk = 2;
         break;
       case MW_N_UMULNO: {
         MW_FETCH_W(oa, x);
@@ -464,7 +434,6 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
 #pragma unroll
         for (int k = 0; k < 8; ++k) ov |= (r[k] & ~limb_mask(w, k)) | hi[k];
         r[0] = ov ? 0u : 1u;
-        wk = 2;
         break;
       }
       case MW_N_ADDC: {
@@ -478,78 +447,83 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
           bit |= (b >= 0 && b < 32) ? ((r[k] >> b) & 1u) : 0u;
         }
         r[0] = (w >= 256) ? c : bit;
-        wk = 2;
         break;
       }
 
       // ---------------------------------------------------------- narrow
-      default: {
-        u32 a = 0, b = 0, v = 0;
-        const u32 m = nmask(w);
-        if (op >= MW_N_ADD) {
-          MW_FETCH_N(oa, a);
-          MW_FETCH_N(ob, b);
-        }
-        switch (op) {
-          case MW_N_ADD: v = (a + b) & m; break;
-          case MW_N_SUB: v = (a - b) & m; break;
-          case MW_N_MUL: v = (a * b) & m; break;
-          case MW_N_AND: v = a & b; break;
-          case MW_N_OR: v = a | b; break;
-          case MW_N_XOR: v = a ^ b; break;
-          case MW_N_NOT: v = (~a) & m; break;
-          case MW_N_SHL: v = n_shl(a, b, w); break;
-          case MW_N_LSHR: v = n_lshr(a, b, w); break;
-          case MW_N_ASHR: v = n_ashr(a, b, w); break;
-          case MW_N_UDIV:
-          case MW_N_UREM:
-          case MW_N_SDIV:
-          case MW_N_SREM:
-          case MW_N_SMOD: v = n_div((int)(op - MW_N_UDIV), a, b, w); break;
-          case MW_N_ITE: {
-            u32 c;
-            MW_FETCH_N(oc, c);
-            v = c ? a : b;
-            break;
-          }
-          case MW_N_SHLI: v = (imm >= 32 ? 0u : (a << imm)) & m; break;
-          case MW_N_LSHRI: v = (imm >= 32 ? 0u : (a >> imm)) & m; break;
-          case MW_N_SEXT: v = n_sext(a, imm) & m; break;
-          case MW_N_ULTN: v = a < b; break;
-          case MW_N_ULEN: v = a <= b; break;
-          case MW_N_SLTN: v = n_slt(a, b, w); break;
-          case MW_N_SLEN: v = n_sle(a, b, w); break;
-          case MW_N_EQN: v = a == b; break;
-          case MW_N_UMULNON: v = n_umulno(a, b, w); break;
-          case MW_N_ADDCN: {
-            u64 s = (u64)a + b;
-            v = (u32)((s >> w) & 1u);
-            break;
-          }
-          default:
-            break;  // unreachable: opcodes are validated on load
-        }
-        r[0] = v;
-        wk = 2;
+      // one case per opcode in the single dispatch switch (a nested switch
+      // under `default` doubled the scalar branch tree for every narrow op)
+#define MW_N2(OPC, EXPR)                                                      \
+  case OPC: {                                                                 \
+    u32 a, b;                                                                 \
+    MW_FETCH_N(oa, a);                                                        \
+    MW_FETCH_N(ob, b);                                                        \
+    const u32 m = nmask(w);                                                   \
+    (void)m;                                                                  \
+    r[0] = (EXPR);                                                            \
+    break;                                                                    \
+  }
+#define MW_N1(OPC, EXPR)                                                      \
+  case OPC: {                                                                 \
+    u32 a;                                                                    \
+    MW_FETCH_N(oa, a);                                                        \
+    const u32 m = nmask(w);                                                   \
+    (void)m;                                                                  \
+    r[0] = (EXPR);                                                            \
+    break;                                                                    \
+  }
+      MW_N2(MW_N_ADD, (a + b) & m)
+      MW_N2(MW_N_SUB, (a - b) & m)
+      MW_N2(MW_N_MUL, (a * b) & m)
+      MW_N2(MW_N_AND, a & b)
+      MW_N2(MW_N_OR, a | b)
+      MW_N2(MW_N_XOR, a ^ b)
+      MW_N1(MW_N_NOT, (~a) & m)
+      MW_N2(MW_N_SHL, n_shl(a, b, w))
+      MW_N2(MW_N_LSHR, n_lshr(a, b, w))
+      MW_N2(MW_N_ASHR, n_ashr(a, b, w))
+      MW_N2(MW_N_UDIV, n_div(0, a, b, w))
+      MW_N2(MW_N_UREM, n_div(1, a, b, w))
+      MW_N2(MW_N_SDIV, n_div(2, a, b, w))
+      MW_N2(MW_N_SREM, n_div(3, a, b, w))
+      MW_N2(MW_N_SMOD, n_div(4, a, b, w))
+      case MW_N_ITE: {
+        u32 a, b, c;
+        MW_FETCH_N(oa, a);
+        MW_FETCH_N(ob, b);
+        MW_FETCH_N(oc, c);
+        r[0] = c ? a : b;
         break;
       }
+      MW_N1(MW_N_SHLI, (imm >= 32 ? 0u : (a << imm)) & m)
+      MW_N1(MW_N_LSHRI, (imm >= 32 ? 0u : (a >> imm)) & m)
+      MW_N1(MW_N_SEXT, n_sext(a, imm) & m)
+      MW_N2(MW_N_ULTN, a < b ? 1u : 0u)
+      MW_N2(MW_N_ULEN, a <= b ? 1u : 0u)
+      MW_N2(MW_N_SLTN, n_slt(a, b, w))
+      MW_N2(MW_N_SLEN, n_sle(a, b, w))
+      MW_N2(MW_N_EQN, a == b ? 1u : 0u)
+      MW_N2(MW_N_UMULNON, n_umulno(a, b, w))
+      MW_N2(MW_N_ADDCN, (u32)((((u64)a + b) >> w) & 1u))
+#undef MW_N1
+#undef MW_N2
+      default:
+        break;  // unreachable: opcodes are validated on load
     }
-    // Single, UNCONDITIONAL write-back: every dispatch writes r into one W
-    // slot and r[0] into one slot of each N half; an op that does not write
-    // that file writes its reserved scratch slot (MW_W_RESERVED, MW_N_RESERVED:
-    // the compiler never allocates them).  A conditional indexed write leaves
-    // two versions of a file live at the loop latch and the register
-    // allocator resolves that with a whole-file copy per dispatch (32
-    // v_mov_b64 for the N file); reading the old value back instead cost a
-    // read + select per element.  Here: 8 + 2 indexed moves, no reads.
-    if (wk == 1 && w - 1u < 255u) canon(r, w);  // results of width 1..255: clear bits >= w
+    // Single, UNCONDITIONAL write-back to the targets the compiler encoded in
+    // dst (mw_prog.h): W slot, N-low slot, N-high slot, each the reserved
+    // scratch slot when the op does not write that file.  A conditional
+    // indexed write leaves two versions of a file live at the loop latch and
+    // the register allocator resolves that with a whole-file copy per dispatch
+    // (32 v_mov_b64 for the N file); per-op write kinds cost ~35 scalar
+    // instructions of selects and lane-mask flow.  Here: 8 + 2 indexed moves.
+    // wide ops (16..38) of width 33..255: clear bits >= w (narrow ops mask their
+    // result; leaves, fills and moves are canonical already)
+    if (op - (u32)MW_W_ADD <= (u32)(MW_W_CDINS - MW_W_ADD) && w - 33u < 223u) canon(r, w);
     {
-      const u32 dw = wk == 1u ? MW_WSLOT(dst) : (u32)MW_W_RESERVED;
+      const u32 dw = MW_DST_W(dst), dlo = MW_DST_NLO(dst), dhi = MW_DST_NHI(dst);
       F0[dw] = r[0]; F1[dw] = r[1]; F2[dw] = r[2]; F3[dw] = r[3];
       F0[dw + MW_NW] = r[4]; F1[dw + MW_NW] = r[5]; F2[dw + MW_NW] = r[6]; F3[dw + MW_NW] = r[7];
-      const bool wn = wk == 2u;
-      const u32 dlo = (wn && !(dst & 32u)) ? (dst & 31u) : (u32)MW_N_RESERVED;
-      const u32 dhi = (wn && (dst & 32u)) ? (dst & 31u) : (u32)MW_N_RESERVED;
       NF[dlo] = r[0];
       NH[dhi] = r[0];
     }

@@ -117,10 +117,20 @@ int mg_validate_desc(const mg_prog_desc* d) {
     if (iflags) {   // only a W_CDINS chain link, followed by the W_CDINS that reads it as its acc
       const u32* N = I + 4;
       if (iflags != MW_FLAG_CHAIN || op != MW_W_CDINS || i + 1 >= n || (N[0] & 0xffu) != MW_W_CDINS ||
-          (N[1] >> 16) != dst)
+          (N[1] >> 16) != MW_DST_W(dst))
         return fail(MG_E_PROG, "bad instruction flags at " + std::to_string(i));
     }
-    if (!check_operand(s.dst, dst, d->nconst_words) || !check_operand(s.a, a, d->nconst_words) ||
+    // dst = write targets (mw_prog.h): the file the op writes names a real slot,
+    // the others their scratch slot
+    {
+      const u32 dw = MW_DST_W(dst), dl = MW_DST_NLO(dst), dh = MW_DST_NHI(dst);
+      bool ok = (dst >> 13) == 0u;
+      if (s.dst == 3) ok = ok && dw != MW_W_RESERVED && dl == MW_N_RESERVED && dh == MW_N_RESERVED;
+      else if (s.dst == 4) ok = ok && dw == MW_W_RESERVED && ((dl == MW_N_RESERVED) != (dh == MW_N_RESERVED));
+      else ok = ok && dst == MW_DST_SCRATCH;
+      if (!ok) return fail(MG_E_PROG, "bad write targets at instruction " + std::to_string(i));
+    }
+    if (!check_operand(s.a, a, d->nconst_words) ||
         !check_operand(s.b, b, d->nconst_words) || !check_operand(s.c, c, d->nconst_words))
       return fail(MG_E_PROG, "operand out of range at instruction " + std::to_string(i));
     if (s.dst == 3 || s.dst == 4 || s.a || s.b) {

@@ -67,6 +67,28 @@ FLAG_STOP_AFTER_HIT = 2
 FLAG_CHAIN = 1   # W_CDINS: result consumed only by the next W_CDINS's acc (kept in registers)
 
 
+def encode_dst(cls: str, slot: int = 0) -> int:
+    """dst field = the interpreter's write targets (csrc/mw_prog.h): W slot
+    [2:0], N low-half slot [7:3], N high-half slot [12:8]; files the op does
+    not write get their scratch slot.  cls: "W", "N" or None."""
+    w, lo, hi = W_RESERVED, N_RESERVED, N_RESERVED
+    if cls == "W":
+        w = slot
+    elif cls == "N":
+        if slot < 32:
+            lo = slot
+        else:
+            hi = slot - 32
+    return w | (lo << 3) | (hi << 8)
+
+
+def decode_dst(dst: int):
+    """(W slot, N slot or None) written by an instruction with this dst field."""
+    w, lo, hi = dst & 7, (dst >> 3) & 31, (dst >> 8) & 31
+    n = lo if lo != N_RESERVED else (32 + hi if hi != N_RESERVED else None)
+    return (None if w == W_RESERVED else w), n
+
+
 def encode(op: str, width: int = 0, dst: int = 0, a: int = 0, b: int = 0, c: int = 0, imm: int = 0,
            flags: int = 0):
     code = OPCODES[op]

@@ -98,8 +98,15 @@ def test_reserved_write_back_slots():
     for w0, w1, w2, _ in p.code.reshape(-1, 4):
         op = inv[int(w0) & 0xFF]
         dcls, srcs = SHAPES[op]
-        fields = [int(w1) & 0xFFFF, int(w1) >> 16, int(w2) & 0xFFFF, int(w2) >> 16]
-        for cls, f in zip([dcls] + srcs, fields):
+        wd, nd = isa.decode_dst(int(w1) & 0xFFFF)
+        if dcls == "W":
+            used_w.add(wd)
+        elif dcls == "N":
+            used_n.add(nd)
+        else:
+            assert (wd, nd) == (None, None)
+        fields = [int(w1) >> 16, int(w2) & 0xFFFF, int(w2) >> 16]
+        for cls, f in zip(srcs, fields):
             if cls and not f & isa.KBIT:
                 (used_w if cls == "W" else used_n).add(f)
     assert isa.W_RESERVED not in used_w and len(used_w) == isa.NW - 1
@@ -108,7 +115,7 @@ def test_reserved_write_back_slots():
         q = compile_program([c.app("bvult", c.var("a", 256), c.const(5, 256))])
         q.code = q.code.copy()
         k = next(i for i in range(0, q.code.size, 4) if inv[int(q.code[i]) & 0xFF] == "LEAF_W")
-        q.code[k + 1] = (int(q.code[k + 1]) & 0xFFFF0000) | bad_dst
+        q.code[k + 1] = (int(q.code[k + 1]) & 0xFFFF0000) | isa.encode_dst("W", bad_dst)
         assert _validate(q) != 0
 
 

@@ -42,13 +42,13 @@ def assemble(p, body, repeat):
     idx = {n.name: i for i, n in enumerate(p.leaf_nodes)}
     code = []
     for i in range(4):
-        code += isa.encode("LEAF_N", 8, i, imm=idx[f"n{i}"])
+        code += isa.encode("LEAF_N", 8, isa.encode_dst("N", i), imm=idx[f"n{i}"])
     for i in range(2):
-        code += isa.encode("LEAF_W", 256, i, imm=idx[f"w{i}"])
+        code += isa.encode("LEAF_W", 256, isa.encode_dst("W", i), imm=idx[f"w{i}"])
     for _ in range(repeat):
         for ins in body:
             code += ins
-    code += isa.encode("END")
+    code += isa.encode("END", 0, isa.encode_dst(None))
     q = copy.copy(p)
     q.code = np.asarray(code, dtype=np.uint32)
     q.n_insn = len(code) // 4
@@ -63,7 +63,8 @@ def kn(p):
 
 
 def variants(p):
-    e = isa.encode
+    def e(op, width=0, dst=0, a=0, b=0, c=0, imm=0):   # dst: a slot of the op's result file
+        return isa.encode(op, width, isa.encode_dst(isa.SHAPES[op][0], dst), a, b, c, imm)
     idx = {n.name: i for i, n in enumerate(p.leaf_nodes)}
     return {
         "CHECK": [e("CHECK", 1, 0, 4)],
