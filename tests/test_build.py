@@ -130,3 +130,29 @@ def test_spill_words_hottest_first():
     offs = {(i.op, i.imm) for i in out}
     # N slot 1 (6 accesses / 1 word) first, then N slot 2 (1/1), then W slot 0 (4/8)
     assert ("FILL_N", 0) in offs and ("SPILL_N", 1) in offs and ("SPILL_W", 2) in offs and ("FILL_W", 2) in offs
+
+
+def test_cdins_chain_flag_set_and_validated():
+    """W_CDINS chains (a calldata word built byte by byte) carry MW_FLAG_CHAIN
+    on every link whose result only feeds the next link; the validator rejects
+    the flag anywhere else."""
+    from mythril_amd.smt2 import parse_file
+    from mythril_amd.engine import prepare
+    s = parse_file(os.path.join(ROOT, "tests", "golden", "solver_log", "c2_token_transfer_ok.smt2"))
+    p = prepare(s.asserts, s.ctx).program
+    code = p.code.reshape(-1, 4)
+    inv = {v: k for k, v in isa.OPCODES.items()}
+    links = [k for k in range(len(code)) if (int(code[k][0]) >> 8) & 0xFF]
+    assert len(links) >= 16
+    for k in links:
+        assert inv[int(code[k][0]) & 0xFF] == "W_CDINS" and inv[int(code[k + 1][0]) & 0xFF] == "W_CDINS"
+        assert int(code[k + 1][1]) >> 16 == isa.decode_dst(int(code[k][1]) & 0xFFFF)[0]
+    assert _validate(p) == 0
+    q = compile_program([Ctx().app("bvult", Ctx().var("a", 256), Ctx().const(5, 256))])
+    q.code = q.code.copy()
+    q.code[0] = int(q.code[0]) | (isa.FLAG_CHAIN << 8)    # a flag on a non-W_CDINS instruction
+    assert _validate(q) != 0
+    p.code = p.code.copy()
+    last = links[-1] + 1                                  # the chain's last link: next is not a W_CDINS
+    p.code[4 * last] = int(p.code[4 * last]) | (isa.FLAG_CHAIN << 8)
+    assert _validate(p) != 0
