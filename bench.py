@@ -271,8 +271,11 @@ def load_traffic(prog, batch, kernel):
         d = json.load(open(path))
     except Exception:
         return None
+    # the profile names the launched symbol (<kernel>_x); the attached program
+    # carries the module's kernel name
+    name = d.get("kernel_name", "?")
     if d.get("ops_per_eval") == prog.ops_per_eval and d.get("batch") == batch and \
-            (kernel or "").startswith(d.get("kernel_name", "?")):
+            kernel and (name == kernel or name.startswith(kernel + "_")):
         return d.get("hbm_bytes_per_launch")
     return None
 

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Experiment: A/B of C5 specialised-kernel code generation variants on one GPU.
+
+Variants are jit.py settings (asm pass on/off); each is compiled into the
+in-tree cache (run with --compile-only on the CPU first), attached to the same
+loaded C5 program, timed over 2^22-candidate exhaustive launches, and checked
+to give the same witness and candidate count as the first variant.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from mythril_amd import hostemu, jit  # noqa: E402
+from mythril_amd.compiler import compile_program  # noqa: E402
+from mythril_amd.synth import build_c5  # noqa: E402
+
+VARIANTS = {"base": {"ASM_PASS": False}, "asm": {"ASM_PASS": True}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--compile-only", action="store_true")
+    ap.add_argument("--variants", default="base,asm")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--out", default="gpurun_out/ab_c5.json")
+    a = ap.parse_args()
+    syn = build_c5(hostemu.term_values)
+    p = compile_program(syn.conjuncts)
+    images = {}
+    for v in a.variants.split(","):
+        for k, val in VARIANTS[v].items():
+            setattr(jit, k, val)
+        image, names, dt = jit.compile_device([p], "x", waves=2, lds_leaves=10)
+        images[v] = (image, names[0])
+        print(f"{v}: {names[0]} {len(image)} B {'compiled in %.0f s' % dt if dt else 'cached'}", flush=True)
+    if a.compile_only:
+        return
+    from mythril_amd.runtime import Device
+    dev = Device(0)
+    res = {}
+    w = syn.witness_index
+    for v, (image, name) in images.items():
+        dp = dev.load(p)
+        dev.attach_kernel(dp, image, name)
+        dev.search([dp], syn.seed, 0, 1 << 22)  # warm
+        ms = []
+        for _ in range(a.reps):
+            _, st = dev.search([dp], syn.seed, 0, 1 << 22)
+            ms.append(st["kernel_ms"])
+        (hit,), st = dev.search([dp], syn.seed, w - (1 << 20), (1 << 20) + 1)
+        res[v] = {"kernel_ms": sorted(ms)[len(ms) // 2], "all_ms": ms, "witness": hit, "evals": st.get("evals")}
+        print(v, json.dumps(res[v]), flush=True)
+        dp.free()
+    res["planted"] = w
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    json.dump(res, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
