@@ -141,3 +141,50 @@ def test_nary_implication_is_right_associative():
     p = compile_program(s.asserts)
     v, _ = emu_eval(p, pack_inputs(p, models), len(models))
     assert list(map(int, v)) == want
+
+
+Z3_FORMS = r"""
+; shapes z3's simplify()/sexpr() gives Mythril's terms (VERDICT r1: parser fed only our printer)
+(declare-fun |2_calldata| () (Array (_ BitVec 256) (_ BitVec 8)))
+(declare-fun balance () (Array (_ BitVec 256) (_ BitVec 256)))
+(declare-fun sender_2 () (_ BitVec 256))
+(declare-fun x () (_ BitVec 256))
+(declare-fun y () (_ BitVec 256))
+(declare-fun b () (_ BitVec 8))
+(assert (let ((a!1 (bvadd x (bvmul #xffffffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff y))))
+        (let ((a!2 (ite (bvule a!1 x) #b1 #b0)))
+          (and (= a!2 #b1) (not (= a!1 #x0000000000000000000000000000000000000000000000000000000000000000))))))
+(assert (= ((_ extract 7 0) x) ((_ sign_extend 0) b)))
+(assert (bvsle ((_ sign_extend 248) b) (_ bv100 256)))
+(assert (let ((a!1 (store balance sender_2 (bvadd (select balance sender_2) y))))
+          (bvuge (select a!1 sender_2) y)))
+(assert (= ((_ rotate_left 8) ((_ repeat 2) b)) ((_ repeat 2) b)))
+(assert (distinct x y))
+(assert (=> (bvult y x) (bvugt (bvsub x y) #x0000000000000000000000000000000000000000000000000000000000000000)))
+(assert (xor true (bvslt (concat #x00 ((_ extract 247 0) x)) #x0000000000000000000000000000000000000000000000000000000000000000)))
+"""
+
+
+def test_z3_simplify_forms_evaluate():
+    """z3 writes a - b as bvadd a (bvmul #xff..ff b), nests lets, and uses
+    indexed extract/sign_extend/rotate/repeat: parsed terms evaluate as the
+    SMT-LIB semantics say (oracle), and the engine finds a witness."""
+    s = parse_script(Z3_FORMS)
+    assert len(s.asserts) == 8
+    M = (1 << 256) - 1
+    m = {"2_calldata": ArrayVal({}), "balance": ArrayVal({}), "sender_2": 7, "x": 0x1234, "y": 0x34,
+         "b": 0x34}
+    vals = eval_nodes(s.asserts, m)
+    assert [vals[a.id] for a in s.asserts] == [1] * 8
+    m["y"] = 0x1235        # x - y wraps: bvule (x - y) x fails
+    vals = eval_nodes(s.asserts, m)
+    assert vals[s.asserts[0].id] == 0
+    m["y"], m["b"], m["x"] = 0x34, 0x80, 0x1280   # sign_extend(0x80) = -128 <= 100 holds
+    vals = eval_nodes(s.asserts, m)
+    assert vals[s.asserts[2].id] == 1 and vals[s.asserts[1].id] == 1
+    m["x"] = M             # top byte 0 after the concat: never negative, so the xor holds
+    vals = eval_nodes(s.asserts, m)
+    assert vals[s.asserts[7].id] == 1 and vals[s.asserts[1].id] == 0
+    q = prepare(s.asserts, s.ctx)
+    (w,) = engine(1 << 16).search([q])
+    assert w is not None and holds(s.asserts, w)
