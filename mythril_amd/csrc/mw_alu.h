@@ -358,6 +358,64 @@ MW_HD u32 div3by2(u32 u2, u32 u1, u32 u0, u32 d1, u32 d0, u32 v, u32& r1, u32& r
   return q1;
 }
 
+// Quotient digit estimate for a full-width divisor (y7 != 0): from the top 64
+// bits of both operands, xh = x7:x6 and yh = y7:y6 >= 2^32, never below the true
+// quotient floor(x / y) (< 2^32) and at most 2 above it:
+//   x / y < (xh + 1) 2^192 / (yh 2^192) = (xh + 1) / yh  <=  estimate,
+//   (xh + 1) / yh - x / y <= (xh + yh + 1) / (yh (yh + 1)) ~ 1 + 2^-32.
+// Device: f64 with every rounding biased upwards (numerator rounded up by
+// 2^-51, denominator down by 2^-51, reciprocal by two Newton steps, quotient
+// up by 2^-48).  Host: the exact 64-bit quotient.
+MW_HD u32 qdigit_est(u32 x7, u32 x6, u32 y7, u32 y6) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double two32 = 4294967296.0;
+  const double xd = __builtin_fma((double)x7, two32, (double)x6);
+  const double yd = __builtin_fma((double)y7, two32, (double)y6);
+  const double A = (xd + 1.0) * (1.0 + 0x1p-51);
+  const double B = yd * (1.0 - 0x1p-51);
+  double rc = __builtin_amdgcn_rcp(B);
+  double e = __builtin_fma(-B, rc, 1.0);
+  rc = __builtin_fma(rc, e, rc);
+  e = __builtin_fma(-B, rc, 1.0);
+  rc = __builtin_fma(rc, e, rc);
+  const double Q = A * rc * (1.0 + 0x1p-48);
+  return Q >= 4294967295.0 ? 0xffffffffu : (u32)Q;
+#else
+  const u64 xh = ((u64)x7 << 32) | x6, yh = ((u64)y7 << 32) | y6;
+  const u64 qe = xh == ~0ull ? xh / yh + 1u : (xh + 1u) / yh;
+  return qe > 0xffffffffull ? 0xffffffffu : (u32)qe;
+#endif
+}
+
+// q = x / y, r = x % y when y's top limb is nonzero (y >= 2^224, so q < 2^32):
+// one estimated digit (qdigit_est, never too small), one multiply-subtract over
+// 9 limbs, and an add-back loop for the (rare) overestimate, run by a wave only
+// if one of its lanes needs it.  No normalisation shifts, 3-by-2 reciprocal or
+// digit loop: tools/ab_c5.py measured division at half of the C5 kernel's time.
+MW_HD void udivrem8_full(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
+  u32 qd = qdigit_est(x[7], x[6], y[7], y[6]);
+  u32 carry = 0, br = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const u64 p = (u64)qd * y[k] + carry;
+    carry = (u32)(p >> 32);
+    r[k] = subb(x[k], (u32)p, br);
+  }
+  u32 hi = 0u - carry - br;  // limb 8 of x - qd*y: 0, or -1/-2 when qd is too large
+  while (MW_ANY(hi != 0u)) {
+    if (hi != 0u) {
+      u32 c = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = addc(r[k], y[k], c);
+      hi += c;
+      qd -= 1u;
+    }
+  }
+  q[0] = qd;
+#pragma unroll
+  for (int k = 1; k < 8; ++k) q[k] = 0u;
+}
+
 // q = x / y, r = x % y for y != 0: Knuth Alg. D, base 2^32, fixed 8x8 shape
 // (the divisor is normalized to a full 8-limb value so every index is static),
 // with 3-by-2 quotient estimates (Moller-Granlund).  A digit estimate is at
@@ -374,6 +432,11 @@ MW_HD u32 div3by2(u32 u2, u32 u1, u32 u0, u32 d1, u32 d0, u32 v, u32& r1, u32& r
 // 256-bit values has one digit: one step of eight).  *steps (optional) counts
 // the steps the wave ran, for the executed-work roofline (bench.py).
 MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], u32* steps = nullptr) {
+  if (!MW_ANY(y[7] == 0u)) {  // every lane's divisor is full width: one digit
+    udivrem8_full(x, y, q, r);
+    if (steps) *steps += 1u;
+    return;
+  }
   const u32 s = clz256(y);
   // Normalisation shifts: with a full-width divisor (top limb nonzero in every
   // lane of the wave, the common case) s < 32 and the limb-moving stages of

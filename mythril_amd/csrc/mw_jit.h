@@ -23,8 +23,21 @@
 
 namespace mw {
 namespace jit {
+MW_HD void xor8(const u32 x[8], const u32 y[8], u32 r[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = x[k] ^ y[k];
+}
 
 // ------------------------------------------------------------------ wide
+// MW_ABLATE_*: timing experiments only (tools/ab_c5.py): the op class becomes an
+// XOR (wrong results, same data flow), so the time it saves is that class's cost
+#if defined(MW_ABLATE_ADD)
+#define add8(x, y, r) ((void)xor8(x, y, r), 0u)
+#define sub8(x, y, r) ((void)xor8(x, y, r), 0u)
+#endif
+#if defined(MW_ABLATE_MUL)
+#define mul8(x, y, r) xor8(x, y, r)
+#endif
 MW_HD void w_add(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { add8(x, y, r); canon(r, w); }
 MW_HD void w_sub(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { sub8(x, y, r); canon(r, w); }
 MW_HD void w_mul(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { mul8(x, y, r); canon(r, w); }
@@ -48,12 +61,22 @@ MW_HD void w_not(const u32 x[8], u32 w, u32 r[8]) {
   for (int k = 0; k < 8; ++k) r[k] = ~x[k];
   canon(r, w);
 }
+#if defined(MW_ABLATE_SHIFT)
+MW_HD void w_shl(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { xor8(x, y, r); }
+MW_HD void w_lshr(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { xor8(x, y, r); }
+MW_HD void w_ashr(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { xor8(x, y, r); }
+#else
 MW_HD void w_shl(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { wshl(x, y, w, r); canon(r, w); }
 MW_HD void w_lshr(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { wlshr(x, y, w, r); canon(r, w); }
 MW_HD void w_ashr(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { washr(x, y, w, r); canon(r, w); }
+#endif
 // kind: 0 udiv, 1 urem, 2 sdiv, 3 srem, 4 smod (wdiv consumes its operands);
 // steps counts the digit steps the wave ran (udivrem8 zero-digit skip)
 MW_HD void w_div(int kind, const u32 x[8], const u32 y[8], u32 w, u32 r[8], u32& steps) {
+#if defined(MW_ABLATE_DIV)
+  xor8(x, y, r);
+  return;
+#endif
   u32 a[8], b[8];
   copy8(a, x);
   copy8(b, y);

@@ -528,8 +528,12 @@ def compile_host(progs: Sequence[Program], lds_leaves: int = 0,
     return path, names
 
 
+# extra device flags for experiments (tools/ab_c5.py ablations); empty in the product
+EXTRA_FLAGS: List[str] = []
+
+
 def _device_flags(waves: int) -> List[str]:
-    return DEVICE_FLAGS + ([f"-DMW_JIT_WAVES={waves}"] if waves != 2 else [])
+    return DEVICE_FLAGS + ([f"-DMW_JIT_WAVES={waves}"] if waves != 2 else []) + list(EXTRA_FLAGS)
 
 
 def compile_parts(p: Program, variants: str = "xe", waves: int = 2, lds_leaves: int = 0,

@@ -205,3 +205,23 @@ def division_check_programs(npairs: int = 256, seed: int = 11):
                  for nm, vals in (("a", [x for x, _ in pairs]), ("b", [y for _, y in pairs]), ("e", exp))}
         progs.append(compile_program([ctx.app("=", ctx.app(op, a, b), e)], leaf_specs=specs))
     return progs
+
+
+def full_width_division_models(seed: int, n: int) -> List[Dict[str, int]]:
+    """Operand pairs whose divisor has a nonzero top limb (y >= 2^224), with the
+    quotient-estimate edge cases of mw_alu.h udivrem8_full: digits near 2^32-1,
+    exact multiples and their neighbours, x < y, x = y, 64-bit heads that round."""
+    rng = random.Random(seed)
+    M = (1 << 256) - 1
+    ys = [1 << 224, (1 << 224) + 1, M, 1 << 255, (1 << 255) - 1, ((1 << 32) - 1) << 224,
+          (1 << 224) | ((1 << 192) - 1), (1 << 224) + (1 << 192), ((1 << 53) + 1) << 203]
+    out = []
+    while len(out) < n:
+        y = rng.choice(ys) if rng.random() < 0.5 else (rng.getrandbits(256) | (1 << (224 + rng.randrange(32))))
+        k = rng.choice([0, 1, 2, 3, (1 << 31), (1 << 32) - 1, (1 << 32) - 2, rng.getrandbits(32)])
+        d = rng.choice([0, 1, -1, y - 1, rng.getrandbits(200)])
+        x = k * y + d
+        if rng.random() < 0.1:
+            x = rng.choice([0, 1, M, y - 1, y, y + 1, M - 1])
+        out.append({"a": x & M, "b": y})
+    return out

@@ -153,3 +153,20 @@ def test_division_rare_correction_paths():
         got = unpack_trace(p, trace, t)
         for j, mm in enumerate(models):
             assert got[j] == eval_nodes([t], mm)[t.id], f"{t.op} a={mm['a']:#x} b={mm['b']:#x}"
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_full_width_divisors(seed):
+    """The one-digit path for divisors with a nonzero top limb (udivrem8_full):
+    estimate never too small, add-back corrections, digits near 2^32-1."""
+    from tests.helpers import full_width_division_models
+    dag = RandDag(1, widths=[256], nvars=2)
+    a, b = dag.ctx.var("a", 256), dag.ctx.var("b", 256)
+    terms = [dag.ctx.app(op, a, b) for op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")]
+    p = compile_program([dag.ctx.true()], trace=terms)
+    models = full_width_division_models(seed, 64 * 12)
+    _, trace = emu_eval(p, pack_inputs(p, models), len(models))
+    for t in terms:
+        got = unpack_trace(p, trace, t)
+        for j, mm in enumerate(models):
+            assert got[j] == eval_nodes([t], mm)[t.id], f"{t.op} a={mm['a']:#x} b={mm['b']:#x}"

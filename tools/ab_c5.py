@@ -17,13 +17,16 @@ from mythril_amd import hostemu, jit  # noqa: E402
 from mythril_amd.compiler import compile_program  # noqa: E402
 from mythril_amd.synth import build_c5  # noqa: E402
 
-VARIANTS = {"base": {"ASM_PASS": False}, "asm": {"ASM_PASS": True}}
+VARIANTS = {"base": {"EXTRA_FLAGS": []},
+            # ablations (wrong results, timing only): one op class replaced by an XOR
+            "abl_mul": {"EXTRA_FLAGS": ["-DMW_ABLATE_MUL"]}, "abl_div": {"EXTRA_FLAGS": ["-DMW_ABLATE_DIV"]},
+            "abl_add": {"EXTRA_FLAGS": ["-DMW_ABLATE_ADD"]}, "abl_shift": {"EXTRA_FLAGS": ["-DMW_ABLATE_SHIFT"]}}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--compile-only", action="store_true")
-    ap.add_argument("--variants", default="base,asm")
+    ap.add_argument("--variants", default="base")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default="gpurun_out/ab_c5.json")
     a = ap.parse_args()
