@@ -295,7 +295,12 @@ MW_HD u32 recip32(u32 d) {
   e = __builtin_fma(-dd, r, 1.0);
   r = __builtin_fma(r, e, r);
   const double n = __builtin_fma((double)nh, 4294967296.0, 4294967295.0);
-  u32 v = (u32)(n * r);
+  // n * r reaches 2^32 for d = 2^31 (the reciprocal is 2^32 - 1): an out-of-range
+  // double -> u32 conversion is undefined, and when d is a compile-time constant
+  // (a specialised kernel dividing by a known limb) LLVM folds it to poison.
+  // The hardware conversion saturates; say so explicitly.
+  const double t = n * r;
+  u32 v = t >= 4294967295.0 ? 0xffffffffu : (u32)t;
   const u64 nx = ((u64)nh << 32) | 0xffffffffu;
   const u64 p = (u64)v * d;
   if (p > nx) v -= 1u;
@@ -416,6 +421,37 @@ MW_HD void udivrem8_full(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
   for (int k = 1; k < 8; ++k) q[k] = 0u;
 }
 
+// q = x / y, r = x % y for a one-limb divisor (0 < y < 2^32): short division,
+// eight 2-by-1 steps (Moller & Granlund 2011, Alg. 4) with one reciprocal of
+// the normalised divisor; the remainder stays one limb throughout.  C5 divides
+// by such values (quotients of earlier divisions) in 42 of its 384 divisions,
+// where Knuth's loop ran all eight 3-by-2 steps.
+MW_HD void udivrem8_short(const u32 x[8], u32 y0, u32 q[8], u32 r[8]) {
+  const u32 s = clz32(y0);
+  const u32 d = y0 << s;
+  const u32 v = recip32(d);
+  u32 rem = fshl32(0u, x[7], s);  // < 2^s <= d
+#pragma unroll
+  for (int k = 7; k >= 0; --k) {
+    const u32 u0 = k > 0 ? fshl32(x[k], x[k - 1], s) : (x[0] << s);
+    const u64 qq = (u64)v * rem + ((((u64)rem) << 32) | u0);
+    u32 q1 = (u32)(qq >> 32) + 1u;
+    const u32 q0 = (u32)qq;
+    u32 rr = u0 - q1 * d;
+    const bool adj1 = rr > q0;
+    q1 = adj1 ? q1 - 1u : q1;
+    rr = adj1 ? rr + d : rr;
+    const bool adj2 = rr >= d;  // unlikely
+    q1 = adj2 ? q1 + 1u : q1;
+    rr = adj2 ? rr - d : rr;
+    q[k] = q1;
+    rem = rr;
+  }
+  r[0] = rem >> s;
+#pragma unroll
+  for (int k = 1; k < 8; ++k) r[k] = 0u;
+}
+
 // q = x / y, r = x % y for y != 0: Knuth Alg. D, base 2^32, fixed 8x8 shape
 // (the divisor is normalized to a full 8-limb value so every index is static),
 // with 3-by-2 quotient estimates (Moller-Granlund).  A digit estimate is at
@@ -435,6 +471,11 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], u32* ste
   if (!MW_ANY(y[7] == 0u)) {  // every lane's divisor is full width: one digit
     udivrem8_full(x, y, q, r);
     if (steps) *steps += 1u;
+    return;
+  }
+  if (!MW_ANY((y[1] | y[2] | y[3] | y[4] | y[5] | y[6] | y[7]) != 0u)) {  // one-limb divisors
+    udivrem8_short(x, y[0], q, r);
+    if (steps) *steps += 8u;
     return;
   }
   const u32 s = clz256(y);

@@ -225,3 +225,53 @@ def full_width_division_models(seed: int, n: int) -> List[Dict[str, int]]:
             x = rng.choice([0, 1, M, y - 1, y, y + 1, M - 1])
         out.append({"a": x & M, "b": y})
     return out
+
+
+def short_division_models(seed: int, n: int) -> List[Dict[str, int]]:
+    """Operand pairs with one-limb divisors (0 < y < 2^32) in every model: the
+    short-division path of mw_alu.h (udivrem8_short), normalisation shifts 0..31
+    and the 2-by-1 corrections."""
+    rng = random.Random(seed)
+    M = (1 << 256) - 1
+    ys = [1, 2, 3, 7, (1 << 31) - 1, 1 << 31, (1 << 31) + 1, (1 << 32) - 1, (1 << 32) - 2, 0x10001]
+    out = []
+    while len(out) < n:
+        y = rng.choice(ys) if rng.random() < 0.5 else rng.randrange(1, 1 << rng.randint(1, 32))
+        x = rng.choice([rng.getrandbits(256), M, 0, y - 1, y, rng.getrandbits(256) // y * y,
+                        rng.getrandbits(256) // y * y - 1, rng.getrandbits(40)])
+        out.append({"a": x & M, "b": y})
+    return out
+
+
+CONSTANT_DIVISORS = [0, 1, 3, 1 << 31, (1 << 31) + 1, (1 << 32) - 1, 1 << 32, 1 << 224, (1 << 224) + 1,
+                     1 << 255, (1 << 256) - 1, 0x10001 << 128]
+
+
+def constant_divisor_programs(npairs: int = 256, seed: int = 12):
+    """One program per constant divisor K asserting op(a, K) == e_op for the five
+    divisions, with a and the oracle's results e_op drawn from bit-field pools
+    (same digit): every verdict over candidates [0, npairs) must be 1.  A
+    specialised kernel sees K as literals, so LLVM constant-folds the divisor's
+    normalisation and reciprocal (d = 2^31 once folded an out-of-range
+    double -> u32 conversion to poison)."""
+    from mythril_amd.compiler import LeafSpec, compile_program
+    from oracle import bvsem
+    rng = random.Random(seed)
+    M = (1 << 256) - 1
+    k = (npairs - 1).bit_length()
+    ops = ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")
+    progs = []
+    for K in CONSTANT_DIVISORS:
+        xs = [0, 1, M, M - 1, 1 << 255, (K - 1) & M, K, (K + 1) & M]
+        while len(xs) < npairs:
+            xs.append(rng.getrandbits(256) if rng.random() < 0.7 else (rng.getrandbits(40) * K + rng.choice([0, 1, K - 1])) & M)
+        ctx = Ctx()
+        a = ctx.var("a", 256)
+        specs = {"a": LeafSpec("a", 256, pool=xs, shift=0, bits=k)}
+        conj = []
+        for op in ops:
+            e = ctx.var("e_" + op, 256)
+            specs["e_" + op] = LeafSpec("e_" + op, 256, pool=[getattr(bvsem, op)(256, x, K) for x in xs], shift=0, bits=k)
+            conj.append(ctx.app("=", ctx.app(op, a, ctx.const(K, 256)), e))
+        progs.append(compile_program(conj, leaf_specs=specs))
+    return progs

@@ -186,3 +186,19 @@ def test_split_program_parts_match_interpreter(dev, planted):
         assert np.array_equal(va, vb) and vb[5000] == 1
         a.free()
         b.free()
+
+
+def test_constant_divisors_specialised(dev):
+    """Divisions by literal divisors (folded by LLVM in the specialised kernel),
+    d = 2^31 after normalisation included: every pooled candidate satisfies."""
+    from tests.helpers import constant_divisor_programs
+    progs = constant_divisor_programs()
+    image, names, _ = jit.compile_device(progs)
+    for p, name in zip(progs, names):
+        for special in (True, False):
+            dp = dev.load(p)
+            if special:
+                dev.attach_kernel(dp, image, name)
+            v, _ = dev.eval_generated(dp, 1, 0, 256, trace=False)
+            assert int(v.sum()) == 256, (name, special)
+            dp.free()

@@ -20,7 +20,8 @@ from mythril_amd import isa
 from oracle.dag_eval import eval_nodes
 from oracle.keccak import keccak256
 from oracle.vmtest_runner import run_case, env_of
-from tests.helpers import RandDag, full_width_division_models, oracle_models, random_assignments
+from tests.helpers import (RandDag, full_width_division_models, oracle_models, random_assignments,
+                           short_division_models)
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -82,12 +83,14 @@ def test_division_and_shift_edges_gpu(dev, w):
 @pytest.mark.parametrize("seed", range(3))
 def test_full_width_divisors_gpu(dev, seed):
     """Waves whose every divisor is full width take the one-digit path
-    (udivrem8_full, f64 estimate + add-back); the models are in blocks of 64,
-    so every wave does."""
+    (udivrem8_full, f64 estimate + add-back), waves of one-limb divisors the
+    short division (udivrem8_short); the models come in blocks of 64, so every
+    wave of each batch takes its path."""
     c = Ctx()
     a, b = c.var("a", 256), c.var("b", 256)
     terms = [c.app(op, a, b) for op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")]
     _parity(dev, [c.true()], terms, full_width_division_models(seed, 64 * 12))
+    _parity(dev, [c.true()], terms, short_division_models(seed, 64 * 12))
 
 
 def test_generated_candidates_gpu(dev):

@@ -159,12 +159,12 @@ def test_division_rare_correction_paths():
 def test_full_width_divisors(seed):
     """The one-digit path for divisors with a nonzero top limb (udivrem8_full):
     estimate never too small, add-back corrections, digits near 2^32-1."""
-    from tests.helpers import full_width_division_models
+    from tests.helpers import full_width_division_models, short_division_models
     dag = RandDag(1, widths=[256], nvars=2)
     a, b = dag.ctx.var("a", 256), dag.ctx.var("b", 256)
     terms = [dag.ctx.app(op, a, b) for op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")]
     p = compile_program([dag.ctx.true()], trace=terms)
-    models = full_width_division_models(seed, 64 * 12)
+    models = full_width_division_models(seed, 64 * 12) + short_division_models(seed, 64 * 12)
     _, trace = emu_eval(p, pack_inputs(p, models), len(models))
     for t in terms:
         got = unpack_trace(p, trace, t)

@@ -26,8 +26,14 @@ def main():
     ap.add_argument("--count", type=int, default=1 << 16)
     ap.add_argument("--compile-only", action="store_true")
     ap.add_argument("--no-full", action="store_true", help="conjunct programs only (no whole-program kernel)")
+    ap.add_argument("--bench", action="store_true",
+                    help="bench.py's C5 program (density 2^-24, leftover comparisons kept), checked around the witness")
     a = ap.parse_args()
-    syn = build_c5(hostemu.term_values, n_nodes=a.nodes, n_conj=a.conj, density_log2=1, keep_pending=False)
+    if a.bench:
+        syn = build_c5(hostemu.term_values, n_nodes=a.nodes, n_conj=a.conj)
+    else:
+        syn = build_c5(hostemu.term_values, n_nodes=a.nodes, n_conj=a.conj, density_log2=1, keep_pending=False)
+    begin = syn.witness_index - a.count // 2 if a.bench else 0
     progs = [compile_program(syn.conjuncts)] + [compile_program([c]) for c in syn.conjuncts]
     if a.no_full:
         progs = progs[1:]
@@ -42,9 +48,12 @@ def main():
         s = dev.load(p)
         dev.attach_kernel(s, image, name)
         i = dev.load(p)
-        vs, _ = dev.eval_generated(s, syn.seed, 0, a.count, trace=False)
-        vi, _ = dev.eval_generated(i, syn.seed, 0, a.count, trace=False)
+        vs, _ = dev.eval_generated(s, syn.seed, begin, a.count, trace=False)
+        vi, _ = dev.eval_generated(i, syn.seed, begin, a.count, trace=False)
         mism = int(np.count_nonzero(vs != vi))
+        if mism and a.bench:
+            extra_idx = (np.nonzero(vs != vi)[0][:4] + begin).tolist()
+            print(f"  first mismatching indices {extra_idx} (witness {syn.witness_index})", flush=True)
         bad += mism
         extra = ""
         print(f"{'program' if k == 0 and not a.no_full else 'conjunct %d' % (k - (0 if a.no_full else 1))}: {mism} mismatches of {a.count}, "

@@ -24,6 +24,9 @@ def main():
     print("tests/test_gpu_jit.py LDS module:", jit.compile_device(progs[:11], lds_leaves=4)[2], "s", flush=True)
     for p in progs[:2]:
         print("tests/test_gpu_jit.py parts:", jit.compile_parts(p, lds_leaves=2, part_weight=3000)[1], "s", flush=True)
+    from tests.helpers import constant_divisor_programs
+    print("tests/test_gpu_jit.py constant divisors:", jit.compile_device(constant_divisor_programs())[2], "s",
+          flush=True)
     from config_bench import warm as warm_configs
     warm_configs()   # tools/config_bench.py (C2-C4 solver-log queries)
     print("tools/config_bench.py kernels warmed", flush=True)
