@@ -222,10 +222,11 @@ def main():
             "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (wave64 VALU op = 2 cycles)",
             "peak_measured": measured_peak / 1e12 if measured_peak else None,
             "frac_measured": achieved / measured_peak if measured_peak else None,
-            # SURVEY §8(d)'s nominal count (every division priced at all 8 digit
-            # steps, round 1's method) beside the executed-work figure above
-            "frac_nominal": prog.ops_per_eval * batch / avg_kernel_s / THEORETICAL_PEAK,
-            "peak_measured_source": "v_add_u32 microbenchmark, 8 chains x 8 waves/SIMD (profiles/valu_peak.json)",
+            # (SURVEY §8(d)'s nominal count, every division at all 8 digit steps,
+            # is config.ops_per_eval; since the division rewrite most divisions
+            # run one step, so a fraction on the nominal count passes 1.0)
+            "peak_measured_source": "v_add_u32_e32 with VGPR operands, 8 chains x 8 waves/SIMD "
+                                    "(tools/exp/irate.hip; profiles/valu_peak.json)",
         },
         "cpu_baseline": cpu,
     }

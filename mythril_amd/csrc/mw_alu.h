@@ -475,7 +475,9 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], u32* ste
   }
   if (!MW_ANY((y[1] | y[2] | y[3] | y[4] | y[5] | y[6] | y[7]) != 0u)) {  // one-limb divisors
     udivrem8_short(x, y[0], q, r);
-    if (steps) *steps += 8u;
+    // eight one-limb digit steps are about one 8-limb step's work (the
+    // executed-work roofline prices a step at the 8-limb multiply-subtract)
+    if (steps) *steps += 1u;
     return;
   }
   const u32 s = clz256(y);
