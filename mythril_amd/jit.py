@@ -580,32 +580,45 @@ def attach(dev, dps, variants: str = "xe", waves: int = 2, lds_leaves: int = 0,
     return dt
 
 
-def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 2, lds_leaves: int = 10,
-                     split: bool = False) -> float:
-    """Pre-compile bench.py's C5 kernel into the in-tree cache (run by build()).
+def bench_programs(n_nodes: int = 10000) -> Dict[int, Program]:
+    """bench.py's C5 program (density 2^-24) and its mixed-verdict variant
+    (density 2^-1 without the leftover comparisons, about half satisfied, for
+    tests/test_gpu_fullsize.py), keyed by density.
 
     The C5 witness is planted with the host build of the interpreter
     (mythril_amd/hostemu.py), which gives bit for bit the values bench.py gets
     from the device interpreter, so the generated source — and the cache key —
-    are the ones the benchmark computes on the GPU box.
-    """
+    are the ones the benchmark computes on the GPU box."""
     from . import hostemu
     from .synth import build_c5
-    t0 = time.perf_counter()
-    # density 24: the benchmark's program; density 1 without the leftover
-    # comparisons: the same chains with mixed verdicts (about half satisfied),
-    # for the full-size parity test (tests/test_gpu_fullsize.py)
+    out = {}
     for dens in (24, 1):
         syn = build_c5(hostemu.term_values, n_nodes=n_nodes, density_log2=dens, keep_pending=dens == 24)
-        prog = compile_program(syn.conjuncts)
-        if dens == 24:
-            # the split kernels too: bench.py falls back to them (a minute of
-            # parallel compiles) when the single kernel's code object is missing
-            objs, dts = compile_parts(prog, "x", waves=waves, lds_leaves=lds_leaves)
-        if split and dens == 24:
-            names, dt = [n for _, n in objs], dts
-        else:
-            _, names, dt = compile_device([prog], "x", waves=waves, lds_leaves=lds_leaves)
-        log(f"[jit] C5 (density 2^-{dens}) kernel {names[0]} ({len(names)} part(s)): "
-            f"{'compiled in %.0f s' % dt if dt else 'cached'}")
+        out[dens] = compile_program(syn.conjuncts)
+    return out
+
+
+def bench_warm_jobs(n_nodes: int = 10000, waves: int = 2, lds_leaves: int = 10, log=print):
+    """Independent compile jobs (callables) that put bench.py's C5 kernels in the
+    in-tree cache: the single kernel of each density, and the benchmark
+    program's split parts (bench.py falls back to them when the single
+    kernel's code object is missing)."""
+    progs = bench_programs(n_nodes)
+
+    def single(dens):
+        _, names, dt = compile_device([progs[dens]], "x", waves=waves, lds_leaves=lds_leaves)
+        log(f"[jit] C5 (density 2^-{dens}) kernel {names[0]}: {'compiled in %.0f s' % dt if dt else 'cached'}")
+
+    def parts():
+        objs, dt = compile_parts(progs[24], "x", waves=waves, lds_leaves=lds_leaves)
+        log(f"[jit] C5 split kernels ({len(objs)} parts): {'compiled in %.0f s' % dt if dt else 'cached'}")
+    return [lambda: single(24), lambda: single(1), parts]
+
+
+def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 2, lds_leaves: int = 10) -> float:
+    """Pre-compile bench.py's C5 kernels into the in-tree cache, one job after
+    the other (tools/jit_warm.py runs the same jobs in parallel)."""
+    t0 = time.perf_counter()
+    for job in bench_warm_jobs(n_nodes, waves, lds_leaves, log):
+        job()
     return time.perf_counter() - t0

@@ -52,12 +52,22 @@ def _groups(files, together):
     return [(files, qs)] if together else [([f], [q]) for f, q in zip(files, qs)]
 
 
-def warm():
-    """Compile the specialised kernels into build/jit (CPU; tools/jit_warm.py)."""
+def warm_jobs():
+    """One compile job per query group (independent hipcc runs; tools/jit_warm.py
+    runs them in parallel).  The queries are prepared here, in the caller's thread."""
     from mythril_amd import jit
+    jobs = []
     for _, files, _, together in CONFIGS:
         for _, g in _groups(files, together):
-            jit.compile_device([q.program for q in g], "xe", waves=2, lds_leaves=0)
+            progs = [q.program for q in g]
+            jobs.append(lambda progs=progs: jit.compile_device(progs, "xe", waves=2, lds_leaves=0))
+    return jobs
+
+
+def warm():
+    """Compile the specialised kernels into build/jit (CPU)."""
+    for job in warm_jobs():
+        job()
 
 
 def main():
