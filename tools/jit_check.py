@@ -26,9 +26,11 @@ def main():
     ap.add_argument("--count", type=int, default=1 << 16)
     ap.add_argument("--compile-only", action="store_true")
     ap.add_argument("--no-full", action="store_true", help="conjunct programs only (no whole-program kernel)")
+    ap.add_argument("--flags", default="", help="extra device flags for the specialised kernels (experiments)")
     ap.add_argument("--bench", action="store_true",
                     help="bench.py's C5 program (density 2^-24, leftover comparisons kept), checked around the witness")
     a = ap.parse_args()
+    jit.EXTRA_FLAGS = a.flags.split()
     if a.bench:
         syn = build_c5(hostemu.term_values, n_nodes=a.nodes, n_conj=a.conj)
     else:
