@@ -20,7 +20,9 @@ from mythril_amd.synth import build_c5  # noqa: E402
 VARIANTS = {"base": {"EXTRA_FLAGS": []},
             # ablations (wrong results, timing only): one op class replaced by an XOR
             "abl_mul": {"EXTRA_FLAGS": ["-DMW_ABLATE_MUL"]}, "abl_div": {"EXTRA_FLAGS": ["-DMW_ABLATE_DIV"]},
-            "abl_add": {"EXTRA_FLAGS": ["-DMW_ABLATE_ADD"]}, "abl_shift": {"EXTRA_FLAGS": ["-DMW_ABLATE_SHIFT"]}}
+            "abl_add": {"EXTRA_FLAGS": ["-DMW_ABLATE_ADD"]}, "abl_shift": {"EXTRA_FLAGS": ["-DMW_ABLATE_SHIFT"]},
+            # code generation: two conjunct chains merged per basic block (jit.interleave_conjuncts)
+            "il2": {"EXTRA_FLAGS": [], "interleave": 2}}
 
 
 def main():
@@ -34,9 +36,11 @@ def main():
     p = compile_program(syn.conjuncts)
     images = {}
     for v in a.variants.split(","):
-        for k, val in VARIANTS[v].items():
+        opts = dict(VARIANTS[v])
+        il = opts.pop("interleave", 1)
+        for k, val in opts.items():
             setattr(jit, k, val)
-        image, names, dt = jit.compile_device([p], "x", waves=2, lds_leaves=10)
+        image, names, dt = jit.compile_device([p], "x", waves=2, lds_leaves=10, interleave=il)
         images[v] = (image, names[0])
         print(f"{v}: {names[0]} {len(image)} B {'compiled in %.0f s' % dt if dt else 'cached'}", flush=True)
     if a.compile_only:
