@@ -22,7 +22,9 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             "abl_mul": {"EXTRA_FLAGS": ["-DMW_ABLATE_MUL"]}, "abl_div": {"EXTRA_FLAGS": ["-DMW_ABLATE_DIV"]},
             "abl_add": {"EXTRA_FLAGS": ["-DMW_ABLATE_ADD"]}, "abl_shift": {"EXTRA_FLAGS": ["-DMW_ABLATE_SHIFT"]},
             # code generation: two conjunct chains merged per basic block (jit.interleave_conjuncts)
-            "il2": {"EXTRA_FLAGS": [], "interleave": 2}}
+            "il2": {"EXTRA_FLAGS": [], "interleave": 2},
+            # one wave per SIMD: 512 registers per lane, no leaves in LDS
+            "w1": {"EXTRA_FLAGS": [], "waves": 1, "lds": 0}}
 
 
 def main():
@@ -38,9 +40,10 @@ def main():
     for v in a.variants.split(","):
         opts = dict(VARIANTS[v])
         il = opts.pop("interleave", 1)
+        waves, lds = opts.pop("waves", 2), opts.pop("lds", 10)
         for k, val in opts.items():
             setattr(jit, k, val)
-        image, names, dt = jit.compile_device([p], "x", waves=2, lds_leaves=10, interleave=il)
+        image, names, dt = jit.compile_device([p], "x", waves=waves, lds_leaves=lds, interleave=il)
         images[v] = (image, names[0])
         print(f"{v}: {names[0]} {len(image)} B {'compiled in %.0f s' % dt if dt else 'cached'}", flush=True)
     if a.compile_only:
