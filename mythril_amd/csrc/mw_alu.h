@@ -195,26 +195,6 @@ MW_HD void shr8(const u32 a[8], u32 s, u32 fill, u32 r[8]) {
   for (int k = 0; k < 7; ++k) r[k] = fshr32(t[k + 1], t[k], b);
   r[7] = fshr32(fill, t[7], b);
 }
-// 16-limb result of x << s, s in [0,255]
-MW_HD void shl8to16(const u32 x[8], u32 s, u32 u[16]) {
-  u32 t[16];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    t[k] = x[k];
-    t[k + 8] = 0;
-  }
-  u32 q = s >> 5, b = s & 31;
-#pragma unroll
-  for (int st = 0; st < 3; ++st) {
-    int n = 1 << st;
-    bool c = (q >> st) & 1;
-#pragma unroll
-    for (int k = 15; k >= 0; --k) t[k] = c ? (k >= n ? t[k - n] : 0u) : t[k];
-  }
-#pragma unroll
-  for (int k = 15; k >= 1; --k) u[k] = fshl32(t[k], t[k - 1], b);
-  u[0] = t[0] << b;
-}
 
 // amount >= w ?  (amount is a w-bit canonical value held in 8 limbs)
 MW_HD bool amount_ge(const u32 b[8], u32 w) {
@@ -268,17 +248,6 @@ MW_HD void washr(const u32 a[8], const u32 b[8], u32 w, u32 r[8]) {
 
 // ---------------------------------------------------------------- division
 MW_HD u32 clz32(u32 x) { return x ? (u32)__builtin_clz(x) : 32u; }
-MW_HD u32 clz256(const u32 y[8]) {
-  u32 n = 0;
-  bool found = false;
-#pragma unroll
-  for (int k = 7; k >= 0; --k) {
-    u32 c = found ? 0u : clz32(y[k]);
-    n += c;
-    found = found || (y[k] != 0);
-  }
-  return n;
-}
 // Moller-Granlund reciprocal of a normalized divisor d (top bit set):
 // floor((2^64 - 1) / d) - 2^32, i.e. the 2-by-1 quotient (~d : 0xffffffff) / d.
 // On the device an f64 reciprocal (two Newton steps) gives the quotient to
@@ -310,58 +279,6 @@ MW_HD u32 recip32(u32 d) {
   return (u32)(~0ull / (u64)d - (1ull << 32));
 #endif
 }
-// (u1:u0) / d with u1 < d, d normalized, v = recip32(d)  (Moller & Granlund 2011, Alg. 4)
-MW_HD u32 div2by1(u32 u1, u32 u0, u32 d, u32 v) {
-  u64 q = (u64)v * u1 + ((((u64)u1) << 32) | u0);
-  u32 q1 = (u32)(q >> 32) + 1u, q0 = (u32)q;
-  u32 r = u0 - q1 * d;
-  bool adj1 = r > q0;
-  q1 = adj1 ? q1 - 1u : q1;
-  r = adj1 ? r + d : r;
-  bool adj2 = r >= d;
-  q1 = adj2 ? q1 + 1u : q1;
-  return q1;
-}
-// reciprocal for 3-by-2 division by (d1:d0), d1 normalized (Moller & Granlund 2011, Alg. 6)
-MW_HD u32 recip3by2(u32 d1, u32 d0) {
-  u32 v = recip32(d1);
-  u32 p = d1 * v + d0;
-  if (p < d0) {
-    v -= 1u;
-    const bool m = p >= d1;
-    p -= d1;
-    v -= m ? 1u : 0u;
-    p -= m ? d1 : 0u;
-  }
-  const u64 t = (u64)v * d0;
-  const u32 t1 = (u32)(t >> 32), t0 = (u32)t;
-  p += t1;
-  if (p < t1) {
-    v -= 1u;
-    if (p > d1 || (p == d1 && t0 >= d0)) v -= 1u;
-  }
-  return v;
-}
-// (u2:u1:u0) / (d1:d0) for (u2:u1) < (d1:d0): quotient digit, remainder (r1:r0)
-// (Moller & Granlund 2011, Alg. 5)
-MW_HD u32 div3by2(u32 u2, u32 u1, u32 u0, u32 d1, u32 d0, u32 v, u32& r1, u32& r0) {
-  const u64 q = (u64)v * u2 + ((((u64)u2) << 32) | u1);
-  u32 q1 = (u32)(q >> 32);
-  const u32 q0 = (u32)q;
-  const u32 r1a = u1 - q1 * d1;
-  const u64 D = (((u64)d1) << 32) | d0;
-  u64 r = ((((u64)r1a) << 32) | u0) - (u64)d0 * q1 - D;
-  q1 += 1u;
-  const bool a1 = (u32)(r >> 32) >= q0;
-  q1 = a1 ? q1 - 1u : q1;
-  r = a1 ? r + D : r;
-  const bool a2 = r >= D;  // unlikely
-  q1 = a2 ? q1 + 1u : q1;
-  r = a2 ? r - D : r;
-  r1 = (u32)(r >> 32);
-  r0 = (u32)r;
-  return q1;
-}
 
 // Quotient digit estimate for a full-width divisor (y7 != 0): from the top 64
 // bits of both operands, xh = x7:x6 and yh = y7:y6 >= 2^32, never below the true
@@ -392,11 +309,36 @@ MW_HD u32 qdigit_est(u32 x7, u32 x6, u32 y7, u32 y6) {
 #endif
 }
 
+// The same estimate for a three-limb window (w2:w1:w0) over a divisor whose top
+// limb y7 is nonzero (not necessarily normalised), when the window's digit is
+// below 2^32: (w2:w1:w0) is rounded up by 2^-50 (three roundings).
+MW_HD u32 qdigit_est3(u32 w2, u32 w1, u32 w0, u32 y7, u32 y6) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double two32 = 4294967296.0;
+  const double wd = __builtin_fma(__builtin_fma((double)w2, two32, (double)w1), two32, (double)w0);
+  const double yd = __builtin_fma((double)y7, two32, (double)y6);
+  const double A = (wd + 1.0) * (1.0 + 0x1p-50);
+  const double B = yd * (1.0 - 0x1p-51);
+  double rc = __builtin_amdgcn_rcp(B);
+  double e = __builtin_fma(-B, rc, 1.0);
+  rc = __builtin_fma(rc, e, rc);
+  e = __builtin_fma(-B, rc, 1.0);
+  rc = __builtin_fma(rc, e, rc);
+  const double Q = A * rc * (1.0 + 0x1p-48);
+  return Q >= 4294967295.0 ? 0xffffffffu : (u32)Q;
+#else
+  const unsigned __int128 W = ((unsigned __int128)w2 << 64) | ((unsigned __int128)w1 << 32) | w0;
+  const u64 yh = ((u64)y7 << 32) | y6;
+  const unsigned __int128 qe = (W + 1u) / yh;
+  return qe > 0xffffffffu ? 0xffffffffu : (u32)qe;
+#endif
+}
+
 // q = x / y, r = x % y when y's top limb is nonzero (y >= 2^224, so q < 2^32):
 // one estimated digit (qdigit_est, never too small), one multiply-subtract over
 // 9 limbs, and an add-back loop for the (rare) overestimate, run by a wave only
-// if one of its lanes needs it.  No normalisation shifts, 3-by-2 reciprocal or
-// digit loop: tools/ab_c5.py measured division at half of the C5 kernel's time.
+// if one of its lanes needs it.  No shifts and no digit loop: tools/ab_c5.py
+// measured division at half of the C5 kernel's time before this path.
 MW_HD void udivrem8_full(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
   u32 qd = qdigit_est(x[7], x[6], y[7], y[6]);
   u32 carry = 0, br = 0;
@@ -425,7 +367,7 @@ MW_HD void udivrem8_full(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
 // eight 2-by-1 steps (Moller & Granlund 2011, Alg. 4) with one reciprocal of
 // the normalised divisor; the remainder stays one limb throughout.  C5 divides
 // by such values (quotients of earlier divisions) in 42 of its 384 divisions,
-// where Knuth's loop ran all eight 3-by-2 steps.
+// where the general loop ran all eight steps.
 MW_HD void udivrem8_short(const u32 x[8], u32 y0, u32 q[8], u32 r[8]) {
   const u32 s = clz32(y0);
   const u32 d = y0 << s;
@@ -452,21 +394,16 @@ MW_HD void udivrem8_short(const u32 x[8], u32 y0, u32 q[8], u32 r[8]) {
   for (int k = 1; k < 8; ++k) r[k] = 0u;
 }
 
-// q = x / y, r = x % y for y != 0: Knuth Alg. D, base 2^32, fixed 8x8 shape
-// (the divisor is normalized to a full 8-limb value so every index is static),
-// with 3-by-2 quotient estimates (Moller-Granlund).  A digit estimate is at
-// most one too large, with probability ~2^-31, so the add-back runs under an
-// exec mask that is almost always empty (the wave skips it with one branch).
-// When the window's top two words equal the divisor's, the estimate B-1 is
-// exact (GMP mpn_sbpi1_div_qr) and the 3-word partial remainder is
-// (d1:d0) + u0: handled with selects, no separate path.
-//
-// Zero digits are skipped per wave: when the window's top limb is 0 and the
-// next one is below d1 (the divisor's normalized top limb), the window is
-// below the divisor, so the digit is 0 and the step would change nothing.
-// A wave runs a step only if some lane needs it (the quotient of two random
-// 256-bit values has one digit: one step of eight).  *steps (optional) counts
-// the steps the wave ran, for the executed-work roofline (bench.py).
+// q = x / y, r = x % y for y != 0, base-2^32 schoolbook division with one of
+// three paths per wave: a single estimated digit when every lane's divisor is
+// full width (udivrem8_full), short division when every lane's divisor is one
+// limb (udivrem8_short), and otherwise limb-aligned digits with the same
+// estimate (below).  Digit estimates are never too small and at most 2 too
+// large; the add-back runs under a wave-uniform branch that is almost never
+// taken.  Zero digits are skipped per wave: when the window's top limb is 0 and
+// the next one is below the divisor's top limb, the window is below the
+// divisor.  *steps (optional) counts the digit steps the wave ran, for the
+// executed-work roofline (bench.py).
 MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], u32* steps = nullptr) {
   if (!MW_ANY(y[7] == 0u)) {  // every lane's divisor is full width: one digit
     udivrem8_full(x, y, q, r);
@@ -480,78 +417,67 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], u32* ste
     if (steps) *steps += 1u;
     return;
   }
-  const u32 s = clz256(y);
-  // Normalisation shifts: with a full-width divisor (top limb nonzero in every
-  // lane of the wave, the common case) s < 32 and the limb-moving stages of
-  // the shifters are identities, so only the funnel shifts run.
-  const bool wide_shift = MW_ANY(s >= 32u);
-  u32 v[8];
-  u32 u[16];
-  if (wide_shift) {
-    shl8(y, s, v);
-    shl8to16(x, s, u);
-  } else {
+  // Any other divisor: schoolbook division on limb-aligned operands.  Both are
+  // shifted left by whole limbs (n = the divisor's zero top limbs, per lane)
+  // so the divisor's top limb is nonzero; no bit normalisation is needed,
+  // because each digit comes from the same upward-biased f64 estimate as the
+  // full-width path (qdigit_est3: never too small, at most 2 too large),
+  // followed by one multiply-subtract over 9 limbs and a wave-skipped
+  // add-back loop.  A digit position runs only if some lane of the wave has a
+  // nonzero digit there.  (Knuth's loop with 3-by-2 estimates, used until
+  // round 2, needed bit normalisation and cost about 1.5x as much per digit;
+  // tools/ab_c5.py put those 25 of C5's 384 divisions at 13 % of the kernel.)
+  const u32 n = y[7] ? 0u : y[6] ? 1u : y[5] ? 2u : y[4] ? 3u : y[3] ? 4u : y[2] ? 5u : y[1] ? 6u : 7u;
+  u32 v[8], u[16];
+  copy8(v, y);
 #pragma unroll
-    for (int k = 7; k >= 1; --k) v[k] = fshl32(y[k], y[k - 1], s);
-    v[0] = y[0] << s;
-    u[8] = fshl32(0u, x[7], s);
-#pragma unroll
-    for (int k = 7; k >= 1; --k) u[k] = fshl32(x[k], x[k - 1], s);
-    u[0] = x[0] << s;
-#pragma unroll
-    for (int k = 9; k < 16; ++k) u[k] = 0u;
+  for (int k = 0; k < 8; ++k) {
+    u[k] = x[k];
+    u[k + 8] = 0u;
   }
-  const u32 d1 = v[7], d0 = v[6];
-  const u32 vinv = recip3by2(d1, d0);
+#pragma unroll
+  for (int st = 0; st < 3; ++st) {  // v <<= 32n, u <<= 32n (limb moves under selects)
+    const int m = 1 << st;
+    const bool c = (n >> st) & 1u;
+#pragma unroll
+    for (int k = 7; k >= 0; --k) v[k] = c ? (k >= m ? v[k - m] : 0u) : v[k];
+#pragma unroll
+    for (int k = 15; k >= 0; --k) u[k] = c ? (k >= m ? u[k - m] : 0u) : u[k];
+  }
 #pragma unroll
   for (int j = 7; j >= 0; --j) {
-    const u32 u2 = u[j + 8], u1 = u[j + 7], u0 = u[j + 6];
     q[j] = 0u;
-    if (!MW_ANY(u2 != 0u || u1 >= d1)) continue;  // digit 0 in every lane: nothing to do
+    if (!MW_ANY(u[j + 8] != 0u || u[j + 7] >= v[7])) continue;  // digit 0 in every lane
     if (steps) *steps += 1u;
-    const bool sat = (u2 == d1) && (u1 == d0);
-    u32 r1, r0;
-    u32 qh = div3by2(u2, u1, u0, d1, d0, vinv, r1, r0);  // meaningless when sat
-    u32 c0 = 0;
-    const u32 s0 = addc(d0, u0, c0);
-    u32 r2 = 0;
-    const u32 s1 = addc(d1, 0u, c0);
-    qh = sat ? 0xffffffffu : qh;
-    r0 = sat ? s0 : r0;
-    r1 = sat ? s1 : r1;
-    r2 = sat ? c0 : 0u;
-    // u[j..j+5] -= qh * v[0..5]; the borrow out comes off (r2:r1:r0)
+    u32 qd = qdigit_est3(u[j + 8], u[j + 7], u[j + 6], v[7], v[6]);
     u32 carry = 0, br = 0;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const u64 p = (u64)qh * v[k] + carry;
+    for (int k = 0; k < 8; ++k) {
+      const u64 p = (u64)qd * v[k] + carry;
       carry = (u32)(p >> 32);
       u[j + k] = subb(u[j + k], (u32)p, br);
     }
-    const u64 R = (((u64)r1) << 32) | r0;
-    const u64 sub = (u64)carry + br;
-    const bool neg = (r2 == 0u) && (R < sub);
-    const u64 Rn = R - sub;
-    u[j + 6] = (u32)Rn;
-    u[j + 7] = (u32)(Rn >> 32);
-    u[j + 8] = 0u;
-    if (MW_ANY(neg)) {
-      if (neg) {  // estimate one too large: add the divisor back once
+    u32 hi = u[j + 8] - carry - br;  // 0, or the negative top limb when qd is too large
+    while (MW_ANY(hi != 0u)) {
+      if (hi != 0u) {
         u32 c = 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) u[j + k] = addc(u[j + k], v[k], c);
-        qh -= 1u;
+        hi += c;
+        qd -= 1u;
       }
     }
-    q[j] = qh;
+    u[j + 8] = 0u;
+    q[j] = qd;
   }
-  if (wide_shift) {
-    shr8(u, s, 0u, r);
-  } else {
 #pragma unroll
-    for (int k = 0; k < 7; ++k) r[k] = fshr32(u[k + 1], u[k], s);
-    r[7] = fshr32(u[8], u[7], s);
+  for (int st = 0; st < 3; ++st) {  // r = u[0..7] >> 32n
+    const int m = 1 << st;
+    const bool c = (n >> st) & 1u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) u[k] = c ? (k + m < 16 ? u[k + m] : 0u) : u[k];
   }
+  copy8(r, u);
 }
 
 MW_HD void neg8(const u32 a[8], u32 r[8]) {

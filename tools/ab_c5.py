@@ -23,6 +23,7 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             "abl_add": {"EXTRA_FLAGS": ["-DMW_ABLATE_ADD"]}, "abl_shift": {"EXTRA_FLAGS": ["-DMW_ABLATE_SHIFT"]},
             # code generation: two conjunct chains merged per basic block (jit.interleave_conjuncts)
             "il2": {"EXTRA_FLAGS": [], "interleave": 2},
+            "abl_knuth": {"EXTRA_FLAGS": ["-DMW_ABLATE_KNUTH"]}, "abl_fulldiv": {"EXTRA_FLAGS": ["-DMW_ABLATE_FULLDIV"]},
             # one wave per SIMD: 512 registers per lane, no leaves in LDS
             "w1": {"EXTRA_FLAGS": [], "waves": 1, "lds": 0}}
 
