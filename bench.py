@@ -9,10 +9,13 @@ step is one exhaustive search launch over a batch of candidate indices per GPU
 Candidates are generated on the device from the index (Philox4x32-10); the
 program is uploaded once before timing.
 
-Multi-GPU: one process per GPU (torchrun); rank r searches its own contiguous
-slice of the index space each step (weak scaling, no data-path collective);
-the per-step witness minimum is combined with one RCCL all-reduce(MIN) of a
-single int64, as the engine's multi-GPU search does (mythril_amd/distributed.py).
+Multi-GPU: one process per GPU; rank r searches its own contiguous slice of
+the index space each step (weak scaling, no data-path collective); the witness
+minimum is combined with one RCCL all-reduce(MIN) of a single int64, as the
+engine's multi-GPU search does (mythril_amd/distributed.py).  Ranks come from
+torchrun (WORLD_SIZE set: it must equal --gpus), or, when `--gpus N` is given
+without a torchrun environment, from N rank processes this script starts
+itself before anything here touches a GPU (launch_ranks).
 
 Prints ONE JSON line on rank 0.
 """
@@ -36,7 +39,15 @@ BENCH_SPLIT = False  # one kernel: 111.7M evals/s; as 5 part kernels (split_ssa)
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs, one rank process each (default: WORLD_SIZE under torchrun, else 1); without a "
+                         "torchrun environment N > 1 starts the N ranks itself")
+    ap.add_argument("--begin", type=int, default=0, help="first candidate index of warmup step 0")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI) on GPUs; gloo only with --host-emulator (CPU tests)")
+    # CPU tests of the rank plumbing: the host build of the interpreter stands in
+    # for the device (tests/fakedev.py); never a product or benchmark path
+    ap.add_argument("--host-emulator", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch-log2", type=int, default=22, help="candidates per GPU per step = 2**k")
@@ -44,6 +55,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ttfw", action="store_true", help="skip the time-to-first-witness search")
+    ap.add_argument("--ttfw-slice-log2", type=int, default=24, help="candidates per rank per stop-after-hit slice")
+    ap.add_argument("--ttfw-max-slices", type=int, default=128)
+    ap.add_argument("--ttfw-begin", type=int, default=0, help="first index of the time-to-first-witness sweep")
     ap.add_argument("--engine", choices=["jit", "interp"], default="jit",
                     help="jit: the program's specialised straight-line kernel (mythril_amd/jit.py); "
                          "interp: the bytecode interpreter")
@@ -61,23 +75,84 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without torchrun: start N rank processes (this same
+    script with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, as torchrun
+    would) and return the first failing exit code.  The parent never touches a
+    GPU (no HIP call, no torch.cuda), so nothing is exec'd from a process that
+    initialised one.  If a rank fails the others are stopped, so a dead peer
+    cannot leave them waiting in a collective."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None:
+        world = args.gpus or 1
+        if world > 1:
+            sys.exit(launch_ranks(world))
+    else:
+        world = int(world_env)
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.devices > 1 and world > 1:
+        # ADVICE r2: both would split the same candidates over overlapping GPUs
+        raise SystemExit("bench.py: --devices (one process, N GPUs) and ranks (one process per GPU) exclude each other")
+    if args.dist_backend == "gloo" and not args.host_emulator:
+        raise SystemExit("bench.py: gloo is for --host-emulator CPU tests; GPUs use nccl (RCCL)")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    coll_dev = "cpu" if args.host_emulator else f"cuda:{local}"
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        if not args.host_emulator:
+            torch.cuda.set_device(local)
+        dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
 
     from mythril_amd.compiler import compile_program
-    from mythril_amd.runtime import Device, unpack_trace
+    from mythril_amd.runtime import unpack_trace
     from mythril_amd.synth import build_c5
 
-    dev = Device(local)
+    if args.host_emulator:
+        from tests.fakedev import FakeDevice
+        dev = FakeDevice(chunk=1 << 12)
+        if args.engine != "interp":
+            raise SystemExit("bench.py: --host-emulator runs the interpreter only")
+    else:
+        from mythril_amd.runtime import Device
+        dev = Device(local)
     multi = None
     if args.devices > 1:
         from mythril_amd.multidev import MultiDevice
@@ -120,10 +195,10 @@ def main():
 
     def step(k):
         if multi is not None:   # one process: every device searches its slice of the step
-            begin = (k * args.devices * batch) % (1 << 62)
+            begin = (args.begin + k * args.devices * batch) % (1 << 62)
             (found,), st = multi.search([mdp], syn.seed, begin, batch * args.devices, 0)
             return found, st
-        begin = ((k * world + rank) * batch) % (1 << 62)
+        begin = (args.begin + (k * world + rank) * batch) % (1 << 62)
         (found,), st = dev.search([dp], syn.seed, begin, batch, 0)
         return found, st
 
@@ -133,9 +208,10 @@ def main():
     def barrier():
         if dist is not None:
             import torch
-            t = torch.zeros(1, device=f"cuda:{local}")
+            t = torch.zeros(1, device=coll_dev)
             dist.all_reduce(t)
-            torch.cuda.synchronize()
+            if not args.host_emulator:
+                torch.cuda.synchronize()
 
     barrier()
     kms = []
@@ -144,19 +220,21 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
         found, st = step(k)
-        kms.append(st["kernel_ms"])
-        dsteps.append(st["lane_div_steps"])
+        kms.append(st.get("kernel_ms", 0.0))
+        dsteps.append(st.get("lane_div_steps", 0))
         if found is not None:
             found_any = found if found_any is None else min(found_any, found)
     barrier()
     elapsed = time.perf_counter() - t0
+    rccl_world = 1
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        rccl_world = dist.get_world_size()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         from mythril_amd.distributed import allreduce_min
-        (found_any,) = allreduce_min([found_any], device=f"cuda:{local}")  # RCCL MIN of the witness index
+        (found_any,) = allreduce_min([found_any], device=coll_dev)  # RCCL MIN of the witness index
 
     total_evals = world * args.steps * batch * max(1, args.devices)
     value = total_evals / elapsed
@@ -164,15 +242,19 @@ def main():
     # executed algorithmic work per launch: the wide divisions' digit steps are
     # priced by the steps the kernel ran (zero digits are skipped per wave)
     ops_launch = prog.executed_ops(batch, sum(dsteps) / len(dsteps) / max(1, args.devices))
-    achieved = ops_launch / avg_kernel_s
+    achieved = ops_launch / avg_kernel_s if avg_kernel_s > 0 else 0.0
     measured_peak = load_measured_peak()
+
+    # time to first witness: every rank searches its share of each slice, and
+    # one all-reduce(MIN) per slice stops all of them at the first slice with a
+    # hit (the cross-rank early stop of SURVEY.md §8(e))
+    ttfw = None if args.no_ttfw else time_to_first_witness(dev, dp, syn.seed, args.ttfw_slice_log2, args.ttfw_max_slices,
+                                                                dist=dist, device=coll_dev, begin=args.ttfw_begin)
 
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
-
-    ttfw = None if args.no_ttfw else time_to_first_witness(dev, dp, syn.seed)
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:   # the CPU baseline is an N=1 figure
@@ -203,11 +285,16 @@ def main():
             "spill_slots": prog.n_spill,
             "engine": args.engine + (f" ({dp.kernel}, {args.jit_waves} wave/SIMD, {args.jit_lds_leaves} leaves in LDS, "
                                      f"interleave {args.jit_interleave}, split {jit.SPLIT_KIND})"
-                                     if dp.kernel else ""),
+                                     if getattr(dp, "kernel", None) else "")
+                      + (" [host emulator: CPU test of the rank plumbing, not a measurement]"
+                         if args.host_emulator else ""),
             "jit_compile_s": jit_s,
             "jit_split": bool(args.jit_split) if args.engine == "jit" else None,
             "parallelism": f"candidate-shard x{world}" + (f" (one process, {args.devices} devices)"
                                                           if args.devices > 1 else ""),
+            "rccl_world": rccl_world,
+            "dist_backend": args.dist_backend if dist is not None else None,
+            "candidate_begin": args.begin,
             "witness_found_in_timed_range": found_any,
             "time_to_first_witness": ttfw,
         },
@@ -217,7 +304,7 @@ def main():
             "peak": THEORETICAL_PEAK / 1e12,
             "unit": "Tops/s (u32)",
             "frac": achieved / THEORETICAL_PEAK,
-            "traffic": load_traffic(prog, batch, dp.kernel),
+            "traffic": load_traffic(prog, batch, getattr(dp, "kernel", None)),
             "kernel_ms_avg": avg_kernel_s * 1e3,
             "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (wave64 VALU op = 2 cycles)",
             "peak_measured": measured_peak / 1e12 if measured_peak else None,
@@ -235,21 +322,32 @@ def main():
         dist.destroy_process_group()
 
 
-def time_to_first_witness(dev, dp, seed, slice_log2=24, max_slices=128):
+def time_to_first_witness(dev, dp, seed, slice_log2=24, max_slices=128, dist=None, device=None, begin=0):
     """time until the lowest satisfying index in [0, ...) is
-    known, searching slices of 2^24 candidates in order with stop-after-hit (one
-    rank, outside the timed region), at most 2^31 candidates.  Reported next to
-    the exhaustive rate.  (C5's planted witness sits at index 0x5EED0005 mod 2^31
-    = 1 592 590 341 and its conjunct thresholds leave few others, so this times
-    a ~1.6 G-candidate sweep with stop-after-hit.)"""
+    known, searching slices of 2^24 candidates per rank in order with
+    stop-after-hit (outside the timed region), at most 2^31 candidates per rank.
+    Reported next to the exhaustive rate.  With N ranks, slice k is
+    [k N 2^24, (k+1) N 2^24), split into contiguous rank shards, and one
+    all-reduce(MIN) per slice ends the search on every rank at the first slice
+    holding a witness.  (C5's planted witness sits at index 0x5EED0005 mod 2^31
+    = 1 592 590 341 and its conjunct thresholds leave few others, so at N=1
+    this times a ~1.6 G-candidate sweep with stop-after-hit.)"""
     from mythril_amd import isa
+    from mythril_amd.distributed import shard_range
     flags = isa.FLAG_STOP_AFTER_HIT | isa.FLAG_EARLY_EXIT
+    world = dist.get_world_size() if dist is not None else 1
+    rank = dist.get_rank() if dist is not None else 0
+    span = (1 << slice_log2) * world
     t0 = time.perf_counter()
     for k in range(max_slices):
-        (found,), _ = dev.search([dp], seed, k << slice_log2, 1 << slice_log2, flags)
+        b, c = shard_range(begin + k * span, span, rank, world)
+        (found,), _ = dev.search([dp], seed, b, c, flags)
+        if dist is not None:
+            from mythril_amd.distributed import allreduce_min
+            (found,) = allreduce_min([found], device=device)
         if found is not None:
-            return {"seconds": time.perf_counter() - t0, "index": found, "candidates_searched": (k + 1) << slice_log2}
-    return {"seconds": time.perf_counter() - t0, "index": None, "candidates_searched": max_slices << slice_log2}
+            return {"seconds": time.perf_counter() - t0, "index": found, "candidates_searched": (k + 1) * span}
+    return {"seconds": time.perf_counter() - t0, "index": None, "candidates_searched": max_slices * span}
 
 
 def load_measured_peak():

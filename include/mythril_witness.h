@@ -18,7 +18,11 @@
  * message for the calling thread is in mg_last_error().  The caller owns all
  * host buffers (copied in/out); program handles are library-owned until
  * mg_prog_free.  Nothing throws across the ABI.  A context serialises its
- * calls.  Programs are validated on load (slot ranges, constant offsets,
+ * calls.  Lifetimes: the library keeps a registry of live contexts and
+ * programs.  mg_free also frees every program still loaded in that context;
+ * mg_prog_free / mg_free of a handle that is not live (already freed, freed
+ * with its context, or never returned by the library) return MG_E_ARG without
+ * touching it, and mg_search / mg_eval reject such program handles.  Programs are validated on load (slot ranges, constant offsets,
  * opcodes) so a malformed program can never be launched.
  */
 #ifndef MYTHRIL_WITNESS_H

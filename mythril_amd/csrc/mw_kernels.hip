@@ -16,6 +16,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/mythril_witness.h"
@@ -417,6 +418,31 @@ int launch_jit(mg_ctx* c, const mg_prog* p, u64 seed, u64 begin, u64 count, u32 
   return 0;
 }
 
+// Registry of live handles (include/mythril_witness.h, "Lifetimes"): a handle
+// is dereferenced only while it is registered, so freeing in the wrong order or
+// twice is an MG_E_ARG, never a use-after-free.
+std::mutex g_reg_mu;
+std::unordered_set<const mg_ctx*> g_ctxs;
+std::unordered_set<const mg_prog*> g_progs;
+
+bool ctx_live(const mg_ctx* c) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  return c && g_ctxs.count(c) != 0;
+}
+
+bool prog_live(const mg_prog* p) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  return p && g_progs.count(p) != 0;
+}
+
+// frees a program that has already left the registry
+void destroy_prog(mg_prog* p) {
+  hipSetDevice(p->ctx->dev);
+  p->unload();
+  if (p->d_buf) hipFree(p->d_buf);
+  delete p;
+}
+
 int ensure_spill(mg_ctx* c, size_t bytes) {
   if (bytes <= c->spill_bytes) return 0;
   if (c->d_spill) HIPCHK(hipFree(c->d_spill));
@@ -479,12 +505,32 @@ int mg_init(int device, mg_ctx** out) {
           hipSuccess) {
     (void)hipGetLastError();  // older runtimes: the default limit already covers it
   }
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_ctxs.insert(c);
+  }
   *out = c;
   return 0;
 }
 
 int mg_free(mg_ctx* c) {
   if (!c) return 0;
+  std::vector<mg_prog*> orphans;  // programs still loaded in this context: freed with it
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    if (!g_ctxs.erase(c)) return fail(MG_E_ARG, "mg_free: not a live context");
+    for (auto it = g_progs.begin(); it != g_progs.end();) {
+      if ((*it)->ctx == c) {
+        orphans.push_back(const_cast<mg_prog*>(*it));
+        it = g_progs.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  hipSetDevice(c->dev);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (mg_prog* p : orphans) destroy_prog(p);
   hipSetDevice(c->dev);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->d_spill) hipFree(c->d_spill);
@@ -502,6 +548,7 @@ int mg_free(mg_ctx* c) {
 int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
   if (!c || !d || !out) return fail(MG_E_ARG, "null argument");
   *out = nullptr;
+  if (!ctx_live(c)) return fail(MG_E_ARG, "mg_prog_load: not a live context");
   int rc = mg_validate_desc(d);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
@@ -541,22 +588,29 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
   p->desc.consts = nullptr;
   p->desc.leaves = nullptr;
   p->desc.pool = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_progs.insert(p);
+  }
   *out = p;
   return 0;
 }
 
 int mg_prog_free(mg_prog* p) {
   if (!p) return 0;
-  hipSetDevice(p->ctx->dev);
-  p->unload();
-  if (p->d_buf) hipFree(p->d_buf);
-  delete p;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    if (!g_progs.erase(p)) return fail(MG_E_ARG, "mg_prog_free: not a live program (already freed, or freed with its context)");
+  }
+  std::lock_guard<std::mutex> lk(p->ctx->mu);
+  destroy_prog(p);
   return 0;
 }
 
 int mg_prog_attach_kernel(mg_prog* p, const void* image, size_t size, const char* name) {
   if (!p || !image || !size || !name) return fail(MG_E_ARG, "null argument");
   if (std::strlen(name) > 200) return fail(MG_E_ARG, "kernel name too long");
+  if (!prog_live(p)) return fail(MG_E_ARG, "mg_prog_attach_kernel: not a live program");
   mg_ctx* c = p->ctx;
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
@@ -614,13 +668,19 @@ int mg_prog_attach_kernel(mg_prog* p, const void* image, size_t size, const char
   return 0;
 }
 
-int mg_prog_has_kernel(const mg_prog* p) { return p && p->jit_ready() ? 1 : 0; }
+int mg_prog_has_kernel(const mg_prog* p) { return prog_live(p) && p->jit_ready() ? 1 : 0; }
 
 int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uint64_t begin,
               uint64_t count, uint32_t flags, uint64_t* out_min_idx, mg_stats* st) {
   if (!c || !progs || !out_min_idx || nprog == 0) return fail(MG_E_ARG, "null argument");
   if (nprog > 65535) return fail(MG_E_ARG, "too many programs per launch");
   if (count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad candidate range");
+  {
+    std::lock_guard<std::mutex> rl(g_reg_mu);
+    if (!g_ctxs.count(c)) return fail(MG_E_ARG, "mg_search: not a live context");
+    for (size_t i = 0; i < nprog; ++i)
+      if (!g_progs.count(progs[i])) return fail(MG_E_ARG, "mg_search: program " + std::to_string(i) + " is not live");
+  }
   std::lock_guard<std::mutex> lk(c->mu);
   const double t0 = now_ms();
   HIPCHK(hipSetDevice(c->dev));
@@ -709,6 +769,7 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
 static int eval_common(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncand, uint64_t seed,
                        uint64_t begin, uint32_t* verdict, uint32_t* trace) {
   if (!c || !p || !verdict || ncand == 0) return fail(MG_E_ARG, "null argument");
+  if (!ctx_live(c) || !prog_live(p) || p->ctx != c) return fail(MG_E_ARG, "eval: not a live context/program pair");
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
   (void)hipGetLastError();  // clean error state before the launch below
@@ -746,6 +807,7 @@ static int eval_common(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, 
 
 int mg_eval(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncand, uint32_t* verdict,
             uint32_t* trace) {
+  if (p && !prog_live(p)) return fail(MG_E_ARG, "mg_eval: not a live program");
   if (p && p->desc.nleaves && p->desc.n_input_rows && !leaves_soa) return fail(MG_E_ARG, "leaves_soa required");
   if (p && p->desc.nleaves && !p->desc.n_input_rows) return fail(MG_E_ARG, "program has no input rows");
   static const u32 dummy = 0;
@@ -755,9 +817,11 @@ int mg_eval(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncan
 
 int mg_eval_generated(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, size_t count,
                       uint32_t* verdict, uint32_t* trace) {
-  if (!p || !p->jit_ready() || trace) return eval_common(c, p, nullptr, count, seed, begin, verdict, trace);
+  if (!p || !prog_live(p) || !p->jit_ready() || trace)
+    return eval_common(c, p, nullptr, count, seed, begin, verdict, trace);  // rejects dead handles
   // verdicts only, on the program's specialised kernel
   if (!c || !verdict || count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad argument");
+  if (!ctx_live(c) || p->ctx != c) return fail(MG_E_ARG, "eval: not a live context/program pair");
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
   int rc = ensure_min(c, 1);
@@ -783,6 +847,7 @@ int mg_eval_generated(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin
 
 int mg_valu_peak(mg_ctx* c, uint32_t mul, double* ops_per_s, double* kernel_ms) {
   if (!c || !ops_per_s) return fail(MG_E_ARG, "null argument");
+  if (!ctx_live(c)) return fail(MG_E_ARG, "not a live context");
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
   const u32 blocks = (u32)c->ncu * 8, iters = 4096;
@@ -804,6 +869,7 @@ int mg_valu_peak(mg_ctx* c, uint32_t mul, double* ops_per_s, double* kernel_ms) 
 int mg_keccak256_device(mg_ctx* c, const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len, size_t n,
                         uint8_t* d_out32, mg_stats* st) {
   if (!c || (!n)) return fail(MG_E_ARG, "bad argument");
+  if (!ctx_live(c)) return fail(MG_E_ARG, "not a live context");
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
   const double t0 = now_ms();
@@ -830,6 +896,7 @@ int mg_keccak256_device(mg_ctx* c, const uint8_t* d_data, const uint64_t* d_off,
 int mg_keccak256(mg_ctx* c, const uint8_t* data, size_t ndata, const uint64_t* off, const uint32_t* len, size_t n,
                  uint8_t* out32, mg_stats* st) {
   if (!c || !off || !len || !out32) return fail(MG_E_ARG, "null argument");
+  if (!ctx_live(c)) return fail(MG_E_ARG, "not a live context");
   if (n == 0) return 0;
   for (size_t i = 0; i < n; ++i)
     if (off[i] + len[i] > ndata) return fail(MG_E_ARG, "message out of range");

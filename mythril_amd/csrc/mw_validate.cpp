@@ -116,8 +116,11 @@ int mg_validate_desc(const mg_prog_desc* d) {
     const u32 iflags = (I[0] >> 8) & 0xffu;
     if (iflags) {   // only a W_CDINS chain link, followed by the W_CDINS that reads it as its acc
       const u32* N = I + 4;
+      // the link's result stays in registers and is never written back, so the
+      // consumer may read it only as its acc operand: a size operand naming the
+      // same slot would read the stale slot
       if (iflags != MW_FLAG_CHAIN || op != MW_W_CDINS || i + 1 >= n || (N[0] & 0xffu) != MW_W_CDINS ||
-          (N[1] >> 16) != MW_DST_W(dst))
+          (N[1] >> 16) != MW_DST_W(dst) || (N[2] & 0xffffu) == MW_DST_W(dst))
         return fail(MG_E_PROG, "bad instruction flags at " + std::to_string(i));
     }
     // dst = write targets (mw_prog.h): the file the op writes names a real slot,

@@ -49,12 +49,14 @@ PENDING_MAX = 64
 # Misses: get_model never caches UNSAT (the reference raises UnsatError, which
 # lru_cache does not keep), so LASER asks the same infeasible set again and
 # again.  A set the device already searched without a witness skips the device
-# the next time (z3 answers, as it would anyway), and so does any extension of
-# such a set by one conjunct (a JUMPI successor of an infeasible-looking state):
-# adding a constraint never creates a witness in the candidate space.
+# the next time (z3 answers, as it would anyway).  Extensions of a missed set
+# by one conjunct are searched again by default: prepare() re-harvests the
+# pools from the extended set, so a successor that pins a value (x == K) gets
+# an exact domain and can hit where its parent missed.
+# MYTHRIL_AMD_SKIP_MISS_PREFIX=1 skips them too (less device time, fewer hits).
 _misses: Dict[tuple, list] = {}          # z3 AST-id key -> raws (kept alive, eq-confirmed)
 MISS_MAX = 1 << 14
-SKIP_EXTENSIONS_OF_MISSES = os.environ.get("MYTHRIL_AMD_SKIP_MISS_PREFIX", "1") != "0"
+SKIP_EXTENSIONS_OF_MISSES = os.environ.get("MYTHRIL_AMD_SKIP_MISS_PREFIX", "0") == "1"
 
 
 def _env():

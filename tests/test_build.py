@@ -156,3 +156,37 @@ def test_cdins_chain_flag_set_and_validated():
     last = links[-1] + 1                                  # the chain's last link: next is not a W_CDINS
     p.code[4 * last] = int(p.code[4 * last]) | (isa.FLAG_CHAIN << 8)
     assert _validate(p) != 0
+
+
+def test_chain_link_result_read_as_size_is_rejected():
+    """a chain link's result stays in registers; a consumer that also
+    names that slot as its size operand would read the stale slot."""
+    from mythril_amd.smt2 import parse_file
+    from mythril_amd.engine import prepare
+    s = parse_file(os.path.join(ROOT, "tests", "golden", "solver_log", "c2_token_transfer_ok.smt2"))
+    p = prepare(s.asserts, s.ctx).program
+    code = p.code.copy().reshape(-1, 4)
+    k = next(k for k in range(len(code)) if (int(code[k][0]) >> 8) & 0xFF)
+    slot = isa.decode_dst(int(code[k][1]) & 0xFFFF)[0]
+    code[k + 1][2] = (int(code[k + 1][2]) & 0xFFFF0000) | slot
+    p.code = code.reshape(-1)
+    assert _validate(p) != 0
+
+
+def test_dead_handles_are_rejected_without_a_gpu():
+    """the library keeps a registry of live handles, so a
+    program freed with (or after) its context, a double free, or a foreign
+    pointer is an MG_E_ARG and is never dereferenced (checked here without a
+    GPU: no such handle can be live)."""
+    from mythril_amd.runtime import bind
+    lib = bind(ctypes.CDLL(LIB_PATH))
+    bogus = ctypes.c_void_p(0xDEAD0000)
+    assert lib.mg_prog_free(bogus) == -1
+    assert b"not a live program" in lib.mg_last_error()
+    assert lib.mg_free(bogus) == -1
+    assert b"not a live context" in lib.mg_last_error()
+    assert lib.mg_prog_has_kernel(bogus) == 0
+    out = (ctypes.c_uint64 * 1)()
+    arr = (ctypes.c_void_p * 1)(0xDEAD1000)
+    assert lib.mg_search(bogus, arr, 1, 0, 0, 1, 0, out, None) == -1
+    assert lib.mg_free(None) == 0 and lib.mg_prog_free(None) == 0

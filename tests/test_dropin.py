@@ -308,10 +308,12 @@ def test_stale_memo_entry_is_not_used(mythril):
     assert res.raw[0][1]["x"] == 9
 
 
-def test_repeated_miss_skips_the_device(mythril):
+def test_repeated_miss_skips_the_device(mythril, monkeypatch):
     """UNSAT is never cached by get_model (reference behaviour), so LASER asks an
-    infeasible set again: the second time, and for a one-conjunct extension of
-    it, the device is skipped and z3 answers directly (same results)."""
+    infeasible set again: the second time the device is skipped and z3 answers
+    directly (same results).  A one-conjunct extension is searched again by
+    default (its re-harvested pools may pin a value the parent lacked: ADVICE
+    r2), and skipped only with MYTHRIL_AMD_SKIP_MISS_PREFIX=1."""
     dropin._misses.clear()
     s0 = dropin._engine.stats["searches"]
     with pytest.raises(UnsatError):
@@ -319,14 +321,32 @@ def test_repeated_miss_skips_the_device(mythril):
     assert dropin._engine.stats["searches"] == s0 + 1
     with pytest.raises(UnsatError):
         dropin.get_model(UNSAT)
+    assert dropin._engine.stats["searches"] == s0 + 1
     ext = UNSAT + (fb(CTX.app("bvugt", X, CTX.const(3, 8))),)
     with pytest.raises(UnsatError):
         dropin.get_model(ext)
-    assert dropin._engine.stats["searches"] == s0 + 1
+    assert dropin._engine.stats["searches"] == s0 + 2      # default: the extension is searched
+    monkeypatch.setattr(dropin, "SKIP_EXTENSIONS_OF_MISSES", True)
+    ext2 = UNSAT + (fb(CTX.app("bvugt", X, CTX.const(4, 8))),)
+    with pytest.raises(UnsatError):
+        dropin.get_model(ext2)
+    assert dropin._engine.stats["searches"] == s0 + 2      # opt-in: skipped
     assert dropin.STATS["miss_skips"] >= 2
-    assert mythril.calls["reference"] == 3
+    assert mythril.calls["reference"] == 4
     # a satisfiable set is still searched
     assert dropin.get_model(SAT).raw[0][0] == "z3"
+
+
+def test_extension_that_pins_a_value_hits_where_its_parent_missed(mythril):
+    """x > 250 misses in a tiny budget of generated candidates, but
+    the extension x == 251 gets an exact pool and the device answers it."""
+    dropin._misses.clear()
+    parent = (fb(CTX.app("bvugt", X, CTX.const(250, 8))), fb(CTX.app("bvult", X, CTX.const(252, 8))))
+    ext = parent + (fb(CTX.app("=", X, CTX.const(251, 8))),)
+    praws = [c.raw for c in parent]
+    dropin._record_miss(praws, dropin.memo_key(praws))     # as if the device had missed the parent
+    r = dropin.get_model(ext)
+    assert r.raw[0][0] == "z3" and r.raw[0][1]["x"] == 251
 
 
 def test_minimize_hint_bounds_only_the_first_objective(mythril, monkeypatch):
