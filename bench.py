@@ -215,13 +215,13 @@ def main():
 
     barrier()
     kms = []
-    dsteps = []
+    dcounts = []
     found_any = None
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
         found, st = step(k)
         kms.append(st.get("kernel_ms", 0.0))
-        dsteps.append(st.get("lane_div_steps", 0))
+        dcounts.append(st)
         if found is not None:
             found_any = found if found_any is None else min(found_any, found)
     barrier()
@@ -239,9 +239,13 @@ def main():
     total_evals = world * args.steps * batch * max(1, args.devices)
     value = total_evals / elapsed
     avg_kernel_s = sum(kms) / len(kms) / 1e3
-    # executed algorithmic work per launch: the wide divisions' digit steps are
-    # priced by the steps the kernel ran (zero digits are skipped per wave)
-    ops_launch = prog.executed_ops(batch, sum(dsteps) / len(dsteps) / max(1, args.devices))
+    # executed algorithmic work per launch: every wide division priced by the
+    # path each wave took (mg_stats.lane_div_*; compiler.DIV_PRICE_*), and the
+    # division-free floor beside it
+    from mythril_amd.multidev import DIV_COUNTS
+    per_launch = {k: sum(st.get(k, 0) for st in dcounts) / len(dcounts) / max(1, args.devices) for k in DIV_COUNTS}
+    ops_launch = prog.executed_ops(batch, per_launch)
+    ops_floor = prog.executed_ops(batch, None)
     achieved = ops_launch / avg_kernel_s if avg_kernel_s > 0 else 0.0
     measured_peak = load_measured_peak()
 
@@ -280,7 +284,8 @@ def main():
             "candidates_per_gpu_step": batch,
             "ops_per_eval": prog.ops_per_eval,
             "ops_per_eval_executed": ops_launch / batch,
-            "division_steps_per_eval": (sum(dsteps) / len(dsteps)) / batch,
+            "ops_per_eval_floor": ops_floor / batch,
+            "division_paths_per_eval": {k[9:]: v / batch for k, v in per_launch.items()},
             "program_insns": prog.n_insn,
             "spill_slots": prog.n_spill,
             "engine": args.engine + (f" ({dp.kernel}, {args.jit_waves} wave/SIMD, {args.jit_lds_leaves} leaves in LDS, "
@@ -304,6 +309,9 @@ def main():
             "peak": THEORETICAL_PEAK / 1e12,
             "unit": "Tops/s (u32)",
             "frac": achieved / THEORETICAL_PEAK,
+            # no credit for any division (SURVEY §8(d) ops minus every wide division)
+            "frac_floor": (ops_floor / avg_kernel_s) / THEORETICAL_PEAK if avg_kernel_s > 0 else None,
+            "valu_issue_frac": valu_issue_frac(prog, batch, getattr(dp, "kernel", None), avg_kernel_s),
             "traffic": load_traffic(prog, batch, getattr(dp, "kernel", None)),
             "kernel_ms_avg": avg_kernel_s * 1e3,
             "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (wave64 VALU op = 2 cycles)",
@@ -360,11 +368,9 @@ def load_measured_peak():
         return None
 
 
-def load_traffic(prog, batch, kernel):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes for this
-    kernel and batch (profiles/pmc_traffic.json, written by tools/pmc_traffic.py:
-    (2 x FETCH_SIZE + WRITE_SIZE) x 1024, the gfx950 correction of
-    MI355X_MICROARCH.md §HBM), else None."""
+def load_pmc(prog, batch, kernel):
+    """The committed rocprofv3 PMC record for this kernel and batch
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), else None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
@@ -375,8 +381,25 @@ def load_traffic(prog, batch, kernel):
     name = d.get("kernel_name", "?")
     if d.get("ops_per_eval") == prog.ops_per_eval and d.get("batch") == batch and \
             kernel and (name == kernel or name.startswith(kernel + "_")):
-        return d.get("hbm_bytes_per_launch")
+        return d
     return None
+
+
+def load_traffic(prog, batch, kernel):
+    """HBM bytes per launch from the committed PMC passes: (2 x FETCH_SIZE +
+    WRITE_SIZE) x 1024, the gfx950 correction of MI355X_MICROARCH.md §HBM."""
+    d = load_pmc(prog, batch, kernel)
+    return d.get("hbm_bytes_per_launch") if d else None
+
+
+def valu_issue_frac(prog, batch, kernel, kernel_s, n_cu=256, clock_hz=2.4e9):
+    """VALU wave-instructions the committed PMC pass counted per launch, over
+    what the CUs can issue in the measured kernel time (2 wave64 VALU
+    instructions per CU-clock: 4 SIMDs, 2 cycles each), or None."""
+    d = load_pmc(prog, batch, kernel)
+    if not d or not d.get("sq_insts_valu_per_launch") or kernel_s <= 0:
+        return None
+    return d["sq_insts_valu_per_launch"] / (kernel_s * n_cu * clock_hz * 2.0)
 
 
 def cpu_baseline(syn, prog, budget_s, dev, dp):

@@ -72,10 +72,14 @@ typedef struct {
   uint64_t evals;        /* program x candidate verdicts determined */
   uint64_t launches;
   double ops;            /* algorithmic u32 ops executed (evals x ops_per_eval) */
-  uint64_t lane_div_steps; /* wide-division digit steps run x lanes running them: the
-                              division zero-digit skip (mw_alu.h udivrem8) makes the
-                              executed share of ops_per_eval data-dependent; bench.py
-                              prices the executed steps from this count */
+  /* Wide divisions (mw_alu.h udivrem8) take one of three paths per wave; each
+   * count is (events per wave) x (valid lanes of that wave), summed.  bench.py
+   * and compiler.Program.executed_ops price the executed division work from
+   * them (tests/test_gpu_divcount.py checks them against oracle/c). */
+  uint64_t lane_div_steps;    /* schoolbook digit positions run (some lane's digit nonzero) */
+  uint64_t lane_div_full;     /* one-digit path: every lane's divisor full width */
+  uint64_t lane_div_short;    /* short division: every lane's divisor one limb */
+  uint64_t lane_div_general;  /* limb-aligned schoolbook entries */
 } mg_stats;
 
 int mg_device_count(int* n);

@@ -122,13 +122,20 @@ class Program:
     stats: Dict[str, int] = field(default_factory=dict)
     ssa: List[MInsn] = field(default_factory=list)   # machine IR before slot allocation (jit.py)
 
-    def executed_ops(self, evals: int, lane_div_steps: int) -> float:
-        """Algorithmic u32 ops a search of `evals` candidates ran: ops_per_eval
-        with the wide divisions' digit steps priced by the steps the kernel
-        counted (mg_stats.lane_div_steps; zero digits are skipped per wave)."""
-        dso, dsm = self.stats.get("div_step_ops", 0), self.stats.get("div_steps_max", 0)
-        per_step = dso / dsm if dsm else 0.0
-        return evals * (self.ops_per_eval - dso) + lane_div_steps * per_step
+    def executed_ops(self, evals: int, st: Optional[dict] = None) -> float:
+        """Algorithmic u32 ops a search of `evals` candidates executed: ops_per_eval
+        with every wide division's nominal price (SURVEY §8(d) via node_cost)
+        replaced by the price of the path the kernel took, from the per-wave
+        counts it reports (mg_stats.lane_div_*, each x the wave's lanes):
+        DIV_PRICE_* below.  st=None gives the division-free floor (no credit
+        for any division)."""
+        floor = evals * (self.ops_per_eval - self.stats.get("div_nominal_ops", 0))
+        if not st:
+            return float(floor)
+        return float(floor + st.get("lane_div_full", 0) * DIV_PRICE_FULL
+                     + st.get("lane_div_short", 0) * DIV_PRICE_SHORT
+                     + st.get("lane_div_general", 0) * DIV_PRICE_GENERAL
+                     + st.get("lane_div_steps", 0) * DIV_PRICE_STEP)
 
     def input_rows_for(self, leaf_index: int) -> Tuple[int, int]:
         off = int(self.leaves[leaf_index * isa.LEAF_WORDS + isa.LEAF_INROW])
@@ -136,6 +143,23 @@ class Program:
 
 
 # --------------------------------------------------------------------------- cost model
+# Executed price of the three udivrem8 paths (csrc/mw_alu.h), in the units of
+# node_cost: a 32x32->64 product is 2 ops (lo, hi), add/sub with carry 2,
+# compare/select 1; the f64 digit estimates are not u32 work and are not
+# counted.  Every wide division runs on 8 limbs (L = 8).
+#   one digit step (multiply-subtract over 8 limbs + top-limb test): 6L + 2
+#   full-width divisor: one step                                      = 50
+#   one-limb divisor: 8 two-by-one steps of 14 ops, normalise/unshift = 115
+#   schoolbook entry: divisor limb count (7), limb shifts of v and u
+#     (3 stages x (8 + 16) selects), remainder unshift (3 x 8), zero-digit
+#     tests (8 x 2)                                                    = 119
+#   schoolbook digit step: as the full-width step                      = 50
+DIV_PRICE_STEP = 6 * 8 + 2
+DIV_PRICE_FULL = DIV_PRICE_STEP
+DIV_PRICE_SHORT = 8 * 14 + 3
+DIV_PRICE_GENERAL = 7 + 3 * (8 + 16) + 3 * 8 + 8 * 2
+
+
 def node_cost(n: Node) -> int:
     """Algorithmic u32 ops to evaluate one node once."""
     op = n.op
@@ -979,20 +1003,19 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
 
     reach = topo(conj + list(trace))
     ops = sum(node_cost(n) for n in reach)
-    # wide divisions: the digit-step part of their cost (all 8 steps of the fixed
-    # shape) and the step count; the kernels skip steps whose digit is 0 in every
-    # lane of a wave and count the steps they ran (mg_stats.lane_div_steps), so
-    # the executed work is ops_per_eval - div_step_ops + steps run x step cost
-    div_step_ops, div_steps_max = 0, 0
+    # wide divisions: their nominal price (without the signed ops' 4L sign
+    # handling, which always runs) is replaced by the executed path's price in
+    # Program.executed_ops
+    div_nominal_ops, n_div = 0, 0
     for n in reach:
         if n.op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod") and _w(n) > isa.NARROW_MAX:
             L = (_w(n) + 31) // 32
-            div_step_ops += L * (6 * L + 20)
-            div_steps_max += 8
+            div_nominal_ops += node_cost(n) - (4 * L if n.op in ("bvsdiv", "bvsrem", "bvsmod") else 0)
+            n_div += 1
     arr = lambda x: np.asarray(x if x else [0], dtype=np.uint32)
     stats = {"nodes": len(reach), "insns": len(code) // 4, "spills": sum(1 for i in insns if i.op.startswith("SPILL")),
              "fills": sum(1 for i in insns if i.op.startswith("FILL")),
-             "div_step_ops": div_step_ops, "div_steps_max": div_steps_max}
+             "div_nominal_ops": div_nominal_ops, "wide_divisions": n_div}
     return Program(code=np.asarray(code, dtype=np.uint32), consts=arr(consts),
                    leaves=np.asarray(leaf_words, dtype=np.uint32), pool=arr(pool_words),
                    n_spill=n_spill, n_trace_rows=rows, n_input_rows=in_row, ops_per_eval=ops,

@@ -402,19 +402,37 @@ MW_HD void udivrem8_short(const u32 x[8], u32 y0, u32 q[8], u32 r[8]) {
 // large; the add-back runs under a wave-uniform branch that is almost never
 // taken.  Zero digits are skipped per wave: when the window's top limb is 0 and
 // the next one is below the divisor's top limb, the window is below the
-// divisor.  *steps (optional) counts the digit steps the wave ran, for the
-// executed-work roofline (bench.py).
-MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], u32* steps = nullptr) {
+// divisor.  *dc (optional) counts the path the wave took and the digit steps
+// it ran, for the executed-work roofline (bench.py).
+// Per-wave division path counts for the executed-work roofline (bench.py,
+// compiler.Program.executed_ops): each field is incremented once per wave
+// (wave-uniform), and the kernels add nvalid x count to mg_stats.
+struct DivCount {
+  u32 full = 0;   // one-digit path (every lane's divisor full width)
+  u32 shrt = 0;   // short division (every lane's divisor one limb)
+  u32 gen = 0;    // limb-aligned schoolbook entries
+  u32 steps = 0;  // digit positions the schoolbook path ran (some lane's digit nonzero)
+};
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// counter[1..4] += nvalid x (steps, full, short, general): one lane per wave
+__device__ inline void add_div_counts(u64* counter, const DivCount& dc, u64 nvalid) {
+  if (dc.steps) atomicAdd((unsigned long long*)(counter + 1), (unsigned long long)(nvalid * dc.steps));
+  if (dc.full) atomicAdd((unsigned long long*)(counter + 2), (unsigned long long)(nvalid * dc.full));
+  if (dc.shrt) atomicAdd((unsigned long long*)(counter + 3), (unsigned long long)(nvalid * dc.shrt));
+  if (dc.gen) atomicAdd((unsigned long long*)(counter + 4), (unsigned long long)(nvalid * dc.gen));
+}
+#endif
+
+MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], DivCount* dc = nullptr) {
   if (!MW_ANY(y[7] == 0u)) {  // every lane's divisor is full width: one digit
     udivrem8_full(x, y, q, r);
-    if (steps) *steps += 1u;
+    if (dc) dc->full += 1u;
     return;
   }
   if (!MW_ANY((y[1] | y[2] | y[3] | y[4] | y[5] | y[6] | y[7]) != 0u)) {  // one-limb divisors
     udivrem8_short(x, y[0], q, r);
-    // eight one-limb digit steps are about one 8-limb step's work (the
-    // executed-work roofline prices a step at the 8-limb multiply-subtract)
-    if (steps) *steps += 1u;
+    if (dc) dc->shrt += 1u;
     return;
   }
   // Any other divisor: schoolbook division on limb-aligned operands.  Both are
@@ -427,6 +445,7 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], u32* ste
   // nonzero digit there.  (Knuth's loop with 3-by-2 estimates, used until
   // round 2, needed bit normalisation and cost about 1.5x as much per digit;
   // tools/ab_c5.py put those 25 of C5's 384 divisions at 13 % of the kernel.)
+  if (dc) dc->gen += 1u;
   const u32 n = y[7] ? 0u : y[6] ? 1u : y[5] ? 2u : y[4] ? 3u : y[3] ? 4u : y[2] ? 5u : y[1] ? 6u : 7u;
   u32 v[8], u[16];
   copy8(v, y);
@@ -448,7 +467,7 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], u32* ste
   for (int j = 7; j >= 0; --j) {
     q[j] = 0u;
     if (!MW_ANY(u[j + 8] != 0u || u[j + 7] >= v[7])) continue;  // digit 0 in every lane
-    if (steps) *steps += 1u;
+    if (dc) dc->steps += 1u;
     u32 qd = qdigit_est3(u[j + 8], u[j + 7], u[j + 6], v[7], v[6]);
     u32 carry = 0, br = 0;
 #pragma unroll
@@ -496,7 +515,7 @@ MW_HD void cneg8(u32 a[8], bool c, u32 w) {  // a = c ? -a mod 2^w : a
 }
 
 // kind: 0 udiv, 1 urem, 2 sdiv, 3 srem, 4 smod.  x, y are consumed (overwritten).
-MW_HD void wdiv(int kind, u32 x[8], u32 y[8], u32 w, u32 r[8], u32* steps = nullptr) {
+MW_HD void wdiv(int kind, u32 x[8], u32 y[8], u32 w, u32 r[8], DivCount* dc = nullptr) {
   bool sa = false, sb = false;
   if (kind >= 2) {
     sa = signbit8(x, w);
@@ -507,7 +526,7 @@ MW_HD void wdiv(int kind, u32 x[8], u32 y[8], u32 w, u32 r[8], u32* steps = null
   const bool yz = is_zero8(y);
   y[0] |= yz ? 1u : 0u;  // divide by 1 instead; result replaced below
   u32 q[8];
-  udivrem8(x, y, q, r, steps);  // r = |s| mod |t|
+  udivrem8(x, y, q, r, dc);  // r = |s| mod |t|
   if (yz) {  // SMT-LIB: q = all ones, r = dividend magnitude
 #pragma unroll
     for (int k = 0; k < 8; ++k) {

@@ -21,7 +21,7 @@ struct HostEnv {
   u32* trace;
   u64 ncand, idx, seed, cand;
   std::vector<u32>* spillv;
-  u32 dsteps = 0;  // division digit steps (one candidate at a time here)
+  DivCount dsteps;  // division paths (one candidate is one 'wave' here)
   void leaf(u32 li, u32 out[8]) {
     const u32* L = leaves + (u64)li * MW_LEAF_WORDS;
     if (in) {
@@ -67,6 +67,29 @@ int mwh_eval(const mg_prog_desc* d, const uint32_t* leaves_soa, uint64_t seed, u
   for (size_t i = 0; i < ncand; ++i) {
     HostEnv env{d->leaves, d->pool, leaves_soa, trace, (u64)ncand, (u64)i, seed, begin + i, &spill};
     verdict[i] = mw_run(code.data(), consts.data(), env, true, flags) ? 1u : 0u;
+  }
+  return 0;
+}
+
+// Division path counts (mw_alu.h DivCount) summed over generated candidates
+// [begin, begin+ncand): out = {general digit steps, full, short, general}, the
+// order of mg_stats.lane_div_*.  A host "wave" is one candidate.
+int mwh_div_counts(const mg_prog_desc* d, uint64_t seed, uint64_t begin, size_t ncand, uint64_t* out) {
+  int rc = mg_validate_desc(d);
+  if (rc) return rc;
+  std::vector<u32> consts(d->nconst_words + MW_KPAD, 0u);
+  if (d->nconst_words) std::memcpy(consts.data(), d->consts, d->nconst_words * 4);
+  std::vector<u32> code(d->ncode_words + 32, 0u);
+  std::memcpy(code.data(), d->code, d->ncode_words * 4);
+  std::vector<u32> spill;
+  for (int k = 0; k < 4; ++k) out[k] = 0;
+  for (size_t i = 0; i < ncand; ++i) {
+    HostEnv env{d->leaves, d->pool, nullptr, nullptr, (u64)ncand, (u64)i, seed, begin + i, &spill};
+    (void)mw_run(code.data(), consts.data(), env, true, 0u);
+    out[0] += env.dsteps.steps;
+    out[1] += env.dsteps.full;
+    out[2] += env.dsteps.shrt;
+    out[3] += env.dsteps.gen;
   }
   return 0;
 }

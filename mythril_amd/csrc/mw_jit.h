@@ -71,8 +71,8 @@ MW_HD void w_lshr(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { wlshr(x, y,
 MW_HD void w_ashr(const u32 x[8], const u32 y[8], u32 w, u32 r[8]) { washr(x, y, w, r); canon(r, w); }
 #endif
 // kind: 0 udiv, 1 urem, 2 sdiv, 3 srem, 4 smod (wdiv consumes its operands);
-// steps counts the digit steps the wave ran (udivrem8 zero-digit skip)
-MW_HD void w_div(int kind, const u32 x[8], const u32 y[8], u32 w, u32 r[8], u32& steps) {
+// dc counts the wave's division paths and digit steps (udivrem8)
+MW_HD void w_div(int kind, const u32 x[8], const u32 y[8], u32 w, u32 r[8], DivCount& dc) {
 #if defined(MW_ABLATE_DIV)
   xor8(x, y, r);
   return;
@@ -80,7 +80,7 @@ MW_HD void w_div(int kind, const u32 x[8], const u32 y[8], u32 w, u32 r[8], u32&
   u32 a[8], b[8];
   copy8(a, x);
   copy8(b, y);
-  wdiv(kind, a, b, w, r, &steps);
+  wdiv(kind, a, b, w, r, &dc);
   canon(r, w);
 }
 MW_HD void w_ite(u32 c, const u32 x[8], const u32 y[8], u32 w, u32 r[8]) {
@@ -277,7 +277,7 @@ MW_HD void tstore(u32* trace, u64 stride, u64 idx, u32 row, const u32* v, int n)
 #define JIT_SPLIT() ((void)ctl)
 #endif
 
-typedef bool (*body_fn)(const u32* __restrict__, u64, u64, bool, u32, u32*, u64, u64, u32&);
+typedef bool (*body_fn)(const u32* __restrict__, u64, u64, bool, u32, u32*, u64, u64, DivCount&);
 
 // stage bits of a launch: a program is one part (FIRST|LAST) or several parts
 // launched in order over the same candidates, passing each candidate's alive
@@ -310,11 +310,11 @@ __device__ __attribute__((always_inline)) inline void search(const u32* __restri
   const bool valid = cand < begin + count;
   bool in = valid;
   if (!(stage & MW_JIT_FIRST) && valid) in = alivebuf[cand - begin] != 0u;
-  u32 dsteps = 0;
-  const bool ok = BODY(pool, seed, cand, in, flags, nullptr, 0, 0, dsteps);
+  DivCount dc;
+  const bool ok = BODY(pool, seed, cand, in, flags, nullptr, 0, 0, dc);
   const u64 nvalid = (u64)__popcll(__ballot(valid));
-  if (lane == 0 && dsteps && nvalid)   // division digit steps x lanes (mg_stats.lane_div_steps)
-    atomicAdd((unsigned long long*)(counter + 1), (unsigned long long)(nvalid * dsteps));
+  if (lane == 0 && nvalid)   // division paths x lanes (mg_stats.lane_div_*)
+    add_div_counts(counter, dc, nvalid);
   if (!(stage & MW_JIT_LAST)) {
     if (valid) alivebuf[cand - begin] = ok ? 1u : 0u;
     return;

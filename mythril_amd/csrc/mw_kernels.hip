@@ -41,6 +41,7 @@ struct ProgDev {
 };
 
 constexpr int kBlock = 256;
+constexpr int kNCounters = 5;  // d_counter words: evals, then DivCount fields x lanes
 // Spill area: n_spill words per lane (a W spill slot is 8 consecutive words, an
 // N slot one; the compiler puts the most-used words first).  Words
 // [0, kLdsSpillWords) live in LDS as [word][lane] (consecutive lanes ->
@@ -58,7 +59,19 @@ typedef const __attribute__((address_space(3))) u32* lptr;
 __device__ __forceinline__ void leaf_value_lds(const u32* __restrict__ leaf_, lptr pool, u64 seed, u64 cand,
                                                u32 out[8]) {
   const __attribute__((address_space(4))) u32* leaf = (const __attribute__((address_space(4))) u32*)leaf_;
-  const u32 w = leaf[MW_LEAF_WIDTH], id = leaf[MW_LEAF_ID], kind = leaf[MW_LEAF_KIND];
+  const u32 w = leaf[MW_LEAF_WIDTH], id = leaf[MW_LEAF_ID];
+#if defined(MW_ABLATE_LEAF)
+  out[0] = (u32)cand ^ id;
+#pragma unroll
+  for (int k = 1; k < 8; ++k) out[k] = 0u;
+  canon(out, w);
+  return;
+#endif
+#if defined(MW_ABLATE_DIGIT)
+  const u32 kind = leaf[MW_LEAF_KIND] == 3u ? 1u : leaf[MW_LEAF_KIND];
+#else
+  const u32 kind = leaf[MW_LEAF_KIND];
+#endif
   if (kind >= 1u && kind <= 3u) {
     const u32 bits = leaf[MW_LEAF_BITS];
     u32 digit;
@@ -119,7 +132,7 @@ struct SearchEnv {
     }
   }
   __device__ bool none(bool alive) { return __ballot(alive) == 0ull; }
-  u32 dsteps = 0;  // division digit steps this wave ran (wave-uniform)
+  DivCount dsteps;  // division paths this wave took (wave-uniform)
 };
 
 struct EvalEnv {
@@ -165,7 +178,7 @@ struct EvalEnv {
     }
   }
   __device__ bool none(bool) { return false; }  // eval: never exit early
-  u32 dsteps = 0;
+  DivCount dsteps;
 };
 
 }  // namespace
@@ -189,7 +202,7 @@ __global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __r
   const u64 nthreads = (u64)gridDim.x * gridDim.y * kBlock;
   const u64 gtid = ((u64)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x;
   const u32 lane = threadIdx.x & 63u;
-  u64 evals = 0, lane_steps = 0;
+  u64 evals = 0, lsteps = 0, lfull = 0, lshort = 0, lgen = 0;   // division paths x lanes
   for (u64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const u64 base = begin + ch * kBlock;
     if (flags & MW_FLAG_STOP_AFTER_HIT) {
@@ -207,11 +220,17 @@ __global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __r
     }
     const u64 nvalid = (u64)__popcll(__ballot(valid));
     evals += nvalid;
-    lane_steps += nvalid * env.dsteps;
+    lsteps += nvalid * env.dsteps.steps;
+    lfull += nvalid * env.dsteps.full;
+    lshort += nvalid * env.dsteps.shrt;
+    lgen += nvalid * env.dsteps.gen;
   }
   if (lane == 0 && evals) {
     atomicAdd((unsigned long long*)counter, (unsigned long long)evals);
-    if (lane_steps) atomicAdd((unsigned long long*)(counter + 1), (unsigned long long)lane_steps);
+    if (lsteps) atomicAdd((unsigned long long*)(counter + 1), (unsigned long long)lsteps);
+    if (lfull) atomicAdd((unsigned long long*)(counter + 2), (unsigned long long)lfull);
+    if (lshort) atomicAdd((unsigned long long*)(counter + 3), (unsigned long long)lshort);
+    if (lgen) atomicAdd((unsigned long long*)(counter + 4), (unsigned long long)lgen);
   }
 }
 
@@ -313,7 +332,7 @@ struct mg_ctx {
   size_t spill_bytes = 0;
   u64* d_min = nullptr;
   size_t nmin = 0;
-  u64* d_counter = nullptr;   // [0] evals, [1] division digit steps x lanes (mg_stats)
+  u64* d_counter = nullptr;   // [0] evals, [1..4] division steps/full/short/general x lanes (mg_stats)
   u32* d_alive = nullptr;     // per-candidate alive bits between the parts of a split program
   size_t alive_cap = 0;
   ProgDev* d_progs = nullptr;
@@ -491,7 +510,7 @@ int mg_init(int device, mg_ctx** out) {
     c->ncu = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
-      hipMalloc(&c->d_counter, 2 * sizeof(u64)) != hipSuccess) {
+      hipMalloc(&c->d_counter, kNCounters * sizeof(u64)) != hipSuccess) {
     delete c;
     return fail(MG_E_HIP, "context setup failed");
   }
@@ -722,7 +741,7 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   }
   std::vector<u64> init(nprog, MG_NONE);
   HIPCHK(hipMemcpyAsync(c->d_min, init.data(), nprog * sizeof(u64), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemsetAsync(c->d_counter, 0, 2 * sizeof(u64), c->stream));
+  HIPCHK(hipMemsetAsync(c->d_counter, 0, kNCounters * sizeof(u64), c->stream));
   HIPCHK(hipEventRecord(c->e0, c->stream));
   if (ni) {
     // stage the pools in LDS when they fit beside the spill words (80 KiB per
@@ -745,10 +764,10 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
     if (rc) return rc;
   }
   HIPCHK(hipEventRecord(c->e1, c->stream));
-  u64 ctr[2] = {0, 0};
+  u64 ctr[kNCounters] = {0, 0, 0, 0, 0};
   std::vector<u64> mins(nprog);
   HIPCHK(hipMemcpyAsync(mins.data(), c->d_min, nprog * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(ctr, c->d_counter, 2 * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(ctr, c->d_counter, kNCounters * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
   const u64 evals = ctr[0];
   HIPCHK(hipStreamSynchronize(c->stream));
   for (size_t j = 0; j < ni; ++j) out_min_idx[interp[j]] = mins[j];
@@ -762,6 +781,9 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
     st->launches = (ni ? 1 : 0) + special.size();
     st->ops = (double)evals / (double)nprog * (double)ops;
     st->lane_div_steps = ctr[1];
+    st->lane_div_full = ctr[2];
+    st->lane_div_short = ctr[3];
+    st->lane_div_general = ctr[4];
   }
   return 0;
 }
@@ -830,7 +852,7 @@ int mg_eval_generated(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin
   if (hipMalloc(&d_v, count * 4) != hipSuccess) return fail(MG_E_NOMEM, "eval verdict alloc");
   const u64 none = MG_NONE;
   hipError_t e = hipMemcpyAsync(c->d_min, &none, sizeof(u64), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, 2 * sizeof(u64), c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, kNCounters * sizeof(u64), c->stream);
   if (e == hipSuccess) {
     rc = launch_jit(c, p, seed, begin, count, 0u, c->d_min, d_v);
     if (rc) {
@@ -889,6 +911,7 @@ int mg_keccak256_device(mg_ctx* c, const uint8_t* d_data, const uint64_t* d_off,
     st->launches = 1;
     st->ops = 0;
     st->lane_div_steps = 0;
+    st->lane_div_full = st->lane_div_short = st->lane_div_general = 0;
   }
   return 0;
 }

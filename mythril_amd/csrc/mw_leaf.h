@@ -45,7 +45,19 @@ MW_HD void philox4x32_10(u32 c[4], u32 k0, u32 k1) {
   }
 }
 
+// MW_ABLATE_* (timing experiments only, tools/leaf_ablate.py; wrong values):
+//   LEAF    every leaf is (u32)cand ^ id in limb 0 (no digit, gather or Philox)
+//   PHILOX  random leaves are one multiply-xor of the index (no Philox rounds)
+//   DIGIT   interleaved digits read as a plain bit-field (no per-bit loop)
 MW_HD void random_leaf(u32 id, u32 w, u64 seed, u64 cand, u32 out[8]) {
+#if defined(MW_ABLATE_PHILOX)
+  out[0] = ((u32)cand ^ id) * 0x9E3779B9u;
+  out[1] = ((u32)(cand >> 32) ^ id) * 0x85EBCA6Bu;
+#pragma unroll
+  for (int k = 2; k < 8; ++k) out[k] = out[k - 2] ^ (u32)seed;
+  canon(out, w);
+  return;
+#endif
   u32 k0 = (u32)seed ^ id, k1 = (u32)(seed >> 32);
   MW_LEAF_KEY_FENCE(k0);
   MW_LEAF_KEY_FENCE(k1);
@@ -76,6 +88,16 @@ MW_HD u64 fmix64(u64 h) {
 // them as literals).
 MW_HD void leaf_fields(u32 w, u32 kind, u32 id, u32 shift, u32 bits, u32 poff, u32 stride,
                        const u32* __restrict__ pool, u64 seed, u64 cand, u32 out[8]) {
+#if defined(MW_ABLATE_LEAF)
+  out[0] = (u32)cand ^ id;
+#pragma unroll
+  for (int k = 1; k < 8; ++k) out[k] = 0u;
+  canon(out, w);
+  return;
+#endif
+#if defined(MW_ABLATE_DIGIT)
+  if (kind == 3u) kind = 1u;
+#endif
   if (kind >= 1u && kind <= 3u) {
     u32 digit;
     if (kind == 3u) {
@@ -108,7 +130,18 @@ MW_HD void leaf_value(const u32* __restrict__ leaf_, const u32* __restrict__ poo
 #endif
   const u32 w = leaf[MW_LEAF_WIDTH];
   const u32 id = leaf[MW_LEAF_ID];
+#if defined(MW_ABLATE_LEAF)
+  out[0] = (u32)cand ^ id;
+#pragma unroll
+  for (int k = 1; k < 8; ++k) out[k] = 0u;
+  canon(out, w);
+  return;
+#endif
+#if defined(MW_ABLATE_DIGIT)
+  const u32 kind = leaf[MW_LEAF_KIND] == 3u ? 1u : leaf[MW_LEAF_KIND];
+#else
   const u32 kind = leaf[MW_LEAF_KIND];
+#endif
   if (kind >= 1u && kind <= 3u) {
     const u32 bits = leaf[MW_LEAF_BITS];
     u32 digit;

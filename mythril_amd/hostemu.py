@@ -34,6 +34,9 @@ def lib():
         L.mwh_eval.restype = ctypes.c_int
         L.mwh_eval.argtypes = [ctypes.POINTER(MgProgDesc), ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        L.mwh_div_counts.restype = ctypes.c_int
+        L.mwh_div_counts.argtypes = [ctypes.POINTER(MgProgDesc), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t,
+                                     ctypes.c_void_p]
         L.mg_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -48,6 +51,18 @@ def eval_generated(p: Program, seed: int, begin: int, n: int):
     if rc != 0:
         raise RuntimeError(lib().mg_last_error().decode())
     return v, t.reshape(max(p.n_trace_rows, 1), n)
+
+
+def div_counts(p: Program, seed: int, begin: int, n: int) -> dict:
+    """Division path counts (mg_stats.lane_div_* names) of the host build over
+    generated candidates [begin, begin+n); a host 'wave' is one candidate."""
+    d, keep = make_desc(p)
+    out = np.zeros(4, dtype=np.uint64)
+    rc = lib().mwh_div_counts(ctypes.byref(d), seed, begin, n, out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(lib().mg_last_error().decode())
+    return {"lane_div_steps": int(out[0]), "lane_div_full": int(out[1]), "lane_div_short": int(out[2]),
+            "lane_div_general": int(out[3])}
 
 
 def term_values(terms: Sequence, index: int, seed: int) -> List[int]:

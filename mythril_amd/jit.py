@@ -302,7 +302,7 @@ class _Gen:
         head = [f"template <bool EARLY>",
                 f"MW_HD bool {self.name}_body(const u32* __restrict__ pool, u64 seed, u64 cand, bool alive,",
                 f"                             u32 ctl, u32* __restrict__ trace, u64 tstride, u64 tidx,",
-                f"                             u32& dsteps) {{"]
+                f"                             DivCount& dsteps) {{"]
         consts = []
         for v, n in self.wconst.items():
             limbs = ", ".join(f"{(v >> (32 * k)) & M32:#x}u" for k in range(8))
@@ -529,7 +529,8 @@ def compile_host(progs: Sequence[Program], lds_leaves: int = 0,
 
 
 # extra device flags for experiments (tools/ab_c5.py ablations); empty in the product
-EXTRA_FLAGS: List[str] = []
+# experiments only (tools/leaf_ablate.py, tools/ab_c5.py): extra -D flags, part of the cache key
+EXTRA_FLAGS: List[str] = os.environ.get("MYTHRIL_AMD_JIT_FLAGS", "").split()
 
 
 def _device_flags(waves: int) -> List[str]:

@@ -30,6 +30,8 @@ import numpy as np
 
 from . import isa
 
+DIV_COUNTS = ("lane_div_steps", "lane_div_full", "lane_div_short", "lane_div_general")   # mg_stats
+
 
 class MultiProgram:
     """A program loaded on every device."""
@@ -89,7 +91,8 @@ class MultiDevice:
     def search(self, mps: Sequence[MultiProgram], seed: int, begin: int, count: int,
                flags: int = 0) -> Tuple[List[Optional[int]], dict]:
         found: List[Optional[int]] = [None] * len(mps)
-        stats = {"evals": 0, "kernel_ms": 0.0, "launches": 0, "rounds": 0, "lane_div_steps": 0}
+        stats = {"evals": 0, "kernel_ms": 0.0, "launches": 0, "rounds": 0}
+        stats.update({k: 0 for k in DIV_COUNTS})
         stop = bool(flags & isa.FLAG_STOP_AFTER_HIT)
         step = self.round_size * self.n if stop else count
         pos, end = begin, begin + count
@@ -103,8 +106,7 @@ class MultiDevice:
             def run(k):
                 b, c = slices[k]
                 if c == 0:
-                    return [None] * len(open_ix), {"evals": 0, "kernel_ms": 0.0, "launches": 0,
-                                                   "lane_div_steps": 0}
+                    return [None] * len(open_ix), {"evals": 0, "kernel_ms": 0.0, "launches": 0}
                 return self.devs[k].search([mps[i].parts[k] for i in open_ix], seed, b, c, flags)
             results = list(self.pool.map(run, range(self.n)))
             for j, i in enumerate(open_ix):
@@ -114,7 +116,8 @@ class MultiDevice:
             stats["evals"] += sum(r[1].get("evals", 0) for r in results)
             stats["kernel_ms"] = max(stats["kernel_ms"], 0.0) + max(r[1].get("kernel_ms", 0.0) for r in results)
             stats["launches"] += sum(r[1].get("launches", 0) for r in results)
-            stats["lane_div_steps"] += sum(r[1].get("lane_div_steps", 0) for r in results)
+            for k in DIV_COUNTS:
+                stats[k] += sum(r[1].get(k, 0) for r in results)
             stats["rounds"] += 1
             pos += n
             if not stop:

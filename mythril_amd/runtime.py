@@ -47,7 +47,8 @@ class MgProgDesc(ctypes.Structure):
 class MgStats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("wall_ms", ctypes.c_double),
                 ("evals", ctypes.c_uint64), ("launches", ctypes.c_uint64), ("ops", ctypes.c_double),
-                ("lane_div_steps", ctypes.c_uint64)]
+                ("lane_div_steps", ctypes.c_uint64), ("lane_div_full", ctypes.c_uint64),
+                ("lane_div_short", ctypes.c_uint64), ("lane_div_general", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

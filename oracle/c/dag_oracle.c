@@ -296,6 +296,116 @@ long long odag_eval_spec(const int32_t* nodes, int nn, const u32* consts, const 
   return r;
 }
 
+/* ---------------------------------------------------------------------------
+ * Division path counts (checks mg_stats.lane_div_* of the product kernels).
+ * The product's wide division (mythril_amd/csrc/mw_alu.h udivrem8, called as
+ * mw_alu.h wdiv does: dividend |s|, divisor |t| or 1 when t = 0, at the op's
+ * width) picks its path per wave of 64 lanes from these documented rules:
+ *   full    every lane's divisor has its top limb (7) nonzero
+ *   short   otherwise, every lane's divisor is one limb
+ *   general otherwise: both operands move up by n = (zero top limbs of the
+ *           divisor) limbs, and digit position j = 7..0 runs when some lane
+ *           has u[j+8] != 0 or u[j+7] >= v[7] for its current remainder u.
+ * Restated here from those rules (not from the product's code): the remainder
+ * above position j is R_j = (x << 32n >> 32(j+1)) mod v, so u[j+8] = R_j[7]
+ * and u[j+7] = R_j[6]; R is advanced one limb at a time by bit-serial
+ * reduction.  Waves are `wave` consecutive candidates from begin (the kernels'
+ * lane -> index map); out = {digit steps, full, short, general}, each x lanes. */
+static void div_operands(const onode* g, int i, const u32* V, u32* x, u32* y) {
+  const onode* nd = &g[i];
+  const u32* s = V + 8 * (size_t)nd->a;
+  const u32* t = V + 8 * (size_t)nd->b;
+  int w = nd->w;
+  if (nd->op == O_SDIV || nd->op == O_SREM || nd->op == O_SMOD) {
+    if (sgnbit(s, w)) neg(s, x, w); else memcpy(x, s, 32);
+    if (sgnbit(t, w)) neg(t, y, w); else memcpy(y, t, 32);
+  } else {
+    memcpy(x, s, 32);
+    memcpy(y, t, 32);
+  }
+  if (iszero(y)) y[0] = 1;
+}
+
+/* conds bit j: digit position j runs for this lane (general path) */
+static u32 general_conds(const u32* x, const u32* y) {
+  int n = 0;
+  while (n < 7 && y[7 - n] == 0) ++n;
+  u32 v[8] = {0}, u[16] = {0}, R[8];
+  for (int k = 0; k + n < 8; ++k) v[k + n] = y[k];
+  for (int k = 0; k < 8; ++k) u[k + n] = x[k];
+  memcpy(R, u + 8, 32);
+  u32 conds = 0;
+  for (int j = 7; j >= 0; --j) {
+    if (R[7] != 0 || R[6] >= v[7]) conds |= 1u << j;
+    for (int b = 31; b >= 0; --b) {   /* R = (R * 2^32 + u[j]) mod v, one bit at a time */
+      u32 carry = R[7] >> 31;
+      shl1(R);
+      R[0] |= (u[j] >> b) & 1u;
+      if (carry || cmpu(R, v) >= 0) sub(R, v, R);
+    }
+  }
+  return conds;
+}
+
+long long odag_div_paths(const int32_t* nodes, int nn, const u32* consts, const int32_t* specs, const u32* pool,
+                         u64 seed, u64 begin, u64 n, int wave, int nthreads, u64* out) {
+  const onode* g = (const onode*)nodes;
+  int ndiv = 0;
+  int* divs = (int*)malloc(sizeof(int) * (size_t)(nn + 1));
+  for (int i = 0; i < nn; ++i)
+    if (g[i].op >= O_UDIV && g[i].op <= O_SMOD && g[i].w > 32) divs[ndiv++] = i;
+  if (wave < 1) wave = 1;
+  g_specs = (const ospec*)specs;
+  g_pool = pool;
+  u64 steps = 0, full = 0, shrt = 0, gen = 0;
+  const long long nwaves = (long long)((n + (u64)wave - 1) / (u64)wave);
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel reduction(+ : steps, full, shrt, gen)
+  {
+    u32* V = (u32*)malloc(sizeof(u32) * 8 * (size_t)nn);
+    u32* X = (u32*)malloc(sizeof(u32) * 8 * (size_t)(ndiv + 1) * (size_t)wave);
+    u32* Y = (u32*)malloc(sizeof(u32) * 8 * (size_t)(ndiv + 1) * (size_t)wave);
+#pragma omp for schedule(dynamic, 4)
+    for (long long wv = 0; wv < nwaves; ++wv) {
+      const u64 first = begin + (u64)wv * (u64)wave;
+      u64 lanes = n - (u64)wv * (u64)wave;
+      if (lanes > (u64)wave) lanes = (u64)wave;
+      /* every lane of the wave runs (lanes past the range too: their index is
+       * evaluated, only valid lanes are counted) */
+      for (int l = 0; l < wave; ++l) {
+        const u64 cand = first + (u64)l;
+        for (int i = 0; i < nn; ++i) eval1(g, consts, i, V, seed, cand);
+        for (int d = 0; d < ndiv; ++d)
+          div_operands(g, divs[d], V, X + 8 * ((size_t)d * wave + l), Y + 8 * ((size_t)d * wave + l));
+      }
+      for (int d = 0; d < ndiv; ++d) {
+        const u32* Yd = Y + 8 * (size_t)d * wave;
+        const u32* Xd = X + 8 * (size_t)d * wave;
+        int all_full = 1, all_short = 1;
+        for (int l = 0; l < wave; ++l) {
+          const u32* yl = Yd + 8 * l;
+          if (yl[7] == 0) all_full = 0;
+          for (int k = 1; k < 8; ++k) if (yl[k]) all_short = 0;
+        }
+        if (all_full) { full += lanes; continue; }
+        if (all_short) { shrt += lanes; continue; }
+        gen += lanes;
+        u32 any = 0;
+        for (int l = 0; l < wave; ++l) any |= general_conds(Xd + 8 * l, Yd + 8 * l);
+        steps += lanes * (u64)__builtin_popcount(any);
+      }
+    }
+    free(V); free(X); free(Y);
+  }
+  g_specs = 0;
+  g_pool = 0;
+  free(divs);
+  out[0] = steps; out[1] = full; out[2] = shrt; out[3] = gen;
+  return ndiv;
+}
+
 int odag_max_threads(void) {
 #ifdef _OPENMP
   return omp_get_max_threads();

@@ -43,6 +43,10 @@ def lib():
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                      ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_uint64)]
+        L.odag_div_paths.restype = ctypes.c_longlong
+        L.odag_div_paths.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.odag_max_threads.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -211,6 +215,26 @@ def evaluate(conjuncts, seed: int, begin: int, n: int, nthreads: int = 0, want_v
                                 seed, begin, n, v.ctypes.data if v is not None else None, nthreads,
                                 ctypes.byref(first))
     return total, (None if first.value == (1 << 64) - 1 else first.value), v
+
+
+def div_paths(conjuncts, seed: int, begin: int, n: int, wave: int = 64, nthreads: int = 0, specs=None):
+    """Division path counts of the product's kernels, restated from udivrem8's
+    documented per-wave rules (dag_oracle.c odag_div_paths): a dict in
+    mg_stats' names (lane_div_steps / _full / _short / _general, each x lanes)
+    for candidates [begin, begin+n) in waves of `wave` consecutive indices."""
+    s = Serialized(specs)
+    for c in conjuncts:
+        s.term(c)
+    nodes = np.asarray(s.nodes, dtype=np.int32).reshape(-1)
+    consts = np.asarray(s.consts or [[0] * 8], dtype=np.uint32).reshape(-1)
+    sp = np.asarray(s.spec_rows or [[0] * 5], dtype=np.int32).reshape(-1)
+    pool = np.asarray(s.pool or [0], dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint64)
+    lib().odag_div_paths(nodes.ctypes.data, len(s.nodes), consts.ctypes.data,
+                         sp.ctypes.data if s.spec_rows else None, pool.ctypes.data, seed, begin, n, wave, nthreads,
+                         out.ctypes.data)
+    return {"lane_div_steps": int(out[0]), "lane_div_full": int(out[1]), "lane_div_short": int(out[2]),
+            "lane_div_general": int(out[3])}
 
 
 def baseline(syn, prog, budget_s: float = 10.0, verdicts: bool = False):

@@ -132,3 +132,39 @@ def test_solver_log_verdict_sweep(name, dev):
         assert np.array_equal(vj.astype(np.uint8), vo), name
     if name.startswith("c3"):
         assert p.n_spill > 10, "C3 exercises the global spill path"
+
+
+DIV_KEYS = ("lane_div_steps", "lane_div_full", "lane_div_short", "lane_div_general")
+
+
+def test_c5_division_path_counts_match_oracle(c5, dev):
+    """the counts the executed-work roofline is priced from
+    (mg_stats.lane_div_*) equal oracle/c's restatement of udivrem8's per-wave
+    path rules, on both tiers, over an exhaustive 2^16 sweep."""
+    dens, syn, prog, special, interp = c5
+    t0 = time.perf_counter()
+    orc = cdag.div_paths(syn.conjuncts, syn.seed, 0, SWEEP, wave=64)
+    _log(f"density {dens}: oracle/c division paths in {time.perf_counter() - t0:.2f} s: {orc}")
+    for dp in (special, interp):
+        _, st = dev.search([dp], syn.seed, 0, SWEEP, 0)
+        got = {k: st[k] for k in DIV_KEYS}
+        assert got == orc, (dp.kernel, got, orc)
+    assert orc["lane_div_full"] + orc["lane_div_short"] + orc["lane_div_general"] == \
+        prog.stats["wide_divisions"] * SWEEP
+
+
+def test_division_dag_path_counts_match_oracle(dev):
+    """Every path, signed and unsigned, zero divisors, a 160-bit division: the
+    interpreter's 64-lane wave counts equal the oracle's (tests/test_divcount.py
+    checks the host build with one-candidate waves)."""
+    from tests.test_divcount import _division_dag
+    conj = _division_dag()
+    p = compile_program(conj)
+    dp = dev.load(p)
+    try:
+        _, st = dev.search([dp], 0x5EED, 0, SWEEP, 0)
+    finally:
+        dp.free()
+    orc = cdag.div_paths(conj, 0x5EED, 0, SWEEP, wave=64)
+    assert {k: st[k] for k in DIV_KEYS} == orc
+    assert orc["lane_div_general"] > 0 and orc["lane_div_steps"] > 0

@@ -2,7 +2,7 @@
 """HBM traffic per launch of the benchmarked kernel from rocprofv3 PMC passes.
 
     python tools/pmc_traffic.py FETCH.csv WRITE.csv --kernel mwj_<sig> \
-        --ops-per-eval N --batch B [--out profiles/pmc_traffic.json]
+        --ops-per-eval N --batch B [--valu-csv SQ.csv] [--out profiles/pmc_traffic.json]
 
 FETCH_SIZE and WRITE_SIZE come from separate `--pmc` passes (they do not fit
 one pass: MI355X_MICROARCH.md counter table) and are in KiB.  On gfx950
@@ -11,7 +11,9 @@ FETCH_SIZE counts half of the bytes of a wide coalesced read, so
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
 
 (cdna_hip_programming.md counter pitfalls; MI355X_MICROARCH.md §HBM), averaged
-over the dispatches of the named kernel.
+over the dispatches of the named kernel.  --valu-csv (a pass holding
+SQ_INSTS_VALU and SQ_WAVES) adds the VALU wave-instructions per launch, from
+which bench.py reports the VALU issue fraction (issued / 2.0 per CU-clock).
 """
 import argparse
 import csv
@@ -38,6 +40,7 @@ def main():
     ap.add_argument("--batch", type=int, required=True)
     ap.add_argument("--out", default=None)
     ap.add_argument("--note", default="")
+    ap.add_argument("--valu-csv", default=None)
     a = ap.parse_args()
     fetch = per_dispatch(a.fetch_csv, "FETCH_SIZE", a.kernel)
     write = per_dispatch(a.write_csv, "WRITE_SIZE", a.kernel)
@@ -56,6 +59,12 @@ def main():
                   "of streamed reads: MI355X_MICROARCH.md §HBM)",
         "sources": [a.fetch_csv, a.write_csv],
     }
+    if a.valu_csv:
+        valu = per_dispatch(a.valu_csv, "SQ_INSTS_VALU", a.kernel)
+        waves = per_dispatch(a.valu_csv, "SQ_WAVES", a.kernel)
+        rec["sq_insts_valu_per_launch"] = sum(valu) / len(valu)
+        rec["sq_waves_per_launch"] = sum(waves) / len(waves)
+        rec["sources"].append(a.valu_csv)
     if a.note:
         rec["note"] = a.note
     s = json.dumps(rec, indent=1)
