@@ -332,6 +332,10 @@ def prefetch(constraint_sets) -> int:
                 _memo.clear()
             _memo[key] = (raws, w, script)
             n += 1
+        else:
+            # searched with the same budget get_model would use: its is_possible
+            # goes straight to the reference instead of searching again
+            _record_miss(raws, key)
     return n
 
 

@@ -11,10 +11,9 @@ registers two batching hooks:
 
 * ``stop_sym_trans`` (``svm.py:243-245``): right before the next
   transaction's reachability prune over ``open_states`` (``svm.py:216-223``)
-  every open state's constraint set is searched in ONE launch;
-  and the likely concrete Keccak preimages of the next transaction (mapping
-  entries and array bases of the actors and accounts, low slots) are hashed
-  in ONE launch of the Keccak kernel;
+  every open state's constraint set is searched in ONE launch (and, opt-in,
+  likely concrete Keccak preimages of the next transaction are hashed in one
+  launch: see KECCAK_SPECULATION);
 * a JUMPI post hook (``svm.py:_execute_post_hook``, run on each successor):
   the successors are queued, and the first per-step ``is_possible``
   (``svm.py:287-292``) searches the pair in one launch.
@@ -27,6 +26,7 @@ order is untouched.  It also installs the batched Keccak-256 service
 from __future__ import annotations
 
 import logging
+import os
 
 log = logging.getLogger(__name__)
 
@@ -41,6 +41,12 @@ except Exception:  # pragma: no cover - exercised only where mythril is installe
 
 
 SLOTS = 16   # storage slots whose mapping entries / array bases are prefetched
+# Speculative mapping-slot hashing at each transaction boundary, OFF by default:
+# replayed in LASER's order over the corpus (tests/laser_replay.py), LASER made
+# no concrete SHA3 request at all (sender_N is symbolic, so keccak(sender .
+# slot) is the keccak256_512 UF, keccak_function_manager.py:104-114), so every
+# speculated digest was wasted.  The memo still serves repeated concrete hashes.
+KECCAK_SPECULATION = os.environ.get("MYTHRIL_AMD_KECCAK_SPECULATION", "0") == "1"
 
 
 def storage_keys(symbolic_vm) -> list:
@@ -73,12 +79,13 @@ class WitnessBatchingLaserPlugin(_LaserPlugin):
                          len(symbolic_vm.open_states))
             except Exception as e:  # never disturb the analysis
                 log.warning("witness engine prefetch skipped: %s", e)
-            try:
-                svc = keccak_service.service()
-                if svc is not None:
-                    svc.prefetch_storage_slots(storage_keys(symbolic_vm), range(SLOTS))
-            except Exception as e:  # never disturb the analysis
-                log.debug("keccak prefetch skipped: %s", e)
+            if KECCAK_SPECULATION:
+                try:
+                    svc = keccak_service.service()
+                    if svc is not None:
+                        svc.prefetch_storage_slots(storage_keys(symbolic_vm), range(SLOTS))
+                except Exception as e:  # never disturb the analysis
+                    log.debug("keccak prefetch skipped: %s", e)
 
         symbolic_vm.register_laser_hooks("stop_sym_trans", prefetch_open_states)
 

@@ -78,6 +78,7 @@ class Query:
     taken: bool                    # the successor the concrete path follows
     constraints: List[Node]        # world-state constraints + keccak conditions
     sat: Optional[bool]            # True for the followed successor; None = unknown
+    keccak_cond: Optional[Node] = None   # the manager's conditions: the last element of constraints
 
 
 @dataclass
@@ -85,6 +86,7 @@ class Run:
     queries: List[Query] = field(default_factory=list)
     model: Dict = field(default_factory=dict)
     halts: List[str] = field(default_factory=list)
+    keccaks: List[Tuple[int, int, int, int]] = field(default_factory=list)   # (tx, queries so far, bits, value)
 
 
 class ConcolicLaser:
@@ -180,6 +182,9 @@ class ConcolicLaser:
         interval value (lower + 64 k, distinct per input) so that the model also
         satisfies create_conditions."""
         if data.op == "const":
+            # LASER hashes concrete data on the spot (find_concrete_keccak): logged
+            # with its position among the queries for tests/laser_replay.py
+            self.run_log.keccaks.append((self.tx, len(self.run_log.queries), data.width, data.val))
             return self.km.create_keccak(data)
         n = data.width
         fx = self.km.create_keccak(data)
@@ -372,8 +377,11 @@ class ConcolicLaser:
                         if succ is pos and dest not in self.jumpdests:
                             continue
                         self.constraints = base + [succ]
-                        self.run_log.queries.append(Query(self.tx, pc - 1, follow, self.query_set(),
-                                                          True if follow else None))
+                        qset = self.query_set()
+                        kc = qset[-1] if len(qset) > len([x for x in self.constraints
+                                                          if not (x.op == "const" and x.val)]) else None
+                        self.run_log.queries.append(Query(self.tx, pc - 1, follow, qset,
+                                                          True if follow else None, kc))
                     self.constraints = base + [pos if taken else neg]
                 if taken:
                     if dest not in self.jumpdests:

@@ -54,6 +54,7 @@ def test_verdict_sweep_matches_oracle(queries, eng):
 def test_search_at_c2_count(queries, eng):
     found = {"sat": 0, "unknown": 0}
     total = {"sat": 0, "unknown": 0}
+    missed = []
     for i in range(0, len(queries), 64):
         chunk = queries[i:i + 64]
         ws = eng.search([q for _, _, q in chunk], count=1 << 24)
@@ -62,5 +63,7 @@ def test_search_at_c2_count(queries, eng):
             if w is not None:
                 assert holds(s.asserts, w), m["file"]
                 found[m["status"]] += 1
-    print(f"LASER corpus at 2^24: witnessed {found} of {total}")
+            elif m["status"] == "sat":
+                missed.append(m["file"])
+    print(f"LASER corpus at 2^24: witnessed {found} of {total}; SAT missed: {missed}")
     assert found["sat"] >= 0.9 * total["sat"], (found, total)

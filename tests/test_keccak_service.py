@@ -289,6 +289,7 @@ def test_transaction_boundary_prefetch_then_memo_hits(monkeypatch):
             pass
 
     vm = VM()
+    monkeypatch.setattr(mythril_plugin, "KECCAK_SPECULATION", True)   # opt-in (off by default)
     mythril_plugin.WitnessBatchingLaserPlugin().initialize(vm)
     n_before = getattr(dev, "keccak_launches", 0)
     ref_before = calls["n"]

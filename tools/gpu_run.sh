@@ -17,6 +17,7 @@
 #   keccak         tools/keccak_bench.py
 #   ipmc=FILE      PMC passes on one exhaustive interpreter launch of FILE (tools/interp_once.py)
 #   opcost         tools/interp_opcost.py (+ one PMC pass: instructions per bytecode op)
+#   ablate         tools/leaf_ablate.py --run (candidate-generation ablations, C2/C2L/C4)
 #   recip          tools/exp/recip_check (device reciprocal vs u64 division; built by hand)
 # Outputs land in gpurun_out/TAG/.
 set -o pipefail
@@ -102,6 +103,9 @@ for step in "$@"; do
       run 200 "$OUT/opcost_pmc.log" timeout -s KILL 190 rocprofv3 --pmc SQ_WAVES,SQ_WAVE_CYCLES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_SMEM,SQ_INSTS_BRANCH,SQ_WAIT_INST_ANY,SQ_WAIT_ANY \
         --output-format csv -d "$OUT/opcost_pmc" -o run -- python3 tools/interp_opcost.py --log2 18
       find "$OUT/opcost_pmc" -name "*counter_collection*" ;;
+    ablate)
+      run 1200 "$OUT/ablate.log" python3 tools/leaf_ablate.py --run "$OUT/ablate"
+      tail -30 "$OUT/ablate.log" ;;
     recip)
       run 120 "$OUT/recip.txt" ./tools/exp/recip_check
       tail -4 "$OUT/recip.txt" ;;
