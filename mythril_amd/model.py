@@ -209,6 +209,12 @@ def _gpu_model(constraints, timeout):
 
 
 MINIMIZE_HINTS = os.environ.get("MYTHRIL_AMD_MINIMIZE_HINTS", "0") == "1"
+MINIMIZE_ROUNDS = int(os.environ.get("MYTHRIL_AMD_MINIMIZE_ROUNDS", "8"))   # device descent searches
+
+
+def _walk(roots):
+    from .ir import topo
+    return topo(list(roots))
 
 
 def _minimize_hint(constraints, minimize, timeout):
@@ -219,7 +225,10 @@ def _minimize_hint(constraints, minimize, timeout):
     minimal ``calldatasize``/``call_value`` per transaction.  A device witness
     of the same constraints bounds the FIRST objective from above: adding
     ``obj_0 <= witness(obj_0)`` cannot change the optimum (the optimal model
-    satisfies it), only prune z3's search.  Later objectives get no bound (the
+    satisfies it), only prune z3's search.  The bound is tightened by up to
+    MINIMIZE_ROUNDS more searches with ``obj_0 <=u target`` added, the target
+    halving the gap to the lowest value not yet ruled out by a miss (a miss
+    proves nothing, it only moves the target up).  Later objectives get no bound (the
     witness need not be optimal in obj_0, so its later values bound nothing in
     the lexicographic order).  The optimum is preserved, but z3 may return a
     different model with the same objective values, i.e. different transaction
@@ -236,19 +245,38 @@ def _minimize_hint(constraints, minimize, timeout):
         return None
     from . import z3bridge
     from .runtime import EngineError
+    obj = minimize[0]
+    name = z3bridge.var_name(obj.raw)
+    if name is None:
+        return None
     try:
         script = z3bridge.to_ir(raws)
         from .engine import prepare
         q = prepare(script.asserts, script.ctx)
         w = eng.search([q])[0]
+        if w is None or name not in w.values:
+            return None
+        best = w.values[name]
+        # descent: search again below the best value so far, aiming at half of
+        # it first (each round adds obj_0 <u target; a miss proves nothing, so
+        # the target moves back up towards the best witness)
+        var = next((n for n in _walk(script.asserts) if n.op == "var" and n.name == name), None)
+        lo = 0
+        for _ in range(MINIMIZE_ROUNDS if var is not None else 0):
+            if best <= lo:
+                break
+            target = lo + (best - lo) // 2
+            extra = script.ctx.app("bvule", var, script.ctx.const(target, var.width))
+            w2 = eng.search([prepare(list(script.asserts) + [extra], script.ctx)])[0]
+            if w2 is not None and name in w2.values and w2.values[name] <= target:
+                best = w2.values[name]
+            else:
+                lo = target + 1
+        STATS["minimize_rounds"] = STATS.get("minimize_rounds", 0) + 1
     except (Unsupported, RecursionError, ValueError, KeyError, EngineError):
         return None
-    obj = minimize[0]
-    name = z3bridge.var_name(obj.raw)
-    if w is None or name is None or name not in w.values:
-        return None
     from mythril.laser.smt import UGE, symbol_factory
-    bound = UGE(symbol_factory.BitVecVal(w.values[name], obj.size()), obj)
+    bound = UGE(symbol_factory.BitVecVal(best, obj.size()), obj)
     STATS["minimize_hints"] = STATS.get("minimize_hints", 0) + 1
     if type(constraints) == tuple:
         return constraints + (bound,)
