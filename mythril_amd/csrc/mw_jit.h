@@ -360,7 +360,7 @@ __device__ __attribute__((always_inline)) inline void search(const u32* __restri
   extern "C" int NAME##_host(const mw::u32* pool, mw::u64 seed, mw::u64 begin, mw::u64 count,        \
                              mw::u32 early, mw::u32* verdict, mw::u32* trace) {                      \
     for (mw::u64 i = 0; i < count; ++i) {                                                            \
-      mw::u32 ds = 0;                                                                                \
+      mw::DivCount ds;                                                                               \
       verdict[i] = (early ? BODY<true>(pool, seed, begin + i, true, 0u, trace, count, i, ds)             \
                           : BODY<false>(pool, seed, begin + i, true, 0u, trace, count, i, ds)) ? 1u : 0u; \
     }                                                                                                \

@@ -16,6 +16,7 @@
 #   opbench        tools/opbench.py jit
 #   keccak         tools/keccak_bench.py
 #   ipmc=FILE      PMC passes on one exhaustive interpreter launch of FILE (tools/interp_once.py)
+#   jpmc=FILE      the same on FILE's cached specialised kernel
 #   opcost         tools/interp_opcost.py (+ one PMC pass: instructions per bytecode op)
 #   ablate         tools/leaf_ablate.py --run (candidate-generation ablations, C2/C2L/C4)
 #   recip          tools/exp/recip_check (device reciprocal vs u64 division; built by hand)
@@ -86,17 +87,20 @@ for step in "$@"; do
     keccak)
       run 300 "$OUT/keccak.log" python3 tools/keccak_bench.py
       tail -8 "$OUT/keccak.log" ;;
-    ipmc=*)
-      F=${step#ipmc=}
+    ipmc=*|jpmc=*)
+      F=${step#*=}
+      J=()
+      P=${step%%=*}
+      [ "$P" = jpmc ] && J=(--jit)
       i=0
       for set in "SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_SCA" \
                  "SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_SMEM,SQ_INSTS_LDS,SQ_INSTS_BRANCH,SQ_INSTS_VMEM,SQ_INST_CYCLES_SALU,SQ_INSTS_FLAT" \
                  "SQ_WAIT_INST_LDS,SQ_ACTIVE_INST_LDS,SQ_ACTIVE_INST_VMEM,SQ_LDS_BANK_CONFLICT"; do
         i=$((i + 1))
-        run 150 "$OUT/ipmc$i.log" timeout -s KILL 140 rocprofv3 --pmc $set --output-format csv -d "$OUT/ipmc/p$i" -o run -- \
-          python3 tools/interp_once.py "$F" 22
+        run 150 "$OUT/$P$i.log" timeout -s KILL 140 rocprofv3 --pmc $set --output-format csv -d "$OUT/$P/p$i" -o run -- \
+          python3 tools/interp_once.py "$F" 22 "${J[@]}"
       done
-      find "$OUT/ipmc" -name "*counter_collection*" ;;
+      find "$OUT/$P" -name "*counter_collection*" ;;
     opcost)
       run 300 "$OUT/opcost.log" python3 tools/interp_opcost.py
       cat "$OUT/opcost.log"

@@ -1,6 +1,7 @@
-"""One exhaustive interpreter launch of a solver-log query (PMC profiling aid).
+"""One exhaustive launch of a solver-log query (PMC profiling aid), on the
+interpreter or (--jit) the query's cached specialised kernel.
 
-    python tools/interp_once.py FILE [log2_candidates]
+    python tools/interp_once.py FILE [log2_candidates] [--jit]
 """
 import os
 import sys
@@ -13,14 +14,18 @@ from mythril_amd.engine import prepare  # noqa: E402
 from mythril_amd.runtime import Device  # noqa: E402
 from mythril_amd.smt2 import parse_file  # noqa: E402
 
-s = parse_file(sys.argv[1])
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+s = parse_file(args[0])
 q = prepare(s.asserts, s.ctx)
-n = 1 << int(sys.argv[2] if len(sys.argv) > 2 else 22)
+n = 1 << int(args[1] if len(args) > 1 else 22)
 dev = Device(0)
 dp = dev.load(q.program)
+if "--jit" in sys.argv:
+    from mythril_amd import jit
+    jit.attach(dev, [dp], variants="xe", waves=2, lds_leaves=0)
 t0 = time.perf_counter()
 found, st = dev.search([dp], 1, 0, n, 0)
-print(os.path.basename(sys.argv[1]), "insns", q.program.n_insn, "cands", n, "kernel_ms", st["kernel_ms"],
-      "wall_ms", (time.perf_counter() - t0) * 1e3, flush=True)
+print(os.path.basename(args[0]), "insns", q.program.n_insn, "cands", n, "kernel", dp.kernel, "kernel_ms",
+      st["kernel_ms"], "wall_ms", (time.perf_counter() - t0) * 1e3, flush=True)
 dp.free()
 dev.close()
