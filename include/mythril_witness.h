@@ -119,6 +119,11 @@ int mg_prog_attach_kernel(mg_prog* prog, const void* image, size_t size, const c
 
 /* 1 if a specialised kernel is attached to the program, else 0. */
 int mg_prog_has_kernel(const mg_prog* prog);
+/* The engine a search of this program runs on: 0 the compiled interpreter,
+ * 1 the threaded-dispatch asm interpreter (every opcode and leaf kind has a
+ * handler; MYTHRIL_AMD_ASM=0 disables it), 2 its specialised kernel.  Replaces
+ * nothing in the reference: a diagnostic for tests and benchmarks. */
+int mg_prog_engine(const mg_prog* prog);
 
 /* Batched Keccak-256 (original 0x01 padding): message i is data[off[i] .. off[i]+len[i]). */
 int mg_keccak256(mg_ctx* ctx, const uint8_t* data, size_t ndata, const uint64_t* off,

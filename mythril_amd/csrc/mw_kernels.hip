@@ -13,6 +13,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -20,6 +21,7 @@
 #include <vector>
 
 #include "../../include/mythril_witness.h"
+#include "mw_asm_interp.inc"
 #include "mw_interp.h"
 #include "mw_keccak.h"
 #include "mw_leaf.h"
@@ -38,6 +40,8 @@ struct ProgDev {
   const u32* pool;
   u32 n_spill;
   u32 npool;   // pool words (LDS staging, mw_search_kernel)
+  u32 n_insn;  // instructions (the asm interpreter's dispatch budget)
+  u32 pad;
 };
 
 constexpr int kBlock = 256;
@@ -234,6 +238,48 @@ __global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __r
   }
 }
 
+// Threaded-dispatch interpreter (tools/gen_asm_interp.py -> mw_asm_interp.inc):
+// the same result protocol as mw_search_kernel, for programs whose opcodes and
+// leaf kinds all have an asm handler and whose pools are staged in LDS
+// (mg_prog.asm_ok, checked on load; the launch checks the LDS fit).  The asm
+// block runs the whole chunk loop of the block (one copy of the code: a loop
+// around it gets unswitched into several copies) and reads its launch
+// arguments from an AsmArgs record in device memory.
+struct AsmArgs {
+  u64 seed, begin, end;
+  u32 flags, nlds, gstride, nchunks, gdx, pad;
+  u32* spillbuf;
+  u32* verdict;   // per-candidate verdicts at cand - begin (mg_eval_generated), or null
+};
+static_assert(sizeof(AsmArgs) == 64, "AsmArgs layout (tools/gen_asm_interp.py)");
+static_assert(sizeof(ProgDev) == 48, "ProgDev layout (tools/gen_asm_interp.py)");
+
+__global__ __launch_bounds__(kBlock, 2) void mw_search_asm_kernel(const ProgDev* __restrict__ progs,
+                                                                const AsmArgs* __restrict__ args,
+                                                                u64* __restrict__ out_min,
+                                                                u64* __restrict__ counter, u32 nlds) {
+  const ProgDev* P = progs + blockIdx.y;
+  {
+    u32* dst = lds_spill + nlds * kBlock;
+    const u32 np = P->npool;
+    const u32* src = P->pool;
+    for (u32 i = threadIdx.x; i < np; i += kBlock) dst[i] = src[i];
+    __syncthreads();
+  }
+  const u64 gtid = ((u64)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x;
+  const u32 goff = (u32)(gtid * 4u);
+  const u32 tid = threadIdx.x;
+  const u32 ch0 = blockIdx.x;
+  u64* om = out_min + blockIdx.y;
+  u64 evals;
+  asm volatile(MW_ASM_BODY
+               : [evals] "=s"(evals)
+               : [args] "s"(args), [prog] "s"(P), [outmin] "s"(om), [ch0] "s"(ch0), [tid] "v"(tid),
+                 [goff] "v"(goff)
+               : MW_ASM_CLOBBERS);
+  if ((threadIdx.x & 63u) == 0 && evals) atomicAdd((unsigned long long*)counter, (unsigned long long)evals);
+}
+
 __global__ __launch_bounds__(kBlock, 2) void mw_eval_kernel(ProgDev P, const u32* __restrict__ in,
                                                          u64 ncand, u64 seed, u64 begin,
                                                          u32* __restrict__ verdict,
@@ -337,6 +383,7 @@ struct mg_ctx {
   size_t alive_cap = 0;
   ProgDev* d_progs = nullptr;
   size_t nprogs_cap = 0;
+  void* d_asmargs = nullptr;  // AsmArgs of the asm interpreter's launch
   std::mutex mu;
 };
 
@@ -347,6 +394,7 @@ struct mg_prog {
   mg_prog_desc desc{};
   u64 ops_per_eval = 0;
   u64 sig = 0;                  // FNV-1a 64 of the program words (mythril_amd/jit.py signature)
+  bool asm_ok = false;          // every opcode and leaf kind has a handler in mw_search_asm_kernel
   // specialised kernels (mg_prog_attach_kernel): one per part, launched in order
   struct Part {
     hipModule_t mod = nullptr;
@@ -484,6 +532,30 @@ int ensure_min(mg_ctx* c, size_t n) {
   return 0;
 }
 
+// mw_search_asm_kernel handles this program: every opcode in MW_ASM_OPCODES,
+// every leaf kind in MW_ASM_LEAF_KINDS (validated programs only)
+bool asm_eligible(const mg_prog_desc* d) {
+  static const u32 ops[] = {MW_ASM_OPCODES};
+  static const u32 kinds[] = {MW_ASM_LEAF_KINDS};
+  bool ok_op[256] = {false};
+  for (u32 o : ops) ok_op[o & 0xffu] = true;
+  for (size_t i = 0; i < d->ncode_words / 4; ++i)
+    if (!ok_op[d->code[4 * i] & 0xffu]) return false;
+  for (size_t l = 0; l < d->nleaves; ++l) {
+    const u32 kind = d->leaves[l * MW_LEAF_WORDS + MW_LEAF_KIND];
+    bool ok = false;
+    for (u32 k : kinds) ok = ok || k == kind;
+    if (!ok) return false;
+  }
+  return true;
+}
+
+// MYTHRIL_AMD_ASM=0 keeps every program on the compiled interpreter (A/B runs, tests)
+bool asm_enabled() {
+  const char* e = std::getenv("MYTHRIL_AMD_ASM");
+  return !(e && e[0] == '0');
+}
+
 }  // namespace
 
 extern "C" {
@@ -555,6 +627,7 @@ int mg_free(mg_ctx* c) {
   if (c->d_spill) hipFree(c->d_spill);
   if (c->d_min) hipFree(c->d_min);
   if (c->d_progs) hipFree(c->d_progs);
+  if (c->d_asmargs) hipFree(c->d_asmargs);
   if (c->d_counter) hipFree(c->d_counter);
   if (c->d_alive) hipFree(c->d_alive);
   if (c->e0) hipEventDestroy(c->e0);
@@ -602,6 +675,8 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
   p->dev.pool = p->d_buf + nc + nk + nl;
   p->dev.n_spill = d->n_spill;
   p->dev.npool = (u32)d->npool_words;
+  p->dev.n_insn = (u32)(nc / 4);
+  p->asm_ok = asm_eligible(d);
   // the desc's host pointers are not retained
   p->desc.code = nullptr;
   p->desc.consts = nullptr;
@@ -689,6 +764,12 @@ int mg_prog_attach_kernel(mg_prog* p, const void* image, size_t size, const char
 
 int mg_prog_has_kernel(const mg_prog* p) { return prog_live(p) && p->jit_ready() ? 1 : 0; }
 
+int mg_prog_engine(const mg_prog* p) {
+  if (!prog_live(p)) return fail(MG_E_ARG, "mg_prog_engine: not a live program");
+  if (p->jit_ready()) return 2;
+  return p->asm_ok && asm_enabled() ? 1 : 0;
+}
+
 int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uint64_t begin,
               uint64_t count, uint32_t flags, uint64_t* out_min_idx, mg_stats* st) {
   if (!c || !progs || !out_min_idx || nprog == 0) return fail(MG_E_ARG, "null argument");
@@ -707,56 +788,106 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   int rc = ensure_min(c, nprog);
   if (rc) return rc;
   // Programs with a specialised kernel (mg_prog_attach_kernel) get one launch
-  // each; the rest share one interpreter launch (grid row per program).
-  // d_min holds the interpreted programs first, then the specialised ones.
-  std::vector<size_t> interp, special;
-  u32 max_spill = 0;
+  // each; the rest share interpreter launches (grid row per program): one of
+  // the threaded-dispatch asm interpreter for the programs it handles, one of
+  // the compiled interpreter for the others.  d_min holds the asm group, then
+  // the compiled group, then the specialised programs.
+  std::vector<size_t> gasm, gcpp, special;
   u64 ops = 0;
+  const bool use_asm = asm_enabled();
   for (size_t i = 0; i < nprog; ++i) {
     if (!progs[i] || progs[i]->ctx != c) return fail(MG_E_ARG, "program from another context");
-    (progs[i]->jit_ready() ? special : interp).push_back(i);
+    if (progs[i]->jit_ready()) special.push_back(i);
+    else (use_asm && progs[i]->asm_ok ? gasm : gcpp).push_back(i);
     ops += progs[i]->ops_per_eval;
   }
-  std::vector<ProgDev> hp;
-  u32 max_pool = 0;
-  for (size_t i : interp) {
-    hp.push_back(progs[i]->dev);
-    max_spill = std::max(max_spill, progs[i]->dev.n_spill);
-    max_pool = std::max(max_pool, progs[i]->dev.npool);
+  // the asm group needs its pools staged in LDS beside the spill words
+  if (!gasm.empty()) {
+    u32 ms = 0, mp = 0;
+    for (size_t i : gasm) {
+      ms = std::max(ms, progs[i]->dev.n_spill);
+      mp = std::max(mp, progs[i]->dev.npool);
+    }
+    if ((size_t)std::min(ms, kLdsSpillWords) * kBlock * 4 + (size_t)mp * 4 > (size_t)kLdsSpillWords * kBlock * 4 ||
+        count >= (1ull << 40)) {
+      gcpp.insert(gcpp.end(), gasm.begin(), gasm.end());
+      gasm.clear();
+    }
   }
+  std::vector<size_t> interp(gasm);
+  interp.insert(interp.end(), gcpp.begin(), gcpp.end());
+  std::vector<ProgDev> hp;
+  for (size_t i : interp) hp.push_back(progs[i]->dev);
   const u64 nchunks = (count + kBlock - 1) / kBlock;
   const size_t ni = interp.size();
-  u64 gx = 1;
-  u32 nlds = 0;
-  if (ni) {
+  struct Group {
+    size_t first, n;
+    u64 gx;
+    u32 nlds, max_pool;
+  } groups[2] = {{0, gasm.size(), 1, 0, 0}, {gasm.size(), gcpp.size(), 1, 0, 0}};
+  size_t spill_need = 4;
+  for (Group& G : groups) {
+    if (!G.n) continue;
+    u32 max_spill = 0;
+    for (size_t j = G.first; j < G.first + G.n; ++j) {
+      max_spill = std::max(max_spill, hp[j].n_spill);
+      G.max_pool = std::max(G.max_pool, hp[j].npool);
+    }
     // enough blocks to fill the chip several times over, split across programs
-    gx = std::max<u64>(1, (u64)c->ncu * 8 / ni);
-    gx = std::min<u64>(gx, nchunks);
-    const u64 nthreads = gx * ni * kBlock;
-    nlds = std::min(max_spill, kLdsSpillWords);
-    const u32 nglob = max_spill - nlds;
-    rc = ensure_spill(c, std::max<size_t>(4, (size_t)nglob * nthreads * sizeof(u32)));
+    G.gx = std::max<u64>(1, (u64)c->ncu * 8 / G.n);
+    G.gx = std::min<u64>(G.gx, nchunks);
+    const u64 nthreads = G.gx * G.n * kBlock;
+    G.nlds = std::min(max_spill, kLdsSpillWords);
+    spill_need = std::max(spill_need, (size_t)(max_spill - G.nlds) * nthreads * sizeof(u32));
+  }
+  if (ni) {
+    rc = ensure_spill(c, spill_need);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(c->d_progs, hp.data(), ni * sizeof(ProgDev), hipMemcpyHostToDevice, c->stream));
+  }
+  AsmArgs aa{};
+  if (groups[0].n) {
+    if (!c->d_asmargs) HIPCHK(hipMalloc(&c->d_asmargs, sizeof(AsmArgs)));
+    aa.seed = seed;
+    aa.begin = begin;
+    aa.end = begin + count;
+    aa.flags = flags;
+    aa.nlds = groups[0].nlds;
+    aa.gstride = (u32)(groups[0].gx * groups[0].n * kBlock * 4);
+    aa.nchunks = (u32)nchunks;
+    aa.gdx = (u32)groups[0].gx;
+    aa.spillbuf = c->d_spill;
+    aa.verdict = nullptr;
+    HIPCHK(hipMemcpyAsync(c->d_asmargs, &aa, sizeof(AsmArgs), hipMemcpyHostToDevice, c->stream));
   }
   std::vector<u64> init(nprog, MG_NONE);
   HIPCHK(hipMemcpyAsync(c->d_min, init.data(), nprog * sizeof(u64), hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemsetAsync(c->d_counter, 0, kNCounters * sizeof(u64), c->stream));
   HIPCHK(hipEventRecord(c->e0, c->stream));
-  if (ni) {
+  if (groups[0].n) {
+    const Group& G = groups[0];
+    const size_t lds = (size_t)G.nlds * kBlock * 4 + (size_t)G.max_pool * 4;
+    hipLaunchKernelGGL(mw_search_asm_kernel, dim3((u32)G.gx, (u32)G.n), dim3(kBlock), lds, c->stream,
+                       c->d_progs, (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, G.nlds);
+    HIPCHK(hipGetLastError());
+  }
+  if (groups[1].n) {
+    const Group& G = groups[1];
     // stage the pools in LDS when they fit beside the spill words (80 KiB per
     // block keeps two blocks per CU)
-    const size_t spill_bytes = (size_t)nlds * kBlock * 4, pool_bytes = (size_t)max_pool * 4;
+    const size_t spill_bytes = (size_t)G.nlds * kBlock * 4, pool_bytes = (size_t)G.max_pool * 4;
+    const ProgDev* dp = c->d_progs + G.first;
+    u64* dm = c->d_min + G.first;
 #ifdef MW_NO_POOL_LDS   // A/B builds only
     if (false)
 #else
-    if (max_pool && spill_bytes + pool_bytes <= (size_t)kLdsSpillWords * kBlock * 4)
+    if (G.max_pool && spill_bytes + pool_bytes <= (size_t)kLdsSpillWords * kBlock * 4)
 #endif
-      hipLaunchKernelGGL(mw_search_kernel<true>, dim3((u32)gx, (u32)ni), dim3(kBlock), spill_bytes + pool_bytes,
-                         c->stream, c->d_progs, seed, begin, count, flags, c->d_min, c->d_counter, c->d_spill, nlds);
+      hipLaunchKernelGGL(mw_search_kernel<true>, dim3((u32)G.gx, (u32)G.n), dim3(kBlock), spill_bytes + pool_bytes,
+                         c->stream, dp, seed, begin, count, flags, dm, c->d_counter, c->d_spill, G.nlds);
     else
-      hipLaunchKernelGGL(mw_search_kernel<false>, dim3((u32)gx, (u32)ni), dim3(kBlock), spill_bytes,
-                         c->stream, c->d_progs, seed, begin, count, flags, c->d_min, c->d_counter, c->d_spill, nlds);
+      hipLaunchKernelGGL(mw_search_kernel<false>, dim3((u32)G.gx, (u32)G.n), dim3(kBlock), spill_bytes,
+                         c->stream, dp, seed, begin, count, flags, dm, c->d_counter, c->d_spill, G.nlds);
     HIPCHK(hipGetLastError());
   }
   for (size_t j = 0; j < special.size(); ++j) {
@@ -778,7 +909,7 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
     st->kernel_ms = ms;
     st->wall_ms = now_ms() - t0;
     st->evals = evals;  // summed over every program's blocks
-    st->launches = (ni ? 1 : 0) + special.size();
+    st->launches = (groups[0].n ? 1 : 0) + (groups[1].n ? 1 : 0) + special.size();
     st->ops = (double)evals / (double)nprog * (double)ops;
     st->lane_div_steps = ctr[1];
     st->lane_div_full = ctr[2];
@@ -837,8 +968,59 @@ int mg_eval(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncan
                      verdict, trace);
 }
 
+// Verdicts of generated candidates on the asm interpreter (mw_search_asm_kernel
+// with a verdict array); 1 = not applicable (the caller uses mw_eval_kernel).
+static int eval_asm(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, size_t count, uint32_t* verdict) {
+  if (!asm_enabled() || !p->asm_ok || begin + count < begin || count >= (1ull << 40)) return 1;
+  const u32 nlds = std::min(p->dev.n_spill, kLdsSpillWords);
+  const size_t lds = (size_t)nlds * kBlock * 4 + (size_t)p->dev.npool * 4;
+  if (lds > (size_t)kLdsSpillWords * kBlock * 4) return 1;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  (void)hipGetLastError();
+  int rc = ensure_min(c, 1);
+  if (rc) return rc;
+  const u64 nchunks = (count + kBlock - 1) / kBlock;
+  const u64 gx = std::min<u64>(nchunks, (u64)c->ncu * 8);
+  rc = ensure_spill(c, std::max<size_t>(4, (size_t)(p->dev.n_spill - nlds) * gx * kBlock * sizeof(u32)));
+  if (rc) return rc;
+  if (!c->d_asmargs) HIPCHK(hipMalloc(&c->d_asmargs, sizeof(AsmArgs)));
+  u32* d_v = nullptr;
+  if (hipMalloc(&d_v, count * 4) != hipSuccess) return fail(MG_E_NOMEM, "eval verdict alloc");
+  AsmArgs aa{};
+  aa.seed = seed;
+  aa.begin = begin;
+  aa.end = begin + count;
+  aa.flags = 0;
+  aa.nlds = nlds;
+  aa.gstride = (u32)(gx * kBlock * 4);
+  aa.nchunks = (u32)nchunks;
+  aa.gdx = (u32)gx;
+  aa.spillbuf = c->d_spill;
+  aa.verdict = d_v;
+  const u64 none = MG_NONE;
+  hipError_t e = hipMemcpyAsync(c->d_progs, &p->dev, sizeof(ProgDev), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->d_min, &none, sizeof(u64), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->d_asmargs, &aa, sizeof(AsmArgs), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, kNCounters * sizeof(u64), c->stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(mw_search_asm_kernel, dim3((u32)gx, 1u), dim3(kBlock), lds, c->stream, c->d_progs,
+                       (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, nlds);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, count * 4, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(d_v);
+  if (e != hipSuccess) return fail(MG_E_HIP, std::string("eval (asm interpreter): ") + hipGetErrorString(e));
+  return 0;
+}
+
 int mg_eval_generated(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, size_t count,
                       uint32_t* verdict, uint32_t* trace) {
+  if (p && prog_live(p) && c && ctx_live(c) && p->ctx == c && !p->jit_ready() && !trace && verdict && count) {
+    const int rc = eval_asm(c, p, seed, begin, count, verdict);
+    if (rc != 1) return rc;
+  }
   if (!p || !prog_live(p) || !p->jit_ready() || trace)
     return eval_common(c, p, nullptr, count, seed, begin, verdict, trace);  // rejects dead handles
   // verdicts only, on the program's specialised kernel

@@ -66,6 +66,7 @@ SIGNATURES = {
     "mg_prog_free": (ctypes.c_int, [_P]),
     "mg_prog_attach_kernel": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
     "mg_prog_has_kernel": (ctypes.c_int, [_P]),
+    "mg_prog_engine": (ctypes.c_int, [_P]),
     "mg_search": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                  ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
                                  ctypes.POINTER(MgStats)]),
@@ -187,6 +188,15 @@ class Device:
 
     def has_kernel(self, dp: DeviceProgram) -> bool:
         return bool(self.lib.mg_prog_has_kernel(dp.handle))
+
+    ENGINES = ("interp", "asm", "jit")
+
+    def engine_of(self, dp: DeviceProgram) -> str:
+        """Which kernel searches this program (mg_prog_engine)."""
+        rc = self.lib.mg_prog_engine(dp.handle)
+        if rc < 0:
+            _check(self.lib, rc, "mg_prog_engine")
+        return self.ENGINES[rc]
 
     def search(self, progs: Sequence[DeviceProgram], seed: int, begin: int, count: int,
                flags: int = 0) -> Tuple[List[Optional[int]], dict]:

@@ -1,0 +1,194 @@
+"""The threaded-dispatch asm interpreter (csrc/mw_asm_interp.inc) on gfx950,
+against the compiled interpreter (MYTHRIL_AMD_ASM=0: same library, same
+programs) and the oracle:
+
+* every opcode the asm interpreter handles, on random DAGs over Philox and
+  pooled leaves (all four leaf kinds), at widths 1..256;
+* every corpus program (C2-C4 solver-log queries, the LASER corpus: W_CDINS
+  chains, keccak UFs, congruence conjuncts, the C3 global-spill path):
+  per-candidate verdicts and batched search results, in every search mode.
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from mythril_amd import isa
+from mythril_amd.compiler import compile_program
+from mythril_amd.engine import DEFAULT_SEED, prepare
+from mythril_amd.ir import BOOL, Ctx
+from mythril_amd.smt2 import parse_file
+from oracle import cdag
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from mythril_amd.runtime import Device
+    d = Device(0)
+    yield d
+    d.close()
+
+
+class compiled_interpreter:
+    """MYTHRIL_AMD_ASM=0 for the duration (read by the library at each call)."""
+
+    def __enter__(self):
+        self.old = os.environ.get("MYTHRIL_AMD_ASM")
+        os.environ["MYTHRIL_AMD_ASM"] = "0"
+
+    def __exit__(self, *a):
+        if self.old is None:
+            os.environ.pop("MYTHRIL_AMD_ASM", None)
+        else:
+            os.environ["MYTHRIL_AMD_ASM"] = self.old
+
+
+def both(dev, p, seed, begin, n):
+    dp = dev.load(p)
+    try:
+        assert dev.engine_of(dp) == "asm"
+        va, _ = dev.eval_generated(dp, seed, begin, n, trace=False)
+        with compiled_interpreter():
+            assert dev.engine_of(dp) == "interp"
+            vi, _ = dev.eval_generated(dp, seed, begin, n, trace=False)
+    finally:
+        dp.free()
+    return va.astype(np.uint8), vi.astype(np.uint8)
+
+
+def test_asm_00_smoke(dev):
+    """One small program first (a hang here stops the run early)."""
+    c = Ctx()
+    x, y = c.var("x", 256), c.var("y", 8)
+    p = compile_program([c.app("bvult", x, c.const(1 << 255, 256)), c.app("bvugt", y, c.const(9, 8))])
+    va, vi = both(dev, p, 7, 0, 1 << 12)
+    assert np.array_equal(va, vi)
+    _, _, vo = cdag.evaluate([c.app("bvult", x, c.const(1 << 255, 256)), c.app("bvugt", y, c.const(9, 8))],
+                             7, 0, 1 << 12, want_verdict=True)
+    assert np.array_equal(va, vo)
+    assert 0 < int(va.sum()) < len(va)
+
+
+WIDTHS = [1, 8, 16, 32, 33, 64, 160, 255, 256]
+
+
+def _random_supported_dag(seed):
+    """A random DAG over the asm interpreter's ops (no division, no variable shifts)."""
+    r = random.Random(seed)
+    c = Ctx()
+    leaves = {w: [c.var(f"v{w}_{i}", w) for i in range(2)] for w in WIDTHS if w > 1}
+    bools = [c.var(f"b{i}", BOOL) for i in range(2)]
+
+    def bv(w, d):
+        if d == 0 or r.random() < 0.25:
+            if r.random() < 0.2:
+                return c.const(r.getrandbits(w), w)
+            if w in leaves:
+                return r.choice(leaves[w])
+            src = r.choice(leaves[256])
+            return c.app("extract", src, params=(w - 1, 0)) if w > 1 else c.app("extract", src, params=(0, 0))
+        k = r.random()
+        a = bv(w, d - 1)
+        if k < 0.35:
+            return c.app(r.choice(["bvadd", "bvsub", "bvand", "bvor", "bvxor", "bvmul"]), a, bv(w, d - 1))
+        if k < 0.45:
+            return c.app("bvnot", a)
+        if k < 0.55:
+            return c.app("ite", boolean(d - 1), a, bv(w, d - 1))
+        if k < 0.7 and w >= 2:
+            amt = r.randrange(0, w)
+            return c.app(r.choice(["bvshl", "bvlshr"]), a, c.const(amt, w))
+        if k < 0.85:
+            ww = r.choice([x for x in WIDTHS if x >= w])
+            lo = r.randrange(0, ww - w + 1)
+            return c.app("extract", bv(ww, d - 1), params=(lo + w - 1, lo)) if ww > w else a
+        if w >= 2:
+            hw = r.randrange(1, w)
+            return c.app("concat", bv(hw, d - 1), bv(w - hw, d - 1)) if hw > 1 and w - hw > 1 else a
+        return a
+
+    def boolean(d):
+        w = r.choice(WIDTHS[1:])
+        k = r.random()
+        if d == 0 or k < 0.15:
+            return r.choice(bools)
+        if k < 0.7:
+            op = r.choice(["bvult", "bvule", "bvslt", "bvsle", "=", "bvugt", "bvsge"])
+            return c.app(op, bv(w, d - 1), bv(w, d - 1))
+        if k < 0.8:
+            return c.app("bvumul_noovfl", bv(w, d - 1), bv(w, d - 1)) if w >= 33 else c.app("=", bv(w, 0), bv(w, 0))
+        if k < 0.9:
+            return c.app(r.choice(["and", "or", "xor"]), boolean(d - 1), boolean(d - 1))
+        return c.app("not", boolean(d - 1))
+
+    conj = [boolean(4) for _ in range(3)]
+    return c, conj
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_asm_random_dags(dev, seed):
+    c, conj = _random_supported_dag(9000 + seed)
+    for pools in (False, True):
+        q = prepare(conj, c, use_pools=pools)
+        p = q.program
+        if not isa.asm_eligible(p.code, p.leaves):
+            pytest.skip("lowered outside the asm opcode set")
+        n = 1 << 12
+        va, vi = both(dev, p, DEFAULT_SEED + seed, 1 << 20, n)
+        assert np.array_equal(va, vi), (seed, pools, int(np.count_nonzero(va != vi)))
+        _, _, vo = cdag.evaluate(q.lowered.conjuncts, DEFAULT_SEED + seed, 1 << 20, n, want_verdict=True,
+                                 specs=cdag.program_specs(p) if pools else None)
+        assert np.array_equal(va, vo), (seed, pools)
+
+
+def _corpus():
+    out = []
+    for d in ("solver_log", "laser"):
+        base = os.path.join(ROOT, "tests", "golden", d)
+        for f in sorted(os.listdir(base)):
+            if f.endswith(".smt2") or f.endswith(".smt2.gz"):
+                out.append(os.path.join(base, f))
+    return out
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    qs = []
+    for f in _corpus():
+        s = parse_file(f)
+        qs.append((os.path.basename(f), prepare(s.asserts, s.ctx)))
+    return qs
+
+
+def test_asm_corpus_verdicts(dev, corpus):
+    n = 1 << 14
+    for name, q in corpus:
+        va, vi = both(dev, q.program, DEFAULT_SEED, 0, n)
+        assert np.array_equal(va, vi), (name, int(np.count_nonzero(va != vi)))
+    # and the oracle on a sample (C3 included: its global spill path)
+    for name, q in corpus[:8] + corpus[-8:]:
+        _, _, vo = cdag.evaluate(q.lowered.conjuncts, DEFAULT_SEED, 0, n, want_verdict=True,
+                                 specs=cdag.program_specs(q.program))
+        va, _ = both(dev, q.program, DEFAULT_SEED, 0, n)
+        assert np.array_equal(va, vo), name
+
+
+def test_asm_corpus_search_modes(dev, corpus):
+    """64 programs per launch, exhaustive / early exit / stop after hit: the
+    same lowest witness index per program as the compiled interpreter."""
+    dps = [dev.load(q.program) for _, q in corpus[:64]]
+    try:
+        for flags in (0, isa.FLAG_EARLY_EXIT, isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT):
+            fa, sta = dev.search(dps, DEFAULT_SEED, 0, 1 << 16, flags)
+            with compiled_interpreter():
+                fi, sti = dev.search(dps, DEFAULT_SEED, 0, 1 << 16, flags)
+            assert fa == fi, flags
+            if flags == 0:
+                assert sta["evals"] == sti["evals"] == 64 << 16
+    finally:
+        for dp in dps:
+            dp.free()

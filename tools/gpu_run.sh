@@ -6,6 +6,7 @@
 # Steps (each under its own time limit; the script stops at the first failure):
 #   smoke          __graft_entry__.smoke()
 #   tests[=EXPR]   pytest -m gpu (optionally -k EXPR)
+#   quick=EXPR     pytest -m gpu -k EXPR under a 180 s limit (first runs of new kernels)
 #   bench          python bench.py (default flags) -> bench.json
 #   bench1         bench.py --steps 5 --no-ttfw --no-cpu-baseline $BENCH_ARGS (quick A/B runs)
 #   prof           rocprofv3 --kernel-trace --stats on a short bench run
@@ -48,6 +49,9 @@ for step in "$@"; do
     smoke)
       run 240 "$OUT/smoke.log" python3 -c "import __graft_entry__ as g; g.smoke()"
       tail -2 "$OUT/smoke.log" ;;
+    quick=*)
+      run 180 "$OUT/gpu_quick.log" python3 -u -m pytest tests -m gpu -x -v -s --timeout 120 --timeout-method thread -k "${step#quick=}"
+      tail -3 "$OUT/gpu_quick.log" ;;
     tests|tests=*)
       K=()
       [ "$step" != tests ] && K=(-k "${step#tests=}")
