@@ -192,3 +192,28 @@ def test_asm_corpus_search_modes(dev, corpus):
     finally:
         for dp in dps:
             dp.free()
+
+
+@pytest.mark.parametrize("k", range(6))
+def test_asm_search_reports_the_satisfying_lane(dev, k):
+    """Witnesses in every wave of a 256-candidate chunk (not only its first
+    64 lanes): an 8-bit Philox leaf equal to a constant, searched exhaustively
+    and with early exit + stop-after-hit, gives the compiled interpreter's
+    lowest index, and that index satisfies the program."""
+    c = Ctx()
+    x = c.var(f"x{k}", 8)
+    p = compile_program([c.app("=", x, c.const(37 * k + 11, 8))])
+    dp = dev.load(p)
+    try:
+        assert dev.engine_of(dp) == "asm"
+        for flags in (0, isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT):
+            (fa,), _ = dev.search([dp], 3 + k, 1000 * k, 1 << 16, flags)
+            with compiled_interpreter():
+                (fi,), _ = dev.search([dp], 3 + k, 1000 * k, 1 << 16, flags)
+            assert fa == fi and fa is not None
+            v, _ = dev.eval_generated(dp, 3 + k, fa, 1, trace=False)
+            assert v[0] == 1
+            va, _ = dev.eval_generated(dp, 3 + k, 1000 * k, fa - 1000 * k, trace=False)
+            assert not va.any()                  # nothing lower
+    finally:
+        dp.free()

@@ -11,8 +11,9 @@ C2L: the LASER-shaped queries of token.sol's runtime bytecode
 The queries are the committed ``--solver-log``-format dumps
 (tests/golden/solver_log, synthetic: no z3/solc exists to dump real ones, see
 tests/make_solver_log_corpus.py).  Each config is timed twice in exhaustive
-mode (early exit off): the interpreter kernel and the specialised kernel
-(mythril_amd/jit.py).  Time to first witness (early exit + stop-after-hit,
+mode (early exit off): the threaded-dispatch asm interpreter (the default for
+these programs), the compiled interpreter (MYTHRIL_AMD_ASM=0) and the
+specialised kernel (mythril_amd/jit.py).  Time to first witness (early exit + stop-after-hit,
 interpreter) is reported beside it.  evals/s = programs x candidates / wall
 time of the mg_search call; the roofline uses the kernel time from the library's
 HIP events and the compiler's ops_per_eval.
@@ -104,10 +105,14 @@ def main():
                 first = [x if x is not None else y for x, y in zip(first, found)]
                 pos += SLICE
             ttfw = time.perf_counter() - t0
-            for engine in (["interp"] if a.no_jit else ["interp", "jit"]):
+            for engine in (["asm", "interp"] if a.no_jit else ["asm", "interp", "jit"]):
                 compile_s = None
+                # asm: the threaded-dispatch interpreter (the default for these
+                # programs); interp: the compiled interpreter (MYTHRIL_AMD_ASM=0)
+                os.environ["MYTHRIL_AMD_ASM"] = "0" if engine == "interp" else "1"
                 if engine == "jit":
                     compile_s = jit.attach(dev, dps, variants="xe", waves=2, lds_leaves=0)
+                ran = sorted({dev.engine_of(dp) for dp in dps})
                 dev.search(dps, DEFAULT_SEED, 0, SLICE, 0)            # warm-up
                 kms, evals = 0.0, 0
                 t0 = time.perf_counter()
@@ -118,6 +123,7 @@ def main():
                 wall = time.perf_counter() - t0
                 achieved = ops * count / (kms / 1e3)
                 line = {"config": name, "files": gfiles, "engine": engine + (f" ({dps[0].kernel})" if dps[0].kernel else ""),
+                        "kernels": ran,
                         "programs": len(g), "candidates": count, "evals": evals,
                         "evals_per_s": len(g) * count / wall, "kernel_ms": kms, "ops_per_eval": ops,
                         "tops": achieved / 1e12, "frac_peak": achieved / peak, "jit_compile_s": compile_s,

@@ -785,13 +785,12 @@ def gen():
       f"global_store_dword {v(T + 1)}, {v(T)}, {sr(VERD, 2)}",
       f"s_mov_b64 exec, {sr(EXECSV, 2)}")
     g.label("Lnoverd_%=")
-    g(f"s_ff1_i32_b64 {s(SX)}, {sr(MSK, 2)}", f"s_cmp_eq_u64 {sr(MSK, 2)}, 0", "s_cbranch_scc1 Lnohit_%=",
-      # index of the first satisfying lane: base + lane (one lane of the wave issues the atomic)
-      f"s_add_u32 {s(SX)}, {s(SX)}, {s(BASE)}", f"s_addc_u32 {s(SX + 1)}, 0, {s(BASE + 1)}",
-      f"s_mov_b64 {sr(EXECSV, 2)}, exec", f"s_ff1_i32_b64 {s(JMP)}, exec", f"s_lshl_b64 {sr(JMP, 2)}, 1, {s(JMP)}",
-      f"s_mov_b64 exec, {sr(JMP, 2)}",
-      f"v_mov_b32_e32 {v(T)}, {s(SX)}", f"v_mov_b32_e32 {v(T + 1)}, {s(SX + 1)}", f"v_mov_b32_e32 {v(T + 2)}, 0",
-      f"global_atomic_umin_x2 {v(T + 2)}, {vr(T, 2)}, {sr(OUTMIN, 2)}",
+    g(f"s_cmp_eq_u64 {sr(MSK, 2)}, 0", "s_cbranch_scc1 Lnohit_%=",
+      # the wave's lowest satisfying lane issues the atomic with its own candidate index
+      f"s_ff1_i32_b64 {s(SX)}, {sr(MSK, 2)}", f"s_lshl_b64 {sr(JMP, 2)}, 1, {s(SX)}",
+      f"s_mov_b64 {sr(EXECSV, 2)}, exec", f"s_mov_b64 exec, {sr(JMP, 2)}",
+      f"v_mov_b32_e32 {v(T + 2)}, 0",
+      f"global_atomic_umin_x2 {v(T + 2)}, {vr(CLO, 2)}, {sr(OUTMIN, 2)}",
       f"s_mov_b64 exec, {sr(EXECSV, 2)}")
     g.label("Lnohit_%=")
     g(f"s_add_u32 {s(CH)}, {s(CH)}, {s(GDX)}", "s_branch Lchunk_%=")

@@ -114,6 +114,9 @@ for step in "$@"; do
     ablate)
       run 1200 "$OUT/ablate.log" python3 tools/leaf_ablate.py --run "$OUT/ablate"
       tail -30 "$OUT/ablate.log" ;;
+    asmdiff)
+      run 300 "$OUT/asm_diff.log" python3 tools/asm_diff.py
+      tail -20 "$OUT/asm_diff.log" ;;
     recip)
       run 120 "$OUT/recip.txt" ./tools/exp/recip_check
       tail -4 "$OUT/recip.txt" ;;
