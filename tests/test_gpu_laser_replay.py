@@ -1,6 +1,6 @@
 """The LaserEVM-order replay of tests/test_laser_replay.py on the MI355X with
 the drop-in's default candidate budget (2^22): one search launch per JUMPI
-pair, every transaction-boundary prune answered from the memo, and every
+pair (and per transaction-boundary prefetch), and every
 device witness confirmed by the oracle's re-check.  Prints one record per
 scenario (launches per query, memo hits, Keccak requests) for DESIGN.md."""
 import json
@@ -30,5 +30,6 @@ def test_replay_on_device(name, monkeypatch, device):
     for q, got, exp in zip(run.queries, answers, expect):
         if q.sat or exp:
             assert got, q.pc
-    assert rec["launches"] * 2 <= rec["jumpi_prunes"] + 1
+    # one launch per JUMPI pair, plus one per transaction-boundary prefetch
+    assert rec["launches"] * 2 <= rec["jumpi_prunes"] + 1 + 2 * rec["tx_prunes"]
     assert rec["z3_confirmed"] == rec["gpu_witnesses"]
