@@ -57,7 +57,7 @@ typedef struct {
   size_t nconst_words;
   const uint32_t* leaves; /* MW_LEAF_WORDS words per free variable */
   size_t nleaves;
-  const uint32_t* pool;   /* candidate pools, MW_POOL_ENTRY_WORDS per entry */
+  const uint32_t* pool;   /* candidate pools, MW_POOL_ENTRY_WORDS_OF(width) per entry */
   size_t npool_words;
   uint32_t n_spill;       /* spill-area words per lane (SPILL_W/FILL_W imm: 8-word slot offset, _N: 1 word) */
   uint32_t n_trace_rows;  /* rows written by MW_STORE_* (mg_eval trace) */
@@ -121,7 +121,8 @@ int mg_prog_attach_kernel(mg_prog* prog, const void* image, size_t size, const c
 int mg_prog_has_kernel(const mg_prog* prog);
 /* The engine a search of this program runs on: 0 the compiled interpreter,
  * 1 the threaded-dispatch asm interpreter (every opcode and leaf kind has a
- * handler; MYTHRIL_AMD_ASM=0 disables it), 2 its specialised kernel.  Replaces
+ * handler and the pool fits in LDS; MYTHRIL_AMD_ASM=0 disables it), 2 its
+ * specialised kernel.  Replaces
  * nothing in the reference: a diagnostic for tests and benchmarks. */
 int mg_prog_engine(const mg_prog* prog);
 

@@ -920,7 +920,9 @@ def layout_leaves(leaf_nodes: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
             pshift, pbits, poff, pstride = spec.shift, spec.bits, len(pool_words), spec.stride
             bit = max(bit, spec.shift + (spec.bits - 1) * max(spec.stride, 1) + 1 if spec.bits else 0)
             for e in spec.pool:
-                if e is None:
+                if w < 32:   # one word per entry (mw_isa.h MW_POOL_NARROW_RANDOM)
+                    pool_words.append(isa.POOL_NARROW_RANDOM if e is None else e & ((1 << w) - 1))
+                elif e is None:
                     pool_words.extend([1] + [0] * 8)
                 else:
                     pool_words.extend([0] + _limbs(e & ((1 << w) - 1)))

@@ -414,6 +414,15 @@ struct DivCount {
   u32 steps = 0;  // digit positions the schoolbook path ran (some lane's digit nonzero)
 };
 
+// The launch counters (evals, then the DivCount fields x lanes) are striped:
+// stripe 0 is the interpreters' (one atomic per wave per launch), stripes
+// 1..MW_CTR_STRIPES the specialised kernels' (one 256-candidate block each,
+// so one set of atomics per wave per chunk: on a single address those
+// serialise across the 8 XCDs, ~12 ns each, and capped small programs at
+// ~5 G evals/s).  Each stripe is a 128-byte line; the host sums them.
+#define MW_CTR_STRIPES 64
+#define MW_CTR_STRIPE_WORDS 16
+
 #if defined(__HIP_DEVICE_COMPILE__)
 // counter[1..4] += nvalid x (steps, full, short, general): one lane per wave
 __device__ inline void add_div_counts(u64* counter, const DivCount& dc, u64 nvalid) {

@@ -29,7 +29,11 @@
 #define MW_N_RESERVED 31   // in each 32-slot half: N slots 31 and 63
 #define MW_KBIT 0x8000u
 #define MW_LEAF_WORDS 8
-#define MW_POOL_ENTRY_WORDS 9
+#define MW_POOL_ENTRY_WORDS 9      // wide leaves (width >= 32): flags + 8 limbs
+#define MW_POOL_NARROW_RANDOM 0x80000000u  // narrow leaves (width < 32): ONE word per entry,
+                                           // bit 31 = RANDOM, bits 0..30 = the value
+// words per pool entry of a width-w leaf
+#define MW_POOL_ENTRY_WORDS_OF(w) ((w) < 32u ? 1u : (uint32_t)MW_POOL_ENTRY_WORDS)
 #define MW_MAX_WIDTH 256
 
 // leaf table entry (MW_LEAF_WORDS u32 per leaf)
@@ -42,7 +46,9 @@
 #define MW_LEAF_POOL 5   // word offset of entry 0 in the pool buffer
 #define MW_LEAF_INROW 6  // first SoA input row (mg_eval)
 #define MW_LEAF_STRIDE 7 // kind 3: index-bit stride between consecutive digit bits
-// pool entry: word 0 = flags (bit0: RANDOM), words 1..8 = limbs
+// pool entry, width >= 32: word 0 = flags (bit0: RANDOM), words 1..8 = limbs;
+// width < 32: one word, MW_POOL_NARROW_RANDOM or the value (calldata bytes and
+// Bools are most pool entries: 9x less LDS when pools are staged there)
 
 enum mw_opcode {
   MW_END = 0,

@@ -313,6 +313,8 @@ __device__ __attribute__((always_inline)) inline void search(const u32* __restri
   DivCount dc;
   const bool ok = BODY(pool, seed, cand, in, flags, nullptr, 0, 0, dc);
   const u64 nvalid = (u64)__popcll(__ballot(valid));
+  // this block's counter stripe (mw_alu.h MW_CTR_STRIPES)
+  counter += MW_CTR_STRIPE_WORDS * (1u + (blockIdx.x & (MW_CTR_STRIPES - 1u)));
   if (lane == 0 && nvalid)   // division paths x lanes (mg_stats.lane_div_*)
     add_div_counts(counter, dc, nvalid);
   if (!(stage & MW_JIT_LAST)) {
@@ -323,7 +325,10 @@ __device__ __attribute__((always_inline)) inline void search(const u32* __restri
   const u64 hit = __ballot(ok);
   if (hit) {
     const u32 first = (u32)__ffsll((unsigned long long)hit) - 1u;
-    if (lane == first) atomicMin((unsigned long long*)out_min, (unsigned long long)cand);
+    // the atomic only when it can lower the minimum: exhaustive searches of
+    // dense programs would otherwise queue one per wave on this one address
+    if (lane == first && cand < __hip_atomic_load(out_min, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMin((unsigned long long*)out_min, (unsigned long long)cand);
   }
   if (lane == 0 && nvalid) atomicAdd((unsigned long long*)counter, (unsigned long long)nvalid);
 }

@@ -45,7 +45,9 @@ struct ProgDev {
 };
 
 constexpr int kBlock = 256;
-constexpr int kNCounters = 5;  // d_counter words: evals, then DivCount fields x lanes
+constexpr int kNCounters = 5;  // counter words: evals, then DivCount fields x lanes
+// d_counter: stripe 0 (interpreters) + MW_CTR_STRIPES stripes (specialised kernels), summed on readback
+constexpr size_t kCounterWords = (size_t)(1 + MW_CTR_STRIPES) * MW_CTR_STRIPE_WORDS;
 // Spill area: n_spill words per lane (a W spill slot is 8 consecutive words, an
 // N slot one; the compiler puts the most-used words first).  Words
 // [0, kLdsSpillWords) live in LDS as [word][lane] (consecutive lanes ->
@@ -87,14 +89,18 @@ __device__ __forceinline__ void leaf_value_lds(const u32* __restrict__ leaf_, lp
       const u64 src = kind == 1u ? (cand >> leaf[MW_LEAF_SHIFT]) : fmix64(cand ^ ((u64)id * 0x9E3779B97F4A7C15ull));
       digit = (u32)src & ((bits >= 32) ? 0xffffffffu : ((1u << bits) - 1u));
     }
-    lptr e = pool + leaf[MW_LEAF_POOL] + digit * MW_POOL_ENTRY_WORDS;
-    if (e[0] & 1u) {
-      random_leaf(id, w, seed, cand, out);
-    } else if (w <= 32u) {
-      out[0] = e[1];
+    lptr e = pool + leaf[MW_LEAF_POOL] + digit * MW_POOL_ENTRY_WORDS_OF(w);
+    if (w < 32u) {  // one-word narrow entry
+      const u32 x = e[0];
+      if (x & MW_POOL_NARROW_RANDOM) {
+        random_leaf(id, w, seed, cand, out);
+      } else {
+        out[0] = x;
 #pragma unroll
-      for (int k = 1; k < 8; ++k) out[k] = 0u;
-      canon(out, w);
+        for (int k = 1; k < 8; ++k) out[k] = 0u;
+      }
+    } else if (e[0] & 1u) {
+      random_leaf(id, w, seed, cand, out);
     } else {
 #pragma unroll
       for (int k = 0; k < 8; ++k) out[k] = e[1 + k];
@@ -220,7 +226,8 @@ __global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __r
     const u64 hit = __ballot(ok);
     if (hit) {
       const u32 first = (u32)__ffsll((unsigned long long)hit) - 1u;
-      if (lane == first) atomicMin((unsigned long long*)&out_min[blockIdx.y], (unsigned long long)cand);
+      if (lane == first && cand < __hip_atomic_load(&out_min[blockIdx.y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMin((unsigned long long*)&out_min[blockIdx.y], (unsigned long long)cand);
     }
     const u64 nvalid = (u64)__popcll(__ballot(valid));
     evals += nvalid;
@@ -550,6 +557,18 @@ bool asm_eligible(const mg_prog_desc* d) {
   return true;
 }
 
+// LDS words of spill area for an asm launch whose largest pool has max_pool
+// words: the pool is staged whole in LDS, the hottest spill words take what is
+// left of the block's 80 KiB and the rest spill to the global buffer.  False if
+// the pool alone does not fit (the programs then run on the compiled interpreter).
+bool asm_lds_fit(u32 max_spill, u32 max_pool, u32* nlds) {
+  const size_t budget = (size_t)kLdsSpillWords * kBlock * 4, pool_bytes = (size_t)max_pool * 4;
+  if (pool_bytes > budget) return false;
+  const u32 pool_words_lds = (u32)((pool_bytes + kBlock * 4 - 1) / (kBlock * 4));  // in spill-word rows
+  *nlds = std::min(max_spill, kLdsSpillWords - pool_words_lds);
+  return true;
+}
+
 // MYTHRIL_AMD_ASM=0 keeps every program on the compiled interpreter (A/B runs, tests)
 bool asm_enabled() {
   const char* e = std::getenv("MYTHRIL_AMD_ASM");
@@ -582,7 +601,7 @@ int mg_init(int device, mg_ctx** out) {
     c->ncu = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
-      hipMalloc(&c->d_counter, kNCounters * sizeof(u64)) != hipSuccess) {
+      hipMalloc(&c->d_counter, kCounterWords * sizeof(u64)) != hipSuccess) {
     delete c;
     return fail(MG_E_HIP, "context setup failed");
   }
@@ -593,6 +612,8 @@ int mg_init(int device, mg_ctx** out) {
       hipFuncSetAttribute((const void*)mw_search_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
           hipSuccess ||
       hipFuncSetAttribute((const void*)mw_eval_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
+          hipSuccess ||
+      hipFuncSetAttribute((const void*)mw_search_asm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
           hipSuccess) {
     (void)hipGetLastError();  // older runtimes: the default limit already covers it
   }
@@ -767,7 +788,8 @@ int mg_prog_has_kernel(const mg_prog* p) { return prog_live(p) && p->jit_ready()
 int mg_prog_engine(const mg_prog* p) {
   if (!prog_live(p)) return fail(MG_E_ARG, "mg_prog_engine: not a live program");
   if (p->jit_ready()) return 2;
-  return p->asm_ok && asm_enabled() ? 1 : 0;
+  u32 nlds = 0;   // the engine mg_search gives this program alone (a pool too big for LDS: compiled)
+  return p->asm_ok && asm_enabled() && asm_lds_fit(p->dev.n_spill, p->dev.npool, &nlds) ? 1 : 0;
 }
 
 int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uint64_t begin,
@@ -801,18 +823,25 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
     else (use_asm && progs[i]->asm_ok ? gasm : gcpp).push_back(i);
     ops += progs[i]->ops_per_eval;
   }
-  // the asm group needs its pools staged in LDS beside the spill words
+  // the asm group needs its pools staged in LDS (programs whose pool does not
+  // fit run on the compiled interpreter)
+  u32 asm_nlds = 0;
   if (!gasm.empty()) {
-    u32 ms = 0, mp = 0;
+    std::vector<size_t> fit;
+    u32 ms = 0;
     for (size_t i : gasm) {
-      ms = std::max(ms, progs[i]->dev.n_spill);
-      mp = std::max(mp, progs[i]->dev.npool);
+      u32 n1 = 0;
+      if (count < (1ull << 40) && asm_lds_fit(progs[i]->dev.n_spill, progs[i]->dev.npool, &n1)) {
+        fit.push_back(i);
+        ms = std::max(ms, progs[i]->dev.n_spill);
+      } else {
+        gcpp.push_back(i);
+      }
     }
-    if ((size_t)std::min(ms, kLdsSpillWords) * kBlock * 4 + (size_t)mp * 4 > (size_t)kLdsSpillWords * kBlock * 4 ||
-        count >= (1ull << 40)) {
-      gcpp.insert(gcpp.end(), gasm.begin(), gasm.end());
-      gasm.clear();
-    }
+    gasm.swap(fit);
+    u32 mp = 0;
+    for (size_t i : gasm) mp = std::max(mp, progs[i]->dev.npool);
+    if (!gasm.empty()) (void)asm_lds_fit(ms, mp, &asm_nlds);
   }
   std::vector<size_t> interp(gasm);
   interp.insert(interp.end(), gcpp.begin(), gcpp.end());
@@ -837,7 +866,7 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
     G.gx = std::max<u64>(1, (u64)c->ncu * 8 / G.n);
     G.gx = std::min<u64>(G.gx, nchunks);
     const u64 nthreads = G.gx * G.n * kBlock;
-    G.nlds = std::min(max_spill, kLdsSpillWords);
+    G.nlds = &G == &groups[0] ? asm_nlds : std::min(max_spill, kLdsSpillWords);
     spill_need = std::max(spill_need, (size_t)(max_spill - G.nlds) * nthreads * sizeof(u32));
   }
   if (ni) {
@@ -862,7 +891,7 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   }
   std::vector<u64> init(nprog, MG_NONE);
   HIPCHK(hipMemcpyAsync(c->d_min, init.data(), nprog * sizeof(u64), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemsetAsync(c->d_counter, 0, kNCounters * sizeof(u64), c->stream));
+  HIPCHK(hipMemsetAsync(c->d_counter, 0, kCounterWords * sizeof(u64), c->stream));
   HIPCHK(hipEventRecord(c->e0, c->stream));
   if (groups[0].n) {
     const Group& G = groups[0];
@@ -895,12 +924,16 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
     if (rc) return rc;
   }
   HIPCHK(hipEventRecord(c->e1, c->stream));
-  u64 ctr[kNCounters] = {0, 0, 0, 0, 0};
+  std::vector<u64> stripes(kCounterWords);
   std::vector<u64> mins(nprog);
   HIPCHK(hipMemcpyAsync(mins.data(), c->d_min, nprog * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(ctr, c->d_counter, kNCounters * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-  const u64 evals = ctr[0];
+  HIPCHK(hipMemcpyAsync(stripes.data(), c->d_counter, kCounterWords * sizeof(u64), hipMemcpyDeviceToHost,
+                        c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  u64 ctr[kNCounters] = {0, 0, 0, 0, 0};
+  for (size_t sidx = 0; sidx <= MW_CTR_STRIPES; ++sidx)
+    for (int k = 0; k < kNCounters; ++k) ctr[k] += stripes[sidx * MW_CTR_STRIPE_WORDS + k];
+  const u64 evals = ctr[0];
   for (size_t j = 0; j < ni; ++j) out_min_idx[interp[j]] = mins[j];
   for (size_t j = 0; j < special.size(); ++j) out_min_idx[special[j]] = mins[ni + j];
   if (st) {
@@ -972,9 +1005,9 @@ int mg_eval(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncan
 // with a verdict array); 1 = not applicable (the caller uses mw_eval_kernel).
 static int eval_asm(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, size_t count, uint32_t* verdict) {
   if (!asm_enabled() || !p->asm_ok || begin + count < begin || count >= (1ull << 40)) return 1;
-  const u32 nlds = std::min(p->dev.n_spill, kLdsSpillWords);
+  u32 nlds = 0;
+  if (!asm_lds_fit(p->dev.n_spill, p->dev.npool, &nlds)) return 1;
   const size_t lds = (size_t)nlds * kBlock * 4 + (size_t)p->dev.npool * 4;
-  if (lds > (size_t)kLdsSpillWords * kBlock * 4) return 1;
   std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
   (void)hipGetLastError();
@@ -1002,7 +1035,7 @@ static int eval_asm(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, 
   hipError_t e = hipMemcpyAsync(c->d_progs, &p->dev, sizeof(ProgDev), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_min, &none, sizeof(u64), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_asmargs, &aa, sizeof(AsmArgs), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, kNCounters * sizeof(u64), c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, kCounterWords * sizeof(u64), c->stream);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(mw_search_asm_kernel, dim3((u32)gx, 1u), dim3(kBlock), lds, c->stream, c->d_progs,
                        (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, nlds);
@@ -1034,7 +1067,7 @@ int mg_eval_generated(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin
   if (hipMalloc(&d_v, count * 4) != hipSuccess) return fail(MG_E_NOMEM, "eval verdict alloc");
   const u64 none = MG_NONE;
   hipError_t e = hipMemcpyAsync(c->d_min, &none, sizeof(u64), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, kNCounters * sizeof(u64), c->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, kCounterWords * sizeof(u64), c->stream);
   if (e == hipSuccess) {
     rc = launch_jit(c, p, seed, begin, count, 0u, c->d_min, d_v);
     if (rc) {

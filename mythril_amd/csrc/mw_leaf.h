@@ -107,8 +107,17 @@ MW_HD void leaf_fields(u32 w, u32 kind, u32 id, u32 shift, u32 bits, u32 poff, u
       const u64 src = kind == 1u ? (cand >> shift) : fmix64(cand ^ ((u64)id * 0x9E3779B97F4A7C15ull));
       digit = (u32)src & ((bits >= 32) ? 0xffffffffu : ((1u << bits) - 1u));
     }
-    const u32* e = pool + poff + (u64)digit * MW_POOL_ENTRY_WORDS;
-    if (e[0] & 1u) {
+    const u32* e = pool + poff + (u64)digit * MW_POOL_ENTRY_WORDS_OF(w);
+    if (w < 32u) {   // one-word narrow entry
+      const u32 x = e[0];
+      if (x & MW_POOL_NARROW_RANDOM) {
+        random_leaf(id, w, seed, cand, out);
+      } else {
+        out[0] = x;
+#pragma unroll
+        for (int k = 1; k < 8; ++k) out[k] = 0u;
+      }
+    } else if (e[0] & 1u) {
       random_leaf(id, w, seed, cand, out);
     } else {
 #pragma unroll
@@ -154,14 +163,18 @@ MW_HD void leaf_value(const u32* __restrict__ leaf_, const u32* __restrict__ poo
                                  : fmix64(cand ^ ((u64)id * 0x9E3779B97F4A7C15ull));
       digit = (u32)src & ((bits >= 32) ? 0xffffffffu : ((1u << bits) - 1u));
     }
-    const u32* e = pool + leaf[MW_LEAF_POOL] + (u64)digit * MW_POOL_ENTRY_WORDS;
-    if (e[0] & 1u) {
-      random_leaf(id, w, seed, cand, out);
-    } else if (w <= 32u) {  // narrow leaf (calldata bytes, Bools): one limb of the entry, not eight
-      out[0] = e[1];
+    const u32* e = pool + leaf[MW_LEAF_POOL] + (u64)digit * MW_POOL_ENTRY_WORDS_OF(w);
+    if (w < 32u) {  // narrow leaf (calldata bytes, Bools): one-word entry
+      const u32 x = e[0];
+      if (x & MW_POOL_NARROW_RANDOM) {
+        random_leaf(id, w, seed, cand, out);
+      } else {
+        out[0] = x;
 #pragma unroll
-      for (int k = 1; k < 8; ++k) out[k] = 0u;
-      canon(out, w);
+        for (int k = 1; k < 8; ++k) out[k] = 0u;
+      }
+    } else if (e[0] & 1u) {
+      random_leaf(id, w, seed, cand, out);
     } else {
 #pragma unroll
       for (int k = 0; k < 8; ++k) out[k] = e[1 + k];

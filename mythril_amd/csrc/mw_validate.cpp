@@ -182,7 +182,7 @@ int mg_validate_desc(const mg_prog_desc* d) {
       if (L[MW_LEAF_KIND] == 3 && L[MW_LEAF_BITS] &&
           (u64)L[MW_LEAF_SHIFT] + (u64)(L[MW_LEAF_BITS] - 1) * L[MW_LEAF_STRIDE] > 63)
         return fail(MG_E_PROG, "interleaved digit beyond the 64-bit index");
-      u64 need = (u64)L[MW_LEAF_POOL] + ((u64)1 << L[MW_LEAF_BITS]) * MW_POOL_ENTRY_WORDS;
+      u64 need = (u64)L[MW_LEAF_POOL] + ((u64)1 << L[MW_LEAF_BITS]) * MW_POOL_ENTRY_WORDS_OF(L[MW_LEAF_WIDTH]);
       if (need > d->npool_words) return fail(MG_E_PROG, "pool out of range");
     } else if (L[MW_LEAF_KIND] != 0) {
       return fail(MG_E_PROG, "bad leaf kind");

@@ -263,7 +263,8 @@ def _pad_pow2(vals: List[int]) -> List[int]:
     return [vals[i % len(vals)] for i in range(n)]
 
 
-def _restrict(pool: List[Optional[int]], name: str, w: int, exact, interval, align, pool_size: int):
+def _restrict(pool: List[Optional[int]], name: str, w: int, exact, interval, align, pool_size: int,
+              props=()):
     lo, hi = interval.get(name, (0, (1 << w) - 1))
     K = align.get(name, 1)
     ok = lambda v: lo <= v <= hi and v % K == 0   # noqa: E731
@@ -279,9 +280,22 @@ def _restrict(pool: List[Optional[int]], name: str, w: int, exact, interval, ali
     keep = [v for v in pool if v is not None and ok(v)]
     steps = (last - first) // K
     spread = [first + (steps * i // 16) * K for i in range(1, 16)]
-    # bounds, the strongest harvested values, then values spread over the interval
-    vals = list(dict.fromkeys(v for v in [first, last, first + K, last - K] + keep[:8] + spread + keep[8:]
-                              if ok(v)))[:pool_size]
+    # Pool order is search order, and with many leaves only the first two
+    # entries vary below 2^24.  Bounds first, then the largest harvested
+    # proposal below 2^(w-1), the signed maximum (above every signed guard,
+    # where the upper bound 2^w-1 is -1), the bounds' neighbours, the other
+    # harvested values and values spread over the interval.  A calldatasize
+    # (calldata.py:214-231) leads with that proposal instead: the highest guard
+    # `i <s size` of a calldata read, so every argument byte reads (0x44 for two
+    # ABI words); the lower bound (selector only) and 2^w-1 (nothing reads, not
+    # even the selector) follow.
+    # (a proposal at most one step above the lower bound is that bound's own +-1)
+    pos = [v for v in props if ok(v) and first + K < v < (1 << (w - 1)) and v != last] if w >= 2 else []
+    top = [max(pos)] if pos else []
+    smax = [(1 << (w - 1)) - 1] if w >= 2 else []
+    head = top + [first, last] if name.endswith("calldatasize") else [first, last] + top
+    vals = list(dict.fromkeys(v for v in head + smax + [first + K, last - K] + keep[:8]
+                              + spread + keep[8:] if ok(v)))[:pool_size]
     if steps + 1 > len(vals) and (hi - lo) >= (1 << max(w - 2, 0)) and K == 1:
         return vals + [None] * max(1, pool_size // 4)   # wide interval: random draws still land often
     return _pad_pow2(vals)   # no RANDOM padding: a random draw would almost never satisfy the facts
@@ -383,7 +397,8 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
             nrand = max(1, pool_size - len(pool)) if len(pool) >= nfixed else max(1, len(pool) // 3)
             pool += [None] * nrand
             if restrict:
-                pool = _restrict(pool, leaf.name, w, exact, interval, dom_align, pool_size)
+                pool = _restrict(pool, leaf.name, w, exact, interval, dom_align, pool_size,
+                                 proposals.get(leaf.name, ()))
         specs[leaf.name] = LeafSpec(leaf.name, w, pool=pool)
     _tie_words(nodes, specs, word_props, set(exact), uniq_consts, pool_size, random_share)
     return specs

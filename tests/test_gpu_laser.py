@@ -5,8 +5,8 @@ on gfx950:
   interpreter equal the C oracle's (oracle/c) on the same indices;
 * search at config C2's count (2^24 candidates per query, early exit +
   stop-after-hit, 64 programs per launch): every witness satisfies the
-  ORIGINAL formula under the oracle (arrays and UFs included), and the SAT
-  queries (satisfied by the concolic model) are witnessed."""
+  ORIGINAL formula under the oracle (arrays and UFs included), and every SAT
+  query (satisfied by the concolic model) is witnessed."""
 import json
 import os
 
@@ -66,4 +66,6 @@ def test_search_at_c2_count(queries, eng):
             elif m["status"] == "sat":
                 missed.append(m["file"])
     print(f"LASER corpus at 2^24: witnessed {found} of {total}; SAT missed: {missed}")
-    assert found["sat"] >= 0.9 * total["sat"], (found, total)
+    # every query the concolic run satisfied is witnessed (VERDICT r2 item 5:
+    # the calldatasize pools now lead with the highest guard of a calldata read)
+    assert found["sat"] == total["sat"], (found, total, missed)

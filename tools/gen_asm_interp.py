@@ -858,21 +858,23 @@ def leaf(g):
     g.label("Lm_or_%=")
     g(f"v_lshl_or_b32 {v(T + 6)}, {v(T + 7)}, {s(S[4])}, {v(T + 6)}",
       f"s_add_u32 {s(S[4])}, {s(S[4])}, 1", f"s_add_u32 {s(S[5])}, {s(S[5])}, {s(D + 7)}", "s_branch Lm_loop_%=")
-    # pool entry (9 words: flag, 8 limbs) in LDS at poolb + 4 * (poff + 9 * digit)
+    # pool entry in LDS at poolb + 4 * poff: width >= 32: 9 words (flag, 8 limbs)
+    # at + 36 * digit; width < 32: one word (bit 31 RANDOM, else the value) at + 4 * digit
     g.label("Lgather_%=")
     g(f"s_lshl_b32 {s(S[6])}, {s(D + 5)}, 2", f"s_add_u32 {s(S[6])}, {s(S[6])}, {s(POOLB)}",
+      f"s_cmp_lt_u32 {s(D)}, 32", "s_cbranch_scc1 Lg_narrow_%=",
       f"v_mov_b32_e32 {v(T + 5)}, 36", f"v_mad_u32_u24 {v(T + 5)}, {v(T + 6)}, {v(T + 5)}, {s(S[6])}",
-      f"ds_read_b32 {v(T + 4)}, {v(T + 5)}",
-      f"s_cmp_le_u32 {s(D)}, 32", "s_cbranch_scc1 Lg_narrow_%=")
+      f"ds_read_b32 {v(T + 4)}, {v(T + 5)}")
     for k in range(4):
         g(f"ds_read2_b32 {vr(XC + 2 * k, 2)}, {v(T + 5)} offset0:{1 + 2 * k} offset1:{2 + 2 * k}")
-    g("s_branch Lg_wait_%=")
+    g("s_waitcnt lgkmcnt(0)", f"v_and_b32_e32 {v(T + 4)}, 1, {v(T + 4)}", "s_branch Lg_flag_%=")
     g.label("Lg_narrow_%=")
-    g(f"ds_read_b32 {v(XC)}, {v(T + 5)} offset:4")
+    g(f"v_lshl_add_u32 {v(T + 5)}, {v(T + 6)}, 2, {s(S[6])}", f"ds_read_b32 {v(XC)}, {v(T + 5)}")
     for k in range(1, 8):
         g(f"v_mov_b32_e32 {v(XC + k)}, 0")
-    g.label("Lg_wait_%=")
-    g("s_waitcnt lgkmcnt(0)", f"v_and_b32_e32 {v(T + 4)}, 1, {v(T + 4)}", f"v_cmp_ne_u32_e32 vcc, 0, {v(T + 4)}",
+    g("s_waitcnt lgkmcnt(0)", f"v_lshrrev_b32_e32 {v(T + 4)}, 31, {v(XC)}")
+    g.label("Lg_flag_%=")
+    g(f"v_cmp_ne_u32_e32 vcc, 0, {v(T + 4)}",
       "s_nop 1", "s_cmp_eq_u64 vcc, 0", "s_cbranch_scc1 Lleaf_canon_%=",
       f"s_mov_b64 {sr(MSK, 2)}, vcc", f"s_call_b64 {sr(PRET, 2)}, Lphilox_%=", "s_nop 1")
     for k in range(8):
