@@ -7,7 +7,7 @@ candidates.  Prints ns per instruction per wave-slot and, under rocprofv3
 --pmc, the per-dispatch counters give VALU/SALU/SMEM instructions per
 bytecode instruction.
 
-    python tools/interp_opcost.py [--repeat 2000] [--log2 20]
+    python tools/interp_opcost.py [--repeat 2000] [--log2 20] [--engines asm,interp]
 """
 import argparse
 import copy
@@ -86,6 +86,7 @@ def main():
     ap.add_argument("--repeat", type=int, default=2000)
     ap.add_argument("--log2", type=int, default=20)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--engines", default="asm,interp")
     a = ap.parse_args()
     from mythril_amd.runtime import Device
     p = base_program()
@@ -98,14 +99,19 @@ def main():
         rep = a.repeat // 4 if name.startswith("LEAF") else a.repeat
         q = assemble(p, body, rep)
         dp = dev.load(q)
-        dev.search([dp], 1, 0, n, 0)   # warm
-        _, st = dev.search([dp], 1, 0, n, 0)
+        # asm: the threaded-dispatch interpreter (default); interp: the compiled
+        # one (MYTHRIL_AMD_ASM=0, read by the library at each call)
+        for engine in a.engines.split(","):
+            os.environ["MYTHRIL_AMD_ASM"] = "0" if engine == "interp" else "1"
+            ran = dev.engine_of(dp)
+            dev.search([dp], 1, 0, n, 0)   # warm
+            _, st = dev.search([dp], 1, 0, n, 0)
+            waves = n // 64
+            ns_per = st["kernel_ms"] * 1e6 / (waves / slots) / rep
+            print(json.dumps({"op": name, "engine": ran, "repeat": rep, "kernel_ms": round(st["kernel_ms"], 3),
+                              "ns_per_insn_per_wave_slot": round(ns_per, 1),
+                              "cycles_at_2p4GHz": round(ns_per * 2.4, 0)}), flush=True)
         dp.free()
-        waves = n // 64
-        ns_per = st["kernel_ms"] * 1e6 / (waves / slots) / rep
-        print(json.dumps({"op": name, "repeat": rep, "kernel_ms": round(st["kernel_ms"], 3),
-                          "ns_per_insn_per_wave_slot": round(ns_per, 1),
-                          "cycles_at_2p4GHz": round(ns_per * 2.4, 0)}), flush=True)
     dev.close()
 
 
