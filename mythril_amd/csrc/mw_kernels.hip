@@ -28,6 +28,7 @@
 
 extern "C" int mw_fail(int code, const char* msg);
 extern "C" int mg_validate_desc(const mg_prog_desc* d);
+extern "C" void mw_asm_predecode(const uint32_t* code, size_t nwords, uint32_t* out);
 
 using namespace mw;
 
@@ -402,6 +403,7 @@ struct mg_prog {
   u64 ops_per_eval = 0;
   u64 sig = 0;                  // FNV-1a 64 of the program words (mythril_amd/jit.py signature)
   bool asm_ok = false;          // every opcode and leaf kind has a handler in mw_search_asm_kernel
+  ProgDev adev{};               // dev with code = its predecoded copy (mw_asm_predecode), in d_buf
   // specialised kernels (mg_prog_attach_kernel): one per part, launched in order
   struct Part {
     hipModule_t mod = nullptr;
@@ -670,7 +672,9 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
   // operand fetch reads cpool[slot] (slot < 64) before selecting the register
   const size_t nc = d->ncode_words, nk = (d->nconst_words + 8 > MW_KPAD ? d->nconst_words + 8 : MW_KPAD), nl = d->nleaves * MW_LEAF_WORDS + 8,
                np = d->npool_words + 8;
-  const size_t total = nc + nk + nl + np;
+  const bool asm_ok = asm_eligible(d);
+  const size_t na = asm_ok ? nc + 8 : 0;   // + the block after END the dispatch prefetches
+  const size_t total = nc + nk + nl + np + na;
   mg_prog* p = new mg_prog();
   p->ctx = c;
   p->desc = *d;
@@ -685,6 +689,7 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
   if (d->nconst_words) std::memcpy(h.data() + nc, d->consts, d->nconst_words * 4);
   if (d->nleaves) std::memcpy(h.data() + nc + nk, d->leaves, d->nleaves * MW_LEAF_WORDS * 4);
   if (d->npool_words) std::memcpy(h.data() + nc + nk + nl, d->pool, d->npool_words * 4);
+  if (asm_ok) mw_asm_predecode(d->code, nc, h.data() + nc + nk + nl + np);
   if (hipMemcpy(p->d_buf, h.data(), total * 4, hipMemcpyHostToDevice) != hipSuccess) {
     hipFree(p->d_buf);
     delete p;
@@ -697,7 +702,9 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
   p->dev.n_spill = d->n_spill;
   p->dev.npool = (u32)d->npool_words;
   p->dev.n_insn = (u32)(nc / 4);
-  p->asm_ok = asm_eligible(d);
+  p->asm_ok = asm_ok;
+  p->adev = p->dev;
+  if (asm_ok) p->adev.code = p->d_buf + nc + nk + nl + np;
   // the desc's host pointers are not retained
   p->desc.code = nullptr;
   p->desc.consts = nullptr;
@@ -846,7 +853,8 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   std::vector<size_t> interp(gasm);
   interp.insert(interp.end(), gcpp.begin(), gcpp.end());
   std::vector<ProgDev> hp;
-  for (size_t i : interp) hp.push_back(progs[i]->dev);
+  for (size_t j = 0; j < interp.size(); ++j)   // the asm group reads the predecoded code
+    hp.push_back(j < gasm.size() ? progs[interp[j]]->adev : progs[interp[j]]->dev);
   const u64 nchunks = (count + kBlock - 1) / kBlock;
   const size_t ni = interp.size();
   struct Group {
@@ -1032,7 +1040,7 @@ static int eval_asm(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, 
   aa.spillbuf = c->d_spill;
   aa.verdict = d_v;
   const u64 none = MG_NONE;
-  hipError_t e = hipMemcpyAsync(c->d_progs, &p->dev, sizeof(ProgDev), hipMemcpyHostToDevice, c->stream);
+  hipError_t e = hipMemcpyAsync(c->d_progs, &p->adev, sizeof(ProgDev), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_min, &none, sizeof(u64), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_asmargs, &aa, sizeof(AsmArgs), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, kCounterWords * sizeof(u64), c->stream);

@@ -193,4 +193,27 @@ int mg_validate_desc(const mg_prog_desc* d) {
   return 0;
 }
 
+// The asm interpreter's copy of a validated program (mw_asm_interp.inc reads
+// operands without decoding them): w0 and w3 unchanged; the dst field becomes
+// the written N slot (0..63) in [5:0] and the written W slot x 8 in [13:8]; a
+// W register operand becomes its slot x 8 (the VGPR offset of its limb 0 in
+// the W file), N register operands and constants stay as they are.
+void mw_asm_predecode(const u32* code, size_t nwords, u32* out) {
+  for (size_t i = 0; i + 3 < nwords; i += 4) {
+    const u32* I = code + i;
+    u32* O = out + i;
+    OpShape sh;
+    (void)op_shape(I[0] & 0xffu, sh);   // validated: every opcode is known
+    const u32 dst = I[1] & 0xffffu, a = I[1] >> 16, b = I[2] & 0xffffu, c = I[2] >> 16;
+    u32 d2 = 0;
+    if (sh.dst == 4) d2 = MW_DST_NLO(dst) != MW_N_RESERVED ? MW_DST_NLO(dst) : 32u + MW_DST_NHI(dst);
+    else if (sh.dst == 3) d2 = (MW_DST_W(dst) * 8u) << 8;
+    auto opnd = [](int kind, u32 f) { return (kind == 1 && !(f & MW_KBIT)) ? f * 8u : f; };
+    O[0] = I[0];
+    O[1] = d2 | (opnd(sh.a, a) << 16);
+    O[2] = opnd(sh.b, b) | (opnd(sh.c, c) << 16);
+    O[3] = I[3];
+  }
+}
+
 }  // extern "C"

@@ -48,13 +48,15 @@ CLO, CHI, ALIVE, LDSOFF, GOFF = 160, 161, 162, 163, 164
 # scalar state
 CUR = 40          # s40..s43 current instruction words w0..w3
 NXT = 44          # s44..s47 next instruction (prefetched)
-ADDR = 48         # s[48:49] address of the next instruction
+SOFF = 48         # byte offset of the next instruction from CODE0
+TABLO = 49        # address of the dispatch table (Ltab), low / high word
+TABHI = 58
+SIDX = 19         # register-file index of an operand / write-back
 CPOOL = 50        # s[50:51] constant pool
 LEAVES = 52       # s[52:53] leaf table
 POOLB = 54        # pool LDS byte base
 FLAGS = 55
 SEED = 56         # s[56:57]
-BUDGET = 58       # instructions left (a malformed program can never loop)
 NLDS = 59         # spill words in LDS
 GSP = 60          # s[60:61] global spill base
 GSTRIDE = 62      # bytes between consecutive global spill words (nthreads x 4)
@@ -72,7 +74,6 @@ SX = 94           # s[94:95] scratch pair
 
 # chunk loop state (s16..s39)
 CH, NCH, GDX = 16, 17, 18
-NINSN = 19
 BEGIN = 20        # s[20:21]
 END = 22          # s[22:23]
 BASE = 24         # s[24:25]
@@ -110,6 +111,7 @@ class Gen:
         self.lines = []
         self.tail = []      # out-of-line blocks (constant operands), emitted after the handler
         self.n = 0
+        self.bound = {}     # name -> operand field (field())
 
     def L(self, base):
         self.n += 1
@@ -126,36 +128,57 @@ class Gen:
         self.tail = []
 
     # ------------------------------------------------------------ operands
+    # Operands come from the asm engine's predecoded copy of the program
+    # (mw_validate.cpp mw_asm_predecode): a register operand field holds the
+    # N slot (0..63) or the W slot x 8, so it is the VGPR index relative to the
+    # file's base as it stands; bit 15 flags a constant (word offset).
+    # field() only binds an operand to a name; fetch_n / fetch_w read it.
+    WORD = {"a": (CUR + 1, "hi"), "b": (CUR + 2, "lo"), "c": (CUR + 2, "hi")}
+
     def field(self, which, dst):
-        """operand field a/b/c (16 bits) into SGPR dst"""
-        if which == "a":
-            self(f"s_lshr_b32 {s(dst)}, {s(CUR + 1)}, 16")
-        elif which == "b":
-            self(f"s_and_b32 {s(dst)}, {s(CUR + 2)}, 0xffff")
+        """bind operand field a/b/c to the name dst (no code)"""
+        self.bound[dst] = which
+
+    def _index(self, which, dst_sgpr):
+        wd, half = self.WORD[which]
+        if half == "hi":
+            self(f"s_lshr_b32 {dst_sgpr}, {s(wd)}, 16")
         else:
-            self(f"s_lshr_b32 {s(dst)}, {s(CUR + 2)}, 16")
+            self(f"s_and_b32 {dst_sgpr}, {s(wd)}, 0xffff")
+
+    def _is_const(self, which, label):
+        wd, half = self.WORD[which]
+        self(f"s_bitcmp1_b32 {s(wd)}, {31 if half == 'hi' else 15}", f"s_cbranch_scc1 {label}")
 
     def fetch_n(self, f, dst):
-        """N/K operand in SGPR f -> VGPR dst"""
+        """N/K operand bound to f -> VGPR dst"""
+        which = self.bound[f]
         lk, lr = self.L("kn"), self.L("rn")
-        self(f"s_bitcmp1_b32 {s(f)}, 15", f"s_cbranch_scc1 {lk}",
-             f"s_set_gpr_idx_on {s(f)}, gpr_idx(SRC0)", f"v_mov_b32_e32 {v(dst)}, {v(N0)}", "s_set_gpr_idx_off")
+        self._is_const(which, lk)
+        self._index(which, s(SIDX))
+        self(f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(SRC0)", f"v_mov_b32_e32 {v(dst)}, {v(N0)}", "s_set_gpr_idx_off")
         self.label(lr)
-        self.tail += [f"{lk}:", f"s_and_b32 {s(f)}, {s(f)}, 0x7fff", f"s_lshl_b32 {s(f)}, {s(f)}, 2",
-                      f"s_load_dword {s(f)}, {sr(CPOOL, 2)}, {s(f)}", "s_waitcnt lgkmcnt(0)",
-                      f"v_mov_b32_e32 {v(dst)}, {s(f)}", f"s_branch {lr}"]
+        wd, half = self.WORD[which]
+        off = f"s_lshr_b32 {s(SX)}, {s(wd)}, 16" if half == "hi" else f"s_and_b32 {s(SX)}, {s(wd)}, 0x7fff"
+        self.tail += [f"{lk}:", off, f"s_and_b32 {s(SX)}, {s(SX)}, 0x7fff", f"s_lshl_b32 {s(SX)}, {s(SX)}, 2",
+                      f"s_load_dword {s(SX)}, {sr(CPOOL, 2)}, {s(SX)}", "s_waitcnt lgkmcnt(0)",
+                      f"v_mov_b32_e32 {v(dst)}, {s(SX)}", f"s_branch {lr}"]
 
     def fetch_w(self, f, dst):
-        """W/K operand in SGPR f -> VGPRs dst..dst+7"""
+        """W/K operand bound to f -> VGPRs dst..dst+7"""
+        which = self.bound[f]
         lk, lr = self.L("kw"), self.L("rw")
-        self(f"s_bitcmp1_b32 {s(f)}, 15", f"s_cbranch_scc1 {lk}", f"s_lshl_b32 {s(f)}, {s(f)}, 3",
-             f"s_set_gpr_idx_on {s(f)}, gpr_idx(SRC0)")
+        self._is_const(which, lk)
+        self._index(which, s(SIDX))
+        self(f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(SRC0)")
         for k in range(8):
             self(f"v_mov_b32_e32 {v(dst + k)}, {v(W0 + k)}")
         self("s_set_gpr_idx_off")
         self.label(lr)
-        t = [f"{lk}:", f"s_and_b32 {s(f)}, {s(f)}, 0x7fff", f"s_lshl_b32 {s(f)}, {s(f)}, 2",
-             f"s_load_dwordx8 {sr(DESC, 8)}, {sr(CPOOL, 2)}, {s(f)}", "s_waitcnt lgkmcnt(0)"]
+        wd, half = self.WORD[which]
+        off = f"s_lshr_b32 {s(SX)}, {s(wd)}, 16" if half == "hi" else f"s_and_b32 {s(SX)}, {s(wd)}, 0x7fff"
+        t = [f"{lk}:", off, f"s_and_b32 {s(SX)}, {s(SX)}, 0x7fff", f"s_lshl_b32 {s(SX)}, {s(SX)}, 2",
+             f"s_load_dwordx8 {sr(DESC, 8)}, {sr(CPOOL, 2)}, {s(SX)}", "s_waitcnt lgkmcnt(0)"]
         t += [f"v_mov_b32_e32 {v(dst + k)}, {s(DESC + k)}" for k in range(8)]
         self.tail += t + [f"s_branch {lr}"]
 
@@ -163,20 +186,19 @@ class Gen:
         self(f"s_lshr_b32 {s(dst)}, {s(CUR)}, 16")
 
     def nmask(self, w, dst):
-        """dst = w >= 32 ? ~0 : (1 << w) - 1 (w in SGPR)"""
-        self(f"s_bfm_b32 {s(dst)}, {s(w)}, 0", f"s_cmp_ge_u32 {s(w)}, 32", f"s_cselect_b32 {s(dst)}, -1, {s(dst)}")
+        """dst = w >= 32 ? ~0 : (1 << w) - 1 (w in SGPR, <= 32): the low word of
+        the 64-bit field mask (dst must start an aligned SGPR pair)"""
+        assert dst % 2 == 0
+        self(f"s_bfm_b64 {sr(dst, 2)}, {s(w)}, 0")
 
     def write_n(self, src):
-        """N result in VGPR src -> the slot the dst field names (NLO, or 32 + NHI)"""
-        a, b = S[6], S[7]
-        self(f"s_bfe_u32 {s(a)}, {s(CUR + 1)}, 0x50003", f"s_bfe_u32 {s(b)}, {s(CUR + 1)}, 0x50008",
-             f"s_add_u32 {s(b)}, {s(b)}, 32", f"s_cmp_eq_u32 {s(a)}, 31", f"s_cselect_b32 {s(a)}, {s(b)}, {s(a)}",
-             f"s_set_gpr_idx_on {s(a)}, gpr_idx(DST)", f"v_mov_b32_e32 {v(N0)}, {v(src)}", "s_set_gpr_idx_off")
+        """N result in VGPR src -> the N slot of the predecoded dst field [5:0]"""
+        self(f"s_and_b32 {s(SIDX)}, {s(CUR + 1)}, 0x3f", f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(DST)",
+             f"v_mov_b32_e32 {v(N0)}, {v(src)}", "s_set_gpr_idx_off")
 
     def write_w(self, src):
-        a = S[6]
-        self(f"s_and_b32 {s(a)}, {s(CUR + 1)}, 7", f"s_lshl_b32 {s(a)}, {s(a)}, 3",
-             f"s_set_gpr_idx_on {s(a)}, gpr_idx(DST)")
+        """W result in VGPRs src.. -> the W slot x 8 of the predecoded dst field [13:8]"""
+        self(f"s_bfe_u32 {s(SIDX)}, {s(CUR + 1)}, 0x60008", f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(DST)")
         for k in range(8):
             self(f"v_mov_b32_e32 {v(W0 + k)}, {v(src + k)}")
         self("s_set_gpr_idx_off")
@@ -223,7 +245,15 @@ class Gen:
         self(f"v_cndmask_b32_e64 {v(dst)}, {1 if invert else 0}, {0 if invert else 1}, vcc")
 
     def next(self):
-        self("s_branch Ldisp_%=")
+        """dispatch the next instruction (each handler ends in its own copy:
+        no jump back to a shared dispatch block).  It was prefetched one ahead;
+        the stream ends in a validated END and no instruction jumps, so the
+        offset only grows to it."""
+        self("s_waitcnt lgkmcnt(0)", f"s_mov_b64 {sr(CUR, 2)}, {sr(NXT, 2)}",
+             f"s_mov_b64 {sr(CUR + 2, 2)}, {sr(NXT + 2, 2)}",
+             f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, {s(SOFF)}",
+             f"s_and_b32 {s(JMP)}, {s(CUR)}, 0x7f", f"s_lshl2_add_u32 {s(SX)}, {s(JMP)}, {s(TABLO)}",
+             f"s_addc_u32 {s(SX + 1)}, {s(TABHI)}, 0", f"s_setpc_b64 {sr(SX, 2)}")
 
 
 def gen():
@@ -247,8 +277,8 @@ def gen():
             g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
             g(expr.format(d=v(XR), a=v(T), b=v(T + 1)))
             if masked:
-                g.width(S[2]), g.nmask(S[2], S[3])
-                g(f"v_and_b32_e32 {v(XR)}, {s(S[3])}, {v(XR)}")
+                g.width(S[2]), g.nmask(S[2], S[4])
+                g(f"v_and_b32_e32 {v(XR)}, {s(S[4])}, {v(XR)}")
             g.write_n(XR)
         handlers[name] = h
 
@@ -257,8 +287,8 @@ def gen():
         g.field("a", S[0]), g.field("b", S[1])
         g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
         g(f"v_mul_lo_u32 {v(XR)}, {v(T)}, {v(T + 1)}")
-        g.width(S[2]), g.nmask(S[2], S[3])
-        g(f"v_and_b32_e32 {v(XR)}, {s(S[3])}, {v(XR)}")
+        g.width(S[2]), g.nmask(S[2], S[4])
+        g(f"v_and_b32_e32 {v(XR)}, {s(S[4])}, {v(XR)}")
         g.write_n(XR)
 
     for name, cmp in (("N_SLTN", "v_cmp_lt_u32_e32"), ("N_SLEN", "v_cmp_le_u32_e32")):
@@ -279,9 +309,9 @@ def gen():
         # a * b < 2^w: the high word is 0 and (w < 32) the low word has no bit >= w
         g.field("a", S[0]), g.field("b", S[1])
         g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
-        g.width(S[2]), g.nmask(S[2], S[3])
+        g.width(S[2]), g.nmask(S[2], S[4])
         g(f"v_mul_hi_u32 {v(T + 2)}, {v(T)}, {v(T + 1)}", f"v_mul_lo_u32 {v(T + 3)}, {v(T)}, {v(T + 1)}",
-          f"s_not_b32 {s(S[3])}, {s(S[3])}", f"v_and_b32_e32 {v(T + 3)}, {s(S[3])}, {v(T + 3)}",
+          f"s_not_b32 {s(S[4])}, {s(S[4])}", f"v_and_b32_e32 {v(T + 3)}, {s(S[4])}, {v(T + 3)}",
           f"v_or_b32_e32 {v(T + 2)}, {v(T + 2)}, {v(T + 3)}", f"v_cmp_eq_u32_e32 vcc, 0, {v(T + 2)}")
         g.bool_from_vcc(XR)
         g.write_n(XR)
@@ -289,8 +319,8 @@ def gen():
     @handler("N_NOT")
     def _(g):
         g.field("a", S[0]), g.fetch_n(S[0], T)
-        g.width(S[2]), g.nmask(S[2], S[3])
-        g(f"v_xor_b32_e32 {v(XR)}, {s(S[3])}, {v(T)}")      # ~a & m == a ^ m (a canonical)
+        g.width(S[2]), g.nmask(S[2], S[4])
+        g(f"v_xor_b32_e32 {v(XR)}, {s(S[4])}, {v(T)}")      # ~a & m == a ^ m (a canonical)
         g.write_n(XR)
 
     for name, cmp in (("N_EQN", "v_cmp_eq_u32_e32"), ("N_ULTN", "v_cmp_lt_u32_e32"), ("N_ULEN", "v_cmp_le_u32_e32")):
@@ -317,8 +347,8 @@ def gen():
             big, j = g.L("sb"), g.L("sj")
             g(f"s_cmp_ge_u32 {s(CUR + 3)}, 32", f"s_cbranch_scc1 {big}",
               f"{op} {v(XR)}, {s(CUR + 3)}, {v(T)}")
-            g.width(S[2]), g.nmask(S[2], S[3])
-            g(f"v_and_b32_e32 {v(XR)}, {s(S[3])}, {v(XR)}", f"s_branch {j}")
+            g.width(S[2]), g.nmask(S[2], S[4])
+            g(f"v_and_b32_e32 {v(XR)}, {s(S[4])}, {v(XR)}", f"s_branch {j}")
             g.label(big)
             g(f"v_mov_b32_e32 {v(XR)}, 0")
             g.label(j)
@@ -602,9 +632,7 @@ def gen():
 
     def consume_next(g):
         g("s_waitcnt lgkmcnt(0)", f"s_mov_b64 {sr(CUR, 2)}, {sr(NXT, 2)}", f"s_mov_b64 {sr(CUR + 2, 2)}, {sr(NXT + 2, 2)}",
-          f"s_add_u32 {s(ADDR)}, {s(ADDR)}, 16", f"s_addc_u32 {s(ADDR + 1)}, {s(ADDR + 1)}, 0",
-          f"s_load_dwordx4 {sr(NXT, 4)}, {sr(ADDR, 2)}, 0x0",
-          f"s_sub_u32 {s(BUDGET)}, {s(BUDGET)}, 1", "s_cbranch_scc1 Lstop_%=")
+          f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, {s(SOFF)}")
 
     # -------------------------------------------------------- leaves
     def call_leaf(g, li):
@@ -711,11 +739,15 @@ def gen():
       f"s_load_dwordx8 {sr(DESC, 8)}, {sr(PROGP, 2)}, 0x0", f"s_load_dwordx4 {sr(72, 4)}, {sr(PROGP, 2)}, 0x20",
       "s_waitcnt lgkmcnt(0)",
       f"s_mov_b64 {sr(CODE0, 2)}, {sr(DESC, 2)}", f"s_mov_b64 {sr(CPOOL, 2)}, {sr(DESC + 2, 2)}",
-      f"s_mov_b64 {sr(LEAVES, 2)}, {sr(DESC + 4, 2)}", f"s_add_u32 {s(NINSN)}, {s(74)}, 1",
+      f"s_mov_b64 {sr(LEAVES, 2)}, {sr(DESC + 4, 2)}",
       f"s_lshl_b32 {s(POOLB)}, {s(NLDS)}, 10",
       f"s_mov_b32 {s(PM0)}, 0xD2511F53", f"s_mov_b32 {s(PM1)}, 0xCD9E8D57",
       f"s_mov_b64 {sr(EVALS, 2)}, 0",
       f"v_lshlrev_b32_e32 {v(LDSOFF)}, 2, {v(T)}", f"v_mov_b32_e32 {v(TID)}, {v(T)}")
+    # the dispatch table's address (s_getpc_b64 gives the next instruction's)
+    g(f"s_getpc_b64 {sr(SX, 2)}")
+    g.label("Lpc0_%=")
+    g(f"s_add_u32 {s(TABLO)}, {s(SX)}, (Ltab_%= - Lpc0_%=)", f"s_addc_u32 {s(TABHI)}, {s(SX + 1)}, 0")
     for k in range(128, 136, 2):
         g(f"v_mov_b64 {vr(k, 2)}, 0")
     for k in range(144, 152, 2):
@@ -740,20 +772,10 @@ def gen():
       f"s_mov_b64 {sr(VALID, 2)}, vcc", f"v_cndmask_b32_e64 {v(ALIVE)}, 0, 1, vcc")
     for k in range(0, 128, 2):
         g(f"v_mov_b64 {vr(k, 2)}, 0")
-    g(f"s_mov_b64 {sr(ADDR, 2)}, {sr(CODE0, 2)}", f"s_mov_b32 {s(BUDGET)}, {s(NINSN)}",
-      f"s_load_dwordx4 {sr(NXT, 4)}, {sr(ADDR, 2)}, 0x0")
+    g(f"s_mov_b32 {s(SOFF)}, 0", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, 0x0")
     # ---- dispatch
     g.label("Ldisp_%=")
-    g("s_waitcnt lgkmcnt(0)", f"s_mov_b64 {sr(CUR, 2)}, {sr(NXT, 2)}", f"s_mov_b64 {sr(CUR + 2, 2)}, {sr(NXT + 2, 2)}",
-      f"s_add_u32 {s(ADDR)}, {s(ADDR)}, 16", f"s_addc_u32 {s(ADDR + 1)}, {s(ADDR + 1)}, 0",
-      f"s_load_dwordx4 {sr(NXT, 4)}, {sr(ADDR, 2)}, 0x0",
-      f"s_sub_u32 {s(BUDGET)}, {s(BUDGET)}, 1", "s_cbranch_scc1 Lstop_%=",
-      f"s_and_b32 {s(JMP)}, {s(CUR)}, 0x7f", f"s_lshl_b32 {s(JMP)}, {s(JMP)}, 2",
-      f"s_getpc_b64 {sr(SX, 2)}")
-    g.label("Lpc_%=")
-    g(f"s_add_u32 {s(SX)}, {s(SX)}, {s(JMP)}", f"s_addc_u32 {s(SX + 1)}, {s(SX + 1)}, 0",
-      f"s_add_u32 {s(SX)}, {s(SX)}, (Ltab_%= - Lpc_%=)", f"s_addc_u32 {s(SX + 1)}, {s(SX + 1)}, 0",
-      f"s_setpc_b64 {sr(SX, 2)}")
+    g.next()
     g.label("Ltab_%=")
     names = {c: n for n, c in isa.OPCODES.items()}
     for code in range(NTAB):
