@@ -28,7 +28,8 @@
 
 extern "C" int mw_fail(int code, const char* msg);
 extern "C" int mg_validate_desc(const mg_prog_desc* d);
-extern "C" void mw_asm_predecode(const uint32_t* code, size_t nwords, uint32_t* out);
+extern "C" void mw_asm_predecode(const uint32_t* code, size_t nwords, const uint32_t* consts, size_t nconst,
+                                 uint32_t* out);
 
 using namespace mw;
 
@@ -689,7 +690,7 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
   if (d->nconst_words) std::memcpy(h.data() + nc, d->consts, d->nconst_words * 4);
   if (d->nleaves) std::memcpy(h.data() + nc + nk, d->leaves, d->nleaves * MW_LEAF_WORDS * 4);
   if (d->npool_words) std::memcpy(h.data() + nc + nk + nl, d->pool, d->npool_words * 4);
-  if (asm_ok) mw_asm_predecode(d->code, nc, h.data() + nc + nk + nl + np);
+  if (asm_ok) mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, h.data() + nc + nk + nl + np);
   if (hipMemcpy(p->d_buf, h.data(), total * 4, hipMemcpyHostToDevice) != hipSuccess) {
     hipFree(p->d_buf);
     delete p;

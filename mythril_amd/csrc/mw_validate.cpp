@@ -197,8 +197,11 @@ int mg_validate_desc(const mg_prog_desc* d) {
 // operands without decoding them): w0 and w3 unchanged; the dst field becomes
 // the written N slot (0..63) in [5:0] and the written W slot x 8 in [13:8]; a
 // W register operand becomes its slot x 8 (the VGPR offset of its limb 0 in
-// the W file), N register operands and constants stay as they are.
-void mw_asm_predecode(const u32* code, size_t nwords, u32* out) {
+// the W file), N register operands and constants stay as they are, except a
+// W_CDINS byte index (always a constant) below 0x4000, which becomes
+// 0x4000 | index (the handler then compares it with one 32-bit summary of the
+// size instead of a signed 256-bit subtraction).
+void mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t nconst, u32* out) {
   for (size_t i = 0; i + 3 < nwords; i += 4) {
     const u32* I = code + i;
     u32* O = out + i;
@@ -211,7 +214,14 @@ void mw_asm_predecode(const u32* code, size_t nwords, u32* out) {
     auto opnd = [](int kind, u32 f) { return (kind == 1 && !(f & MW_KBIT)) ? f * 8u : f; };
     O[0] = I[0];
     O[1] = d2 | (opnd(sh.a, a) << 16);
-    O[2] = opnd(sh.b, b) | (opnd(sh.c, c) << 16);
+    u32 c2 = opnd(sh.c, c);
+    if ((I[0] & 0xffu) == MW_W_CDINS && (c & MW_KBIT)) {
+      const size_t o = c & 0x7fffu;   // validated: o + 8 <= nconst
+      bool small = o + 8 <= nconst && consts[o] < 0x4000u;
+      for (int k = 1; k < 8 && small; ++k) small = consts[o + k] == 0u;
+      if (small) c2 = 0x4000u | consts[o];
+    }
+    O[2] = opnd(sh.b, b) | (c2 << 16);
     O[3] = I[3];
   }
 }

@@ -50,3 +50,46 @@ def test_mythril_corpora_are_asm_eligible():
     bad = [f for f, p in progs if not isa.asm_eligible(p.code, p.leaves)]
     assert not bad, bad
     assert len(progs) >= 170
+
+
+def _predecode(code, consts):
+    """mw_asm_predecode (mw_validate.cpp) through the library, on the CPU."""
+    import ctypes
+
+    import numpy as np
+
+    from mythril_amd.runtime import LIB_PATH
+    lib = ctypes.CDLL(LIB_PATH)
+    f = lib.mw_asm_predecode
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    code = np.ascontiguousarray(code, dtype=np.uint32)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32)
+    out = np.zeros_like(code)
+    f(code.ctypes.data, code.size, consts.ctypes.data, consts.size, out.ctypes.data)
+    return out.reshape(-1, 4)
+
+
+def test_predecode_operand_layout():
+    """The asm engine's copy of the code: N dst -> slot in [5:0], W dst -> slot
+    x 8 in [13:8], W register operands -> slot x 8, constants and N operands
+    unchanged, a W_CDINS index constant below 0x4000 -> 0x4000 | index."""
+    e = isa.encode
+    consts = [0] * 16
+    consts[0], consts[8] = 0x24, 0x5000   # two 256-bit constants (limbs 1..7 zero)
+    code = (e("N_ADD", 8, isa.encode_dst("N", 37), 3, isa.KBIT | 8)
+            + e("W_ADD", 256, isa.encode_dst("W", 5), 2, isa.KBIT | 0)
+            + e("N_ULT", 256, isa.encode_dst("N", 4), 6, 1)
+            + e("W_ITE", 256, isa.encode_dst("W", 1), 3, 4, 9)
+            + e("W_CDINS", 256, isa.encode_dst("W", 2), 2, 1, isa.KBIT | 0, imm=7 | (8 << 16))
+            + e("W_CDINS", 256, isa.encode_dst("W", 2), 2, 1, isa.KBIT | 8, imm=7)
+            + e("END", 0, isa.encode_dst(None)))
+    o = _predecode(code, consts)
+    src = __import__("numpy").asarray(code, dtype="uint32").reshape(-1, 4)
+    assert (o[:, 0] == src[:, 0]).all() and (o[:, 3] == src[:, 3]).all()
+    assert o[0, 1] == 37 | (3 << 16) and o[0, 2] == isa.KBIT | 8
+    assert o[1, 1] == (40 << 8) | (16 << 16) and o[1, 2] == isa.KBIT | 0
+    assert o[2, 1] == 4 | (48 << 16) and o[2, 2] == 8
+    assert o[3, 1] == (8 << 8) | (24 << 16) and o[3, 2] == 32 | (9 << 16)   # c is the N condition
+    assert o[4, 2] == 8 | ((0x4000 | 0x24) << 16)
+    assert o[5, 2] == 8 | ((isa.KBIT | 8) << 16)                          # 0x5000: stays a constant

@@ -596,14 +596,40 @@ def gen():
         # acc | ((K[c] <s size) ? leaf(imm & 0xffff) : 0) << (imm >> 16), chained
         # links keep the word in XR (mw_interp.h MW_W_CDINS, MW_FLAG_CHAIN)
         g.field("a", S[0]), g.fetch_w(S[0], XR)
-        top = g.L("cdtop")
+        g(f"s_mov_b32 {s(S[0])}, -1")                 # b operand of the cached size summary: none
+        top, slow, rng, ins = g.L("cdtop"), g.L("cdslow"), g.L("cdrng"), g.L("cdins")
         g.label(top)
-        # index (W/K c) -> XA, size (W b) -> XB; signed 256-bit k <s size
+        # predecoded small index (mw_asm_predecode): c = 0x4000 | i, i < 0x4000
+        g(f"s_bitcmp1_b32 {s(CUR + 2)}, 30", f"s_cbranch_scc0 {slow}",
+          f"s_bfe_u32 {s(S[1])}, {s(CUR + 2)}, 0xe0010",        # i = bits [29:16]
+          f"s_and_b32 {s(S[2])}, {s(CUR + 2)}, 0xffff",
+          f"s_cmp_eq_u32 {s(S[2])}, {s(S[0])}", f"s_cbranch_scc1 {rng}",
+          f"s_mov_b32 {s(S[0])}, {s(S[2])}")
+        # size summary in XA: i <s size  <=>  i <u XA, XA = size < 0 ? 0 :
+        # (size >= 2^32 ? 2^32 - 1 : size)   (i < 2^14)
+        g.field("b", S[2]), g.fetch_w(S[2], XB)
+        g(f"v_or3_b32 {v(T)}, {v(XB + 1)}, {v(XB + 2)}, {v(XB + 3)}",
+          f"v_and_b32_e32 {v(T + 1)}, 0x7fffffff, {v(XB + 7)}",
+          f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 4)}, {v(XB + 5)}",
+          f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 6)}, {v(T + 1)}",
+          f"v_cmp_ne_u32_e32 vcc, 0, {v(T)}", "s_nop 1",
+          f"v_cndmask_b32_e64 {v(XA)}, {v(XB)}, -1, vcc",
+          f"v_cmp_gt_i32_e32 vcc, 0, {v(XB + 7)}", "s_nop 1",
+          f"v_cndmask_b32_e64 {v(XA)}, {v(XA)}, 0, vcc")
+        g.label(rng)
+        g(f"v_cmp_lt_u32_e64 {sr(MSK2, 2)}, {s(S[1])}, {v(XA)}", "s_branch " + ins)
+        # any other index: the full signed 256-bit compare
+        g.label(slow)
+        g(f"s_mov_b32 {s(S[0])}, -1")
         g.field("b", S[1]), g.fetch_w(S[1], XB)
         g.field("c", S[2]), g.fetch_w(S[2], XA)
         g(f"v_xor_b32_e32 {v(XA + 7)}, 0x80000000, {v(XA + 7)}", f"v_xor_b32_e32 {v(XB + 7)}, 0x80000000, {v(XB + 7)}")
         g.sub_chain(XA, XB)
         g(f"s_mov_b64 {sr(MSK2, 2)}, vcc")            # lanes whose byte is in range
+        g.label(ins)
+        # no lane in range: the inserted byte is 0 in every lane (no leaf draw)
+        nos = g.L("cdns")
+        g("s_nop 1", f"s_cmp_eq_u64 {sr(MSK2, 2)}, 0", f"s_cbranch_scc1 {nos}")
         g(f"s_and_b32 {s(S[3])}, {s(CUR + 3)}, 0xffff")
         call_leaf(g, S[3])
         # t = in range ? byte : 0, inserted at bit off = imm >> 16 (limb off >> 5)
@@ -613,7 +639,6 @@ def gen():
           f"s_set_gpr_idx_on {s(S[5])}, gpr_idx(SRC2,DST)",
           f"v_lshl_or_b32 {v(XR)}, {v(T)}, {s(S[4])}, {v(XR)}", "s_set_gpr_idx_off")
         # a byte straddling a limb boundary (off & 31 > 24): its high bits go to the next limb
-        nos = g.L("cdns")
         g(f"s_cmp_le_u32 {s(S[4])}, 24", f"s_cbranch_scc1 {nos}",
           f"s_sub_u32 {s(S[4])}, 32, {s(S[4])}", f"s_add_u32 {s(S[5])}, {s(S[5])}, 1",
           f"v_lshrrev_b32_e32 {v(T)}, {s(S[4])}, {v(T)}",
@@ -868,18 +893,17 @@ def leaf(g):
     xs33()
     g(f"s_bfm_b32 {s(S[6])}, {s(D + 4)}, 0", f"s_cmp_ge_u32 {s(D + 4)}, 32", f"s_cselect_b32 {s(S[6])}, -1, {s(S[6])}",
       f"v_and_b32_e32 {v(T + 6)}, {s(S[6])}, {v(lo)}", "s_branch Lgather_%=")
-    # kind 3: digit bit b = index bit (shift + b * stride)
+    # kind 3: digit bit b = index bit (shift + b * stride): one 64-bit shift
+    # of the index per bit, one loop branch (shift + (bits-1) * stride <= 63,
+    # validated)
     g.label("Lk3_%=")
-    g(f"v_mov_b32_e32 {v(T + 6)}, 0", f"s_mov_b32 {s(S[4])}, 0", f"s_mov_b32 {s(S[5])}, {s(D + 3)}")
+    g(f"v_mov_b32_e32 {v(T + 6)}, 0", f"s_mov_b32 {s(S[4])}, 0", f"s_mov_b32 {s(S[5])}, {s(D + 3)}",
+      f"s_cmp_eq_u32 {s(D + 4)}, 0", "s_cbranch_scc1 Lgather_%=")
     g.label("Lm_loop_%=")
-    g(f"s_cmp_ge_u32 {s(S[4])}, {s(D + 4)}", "s_cbranch_scc1 Lgather_%=",
-      f"s_cmp_lt_u32 {s(S[5])}, 32", "s_cbranch_scc0 Lm_hi_%=",
-      f"v_bfe_u32 {v(T + 7)}, {v(CLO)}, {s(S[5])}, 1", "s_branch Lm_or_%=")
-    g.label("Lm_hi_%=")
-    g(f"s_sub_u32 {s(S[6])}, {s(S[5])}, 32", f"v_bfe_u32 {v(T + 7)}, {v(CHI)}, {s(S[6])}, 1")
-    g.label("Lm_or_%=")
-    g(f"v_lshl_or_b32 {v(T + 6)}, {v(T + 7)}, {s(S[4])}, {v(T + 6)}",
-      f"s_add_u32 {s(S[4])}, {s(S[4])}, 1", f"s_add_u32 {s(S[5])}, {s(S[5])}, {s(D + 7)}", "s_branch Lm_loop_%=")
+    g(f"v_lshrrev_b64 {vr(T + 4, 2)}, {s(S[5])}, {vr(CLO, 2)}", f"v_and_b32_e32 {v(T + 7)}, 1, {v(T + 4)}",
+      f"v_lshl_or_b32 {v(T + 6)}, {v(T + 7)}, {s(S[4])}, {v(T + 6)}",
+      f"s_add_u32 {s(S[4])}, {s(S[4])}, 1", f"s_add_u32 {s(S[5])}, {s(S[5])}, {s(D + 7)}",
+      f"s_cmp_lt_u32 {s(S[4])}, {s(D + 4)}", "s_cbranch_scc1 Lm_loop_%=")
     # pool entry in LDS at poolb + 4 * poff: width >= 32: 9 words (flag, 8 limbs)
     # at + 36 * digit; width < 32: one word (bit 31 RANDOM, else the value) at + 4 * digit
     g.label("Lgather_%=")

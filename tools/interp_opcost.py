@@ -27,14 +27,21 @@ from mythril_amd.ir import Ctx  # noqa: E402
 K = isa.KBIT
 
 
-def base_program():
-    """4 narrow leaves (8-bit) and 2 wide ones, a narrow and a wide constant."""
+def base_program(pooled=False):
+    """4 narrow leaves (8-bit) and 2 wide ones, a narrow and two wide constants.
+    pooled: the leaves draw from 8-entry pools (bit-interleaved digits, as
+    the calldata bytes of Mythril's queries) instead of Philox."""
     c = Ctx()
     n = [c.var(f"n{i}", 8) for i in range(4)]
     w = [c.var(f"w{i}", 256) for i in range(2)]
     conj = [c.app("=", n[0], c.const(5, 8)), c.app("=", n[1], n[2]), c.app("=", n[3], n[0]),
-            c.app("bvult", w[0], c.const(1 << 200, 256)), c.app("=", w[1], w[0])]
-    return compile_program(conj)
+            c.app("bvult", w[0], c.const(1 << 200, 256)), c.app("=", w[1], w[0]),
+            c.app("bvult", w[1], c.const(0x24, 256))]
+    pools = None
+    if pooled:
+        pools = {f"n{i}": [1, 2, 3, 5, 7, 11, 13, None] for i in range(4)}
+        pools.update({f"w{i}": [0x44, 4, 1 << 255, None] for i in range(2)})
+    return compile_program(conj, pools=pools)
 
 
 def assemble(p, body, repeat):
@@ -62,6 +69,15 @@ def kn(p):
     return K | int(np.nonzero(p.consts == 5)[0][0])
 
 
+def kw(p, val):
+    """Constant-pool offset of the 256-bit constant val."""
+    k = p.consts.reshape(-1)
+    for o in range(0, len(k) - 7):
+        if int(k[o]) == val and not k[o + 1:o + 8].any():
+            return K | o
+    raise KeyError(val)
+
+
 def variants(p):
     def e(op, width=0, dst=0, a=0, b=0, c=0, imm=0):   # dst: a slot of the op's result file
         return isa.encode(op, width, isa.encode_dst(isa.SHAPES[op][0], dst), a, b, c, imm)
@@ -78,6 +94,8 @@ def variants(p):
         "W_AND": [e("W_AND", 256, 2, 0, 1)],
         "LEAF_N": [e("LEAF_N", 8, 5, imm=idx["n0"])],
         "LEAF_W": [e("LEAF_W", 256, 2, imm=idx["w0"])],
+        # one guarded calldata byte (index 0x24 < size w1) into W2, unchained
+        "W_CDINS": [e("W_CDINS", 256, 2, 2, 1, kw(p, 0x24), imm=idx["n0"] | (8 << 16))],
     }
 
 
@@ -89,18 +107,23 @@ def main():
     ap.add_argument("--engines", default="asm,interp")
     a = ap.parse_args()
     from mythril_amd.runtime import Device
-    p = base_program()
     dev = Device(0)
     n = 1 << a.log2
     slots = 256 * 4 * 2   # CUs x SIMDs x waves per SIMD
-    for name, body in variants(p).items():
+    cases = [(p, name + suffix, body)
+             for p, suffix in ((base_program(False), ""), (base_program(True), "_pool"))
+             for name, body in variants(p).items()]
+    for p, name, body in cases:
         if a.only and name != a.only:
             continue
-        rep = a.repeat // 4 if name.startswith("LEAF") else a.repeat
+        # leaf-drawing instructions cost several dispatches: fewer repeats
+        rep = a.repeat // 4 if name.startswith(("LEAF", "W_CDINS")) else a.repeat
         q = assemble(p, body, rep)
         dp = dev.load(q)
         # asm: the threaded-dispatch interpreter (default); interp: the compiled
-        # one (MYTHRIL_AMD_ASM=0, read by the library at each call)
+        # one (MYTHRIL_AMD_ASM=0, read by the library at each call).  Two
+        # launches each (warm-up, measured): tools/opcost_summary.py pairs the
+        # PMC rows with these lines in order.
         for engine in a.engines.split(","):
             os.environ["MYTHRIL_AMD_ASM"] = "0" if engine == "interp" else "1"
             ran = dev.engine_of(dp)
@@ -108,7 +131,8 @@ def main():
             _, st = dev.search([dp], 1, 0, n, 0)
             waves = n // 64
             ns_per = st["kernel_ms"] * 1e6 / (waves / slots) / rep
-            print(json.dumps({"op": name, "engine": ran, "repeat": rep, "kernel_ms": round(st["kernel_ms"], 3),
+            print(json.dumps({"op": name, "engine": ran, "repeat": rep, "log2": a.log2,
+                              "kernel_ms": round(st["kernel_ms"], 3),
                               "ns_per_insn_per_wave_slot": round(ns_per, 1),
                               "cycles_at_2p4GHz": round(ns_per * 2.4, 0)}), flush=True)
         dp.free()
