@@ -4,8 +4,9 @@
 // call_valueN, N_calldata bytes, calldatasize, storage/balance reads,
 // keccak UF results — the leaf schema of SURVEY.md §8a row A8,
 // mythril/laser/ethereum/transaction/symbolic.py:118-136, calldata.py:214-215).
-//   random leaf: Philox4x32-10(key=(seed_lo ^ id, seed_hi), ctr=(c_lo, c_hi, blk, 0)),
-//                blk 0 -> limbs 0..3, blk 1 -> limbs 4..7, masked to width
+//   random leaf: w > 32: Philox4x32-10(key=(seed_lo ^ id, seed_hi), ctr=(c_lo, c_hi, blk, 0)),
+//                blk 0 -> limbs 0..3, blk 1 -> limbs 4..7, masked to width;
+//                w <= 32: fmix64(c ^ seed ^ id * 0xC2B2AE3D27D4EB4F), masked to width
 //   pool leaf:   digit = (c >> shift) & (2^bits - 1); entry = pool[digit];
 //                entry flag RANDOM -> random value above, else the constant.
 //   interleaved: digit bit b = index bit (shift + b*stride)  (Morton order: indices
@@ -45,10 +46,23 @@ MW_HD void philox4x32_10(u32 c[4], u32 k0, u32 k1) {
   }
 }
 
+MW_HD u64 fmix64(u64 h) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  h ^= h >> 33;
+  return h;
+}
+
 // MW_ABLATE_* (timing experiments only, tools/leaf_ablate.py; wrong values):
 //   LEAF    every leaf is (u32)cand ^ id in limb 0 (no digit, gather or Philox)
 //   PHILOX  random leaves are one multiply-xor of the index (no Philox rounds)
 //   DIGIT   interleaved digits read as a plain bit-field (no per-bit loop)
+//
+// Random leaf value: w > 32 Philox4x32-10 blocks 0 and (w > 128) 1; w <= 32
+// (calldata bytes, Bools) one MurmurHash3 finalizer of index ^ seed ^ salt,
+// a tenth of Philox's work (oracle/philox.py random_leaf restates both).
 MW_HD void random_leaf(u32 id, u32 w, u64 seed, u64 cand, u32 out[8]) {
 #if defined(MW_ABLATE_PHILOX)
   out[0] = ((u32)cand ^ id) * 0x9E3779B9u;
@@ -58,6 +72,13 @@ MW_HD void random_leaf(u32 id, u32 w, u64 seed, u64 cand, u32 out[8]) {
   canon(out, w);
   return;
 #endif
+  if (w <= 32u) {
+    out[0] = (u32)fmix64(cand ^ seed ^ ((u64)id * 0xC2B2AE3D27D4EB4Full));
+#pragma unroll
+    for (int k = 1; k < 8; ++k) out[k] = 0u;
+    canon(out, w);
+    return;
+  }
   u32 k0 = (u32)seed ^ id, k1 = (u32)(seed >> 32);
   MW_LEAF_KEY_FENCE(k0);
   MW_LEAF_KEY_FENCE(k1);
@@ -74,14 +95,6 @@ MW_HD void random_leaf(u32 id, u32 w, u64 seed, u64 cand, u32 out[8]) {
   canon(out, w);
 }
 
-MW_HD u64 fmix64(u64 h) {
-  h ^= h >> 33;
-  h *= 0xff51afd7ed558ccdull;
-  h ^= h >> 33;
-  h *= 0xc4ceb9fe1a85ec53ull;
-  h ^= h >> 33;
-  return h;
-}
 
 // Candidate value of one leaf from its descriptor fields (the interpreter
 // reads them from the leaf table below; specialised kernels, mw_jit.h, pass

@@ -140,7 +140,21 @@ static void philox(u32 c[4], u32 k0, u32 k1) {
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
 }
+static u64 fmix64(u64 h) {
+  h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; h ^= h >> 33;
+  return h;
+}
+
+/* Random leaf (oracle/philox.py random_leaf): w > 32 Philox4x32-10 blocks 0
+ * and 1; w <= 32 one fmix64 of the index, seed and salt. */
 static void leaf(u64 seed, u32 salt, u64 cand, int w, u32* out) {
+  if (w <= 32) {
+    const u64 h = fmix64(cand ^ seed ^ ((u64)salt * 0xC2B2AE3D27D4EB4Full));
+    out[0] = (u32)h;
+    for (int k = 1; k < 8; ++k) out[k] = 0;
+    mask(out, w);
+    return;
+  }
   u32 k0 = (u32)seed ^ salt, k1 = (u32)(seed >> 32);
   for (u32 blk = 0; blk < 2; ++blk) {
     u32 c[4] = {(u32)cand, (u32)(cand >> 32), blk, 0};
@@ -154,11 +168,6 @@ static void leaf(u64 seed, u32 salt, u64 cand, int w, u32* out) {
  * kind 0 random, 1 pool digit = index bit-field, 2 hashed digit, 3 bit-interleaved
  * digit.  Pool entries are 9 words: flags (bit 0 = RANDOM) + 8 limbs. */
 typedef struct { int32_t kind, shift, bits, stride, pool; } ospec;
-
-static u64 fmix64(u64 h) {
-  h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; h ^= h >> 33;
-  return h;
-}
 
 static void spec_leaf(const ospec* sp, const u32* pool, u64 seed, u32 salt, u64 cand, int w, u32* out) {
   if (sp && sp->kind >= 1 && sp->kind <= 3) {

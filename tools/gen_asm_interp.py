@@ -878,19 +878,7 @@ def leaf(g):
       f"s_mul_i32 {s(S[4])}, {s(D + 2)}, 0x9E3779B9", f"s_add_u32 {s(S[7])}, {s(S[7])}, {s(S[4])}",
       f"v_xor_b32_e32 {v(lo)}, {s(S[6])}, {v(CLO)}", f"v_xor_b32_e32 {v(hi)}, {s(S[7])}, {v(CHI)}")
 
-    def xs33():   # h ^= h >> 33
-        g(f"v_lshrrev_b32_e32 {v(t1)}, 1, {v(hi)}", f"v_xor_b32_e32 {v(lo)}, {v(lo)}, {v(t1)}")
-
-    def mul64(c):  # h *= c (mod 2^64)
-        g(f"s_mov_b32 {s(S[4])}, {c & 0xFFFFFFFF:#x}", f"s_mov_b32 {s(S[5])}, {c >> 32:#x}",
-          f"v_mul_lo_u32 {v(t1)}, {v(lo)}, {s(S[5])}", f"v_mul_lo_u32 {v(t2)}, {v(hi)}, {s(S[4])}",
-          f"v_mad_u64_u32 {vr(T + 4, 2)}, {sr(SX, 2)}, {v(lo)}, {s(S[4])}, 0",
-          f"v_mov_b32_e32 {v(lo)}, {v(T + 4)}", f"v_add3_u32 {v(hi)}, {v(T + 5)}, {v(t1)}, {v(t2)}")
-    xs33()
-    mul64(0xFF51AFD7ED558CCD)
-    xs33()
-    mul64(0xC4CEB9FE1A85EC53)
-    xs33()
+    fmix64(g, lo, hi, t1, t2)
     g(f"s_bfm_b32 {s(S[6])}, {s(D + 4)}, 0", f"s_cmp_ge_u32 {s(D + 4)}, 32", f"s_cselect_b32 {s(S[6])}, -1, {s(S[6])}",
       f"v_and_b32_e32 {v(T + 6)}, {s(S[6])}, {v(lo)}", "s_branch Lgather_%=")
     # kind 3: digit bit b = index bit (shift + b * stride): one 64-bit shift
@@ -930,11 +918,43 @@ def leaf(g):
     g(f"s_setpc_b64 {sr(LRET, 2)}")
 
 
+def fmix64(g, lo, hi, t1, t2):
+    """(hi:lo) = MurmurHash3's 64-bit finalizer of (hi:lo) (mw_leaf.h fmix64);
+    temporaries t1, t2, T+4..T+5, S[4], S[5] and the carry pair SX"""
+    def xs33():   # h ^= h >> 33
+        g(f"v_lshrrev_b32_e32 {v(t1)}, 1, {v(hi)}", f"v_xor_b32_e32 {v(lo)}, {v(lo)}, {v(t1)}")
+
+    def mul64(c):  # h *= c (mod 2^64)
+        g(f"s_mov_b32 {s(S[4])}, {c & 0xFFFFFFFF:#x}", f"s_mov_b32 {s(S[5])}, {c >> 32:#x}",
+          f"v_mul_lo_u32 {v(t1)}, {v(lo)}, {s(S[5])}", f"v_mul_lo_u32 {v(t2)}, {v(hi)}, {s(S[4])}",
+          f"v_mad_u64_u32 {vr(T + 4, 2)}, {sr(SX, 2)}, {v(lo)}, {s(S[4])}, 0",
+          f"v_mov_b32_e32 {v(lo)}, {v(T + 4)}", f"v_add3_u32 {v(hi)}, {v(T + 5)}, {v(t1)}, {v(t2)}")
+    xs33()
+    mul64(0xFF51AFD7ED558CCD)
+    xs33()
+    mul64(0xC4CEB9FE1A85EC53)
+    xs33()
+
+
 def philox_sub(g):
-    """Lphilox: T..T+7 = Philox4x32-10 blocks 0 and (w > 128) 1 of the
-    candidate index, key (seed_lo ^ id, seed_hi) (mw_leaf.h random_leaf)."""
+    """Lphilox: T..T+7 = the random leaf value of the candidate index
+    (mw_leaf.h random_leaf): w > 32 Philox4x32-10 blocks 0 and (w > 128) 1,
+    key (seed_lo ^ id, seed_hi); w <= 32 fmix64(c ^ seed ^ id * 0xC2B2AE3D27D4EB4F)."""
     D = DESC
     g.label("Lphilox_%=")
+    narrow = 0xC2B2AE3D27D4EB4F
+    g(f"s_cmp_gt_u32 {s(D)}, 32", "s_cbranch_scc1 Lphx_wide_%=",
+      # key (PK1:PK0) = seed ^ id * narrow (mod 2^64)
+      f"s_mul_i32 {s(PK0)}, {s(D + 2)}, {narrow & 0xFFFFFFFF:#x}",
+      f"s_mul_hi_u32 {s(PK1)}, {s(D + 2)}, {narrow & 0xFFFFFFFF:#x}",
+      f"s_mul_i32 {s(S[4])}, {s(D + 2)}, {narrow >> 32:#x}", f"s_add_u32 {s(PK1)}, {s(PK1)}, {s(S[4])}",
+      f"s_xor_b32 {s(PK0)}, {s(PK0)}, {s(SEED)}", f"s_xor_b32 {s(PK1)}, {s(PK1)}, {s(SEED + 1)}",
+      f"v_xor_b32_e32 {v(T)}, {s(PK0)}, {v(CLO)}", f"v_xor_b32_e32 {v(T + 1)}, {s(PK1)}, {v(CHI)}")
+    fmix64(g, T, T + 1, T + 2, T + 3)
+    for k in range(1, 8):
+        g(f"v_mov_b32_e32 {v(T + k)}, 0")
+    g(f"s_setpc_b64 {sr(PRET, 2)}")
+    g.label("Lphx_wide_%=")
     g(f"v_mov_b32_e32 {v(T + 4)}, 0", f"v_mov_b32_e32 {v(T + 5)}, 0", f"v_mov_b32_e32 {v(T + 6)}, 0",
       f"v_mov_b32_e32 {v(T + 7)}, 0")
     for blk in (0, 1):

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--note", default="")
     ap.add_argument("--valu-csv", default=None)
+    ap.add_argument("--waves-csv", default=None)
     a = ap.parse_args()
     fetch = per_dispatch(a.fetch_csv, "FETCH_SIZE", a.kernel)
     write = per_dispatch(a.write_csv, "WRITE_SIZE", a.kernel)
@@ -61,10 +62,13 @@ def main():
     }
     if a.valu_csv:
         valu = per_dispatch(a.valu_csv, "SQ_INSTS_VALU", a.kernel)
-        waves = per_dispatch(a.valu_csv, "SQ_WAVES", a.kernel)
+        # SQ_WAVES: from the same pass, or from --waves-csv (gpu_run.sh pmc puts it in pass 1)
+        waves = per_dispatch(a.waves_csv or a.valu_csv, "SQ_WAVES", a.kernel)
         rec["sq_insts_valu_per_launch"] = sum(valu) / len(valu)
         rec["sq_waves_per_launch"] = sum(waves) / len(waves)
         rec["sources"].append(a.valu_csv)
+        if a.waves_csv:
+            rec["sources"].append(a.waves_csv)
     if a.note:
         rec["note"] = a.note
     s = json.dumps(rec, indent=1)
