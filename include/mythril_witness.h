@@ -117,12 +117,24 @@ int mg_eval_generated(mg_ctx* ctx, const mg_prog* prog, uint64_t seed, uint64_t 
  * mg_search (z3 Optimize.check, mythril/laser/smt/solver/solver.py:50-66). */
 int mg_prog_attach_kernel(mg_prog* prog, const void* image, size_t size, const char* name);
 
+/* Attach an assembled kernel to a loaded program: `image` is a gfx950 code
+ * object that mythril_amd/asmjit.py assembled (llvm-mc + ld.lld, milliseconds)
+ * from this program's own code, the asm interpreter's handlers instantiated
+ * with literal operands in straight-line order (csrc/mw_asmjit_shell.hip).
+ * It must export kernel `<name>` and `<name>_sig` (the program signature,
+ * checked as for mg_prog_attach_kernel); the program must be one the asm
+ * interpreter runs.  mg_search and mg_eval_generated (verdicts only) then
+ * launch it on the asm interpreter's records; results are identical.  A
+ * specialised kernel, when also attached, takes precedence.  Same crossing as
+ * mg_search (z3 Optimize.check, mythril/laser/smt/solver/solver.py:50-66). */
+int mg_prog_attach_asm(mg_prog* prog, const void* image, size_t size, const char* name);
+
 /* 1 if a specialised kernel is attached to the program, else 0. */
 int mg_prog_has_kernel(const mg_prog* prog);
 /* The engine a search of this program runs on: 0 the compiled interpreter,
  * 1 the threaded-dispatch asm interpreter (every opcode and leaf kind has a
  * handler and the pool fits in LDS; MYTHRIL_AMD_ASM=0 disables it), 2 its
- * specialised kernel.  Replaces
+ * specialised kernel, 3 its assembled kernel.  Replaces
  * nothing in the reference: a diagnostic for tests and benchmarks. */
 int mg_prog_engine(const mg_prog* prog);
 

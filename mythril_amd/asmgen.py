@@ -1,0 +1,1475 @@
+"""gfx950 assembly generator for the witness engine's two asm engines:
+
+* the threaded-dispatch interpreter core (``render_interp`` ->
+  csrc/mw_asm_interp.inc, written by tools/gen_asm_interp.py): one inline-asm
+  block that runs any eligible program.  Every handler ends in its own copy
+  of the dispatch, which loads the next instruction (prefetched one ahead
+  with s_load_dwordx4), indexes a table of s_branch entries and jumps with
+  s_setpc_b64.  The register files live in fixed VGPRs and are indexed with
+  s_set_gpr_idx_on; operands come predecoded (mw_validate.cpp
+  mw_asm_predecode);
+* assembled kernels (``render_template`` + ``static_body``, used by
+  mythril_amd/asmjit.py): the same prologue, chunk loop, result protocol and
+  leaf subroutines, with the program itself emitted as straight-line code -
+  every handler instantiated with its operands as literal registers and
+  constants, no dispatch and no operand indexing - and assembled by llvm-mc
+  in milliseconds (hipcc's specialised kernels take seconds to minutes).
+
+Semantics are the interpreter's, opcode by opcode (mw_interp.h).  Programs
+qualify when every opcode and leaf kind is listed in ASM_OPCODES /
+ASM_LEAF_KINDS (mythril_amd/isa.py, checked by tests/test_asm_interp.py);
+the GPU tests compare both engines' verdicts with the compiled interpreter's
+and the oracle's.
+
+Registers (per lane; all clobbered by the block):
+  v0..v63     W file: slot s, limb k at v[8s + k]
+  v64..v127   N file: slot s at v[64 + s]
+  v128..v135  zeros (shift padding below XA)   v136..v143 XA (operand a)
+  v144..v151  zeros (padding above XA)         v152..v159 XB (operand b)
+  v160/v161 candidate index lo/hi  v162 alive (0/1)  v163 LDS lane byte offset
+  v164 global-spill lane byte offset  v165 thread id  v168..v175 XR (result)
+  v176..v183 XC (third operand / Philox output)  v184..v191 temporaries
+  s16..s95    chunk loop and interpreter state (see the constants below)
+"""
+import re
+
+from mythril_amd import isa
+
+# opcodes / leaf kinds with an asm handler (the list lives in mythril_amd/isa.py)
+ASM_OPCODES = isa.ASM_OPCODES
+ASM_LEAF_KINDS = isa.ASM_LEAF_KINDS
+
+# ---------------------------------------------------------------- registers
+W0, N0 = 0, 64
+XA, XB, XR, XC, T = 136, 152, 168, 176, 184
+CLO, CHI, ALIVE, LDSOFF, GOFF = 160, 161, 162, 163, 164
+# scalar state
+CUR = 40          # s40..s43 current instruction words w0..w3
+NXT = 44          # s44..s47 next instruction (prefetched)
+SOFF = 48         # byte offset of the next instruction from CODE0
+TABLO = 49        # address of the dispatch table (Ltab), low / high word
+TABHI = 58
+SIDX = 19         # register-file index of an operand / write-back
+# assembled kernels (template mode): addresses the straight-line body leaves
+# through (it can outgrow a branch's reach); the interpreter's CUR/NXT words
+# are unused there (only CUR + 3, the immediate, is)
+LEAFADDR = 44     # s[44:45] Lleaf
+PHILOXADDR = 48   # s[48:49] Lphilox
+STOPADDR = 46     # s[46:47] Lstop
+ENDADDR = 40      # s[40:41] Lh_END
+CPOOL = 50        # s[50:51] constant pool
+LEAVES = 52       # s[52:53] leaf table
+POOLB = 54        # pool LDS byte base
+FLAGS = 55
+SEED = 56         # s[56:57]
+NLDS = 59         # spill words in LDS
+GSP = 60          # s[60:61] global spill base
+GSTRIDE = 62      # bytes between consecutive global spill words (nthreads x 4)
+PM0, PM1 = 63, 64  # Philox multipliers
+PK0, PK1 = 65, 66  # Philox keys
+S67 = 67
+LRET = 68         # s[68:69] leaf return address
+PRET = 70         # s[70:71] Philox / canon return address
+S = list(range(72, 80))   # scratch s72..s79
+DESC = 80         # s[80:87] leaf descriptor / wide constant
+MSK = 88          # s[88:89] saved lane mask
+MSK2 = 90         # s[90:91]
+JMP = 92          # s[92:93]
+SX = 94           # s[94:95] scratch pair
+
+# chunk loop state (s16..s39)
+CH, NCH, GDX = 16, 17, 18
+BEGIN = 20        # s[20:21]
+END = 22          # s[22:23]
+BASE = 24         # s[24:25]
+OUTMIN = 26       # s[26:27] this program's witness slot
+VERD = 28         # s[28:29] verdict array or 0
+EVALS = 30        # s[30:31]
+CODE0 = 32        # s[32:33]
+EXECSV = 34       # s[34:35]
+VALID = 36        # s[36:37] valid lanes of the chunk
+ARGP = 36         # s[36:37] AsmArgs (prologue only; then VALID)
+PROGP = 38        # s[38:39] ProgDev (prologue only)
+TID, LO_SREG = 165, 0
+
+NTAB = 128
+
+
+def v(i):
+    return f"v{i}"
+
+
+def s(i):
+    return f"s{i}"
+
+
+def vr(a, n):
+    return f"v[{a}:{a + n - 1}]"
+
+
+def sr(a, n):
+    return f"s[{a}:{a + n - 1}]"
+
+
+class Gen:
+    def __init__(self):
+        self.lines = []
+        self.tail = []      # out-of-line blocks (constant operands), emitted after the handler
+        self.n = 0
+        self.bound = {}     # name -> operand field (field())
+
+    def L(self, base):
+        self.n += 1
+        return f"L{base}{self.n}_%="
+
+    def __call__(self, *xs):
+        self.lines.extend(xs)
+
+    def label(self, lab):
+        self.lines.append(f"{lab}:")
+
+    def flush_tail(self):
+        self.lines.extend(self.tail)
+        self.tail = []
+
+    # ------------------------------------------------------------ operands
+    # Operands come from the asm engine's predecoded copy of the program
+    # (mw_validate.cpp mw_asm_predecode): a register operand field holds the
+    # N slot (0..63) or the W slot x 8, so it is the VGPR index relative to the
+    # file's base as it stands; bit 15 flags a constant (word offset).
+    # field() only binds an operand to a name; fetch_n / fetch_w read it.
+    WORD = {"a": (CUR + 1, "hi"), "b": (CUR + 2, "lo"), "c": (CUR + 2, "hi")}
+
+    def field(self, which, dst):
+        """bind operand field a/b/c to the name dst (no code)"""
+        self.bound[dst] = which
+
+    def _index(self, which, dst_sgpr):
+        wd, half = self.WORD[which]
+        if half == "hi":
+            self(f"s_lshr_b32 {dst_sgpr}, {s(wd)}, 16")
+        else:
+            self(f"s_and_b32 {dst_sgpr}, {s(wd)}, 0xffff")
+
+    def _is_const(self, which, label):
+        wd, half = self.WORD[which]
+        self(f"s_bitcmp1_b32 {s(wd)}, {31 if half == 'hi' else 15}", f"s_cbranch_scc1 {label}")
+
+    def fetch_n(self, f, dst):
+        """N/K operand bound to f -> VGPR dst"""
+        which = self.bound[f]
+        lk, lr = self.L("kn"), self.L("rn")
+        self._is_const(which, lk)
+        self._index(which, s(SIDX))
+        self(f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(SRC0)", f"v_mov_b32_e32 {v(dst)}, {v(N0)}", "s_set_gpr_idx_off")
+        self.label(lr)
+        wd, half = self.WORD[which]
+        off = f"s_lshr_b32 {s(SX)}, {s(wd)}, 16" if half == "hi" else f"s_and_b32 {s(SX)}, {s(wd)}, 0x7fff"
+        self.tail += [f"{lk}:", off, f"s_and_b32 {s(SX)}, {s(SX)}, 0x7fff", f"s_lshl_b32 {s(SX)}, {s(SX)}, 2",
+                      f"s_load_dword {s(SX)}, {sr(CPOOL, 2)}, {s(SX)}", "s_waitcnt lgkmcnt(0)",
+                      f"v_mov_b32_e32 {v(dst)}, {s(SX)}", f"s_branch {lr}"]
+
+    def fetch_w(self, f, dst):
+        """W/K operand bound to f -> VGPRs dst..dst+7"""
+        which = self.bound[f]
+        lk, lr = self.L("kw"), self.L("rw")
+        self._is_const(which, lk)
+        self._index(which, s(SIDX))
+        self(f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(SRC0)")
+        for k in range(8):
+            self(f"v_mov_b32_e32 {v(dst + k)}, {v(W0 + k)}")
+        self("s_set_gpr_idx_off")
+        self.label(lr)
+        wd, half = self.WORD[which]
+        off = f"s_lshr_b32 {s(SX)}, {s(wd)}, 16" if half == "hi" else f"s_and_b32 {s(SX)}, {s(wd)}, 0x7fff"
+        t = [f"{lk}:", off, f"s_and_b32 {s(SX)}, {s(SX)}, 0x7fff", f"s_lshl_b32 {s(SX)}, {s(SX)}, 2",
+             f"s_load_dwordx8 {sr(DESC, 8)}, {sr(CPOOL, 2)}, {s(SX)}", "s_waitcnt lgkmcnt(0)"]
+        t += [f"v_mov_b32_e32 {v(dst + k)}, {s(DESC + k)}" for k in range(8)]
+        self.tail += t + [f"s_branch {lr}"]
+
+    def width(self, dst):
+        self(f"s_lshr_b32 {s(dst)}, {s(CUR)}, 16")
+
+    def nmask(self, w, dst):
+        """dst = w >= 32 ? ~0 : (1 << w) - 1 (w in SGPR, <= 32): the low word of
+        the 64-bit field mask (dst must start an aligned SGPR pair)"""
+        assert dst % 2 == 0
+        self(f"s_bfm_b64 {sr(dst, 2)}, {s(w)}, 0")
+
+    def write_n(self, src):
+        """N result in VGPR src -> the N slot of the predecoded dst field [5:0]"""
+        self(f"s_and_b32 {s(SIDX)}, {s(CUR + 1)}, 0x3f", f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(DST)",
+             f"v_mov_b32_e32 {v(N0)}, {v(src)}", "s_set_gpr_idx_off")
+
+    def write_w(self, src):
+        """W result in VGPRs src.. -> the W slot x 8 of the predecoded dst field [13:8]"""
+        self(f"s_bfe_u32 {s(SIDX)}, {s(CUR + 1)}, 0x60008", f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(DST)")
+        for k in range(8):
+            self(f"v_mov_b32_e32 {v(W0 + k)}, {v(src + k)}")
+        self("s_set_gpr_idx_off")
+
+    def canon(self, base, w):
+        """clear the bits >= w (SGPR) of the 8 limbs at VGPR base (no-op for w >= 256)"""
+        done = self.L("cd")
+        q, r = S[4], S[5]
+        self(f"s_cmp_ge_u32 {s(w)}, 256", f"s_cbranch_scc1 {done}",
+             f"s_lshr_b32 {s(q)}, {s(w)}, 5", f"s_and_b32 {s(r)}, {s(w)}, 31")
+        for k in range(1, 8):
+            sk = self.L("cz")
+            # zero limb k when k > q, i.e. q < k
+            self(f"s_cmp_lt_u32 {s(q)}, {k}", f"s_cbranch_scc0 {sk}", f"v_mov_b32_e32 {v(base + k)}, 0")
+            self.label(sk)
+        # partial limb q: keep its low r bits (r == 0: the limb is above w, zero it)
+        self(f"s_bfm_b32 {s(r)}, {s(r)}, 0", f"s_set_gpr_idx_on {s(q)}, gpr_idx(SRC1,DST)",
+             f"v_and_b32_e32 {v(base)}, {s(r)}, {v(base)}", "s_set_gpr_idx_off")
+        self.label(done)
+
+    def nop_vcc(self):
+        self("s_nop 1")
+
+    def sub_chain(self, a, b, dst=None, borrow_only=False):
+        """a - b over 8 limbs (VGPR bases); borrow out in vcc"""
+        for k in range(8):
+            d = v(T) if dst is None else v(dst + k)
+            if k == 0:
+                self(f"v_sub_co_u32_e32 {d}, vcc, {v(a)}, {v(b)}")
+            else:
+                self.nop_vcc()
+                self(f"v_subb_co_u32_e32 {d}, vcc, {v(a + k)}, {v(b + k)}, vcc")
+
+    def add_chain(self, a, b, dst):
+        for k in range(8):
+            if k == 0:
+                self(f"v_add_co_u32_e32 {v(dst)}, vcc, {v(a)}, {v(b)}")
+            else:
+                self.nop_vcc()
+                self(f"v_addc_co_u32_e32 {v(dst + k)}, vcc, {v(a + k)}, {v(b + k)}, vcc")
+
+    def bool_from_vcc(self, dst, invert=False):
+        self.nop_vcc()
+        self(f"v_cndmask_b32_e64 {v(dst)}, {1 if invert else 0}, {0 if invert else 1}, vcc")
+
+    def long_addr(self, reg, label):
+        """s[reg:reg+1] = the address of label (any distance)"""
+        here = self.L("pc")
+        self(f"s_getpc_b64 {sr(reg, 2)}")
+        self.label(here)
+        self(f"s_add_u32 {s(reg)}, {s(reg)}, ({label} - {here})", f"s_addc_u32 {s(reg + 1)}, {s(reg + 1)}, 0")
+
+    def stop_if_scc1(self):
+        """end this chunk's evaluation (every lane dead) when SCC is set"""
+        self("s_cbranch_scc1 Lstop_%=")
+
+    def call_leaf_sub(self):
+        self(f"s_call_b64 {sr(LRET, 2)}, Lleaf_%=")
+
+    def next(self):
+        """dispatch the next instruction (each handler ends in its own copy:
+        no jump back to a shared dispatch block).  It was prefetched one ahead;
+        the stream ends in a validated END and no instruction jumps, so the
+        offset only grows to it."""
+        self("s_waitcnt lgkmcnt(0)", f"s_mov_b64 {sr(CUR, 2)}, {sr(NXT, 2)}",
+             f"s_mov_b64 {sr(CUR + 2, 2)}, {sr(NXT + 2, 2)}",
+             f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, {s(SOFF)}",
+             f"s_and_b32 {s(JMP)}, {s(CUR)}, 0x7f", f"s_lshl2_add_u32 {s(SX)}, {s(JMP)}, {s(TABLO)}",
+             f"s_addc_u32 {s(SX + 1)}, {s(TABHI)}, 0", f"s_setpc_b64 {sr(SX, 2)}")
+
+
+def build_handlers():
+    """{opcode name: fn(g)} emitting that opcode's semantics with g's operand
+    access (runtime-indexed in the interpreter, literal in assembled kernels)"""
+    handlers = {}
+
+    def handler(name):
+        def deco(fn):
+            handlers[name] = fn
+            return fn
+        return deco
+
+    # -------------------------------------------------------- narrow
+    for name, expr, masked in (("N_ADD", "v_add_u32_e32 {d}, {a}, {b}", True),
+                               ("N_SUB", "v_sub_u32_e32 {d}, {a}, {b}", True),
+                               ("N_AND", "v_and_b32_e32 {d}, {a}, {b}", False),
+                               ("N_OR", "v_or_b32_e32 {d}, {a}, {b}", False),
+                               ("N_XOR", "v_xor_b32_e32 {d}, {a}, {b}", False)):
+        def h(g, expr=expr, masked=masked):
+            g.field("a", S[0]), g.field("b", S[1])
+            g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
+            g(expr.format(d=v(XR), a=v(T), b=v(T + 1)))
+            if masked:
+                g.width(S[2]), g.nmask(S[2], S[4])
+                g(f"v_and_b32_e32 {v(XR)}, {s(S[4])}, {v(XR)}")
+            g.write_n(XR)
+        handlers[name] = h
+
+    @handler("N_MUL")
+    def _(g):
+        g.field("a", S[0]), g.field("b", S[1])
+        g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
+        g(f"v_mul_lo_u32 {v(XR)}, {v(T)}, {v(T + 1)}")
+        g.width(S[2]), g.nmask(S[2], S[4])
+        g(f"v_and_b32_e32 {v(XR)}, {s(S[4])}, {v(XR)}")
+        g.write_n(XR)
+
+    for name, cmp in (("N_SLTN", "v_cmp_lt_u32_e32"), ("N_SLEN", "v_cmp_le_u32_e32")):
+        def h(g, cmp=cmp):
+            # signed w-bit compare of canonical values: flip bit w-1, compare unsigned
+            g.field("a", S[0]), g.field("b", S[1])
+            g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
+            g.width(S[2])
+            g(f"s_sub_u32 {s(S[2])}, {s(S[2])}, 1", f"s_lshl_b32 {s(S[2])}, 1, {s(S[2])}",
+              f"v_xor_b32_e32 {v(T)}, {s(S[2])}, {v(T)}", f"v_xor_b32_e32 {v(T + 1)}, {s(S[2])}, {v(T + 1)}",
+              f"{cmp} vcc, {v(T)}, {v(T + 1)}")
+            g.bool_from_vcc(XR)
+            g.write_n(XR)
+        handlers[name] = h
+
+    @handler("N_UMULNON")
+    def _(g):
+        # a * b < 2^w: the high word is 0 and (w < 32) the low word has no bit >= w
+        g.field("a", S[0]), g.field("b", S[1])
+        g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
+        g.width(S[2]), g.nmask(S[2], S[4])
+        g(f"v_mul_hi_u32 {v(T + 2)}, {v(T)}, {v(T + 1)}", f"v_mul_lo_u32 {v(T + 3)}, {v(T)}, {v(T + 1)}",
+          f"s_not_b32 {s(S[4])}, {s(S[4])}", f"v_and_b32_e32 {v(T + 3)}, {s(S[4])}, {v(T + 3)}",
+          f"v_or_b32_e32 {v(T + 2)}, {v(T + 2)}, {v(T + 3)}", f"v_cmp_eq_u32_e32 vcc, 0, {v(T + 2)}")
+        g.bool_from_vcc(XR)
+        g.write_n(XR)
+
+    @handler("N_NOT")
+    def _(g):
+        g.field("a", S[0]), g.fetch_n(S[0], T)
+        g.width(S[2]), g.nmask(S[2], S[4])
+        g(f"v_xor_b32_e32 {v(XR)}, {s(S[4])}, {v(T)}")      # ~a & m == a ^ m (a canonical)
+        g.write_n(XR)
+
+    for name, cmp in (("N_EQN", "v_cmp_eq_u32_e32"), ("N_ULTN", "v_cmp_lt_u32_e32"), ("N_ULEN", "v_cmp_le_u32_e32")):
+        def h(g, cmp=cmp):
+            g.field("a", S[0]), g.field("b", S[1])
+            g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
+            g(f"{cmp} vcc, {v(T)}, {v(T + 1)}")
+            g.bool_from_vcc(XR)
+            g.write_n(XR)
+        handlers[name] = h
+
+    @handler("N_ITE")
+    def _(g):
+        g.field("a", S[0]), g.field("b", S[1]), g.field("c", S[2])
+        g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1), g.fetch_n(S[2], T + 2)
+        g(f"v_cmp_ne_u32_e32 vcc, 0, {v(T + 2)}")
+        g.nop_vcc()
+        g(f"v_cndmask_b32_e32 {v(XR)}, {v(T + 1)}, {v(T)}, vcc")
+        g.write_n(XR)
+
+    for name, op in (("N_SHLI", "v_lshlrev_b32_e32"), ("N_LSHRI", "v_lshrrev_b32_e32")):
+        def h(g, op=op):
+            g.field("a", S[0]), g.fetch_n(S[0], T)
+            big, j = g.L("sb"), g.L("sj")
+            g(f"s_cmp_ge_u32 {s(CUR + 3)}, 32", f"s_cbranch_scc1 {big}",
+              f"{op} {v(XR)}, {s(CUR + 3)}, {v(T)}")
+            g.width(S[2]), g.nmask(S[2], S[4])
+            g(f"v_and_b32_e32 {v(XR)}, {s(S[4])}, {v(XR)}", f"s_branch {j}")
+            g.label(big)
+            g(f"v_mov_b32_e32 {v(XR)}, 0")
+            g.label(j)
+            g.write_n(XR)
+        handlers[name] = h
+
+    @handler("MOV_N")
+    def _(g):
+        g.field("a", S[0]), g.fetch_n(S[0], XR), g.write_n(XR)
+
+    # -------------------------------------------------------- checks
+    def update_alive(g):
+        """alive &= vcc, then the early-exit test"""
+        g.nop_vcc()
+        g(f"v_cndmask_b32_e32 {v(ALIVE)}, 0, {v(ALIVE)}, vcc")
+        skip = g.L("ee")
+        g(f"s_bitcmp1_b32 {s(FLAGS)}, 0", f"s_cbranch_scc0 {skip}",
+          f"v_cmp_ne_u32_e32 vcc, 0, {v(ALIVE)}", "s_nop 1", "s_cmp_eq_u64 vcc, 0")
+        g.stop_if_scc1()
+        g.label(skip)
+
+    @handler("CHECK")
+    def _(g):
+        g.field("a", S[0]), g.fetch_n(S[0], T)
+        g(f"v_cmp_ne_u32_e32 vcc, 0, {v(T)}")
+        update_alive(g)
+
+    @handler("CHECK_IMP")
+    def _(g):
+        g.field("a", S[0]), g.field("b", S[1])
+        g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
+        g(f"v_cmp_eq_u32_e64 {sr(MSK, 2)}, 0, {v(T)}", f"v_cmp_ne_u32_e32 vcc, 0, {v(T + 1)}",
+          "s_nop 1", f"s_or_b64 vcc, vcc, {sr(MSK, 2)}")
+        update_alive(g)
+
+    @handler("CHECK_IMPEQ")
+    def _(g):
+        g.field("a", S[0]), g.field("b", S[1]), g.field("c", S[2])
+        g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1), g.fetch_n(S[2], T + 2)
+        g(f"v_cmp_eq_u32_e64 {sr(MSK, 2)}, 0, {v(T)}", f"v_cmp_eq_u32_e32 vcc, {v(T + 1)}, {v(T + 2)}",
+          "s_nop 1", f"s_or_b64 vcc, vcc, {sr(MSK, 2)}")
+        update_alive(g)
+
+    def eq8(g, a, b, dst_v):
+        """dst_v = OR of the limb XORs (0 iff equal)"""
+        for k in range(8):
+            g(f"v_xor_b32_e32 {v(T + k)}, {v(a + k)}, {v(b + k)}")
+        g(f"v_or3_b32 {v(T)}, {v(T)}, {v(T + 1)}, {v(T + 2)}", f"v_or3_b32 {v(T + 3)}, {v(T + 3)}, {v(T + 4)}, {v(T + 5)}",
+          f"v_or3_b32 {v(dst_v)}, {v(T + 6)}, {v(T + 7)}, {v(T)}", f"v_or_b32_e32 {v(dst_v)}, {v(dst_v)}, {v(T + 3)}")
+
+    @handler("CHECK_IMPEQW")
+    def _(g):
+        g.field("a", S[0]), g.field("b", S[1]), g.field("c", S[2])
+        g.fetch_n(S[0], XC), g.fetch_w(S[1], XA), g.fetch_w(S[2], XB)
+        eq8(g, XA, XB, XC + 1)
+        g(f"v_cmp_eq_u32_e64 {sr(MSK, 2)}, 0, {v(XC)}", f"v_cmp_eq_u32_e32 vcc, 0, {v(XC + 1)}",
+          "s_nop 1", f"s_or_b64 vcc, vcc, {sr(MSK, 2)}")
+        update_alive(g)
+
+    # -------------------------------------------------------- wide -> narrow
+    @handler("N_EQ")
+    def _(g):
+        g.field("a", S[0]), g.field("b", S[1])
+        g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
+        eq8(g, XA, XB, XC)
+        g(f"v_cmp_eq_u32_e32 vcc, 0, {v(XC)}")
+        g.bool_from_vcc(XR)
+        g.write_n(XR)
+
+    @handler("N_ULT")
+    def _(g):
+        g.field("a", S[0]), g.field("b", S[1])
+        g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
+        g.sub_chain(XA, XB)
+        g.bool_from_vcc(XR)
+        g.write_n(XR)
+
+    @handler("N_ULE")
+    def _(g):
+        g.field("a", S[0]), g.field("b", S[1])
+        g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
+        g.sub_chain(XB, XA)                     # b < a  ->  not (a <= b)
+        g.bool_from_vcc(XR, invert=True)
+        g.write_n(XR)
+
+    for name, le in (("N_SLT", False), ("N_SLE", True)):
+        def h(g, le=le):
+            g.field("a", S[0]), g.field("b", S[1])
+            g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
+            # flip bit w-1 of both (width = operand width), then compare unsigned
+            g.width(S[2])
+            g(f"s_sub_u32 {s(S[2])}, {s(S[2])}, 1", f"s_lshr_b32 {s(S[3])}, {s(S[2])}, 5",
+              f"s_and_b32 {s(S[2])}, {s(S[2])}, 31", f"s_lshl_b32 {s(S[2])}, 1, {s(S[2])}",
+              f"s_set_gpr_idx_on {s(S[3])}, gpr_idx(SRC1,DST)", f"v_xor_b32_e32 {v(XA)}, {s(S[2])}, {v(XA)}",
+              "s_set_gpr_idx_off", f"s_set_gpr_idx_on {s(S[3])}, gpr_idx(SRC1,DST)",
+              f"v_xor_b32_e32 {v(XB)}, {s(S[2])}, {v(XB)}", "s_set_gpr_idx_off")
+            if le:
+                g.sub_chain(XB, XA)
+                g.bool_from_vcc(XR, invert=True)
+            else:
+                g.sub_chain(XA, XB)
+                g.bool_from_vcc(XR)
+            g.write_n(XR)
+        handlers[name] = h
+
+    @handler("N_EXTRACTW")
+    def _(g):
+        g.field("a", S[0]), g.fetch_w(S[0], XA)
+        # (x >> imm)[0] & nmask(w): limb q = imm >> 5 and the next, funnel by imm & 31
+        g(f"s_lshr_b32 {s(S[1])}, {s(CUR + 3)}, 5", f"s_and_b32 {s(S[2])}, {s(CUR + 3)}, 31",
+          f"s_set_gpr_idx_on {s(S[1])}, gpr_idx(SRC0,SRC1)",
+          f"v_alignbit_b32 {v(XR)}, {v(XA + 1)}, {v(XA)}, {s(S[2])}", "s_set_gpr_idx_off")
+        g.width(S[3]), g.nmask(S[3], S[4])
+        g(f"v_and_b32_e32 {v(XR)}, {s(S[4])}, {v(XR)}")
+        g.write_n(XR)
+
+    @handler("N_UMULNO")
+    def _(g):
+        g.field("a", S[0]), g.field("b", S[1])
+        g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
+        mul_full(g, hi=True)
+        # overflow iff any product bit >= w: low limbs above w (masked by ~limb_mask), or any high limb
+        g.width(S[2])
+        g(f"v_or3_b32 {v(T)}, {v(XC)}, {v(XC + 1)}, {v(XC + 2)}", f"v_or3_b32 {v(T)}, {v(T)}, {v(XC + 3)}, {v(XC + 4)}",
+          f"v_or3_b32 {v(T)}, {v(T)}, {v(XC + 5)}, {v(XC + 6)}", f"v_or_b32_e32 {v(T)}, {v(T)}, {v(XC + 7)}")
+        # low part: copy XR, canon it to w, and compare with XR (a difference = bits >= w)
+        for k in range(8):
+            g(f"v_mov_b32_e32 {v(XB + k)}, {v(XR + k)}")
+        g.canon(XB, S[2])
+        for k in range(8):
+            g(f"v_xor_b32_e32 {v(XB + k)}, {v(XB + k)}, {v(XR + k)}")
+        g(f"v_or3_b32 {v(T)}, {v(T)}, {v(XB)}, {v(XB + 1)}", f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 2)}, {v(XB + 3)}",
+          f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 4)}, {v(XB + 5)}", f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 6)}, {v(XB + 7)}",
+          f"v_cmp_eq_u32_e32 vcc, 0, {v(T)}")
+        g.bool_from_vcc(XR)
+        g.write_n(XR)
+
+    # -------------------------------------------------------- wide
+    def wbin(name, fn, canon=True):
+        def h(g):
+            g.field("a", S[0]), g.field("b", S[1])
+            g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
+            fn(g)
+            if canon:
+                g.width(S[2]), g.canon(XR, S[2])
+            g.write_w(XR)
+        handlers[name] = h
+
+    wbin("W_ADD", lambda g: g.add_chain(XA, XB, XR))
+    wbin("W_SUB", lambda g: g.sub_chain(XA, XB, XR))
+    for name, op in (("W_AND", "v_and_b32_e32"), ("W_OR", "v_or_b32_e32"), ("W_XOR", "v_xor_b32_e32")):
+        wbin(name, lambda g, op=op: [g(f"{op} {v(XR + k)}, {v(XA + k)}, {v(XB + k)}") for k in range(8)])
+    wbin("W_MUL", lambda g: mul_full(g, hi=False))
+
+    @handler("W_NOT")
+    def _(g):
+        g.field("a", S[0]), g.fetch_w(S[0], XA)
+        for k in range(8):
+            g(f"v_not_b32_e32 {v(XR + k)}, {v(XA + k)}")
+        g.width(S[2]), g.canon(XR, S[2])
+        g.write_w(XR)
+
+    @handler("MOV_W")
+    def _(g):
+        g.field("a", S[0]), g.fetch_w(S[0], XR), g.write_w(XR)
+
+    @handler("W_ITE")
+    def _(g):
+        g.field("a", S[0]), g.field("b", S[1]), g.field("c", S[2])
+        g.fetch_n(S[2], T), g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
+        g(f"v_cmp_ne_u32_e32 vcc, 0, {v(T)}")
+        g.nop_vcc()
+        for k in range(8):
+            g(f"v_cndmask_b32_e32 {v(XR + k)}, {v(XB + k)}, {v(XA + k)}, vcc")
+        g.width(S[2]), g.canon(XR, S[2])
+        g.write_w(XR)
+
+    def shl_into(g, amount, dst):
+        """dst..dst+7 = XA << amount (SGPR, < 256): written through a positive
+        destination index (limbs past dst+7 land in the next 8 temporaries
+        and are dropped); XA has zeros below it"""
+        q, b = S[4], S[5]
+        zb, j = g.L("z0"), g.L("sj")
+        for k in range(8):
+            g(f"v_mov_b32_e32 {v(dst + k)}, 0")
+        g(f"s_lshr_b32 {s(q)}, {s(amount)}, 5", f"s_and_b32 {s(b)}, {s(amount)}, 31",
+          f"s_cmp_eq_u32 {s(b)}, 0", f"s_cbranch_scc1 {zb}",
+          f"s_sub_u32 {s(b)}, 32, {s(b)}",             # fshl(hi, lo, b) = alignbit(hi, lo, 32 - b)
+          f"s_set_gpr_idx_on {s(q)}, gpr_idx(DST)")
+        for k in range(8):
+            g(f"v_alignbit_b32 {v(dst + k)}, {v(XA + k)}, {v(XA + k - 1)}, {s(b)}")
+        g("s_set_gpr_idx_off", f"s_branch {j}")
+        g.label(zb)
+        g(f"s_set_gpr_idx_on {s(q)}, gpr_idx(DST)")
+        for k in range(8):
+            g(f"v_mov_b32_e32 {v(dst + k)}, {v(XA + k)}")
+        g("s_set_gpr_idx_off")
+        g.label(j)
+
+    @handler("W_SHLI")
+    def _(g):
+        g.field("a", S[0]), g.fetch_w(S[0], XA)
+        shl_into(g, CUR + 3, XR)
+        g.width(S[2]), g.canon(XR, S[2])
+        g.write_w(XR)
+
+    @handler("W_LSHRI")
+    def _(g):
+        g.field("a", S[0]), g.fetch_w(S[0], XA)
+        q, b = S[4], S[5]
+        g(f"s_lshr_b32 {s(q)}, {s(CUR + 3)}, 5", f"s_and_b32 {s(b)}, {s(CUR + 3)}, 31",
+          f"s_set_gpr_idx_on {s(q)}, gpr_idx(SRC0,SRC1)")
+        for k in range(8):
+            g(f"v_alignbit_b32 {v(XR + k)}, {v(XA + k + 1)}, {v(XA + k)}, {s(b)}")
+        g("s_set_gpr_idx_off")
+        g.width(S[2]), g.canon(XR, S[2])
+        g.write_w(XR)
+
+    @handler("W_ZEXTN")
+    def _(g):
+        g.field("a", S[0]), g.fetch_n(S[0], XR)
+        for k in range(1, 8):
+            g(f"v_mov_b32_e32 {v(XR + k)}, 0")
+        g.width(S[2]), g.canon(XR, S[2])
+        g.write_w(XR)
+
+    @handler("W_INSN")
+    def _(g):
+        # r = a | (zext(N b) << imm)
+        g.field("a", S[0]), g.field("b", S[1])
+        g.fetch_w(S[0], XR), g.fetch_n(S[1], XA)
+        for k in range(1, 8):
+            g(f"v_mov_b32_e32 {v(XA + k)}, 0")
+        shl_imm_into_or(g, CUR + 3)
+        g.width(S[2]), g.canon(XR, S[2])
+        g.write_w(XR)
+
+    def shl_imm_into_or(g, amount):
+        """XR |= XA << amount (XA: an N value in limb 0, zeros above)"""
+        shl_into(g, amount, XC)
+        for k in range(8):
+            g(f"v_or_b32_e32 {v(XR + k)}, {v(XR + k)}, {v(XC + k)}")
+
+    @handler("W_CDINS")
+    def _(g):
+        # acc | ((K[c] <s size) ? leaf(imm & 0xffff) : 0) << (imm >> 16), chained
+        # links keep the word in XR (mw_interp.h MW_W_CDINS, MW_FLAG_CHAIN)
+        g.field("a", S[0]), g.fetch_w(S[0], XR)
+        g(f"s_mov_b32 {s(S[0])}, -1")                 # b operand of the cached size summary: none
+        top, slow, rng, ins = g.L("cdtop"), g.L("cdslow"), g.L("cdrng"), g.L("cdins")
+        g.label(top)
+        # predecoded small index (mw_asm_predecode): c = 0x4000 | i, i < 0x4000
+        g(f"s_bitcmp1_b32 {s(CUR + 2)}, 30", f"s_cbranch_scc0 {slow}",
+          f"s_bfe_u32 {s(S[1])}, {s(CUR + 2)}, 0xe0010",        # i = bits [29:16]
+          f"s_and_b32 {s(S[2])}, {s(CUR + 2)}, 0xffff",
+          f"s_cmp_eq_u32 {s(S[2])}, {s(S[0])}", f"s_cbranch_scc1 {rng}",
+          f"s_mov_b32 {s(S[0])}, {s(S[2])}")
+        # size summary in XA: i <s size  <=>  i <u XA, XA = size < 0 ? 0 :
+        # (size >= 2^32 ? 2^32 - 1 : size)   (i < 2^14)
+        g.field("b", S[2]), g.fetch_w(S[2], XB)
+        g(f"v_or3_b32 {v(T)}, {v(XB + 1)}, {v(XB + 2)}, {v(XB + 3)}",
+          f"v_and_b32_e32 {v(T + 1)}, 0x7fffffff, {v(XB + 7)}",
+          f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 4)}, {v(XB + 5)}",
+          f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 6)}, {v(T + 1)}",
+          f"v_cmp_ne_u32_e32 vcc, 0, {v(T)}", "s_nop 1",
+          f"v_cndmask_b32_e64 {v(XA)}, {v(XB)}, -1, vcc",
+          f"v_cmp_gt_i32_e32 vcc, 0, {v(XB + 7)}", "s_nop 1",
+          f"v_cndmask_b32_e64 {v(XA)}, {v(XA)}, 0, vcc")
+        g.label(rng)
+        g(f"v_cmp_lt_u32_e64 {sr(MSK2, 2)}, {s(S[1])}, {v(XA)}", "s_branch " + ins)
+        # any other index: the full signed 256-bit compare
+        g.label(slow)
+        g(f"s_mov_b32 {s(S[0])}, -1")
+        g.field("b", S[1]), g.fetch_w(S[1], XB)
+        g.field("c", S[2]), g.fetch_w(S[2], XA)
+        g(f"v_xor_b32_e32 {v(XA + 7)}, 0x80000000, {v(XA + 7)}", f"v_xor_b32_e32 {v(XB + 7)}, 0x80000000, {v(XB + 7)}")
+        g.sub_chain(XA, XB)
+        g(f"s_mov_b64 {sr(MSK2, 2)}, vcc")            # lanes whose byte is in range
+        g.label(ins)
+        # no lane in range: the inserted byte is 0 in every lane (no leaf draw)
+        nos = g.L("cdns")
+        g("s_nop 1", f"s_cmp_eq_u64 {sr(MSK2, 2)}, 0", f"s_cbranch_scc1 {nos}")
+        g(f"s_and_b32 {s(S[3])}, {s(CUR + 3)}, 0xffff")
+        call_leaf(g, S[3])
+        # t = in range ? byte : 0, inserted at bit off = imm >> 16 (limb off >> 5)
+        g(f"v_cndmask_b32_e64 {v(T)}, 0, {v(XC)}, {sr(MSK2, 2)}",
+          f"s_lshr_b32 {s(S[4])}, {s(CUR + 3)}, 16",
+          f"s_lshr_b32 {s(S[5])}, {s(S[4])}, 5", f"s_and_b32 {s(S[4])}, {s(S[4])}, 31",
+          f"s_set_gpr_idx_on {s(S[5])}, gpr_idx(SRC2,DST)",
+          f"v_lshl_or_b32 {v(XR)}, {v(T)}, {s(S[4])}, {v(XR)}", "s_set_gpr_idx_off")
+        # a byte straddling a limb boundary (off & 31 > 24): its high bits go to the next limb
+        g(f"s_cmp_le_u32 {s(S[4])}, 24", f"s_cbranch_scc1 {nos}",
+          f"s_sub_u32 {s(S[4])}, 32, {s(S[4])}", f"s_add_u32 {s(S[5])}, {s(S[5])}, 1",
+          f"v_lshrrev_b32_e32 {v(T)}, {s(S[4])}, {v(T)}",
+          f"s_set_gpr_idx_on {s(S[5])}, gpr_idx(SRC1,DST)",
+          f"v_or_b32_e32 {v(XR)}, {v(T)}, {v(XR)}", "s_set_gpr_idx_off")
+        g.label(nos)
+        # chained: consume the next instruction (a W_CDINS whose acc is this word)
+        last = g.L("cdlast")
+        g(f"s_bitcmp1_b32 {s(CUR)}, 8", f"s_cbranch_scc0 {last}")
+        g.width(S[2]), g.canon(XR, S[2])
+        consume_next(g)
+        g(f"s_branch {top}")
+        g.label(last)
+        g.width(S[2]), g.canon(XR, S[2])
+        g.write_w(XR)
+
+    def consume_next(g):
+        g("s_waitcnt lgkmcnt(0)", f"s_mov_b64 {sr(CUR, 2)}, {sr(NXT, 2)}", f"s_mov_b64 {sr(CUR + 2, 2)}, {sr(NXT + 2, 2)}",
+          f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, {s(SOFF)}")
+
+    # -------------------------------------------------------- leaves
+    def call_leaf(g, li):
+        """XC..XC+7 = candidate value of leaf index li (SGPR)"""
+        g(f"s_mov_b32 {s(S67)}, {s(li)}")
+        g.call_leaf_sub()
+
+    @handler("LEAF_W")
+    def _(g):
+        g(f"s_mov_b32 {s(S[0])}, {s(CUR + 3)}")
+        call_leaf(g, S[0])
+        g.write_w(XC)
+
+    @handler("LEAF_N")
+    def _(g):
+        g(f"s_mov_b32 {s(S[0])}, {s(CUR + 3)}")
+        call_leaf(g, S[0])
+        g.write_n(XC)
+
+    # -------------------------------------------------------- spills
+    def spill_word(g, wd_sgpr, src, store=True):
+        """word wd (SGPR) of this lane's spill area: LDS [wd][lane] below nlds, else the global buffer"""
+        glob, j = g.L("sg"), g.L("sj")
+        a = S[7]
+        g(f"s_cmp_lt_u32 {s(wd_sgpr)}, {s(NLDS)}", f"s_cbranch_scc0 {glob}",
+          f"s_lshl_b32 {s(a)}, {s(wd_sgpr)}, 10", f"v_add_u32_e32 {v(T + 7)}, {s(a)}, {v(LDSOFF)}")
+        g(f"ds_write_b32 {v(T + 7)}, {v(src)}" if store else f"ds_read_b32 {v(src)}, {v(T + 7)}")
+        g(f"s_branch {j}")
+        g.label(glob)
+        g(f"s_sub_u32 {s(a)}, {s(wd_sgpr)}, {s(NLDS)}", f"s_mul_i32 {s(a)}, {s(a)}, {s(GSTRIDE)}",
+          f"v_add_u32_e32 {v(T + 7)}, {s(a)}, {v(GOFF)}")
+        g(f"global_store_dword {v(T + 7)}, {v(src)}, {sr(GSP, 2)}" if store
+          else f"global_load_dword {v(src)}, {v(T + 7)}, {sr(GSP, 2)}")
+        g.label(j)
+
+    @handler("SPILL_W")
+    def _(g):
+        g.field("a", S[0]), g.fetch_w(S[0], XA)
+        for k in range(8):
+            g(f"s_add_u32 {s(S[1])}, {s(CUR + 3)}, {k}")
+            spill_word(g, S[1], XA + k)
+        g("s_waitcnt vmcnt(0) lgkmcnt(0)")
+
+    @handler("SPILL_N")
+    def _(g):
+        g.field("a", S[0]), g.fetch_n(S[0], XA)
+        g(f"s_mov_b32 {s(S[1])}, {s(CUR + 3)}")
+        spill_word(g, S[1], XA)
+        g("s_waitcnt vmcnt(0) lgkmcnt(0)")
+
+    @handler("FILL_W")
+    def _(g):
+        for k in range(8):
+            g(f"s_add_u32 {s(S[1])}, {s(CUR + 3)}, {k}")
+            spill_word(g, S[1], XR + k, store=False)
+        g("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        g.write_w(XR)
+
+    @handler("FILL_N")
+    def _(g):
+        g(f"s_mov_b32 {s(S[1])}, {s(CUR + 3)}")
+        spill_word(g, S[1], XR, store=False)
+        g("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        g.write_n(XR)
+
+    # -------------------------------------------------------- multiply
+    def mul_full(g, hi):
+        """XR = low 256 bits of XA * XB; with hi, XC = the high 256 bits.
+        Row by row: acc[i+j] += a_i b_j + carry with one 64-bit mad each
+        (mw_alu.h mul8 / mulhi8)."""
+        acc = [XR + k for k in range(8)] + ([XC + k for k in range(8)] if hi else [])
+        n = len(acc)
+        for k in range(n):
+            g(f"v_mov_b32_e32 {v(acc[k])}, 0")
+        for i in range(8):
+            g(f"v_mov_b32_e32 {v(T + 1)}, 0")                 # carry
+            for j in range(8):
+                if i + j >= n:
+                    break
+                g(f"v_mov_b32_e32 {v(T + 2)}, {v(acc[i + j])}", f"v_mov_b32_e32 {v(T + 3)}, 0",
+                  f"v_mad_u64_u32 {vr(T + 4, 2)}, {sr(SX, 2)}, {v(XA + i)}, {v(XB + j)}, {vr(T + 2, 2)}",
+                  f"v_add_co_u32_e32 {v(acc[i + j])}, vcc, {v(T + 4)}, {v(T + 1)}")
+                g.nop_vcc()
+                g(f"v_addc_co_u32_e32 {v(T + 1)}, vcc, 0, {v(T + 5)}, vcc")
+            if i + 8 < n:
+                g(f"v_mov_b32_e32 {v(acc[i + 8])}, {v(T + 1)}")
+
+    handlers["_call_leaf"] = call_leaf
+    return handlers
+
+
+HANDLERS = build_handlers()
+MARKER = "; MWJIT_BODY"
+
+
+def gen(mode="interp"):
+    """The inline-asm body, as a list of lines.  mode "interp": the
+    threaded-dispatch interpreter; "template": the same kernel with the
+    program's place marked by MARKER (an assembled kernel's straight-line body
+    goes there and falls through to the chunk's result protocol)."""
+    g = Gen()
+    handlers = HANDLERS
+    body = []
+    g.lines = body
+    # ---- once per block: launch arguments (AsmArgs) and the program (ProgDev)
+    # from memory, per-lane constants from the operands
+    g(f"s_mov_b64 {sr(ARGP, 2)}, %[args]", f"s_mov_b64 {sr(PROGP, 2)}, %[prog]",
+      f"s_mov_b64 {sr(OUTMIN, 2)}, %[outmin]", f"s_mov_b32 {s(CH)}, %[ch0]",
+      f"v_mov_b32_e32 {v(T)}, %[tid]", f"v_mov_b32_e32 {v(GOFF)}, %[goff]",
+      f"s_load_dwordx8 {sr(DESC, 8)}, {sr(ARGP, 2)}, 0x0",
+      f"s_load_dwordx8 {sr(72, 8)}, {sr(ARGP, 2)}, 0x20",
+      "s_waitcnt lgkmcnt(0)",
+      # AsmArgs: seed(2) begin(2) end(2) flags nlds | gstride nch gdx pad gsp(2) verdict(2)
+      f"s_mov_b64 {sr(SEED, 2)}, {sr(DESC, 2)}", f"s_mov_b64 {sr(BEGIN, 2)}, {sr(DESC + 2, 2)}",
+      f"s_mov_b64 {sr(END, 2)}, {sr(DESC + 4, 2)}", f"s_mov_b32 {s(FLAGS)}, {s(DESC + 6)}",
+      f"s_mov_b32 {s(NLDS)}, {s(DESC + 7)}", f"s_mov_b32 {s(GSTRIDE)}, {s(72)}", f"s_mov_b32 {s(NCH)}, {s(73)}",
+      f"s_mov_b32 {s(GDX)}, {s(74)}", f"s_mov_b64 {sr(GSP, 2)}, {sr(76, 2)}", f"s_mov_b64 {sr(VERD, 2)}, {sr(78, 2)}",
+      # ProgDev: code(2) consts(2) leaves(2) pool(2) | n_spill npool n_insn pad
+      f"s_load_dwordx8 {sr(DESC, 8)}, {sr(PROGP, 2)}, 0x0", f"s_load_dwordx4 {sr(72, 4)}, {sr(PROGP, 2)}, 0x20",
+      "s_waitcnt lgkmcnt(0)",
+      f"s_mov_b64 {sr(CODE0, 2)}, {sr(DESC, 2)}", f"s_mov_b64 {sr(CPOOL, 2)}, {sr(DESC + 2, 2)}",
+      f"s_mov_b64 {sr(LEAVES, 2)}, {sr(DESC + 4, 2)}",
+      f"s_lshl_b32 {s(POOLB)}, {s(NLDS)}, 10",
+      f"s_mov_b32 {s(PM0)}, 0xD2511F53", f"s_mov_b32 {s(PM1)}, 0xCD9E8D57",
+      f"s_mov_b64 {sr(EVALS, 2)}, 0",
+      f"v_lshlrev_b32_e32 {v(LDSOFF)}, 2, {v(T)}", f"v_mov_b32_e32 {v(TID)}, {v(T)}")
+    if mode == "interp":
+        # the dispatch table's address (s_getpc_b64 gives the next instruction's)
+        g(f"s_getpc_b64 {sr(SX, 2)}")
+        g.label("Lpc0_%=")
+        g(f"s_add_u32 {s(TABLO)}, {s(SX)}, (Ltab_%= - Lpc0_%=)", f"s_addc_u32 {s(TABHI)}, {s(SX + 1)}, 0")
+    else:
+        for reg, lab in ((LEAFADDR, "Lleaf_%="), (STOPADDR, "Lstop_%="), (ENDADDR, "Lh_END_%="),
+                         (PHILOXADDR, "Lphilox_%=")):
+            g.long_addr(reg, lab)
+    for k in range(128, 136, 2):
+        g(f"v_mov_b64 {vr(k, 2)}, 0")
+    for k in range(144, 152, 2):
+        g(f"v_mov_b64 {vr(k, 2)}, 0")
+    # ---- chunk loop: chunk ch covers [begin + 256 ch, +256)
+    g.label("Lchunk_%=")
+    g(f"s_cmp_lt_u32 {s(CH)}, {s(NCH)}", "s_cbranch_scc0 Lexit_%=",
+      f"s_lshl_b32 {s(BASE)}, {s(CH)}, 8", f"s_lshr_b32 {s(BASE + 1)}, {s(CH)}, 24",
+      f"s_add_u32 {s(BASE)}, {s(BASE)}, {s(BEGIN)}", f"s_addc_u32 {s(BASE + 1)}, {s(BASE + 1)}, {s(BEGIN + 1)}",
+      # stop after hit: a witness below this chunk is known (a stale read only delays the stop)
+      f"s_bitcmp1_b32 {s(FLAGS)}, 1", "s_cbranch_scc0 Lnostop_%=",
+      f"s_load_dwordx2 {sr(SX, 2)}, {sr(OUTMIN, 2)}, 0x0 glc", "s_waitcnt lgkmcnt(0)",
+      # m <= base  <=>  !(base < m): compare (hi, lo) lexicographically
+      f"s_cmp_lt_u32 {s(SX + 1)}, {s(BASE + 1)}", "s_cbranch_scc1 Lexit_%=",
+      f"s_cmp_eq_u32 {s(SX + 1)}, {s(BASE + 1)}", "s_cbranch_scc0 Lnostop_%=",
+      f"s_cmp_le_u32 {s(SX)}, {s(BASE)}", "s_cbranch_scc1 Lexit_%=")
+    g.label("Lnostop_%=")
+    g(f"v_mov_b32_e32 {v(T + 7)}, {s(BASE + 1)}",
+      f"v_add_co_u32_e32 {v(CLO)}, vcc, {s(BASE)}, {v(TID)}", "s_nop 1",
+      f"v_addc_co_u32_e32 {v(CHI)}, vcc, 0, {v(T + 7)}, vcc",
+      f"v_cmp_gt_u64_e32 vcc, {sr(END, 2)}, {vr(CLO, 2)}", "s_nop 1",
+      f"s_mov_b64 {sr(VALID, 2)}, vcc", f"v_cndmask_b32_e64 {v(ALIVE)}, 0, 1, vcc")
+    for k in range(0, 128, 2):
+        g(f"v_mov_b64 {vr(k, 2)}, 0")
+    if mode == "template":
+        g.long_addr(SX, "Lbody_%=")
+        g(f"s_setpc_b64 {sr(SX, 2)}")
+    else:
+        g(f"s_mov_b32 {s(SOFF)}, 0", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, 0x0")
+        # ---- dispatch
+        g.label("Ldisp_%=")
+        g.next()
+        g.label("Ltab_%=")
+        names = {c: n for n, c in isa.OPCODES.items()}
+        for code in range(NTAB):
+            n = names.get(code)
+            g(f"s_branch Lh_{n}_%=" if n in handlers or n == "END" else "s_branch Lunsup_%=")
+        # handlers
+        for n in ASM_OPCODES:
+            if n == "END":
+                continue
+            g.label(f"Lh_{n}_%=")
+            handlers[n](g)
+            g.next()
+            g.flush_tail()
+    g.label("Lunsup_%=")
+    g.label("Lstop_%=")
+    g(f"v_mov_b32_e32 {v(ALIVE)}, 0")
+    g.label("Lh_END_%=")
+    # ---- this chunk's result: verdicts, evals, lowest satisfying lane -> atomic min
+    g("s_waitcnt vmcnt(0) lgkmcnt(0)",
+      f"v_cmp_ne_u32_e32 vcc, 0, {v(ALIVE)}", "s_nop 1",
+      f"s_and_b64 {sr(MSK, 2)}, vcc, {sr(VALID, 2)}",
+      f"s_bcnt1_i32_b64 {s(SX)}, {sr(VALID, 2)}",
+      f"s_add_u32 {s(EVALS)}, {s(EVALS)}, {s(SX)}", f"s_addc_u32 {s(EVALS + 1)}, {s(EVALS + 1)}, 0",
+      f"s_cmp_eq_u64 {sr(VERD, 2)}, 0", "s_cbranch_scc1 Lnoverd_%=",
+      f"v_cndmask_b32_e64 {v(T)}, 0, 1, {sr(MSK, 2)}",
+      # verdict[cand - begin]: byte offset (ch * 256 + tid) * 4
+      f"s_lshl_b32 {s(SX)}, {s(CH)}, 10", f"v_add_u32_e32 {v(T + 1)}, {s(SX)}, {v(LDSOFF)}",
+      f"s_mov_b64 {sr(EXECSV, 2)}, exec", f"s_mov_b64 exec, {sr(VALID, 2)}",
+      f"global_store_dword {v(T + 1)}, {v(T)}, {sr(VERD, 2)}",
+      f"s_mov_b64 exec, {sr(EXECSV, 2)}")
+    g.label("Lnoverd_%=")
+    g(f"s_cmp_eq_u64 {sr(MSK, 2)}, 0", "s_cbranch_scc1 Lnohit_%=",
+      # the wave's lowest satisfying lane issues the atomic with its own candidate index
+      f"s_ff1_i32_b64 {s(SX)}, {sr(MSK, 2)}", f"s_lshl_b64 {sr(JMP, 2)}, 1, {s(SX)}",
+      f"s_mov_b64 {sr(EXECSV, 2)}, exec", f"s_mov_b64 exec, {sr(JMP, 2)}",
+      f"v_mov_b32_e32 {v(T + 2)}, 0",
+      f"global_atomic_umin_x2 {v(T + 2)}, {vr(CLO, 2)}, {sr(OUTMIN, 2)}",
+      f"s_mov_b64 exec, {sr(EXECSV, 2)}")
+    g.label("Lnohit_%=")
+    g(f"s_add_u32 {s(CH)}, {s(CH)}, {s(GDX)}", "s_branch Lchunk_%=")
+    # ------------------------------------------------------ subroutines
+    leaf(g)
+    philox_sub(g)
+    g.label("Lexit_%=")
+    g("s_waitcnt vmcnt(0) lgkmcnt(0)", f"s_mov_b64 %[evals], {sr(EVALS, 2)}")
+    if mode == "template":
+        # the program's straight-line body last (it ends in a jump to Lh_END)
+        g.long_addr(SX, "Ldone_%=")
+        g(f"s_setpc_b64 {sr(SX, 2)}")
+        g.label("Lbody_%=")
+        g(MARKER)
+        g.label("Ldone_%=")
+    return body
+
+
+def leaf(g):
+    """Lleaf: XC = value of leaf S67 for this lane's candidate (mw_leaf.h
+    leaf_value with the pool in LDS: kinds 0 random, 1 bit-field digit,
+    2 hashed digit, 3 bit-interleaved digit; a pool entry flagged RANDOM draws
+    Philox)."""
+    D = DESC   # s80 w, s81 kind, s82 id, s83 shift, s84 bits, s85 poff, s86 inrow, s87 stride
+    g.label("Lleaf_%=")
+    g(f"s_lshl_b32 {s(S[7])}, {s(S67)}, 5", f"s_load_dwordx8 {sr(D, 8)}, {sr(LEAVES, 2)}, {s(S[7])}",
+      "s_waitcnt lgkmcnt(0)",
+      f"s_cmp_eq_u32 {s(D + 1)}, 1", "s_cbranch_scc1 Lk1_%=",
+      f"s_cmp_eq_u32 {s(D + 1)}, 3", "s_cbranch_scc1 Lk3_%=",
+      f"s_cmp_eq_u32 {s(D + 1)}, 2", "s_cbranch_scc1 Lk2_%=",
+      # kind 0 (or anything else: the host never launches other kinds here): Philox
+      f"s_call_b64 {sr(PRET, 2)}, Lphilox_%=")
+    for k in range(8):
+        g(f"v_mov_b32_e32 {v(XC + k)}, {v(T + k)}")
+    g("s_branch Lleaf_canon_%=")
+    # kind 1: digit = (cand >> shift) & (2^bits - 1)
+    g.label("Lk1_%=")
+    g(f"v_lshrrev_b64 {vr(T, 2)}, {s(D + 3)}, {vr(CLO, 2)}")
+    g(f"s_bfm_b32 {s(S[6])}, {s(D + 4)}, 0", f"s_cmp_ge_u32 {s(D + 4)}, 32", f"s_cselect_b32 {s(S[6])}, -1, {s(S[6])}",
+      f"v_and_b32_e32 {v(T + 6)}, {s(S[6])}, {v(T)}", "s_branch Lgather_%=")
+    # kind 2: digit = fmix64(cand ^ id * 0x9E3779B97F4A7C15) & (2^bits - 1) (MurmurHash3 finalizer)
+    g.label("Lk2_%=")
+    lo, hi, t1, t2 = T, T + 1, T + 2, T + 3
+    g(f"s_mul_i32 {s(S[6])}, {s(D + 2)}, 0x7F4A7C15", f"s_mul_hi_u32 {s(S[7])}, {s(D + 2)}, 0x7F4A7C15",
+      f"s_mul_i32 {s(S[4])}, {s(D + 2)}, 0x9E3779B9", f"s_add_u32 {s(S[7])}, {s(S[7])}, {s(S[4])}",
+      f"v_xor_b32_e32 {v(lo)}, {s(S[6])}, {v(CLO)}", f"v_xor_b32_e32 {v(hi)}, {s(S[7])}, {v(CHI)}")
+
+    fmix64(g, lo, hi, t1, t2)
+    g(f"s_bfm_b32 {s(S[6])}, {s(D + 4)}, 0", f"s_cmp_ge_u32 {s(D + 4)}, 32", f"s_cselect_b32 {s(S[6])}, -1, {s(S[6])}",
+      f"v_and_b32_e32 {v(T + 6)}, {s(S[6])}, {v(lo)}", "s_branch Lgather_%=")
+    # kind 3: digit bit b = index bit (shift + b * stride): one 64-bit shift
+    # of the index per bit, one loop branch (shift + (bits-1) * stride <= 63,
+    # validated)
+    g.label("Lk3_%=")
+    g(f"v_mov_b32_e32 {v(T + 6)}, 0", f"s_mov_b32 {s(S[4])}, 0", f"s_mov_b32 {s(S[5])}, {s(D + 3)}",
+      f"s_cmp_eq_u32 {s(D + 4)}, 0", "s_cbranch_scc1 Lgather_%=")
+    g.label("Lm_loop_%=")
+    g(f"v_lshrrev_b64 {vr(T + 4, 2)}, {s(S[5])}, {vr(CLO, 2)}", f"v_and_b32_e32 {v(T + 7)}, 1, {v(T + 4)}",
+      f"v_lshl_or_b32 {v(T + 6)}, {v(T + 7)}, {s(S[4])}, {v(T + 6)}",
+      f"s_add_u32 {s(S[4])}, {s(S[4])}, 1", f"s_add_u32 {s(S[5])}, {s(S[5])}, {s(D + 7)}",
+      f"s_cmp_lt_u32 {s(S[4])}, {s(D + 4)}", "s_cbranch_scc1 Lm_loop_%=")
+    # pool entry in LDS at poolb + 4 * poff: width >= 32: 9 words (flag, 8 limbs)
+    # at + 36 * digit; width < 32: one word (bit 31 RANDOM, else the value) at + 4 * digit
+    g.label("Lgather_%=")
+    g(f"s_lshl_b32 {s(S[6])}, {s(D + 5)}, 2", f"s_add_u32 {s(S[6])}, {s(S[6])}, {s(POOLB)}",
+      f"s_cmp_lt_u32 {s(D)}, 32", "s_cbranch_scc1 Lg_narrow_%=",
+      f"v_mov_b32_e32 {v(T + 5)}, 36", f"v_mad_u32_u24 {v(T + 5)}, {v(T + 6)}, {v(T + 5)}, {s(S[6])}",
+      f"ds_read_b32 {v(T + 4)}, {v(T + 5)}")
+    for k in range(4):
+        g(f"ds_read2_b32 {vr(XC + 2 * k, 2)}, {v(T + 5)} offset0:{1 + 2 * k} offset1:{2 + 2 * k}")
+    g("s_waitcnt lgkmcnt(0)", f"v_and_b32_e32 {v(T + 4)}, 1, {v(T + 4)}", "s_branch Lg_flag_%=")
+    g.label("Lg_narrow_%=")
+    g(f"v_lshl_add_u32 {v(T + 5)}, {v(T + 6)}, 2, {s(S[6])}", f"ds_read_b32 {v(XC)}, {v(T + 5)}")
+    for k in range(1, 8):
+        g(f"v_mov_b32_e32 {v(XC + k)}, 0")
+    g("s_waitcnt lgkmcnt(0)", f"v_lshrrev_b32_e32 {v(T + 4)}, 31, {v(XC)}")
+    g.label("Lg_flag_%=")
+    g(f"v_cmp_ne_u32_e32 vcc, 0, {v(T + 4)}",
+      "s_nop 1", "s_cmp_eq_u64 vcc, 0", "s_cbranch_scc1 Lleaf_canon_%=",
+      f"s_mov_b64 {sr(MSK, 2)}, vcc", f"s_call_b64 {sr(PRET, 2)}, Lphilox_%=", "s_nop 1")
+    for k in range(8):
+        g(f"v_cndmask_b32_e64 {v(XC + k)}, {v(XC + k)}, {v(T + k)}, {sr(MSK, 2)}")
+    g.label("Lleaf_canon_%=")
+    g.canon(XC, D)
+    g(f"s_setpc_b64 {sr(LRET, 2)}")
+
+
+def fmix64(g, lo, hi, t1, t2):
+    """(hi:lo) = MurmurHash3's 64-bit finalizer of (hi:lo) (mw_leaf.h fmix64);
+    temporaries t1, t2, T+4..T+5, S[4], S[5] and the carry pair SX"""
+    def xs33():   # h ^= h >> 33
+        g(f"v_lshrrev_b32_e32 {v(t1)}, 1, {v(hi)}", f"v_xor_b32_e32 {v(lo)}, {v(lo)}, {v(t1)}")
+
+    def mul64(c):  # h *= c (mod 2^64)
+        g(f"s_mov_b32 {s(S[4])}, {c & 0xFFFFFFFF:#x}", f"s_mov_b32 {s(S[5])}, {c >> 32:#x}",
+          f"v_mul_lo_u32 {v(t1)}, {v(lo)}, {s(S[5])}", f"v_mul_lo_u32 {v(t2)}, {v(hi)}, {s(S[4])}",
+          f"v_mad_u64_u32 {vr(T + 4, 2)}, {sr(SX, 2)}, {v(lo)}, {s(S[4])}, 0",
+          f"v_mov_b32_e32 {v(lo)}, {v(T + 4)}", f"v_add3_u32 {v(hi)}, {v(T + 5)}, {v(t1)}, {v(t2)}")
+    xs33()
+    mul64(0xFF51AFD7ED558CCD)
+    xs33()
+    mul64(0xC4CEB9FE1A85EC53)
+    xs33()
+
+
+def philox_sub(g):
+    """Lphilox: T..T+7 = the random leaf value of the candidate index
+    (mw_leaf.h random_leaf): w > 32 Philox4x32-10 blocks 0 and (w > 128) 1,
+    key (seed_lo ^ id, seed_hi); w <= 32 fmix64(c ^ seed ^ id * 0xC2B2AE3D27D4EB4F)."""
+    D = DESC
+    g.label("Lphilox_%=")
+    narrow = 0xC2B2AE3D27D4EB4F
+    g(f"s_cmp_gt_u32 {s(D)}, 32", "s_cbranch_scc1 Lphx_wide_%=",
+      # key (PK1:PK0) = seed ^ id * narrow (mod 2^64)
+      f"s_mul_i32 {s(PK0)}, {s(D + 2)}, {narrow & 0xFFFFFFFF:#x}",
+      f"s_mul_hi_u32 {s(PK1)}, {s(D + 2)}, {narrow & 0xFFFFFFFF:#x}",
+      f"s_mul_i32 {s(S[4])}, {s(D + 2)}, {narrow >> 32:#x}", f"s_add_u32 {s(PK1)}, {s(PK1)}, {s(S[4])}",
+      f"s_xor_b32 {s(PK0)}, {s(PK0)}, {s(SEED)}", f"s_xor_b32 {s(PK1)}, {s(PK1)}, {s(SEED + 1)}",
+      f"v_xor_b32_e32 {v(T)}, {s(PK0)}, {v(CLO)}", f"v_xor_b32_e32 {v(T + 1)}, {s(PK1)}, {v(CHI)}")
+    fmix64(g, T, T + 1, T + 2, T + 3)
+    for k in range(1, 8):
+        g(f"v_mov_b32_e32 {v(T + k)}, 0")
+    g(f"s_setpc_b64 {sr(PRET, 2)}")
+    g.label("Lphx_wide_%=")
+    g(f"v_mov_b32_e32 {v(T + 4)}, 0", f"v_mov_b32_e32 {v(T + 5)}, 0", f"v_mov_b32_e32 {v(T + 6)}, 0",
+      f"v_mov_b32_e32 {v(T + 7)}, 0")
+    for blk in (0, 1):
+        base = T + 4 * blk
+        if blk == 1:
+            g(f"s_cmp_le_u32 {s(D)}, 128", "s_cbranch_scc1 Lphx_done_%=")
+        # counter (c0, c1, c2, c3) = (cand_lo, cand_hi, blk, 0) in base..base+3; temporaries XB..XB+3
+        c = [base, base + 1, base + 2, base + 3]
+        g(f"v_mov_b32_e32 {v(c[0])}, {v(CLO)}", f"v_mov_b32_e32 {v(c[1])}, {v(CHI)}",
+          f"v_mov_b32_e32 {v(c[2])}, {blk}", f"v_mov_b32_e32 {v(c[3])}, 0",
+          f"s_xor_b32 {s(PK0)}, {s(SEED)}, {s(D + 2)}", f"s_mov_b32 {s(PK1)}, {s(SEED + 1)}")
+        for r in range(10):
+            hi0, lo0, hi1, lo1 = XB, XB + 1, XB + 2, XB + 3
+            g(f"v_mul_hi_u32 {v(hi0)}, {v(c[0])}, {s(PM0)}", f"v_mul_lo_u32 {v(lo0)}, {v(c[0])}, {s(PM0)}",
+              f"v_mul_hi_u32 {v(hi1)}, {v(c[2])}, {s(PM1)}", f"v_mul_lo_u32 {v(lo1)}, {v(c[2])}, {s(PM1)}",
+              # n0 = hi1 ^ c1 ^ k0 ; n2 = hi0 ^ c3 ^ k1 ; c = (n0, lo1, n2, lo0)
+              f"v_xor_b32_e32 {v(c[0])}, {s(PK0)}, {v(hi1)}", f"v_xor_b32_e32 {v(c[0])}, {v(c[0])}, {v(c[1])}",
+              f"v_xor_b32_e32 {v(c[2])}, {s(PK1)}, {v(hi0)}", f"v_xor_b32_e32 {v(c[2])}, {v(c[2])}, {v(c[3])}",
+              f"v_mov_b32_e32 {v(c[1])}, {v(lo1)}", f"v_mov_b32_e32 {v(c[3])}, {v(lo0)}",
+              f"s_add_u32 {s(PK0)}, {s(PK0)}, 0x9E3779B9", f"s_add_u32 {s(PK1)}, {s(PK1)}, 0xBB67AE85")
+    g.label("Lphx_done_%=")
+    g(f"s_setpc_b64 {sr(PRET, 2)}")
+
+
+CLOBBERS = (", ".join(f'"v{i}"' for i in range(192)) + ", " + ", ".join(f'"s{i}"' for i in range(16, 96))
+            + ', "vcc", "scc", "m0", "memory"')
+
+
+def _inc(lines, macro):
+    out = [f"#define {macro} \\"]
+    for ln in lines:
+        out.append(f'  "{ln}\\n" \\')
+    out.append('  ""')
+    return out
+
+
+def render_interp() -> str:
+    """csrc/mw_asm_interp.inc: the interpreter body and the assembled kernels'
+    template body (csrc/mw_asmjit_shell.hip)."""
+    out = ["// GENERATED by tools/gen_asm_interp.py (mythril_amd/asmgen.py) -- do not edit",
+           "// (tests/test_asm_interp.py checks it is current).",
+           "// Threaded-dispatch interpreter core for mw_search_asm_kernel (mw_kernels.hip) and the",
+           "// template of the assembled kernels (mw_asmjit_shell.hip, mythril_amd/asmjit.py).",
+           "#pragma once",
+           f"#define MW_ASM_NOPS {len(ASM_OPCODES)}",
+           "#define MW_ASM_OPCODES " + ", ".join(f"MW_{n}" for n in ASM_OPCODES),
+           "#define MW_ASM_LEAF_KINDS " + ", ".join(str(k) for k in ASM_LEAF_KINDS)]
+    out += _inc(gen("interp"), "MW_ASM_BODY")
+    out += _inc(gen("template"), "MW_ASMJIT_TEMPLATE_BODY")
+    out.append(f"#define MW_ASM_CLOBBERS {CLOBBERS}")
+    return "\n".join(out) + "\n"
+
+
+# ======================================================== assembled kernels
+# An assembled kernel is the template (gen("template")) with the program in
+# place of MARKER: every instruction is its handler instantiated by StaticGen,
+# whose operand access is literal.  Register operands are named directly (no
+# s_set_gpr_idx), constants become instruction literals, widths and masks are
+# known (canonicalisation emits only the limbs it changes), and there is no
+# dispatch.  mythril_amd/asmjit.py assembles and loads the result.
+
+KBIT = isa.KBIT
+
+
+def _lit(x: int) -> str:
+    x &= 0xFFFFFFFF
+    return str(x) if x <= 64 else f"{x:#x}"
+
+
+class StaticGen(Gen):
+    """Gen for one program whose fields are known at generation time."""
+
+    def __init__(self, consts, leaves=None):
+        super().__init__()
+        self.consts = [int(x) for x in consts]
+        self.leaves = [int(x) for x in leaves] if leaves is not None else None
+        self.cur = {}
+        self.sval = {}          # SGPR -> value this instruction set by width() / nmask()
+        self.chain_open = False  # XR holds the acc of a W_CDINS chain
+        self.summary_b = None    # b field whose size summary XA holds (W_CDINS)
+        self.digit_spec = None   # pool digit spec whose digit T+6 holds
+
+    def L(self, base):          # distinct from the template's labels
+        self.n += 1
+        return f"LS{base}{self.n}_%="
+
+    def set_insn(self, words):
+        w0, w1, w2, w3 = (int(x) & 0xFFFFFFFF for x in words)
+        self.cur = {"op": w0 & 0xFF, "flags": (w0 >> 8) & 0xFF, "w": w0 >> 16, "dst": w1 & 0xFFFF,
+                    "a": w1 >> 16, "b": w2 & 0xFFFF, "c": w2 >> 16, "imm": w3}
+        self.sval = {}
+
+    def _field(self, f):
+        return self.cur[self.bound[f]]
+
+    def fetch_n(self, f, dst):
+        val = self._field(f)
+        if val & KBIT:
+            self(f"v_mov_b32_e32 {v(dst)}, {_lit(self.consts[val & 0x7FFF])}")
+        else:
+            self(f"v_mov_b32_e32 {v(dst)}, {v(N0 + val)}")
+
+    def fetch_w(self, f, dst):
+        val = self._field(f)
+        if val & KBIT:
+            o = val & 0x7FFF
+            for k in range(8):
+                self(f"v_mov_b32_e32 {v(dst + k)}, {_lit(self.consts[o + k])}")
+        else:
+            for k in range(8):
+                self(f"v_mov_b32_e32 {v(dst + k)}, {v(W0 + 8 * val + k)}")
+
+    def _dst(self):
+        w, n = isa.decode_dst(self.cur["dst"])
+        return w, n
+
+    def write_n(self, src):
+        _, n = self._dst()
+        self(f"v_mov_b32_e32 {v(N0 + n)}, {v(src)}")
+
+    def write_w(self, src):
+        w, _ = self._dst()
+        for k in range(8):
+            self(f"v_mov_b32_e32 {v(W0 + 8 * w + k)}, {v(src + k)}")
+
+    def width(self, dst):
+        self(f"s_mov_b32 {s(dst)}, {self.cur['w']}")
+        self.sval[dst] = self.cur["w"]
+
+    def nmask(self, w, dst):
+        if w in self.sval:
+            m = 0xFFFFFFFF if self.sval[w] >= 32 else (1 << self.sval[w]) - 1
+            self(f"s_mov_b32 {s(dst)}, {_lit(m)}")
+            self.sval[dst] = m
+        else:
+            super().nmask(w, dst)
+
+    def canon(self, base, w):
+        if w not in self.sval:
+            super().canon(base, w)
+            return
+        self._canon_static(base, self.sval[w])
+
+    def next(self):
+        pass
+
+    # the body sits after the template's code and may be longer than a
+    # branch reaches (simm16 words): it leaves through addresses the template
+    # computes once per block (gen("template"))
+    def stop_if_scc1(self):
+        lab = self.L("go")
+        self(f"s_cbranch_scc0 {lab}", f"s_setpc_b64 {sr(STOPADDR, 2)}")
+        self.label(lab)
+
+    def call_leaf_sub(self):
+        self(f"s_swappc_b64 {sr(LRET, 2)}, {sr(LEAFADDR, 2)}")
+
+    # ------------------------------------------------------------ leaves
+    def _narrow_random(self, lid, dst):
+        """v(dst) = fmix64(cand ^ seed ^ lid * 0xC2B2AE3D27D4EB4F) low word
+        (mw_leaf.h random_leaf, w <= 32); temporaries T..T+5, S[4], S[5], SX, PK*"""
+        k = (lid * 0xC2B2AE3D27D4EB4F) & ((1 << 64) - 1)
+        self(f"s_xor_b32 {s(PK0)}, {s(SEED)}, {_lit(k & 0xFFFFFFFF)}",
+             f"s_xor_b32 {s(PK1)}, {s(SEED + 1)}, {_lit(k >> 32)}",
+             f"v_xor_b32_e32 {v(T)}, {s(PK0)}, {v(CLO)}", f"v_xor_b32_e32 {v(T + 1)}, {s(PK1)}, {v(CHI)}")
+        fmix64(self, T, T + 1, T + 2, T + 3)
+        if dst != T:
+            self(f"v_mov_b32_e32 {v(dst)}, {v(T)}")
+
+    def _wide_random(self, w, lid):
+        """T..T+7 = Philox4x32-10 of the candidate (the Lphilox subroutine)"""
+        self(f"s_mov_b32 {s(DESC)}, {w}", f"s_mov_b32 {s(DESC + 2)}, {_lit(lid)}",
+             f"s_swappc_b64 {sr(PRET, 2)}, {sr(PHILOXADDR, 2)}")
+        self.digit_spec = None   # the subroutine uses T..T+7
+
+    def _bit(self, dst, pos, first):
+        src = CLO if pos < 32 else CHI
+        if first:
+            self(f"v_bfe_u32 {v(dst)}, {v(src)}, {pos & 31}, 1")
+        else:
+            self(f"v_bfe_u32 {v(T + 7)}, {v(src)}, {pos & 31}, 1")
+
+    def leaf_digit(self, li):
+        """T+6 = leaf li's pool digit (kept when the previous leaf's digit
+        spec is the same: T+6 survives the gather and the random draw)"""
+        w, kind, lid, shift, bits, poff, _, stride = self.leaves[8 * li: 8 * li + 8]
+        if kind not in (1, 2, 3):
+            return
+        dig = T + 6
+        spec = (kind, shift, bits, stride, lid if kind == 2 else None)
+        if spec == self.digit_spec:
+            pass
+        elif bits == 0:
+            self(f"v_mov_b32_e32 {v(dig)}, 0")
+        elif kind == 1:
+            if shift + bits <= 32:
+                self(f"v_bfe_u32 {v(dig)}, {v(CLO)}, {shift}, {bits}")
+            elif shift >= 32:
+                self(f"v_bfe_u32 {v(dig)}, {v(CHI)}, {shift - 32}, {bits}")
+            else:
+                self(f"v_lshrrev_b64 {vr(T + 4, 2)}, {shift}, {vr(CLO, 2)}",
+                     f"v_bfe_u32 {v(dig)}, {v(T + 4)}, 0, {bits}")
+        elif kind == 2:
+            k = (lid * 0x9E3779B97F4A7C15) & ((1 << 64) - 1)
+            self(f"v_xor_b32_e32 {v(T)}, {_lit(k & 0xFFFFFFFF)}, {v(CLO)}",
+                 f"v_xor_b32_e32 {v(T + 1)}, {_lit(k >> 32)}, {v(CHI)}")
+            fmix64(self, T, T + 1, T + 2, T + 3)
+            self(f"v_bfe_u32 {v(dig)}, {v(T)}, 0, {bits}")
+        else:
+            for b in range(bits):
+                pos = shift + b * stride
+                self._bit(dig, pos, b == 0)
+                if b:
+                    self(f"v_lshl_or_b32 {v(dig)}, {v(T + 7)}, {b}, {v(dig)}")
+        self.digit_spec = spec
+
+    def inline_leaf(self, li, limb0_only=False):
+        """XC..XC+7 = leaf li's candidate value, its descriptor folded in
+        (mw_leaf.h leaf_value; the asm interpreter's Lleaf subroutine).
+        limb0_only: a narrow leaf whose consumer reads XC alone (the upper
+        limbs are left as they are).  The pool digit stays in T+6 for the next
+        leaf with the same digit (the bytes of one calldata word share it)."""
+        L = self.leaves[8 * li: 8 * li + 8]
+        w, kind, lid, shift, bits, poff, _, stride = L
+        upper = not (limb0_only and w <= 32)
+        if kind not in (1, 2, 3):
+            if w <= 32:
+                self._narrow_random(lid, XC)
+                if upper:
+                    for k in range(1, 8):
+                        self(f"v_mov_b32_e32 {v(XC + k)}, 0")
+            else:
+                self._wide_random(w, lid)
+                for k in range(8):
+                    self(f"v_mov_b32_e32 {v(XC + k)}, {v(T + k)}")
+            self._canon_static(XC, w)
+            return
+        dig = T + 6
+        self.leaf_digit(li)
+        # pool entry in LDS at POOLB + 4 * poff
+        self(f"s_add_u32 {s(S[6])}, {s(POOLB)}, {_lit(4 * poff)}")
+        rnd = self.L("lr")
+        done = self.L("ld")
+        if w < 32:
+            self(f"v_lshl_add_u32 {v(T + 5)}, {v(dig)}, 2, {s(S[6])}", f"ds_read_b32 {v(XC)}, {v(T + 5)}")
+            if upper:
+                for k in range(1, 8):
+                    self(f"v_mov_b32_e32 {v(XC + k)}, 0")
+            # the random draw only when a lane's entry says RANDOM (bit 31): with
+            # interleaved digits most waves pick one entry for all their lanes
+            self("s_waitcnt lgkmcnt(0)", f"v_cmp_gt_i32_e32 vcc, 0, {v(XC)}", "s_nop 1",
+                 f"s_cbranch_vccz {done}", f"s_mov_b64 {sr(MSK, 2)}, vcc")
+            self._narrow_random(lid, T)
+            self(f"v_cndmask_b32_e64 {v(XC)}, {v(XC)}, {v(T)}, {sr(MSK, 2)}")
+        else:
+            self(f"v_mov_b32_e32 {v(T + 5)}, 36", f"v_mad_u32_u24 {v(T + 5)}, {v(dig)}, {v(T + 5)}, {s(S[6])}",
+                 f"ds_read_b32 {v(T + 4)}, {v(T + 5)}")
+            for k in range(4):
+                self(f"ds_read2_b32 {vr(XC + 2 * k, 2)}, {v(T + 5)} offset0:{1 + 2 * k} offset1:{2 + 2 * k}")
+            self("s_waitcnt lgkmcnt(0)", f"v_and_b32_e32 {v(T + 4)}, 1, {v(T + 4)}",
+                 f"v_cmp_ne_u32_e32 vcc, 0, {v(T + 4)}", "s_nop 1", f"s_cbranch_vccz {done}",
+                 f"s_mov_b64 {sr(MSK, 2)}, vcc")
+            self._wide_random(w, lid)
+            self("s_nop 1")
+            for k in range(8):
+                self(f"v_cndmask_b32_e64 {v(XC + k)}, {v(XC + k)}, {v(T + k)}, {sr(MSK, 2)}")
+        self.label(done)
+        del rnd
+        if upper:
+            self._canon_static(XC, w)
+        elif w < 32:
+            self(f"v_and_b32_e32 {v(XC)}, {_lit((1 << w) - 1)}, {v(XC)}")
+
+    def _canon_static(self, base, wv):
+        if wv >= 256:
+            return
+        q, r = wv >> 5, wv & 31
+        for k in range(q + (1 if r else 0), 8):
+            self(f"v_mov_b32_e32 {v(base + k)}, 0")
+        if r:
+            self(f"v_and_b32_e32 {v(base + q)}, {_lit((1 << r) - 1)}, {v(base + q)}")
+
+
+def _cdins_static(g):
+    """W_CDINS with literal operands (mw_interp.h MW_W_CDINS): acc | ((K[c] <s
+    size) ? leaf : 0) << off; a chained link leaves the word in XR for the next"""
+    cur = g.cur
+    if not g.chain_open:
+        g.field("a", S[0]), g.fetch_w(S[0], XR)
+    o = cur["c"] & 0x7FFF                      # validated: c is a constant
+    idx = g.consts[o:o + 8]
+    if not any(idx[1:]) and idx[0] < 0x4000:   # i <s size  <=>  i <u summary(size)
+        if g.summary_b != cur["b"]:
+            g.field("b", S[2]), g.fetch_w(S[2], XB)
+            g(f"v_or3_b32 {v(T)}, {v(XB + 1)}, {v(XB + 2)}, {v(XB + 3)}",
+              f"v_and_b32_e32 {v(T + 1)}, 0x7fffffff, {v(XB + 7)}",
+              f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 4)}, {v(XB + 5)}",
+              f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 6)}, {v(T + 1)}",
+              f"v_cmp_ne_u32_e32 vcc, 0, {v(T)}", "s_nop 1",
+              f"v_cndmask_b32_e64 {v(XA)}, {v(XB)}, -1, vcc",
+              f"v_cmp_gt_i32_e32 vcc, 0, {v(XB + 7)}", "s_nop 1",
+              f"v_cndmask_b32_e64 {v(XA)}, {v(XA)}, 0, vcc")
+            g.summary_b = cur["b"]
+        if idx[0] <= 64:
+            g(f"v_cmp_lt_u32_e64 {sr(MSK2, 2)}, {idx[0]}, {v(XA)}")
+        else:
+            g(f"s_mov_b32 {s(S[1])}, {idx[0]:#x}", f"v_cmp_lt_u32_e64 {sr(MSK2, 2)}, {s(S[1])}, {v(XA)}")
+    else:
+        g.summary_b = None
+        g.field("b", S[1]), g.fetch_w(S[1], XB)
+        g.field("c", S[2]), g.fetch_w(S[2], XA)
+        g(f"v_xor_b32_e32 {v(XA + 7)}, 0x80000000, {v(XA + 7)}", f"v_xor_b32_e32 {v(XB + 7)}, 0x80000000, {v(XB + 7)}")
+        g.sub_chain(XA, XB)
+        g(f"s_mov_b64 {sr(MSK2, 2)}, vcc")
+    skip = g.L("cdns")
+    g.leaf_digit(cur["imm"] & 0xFFFF)     # before the skip: T+6 then holds it either way
+    g("s_nop 1", f"s_cmp_eq_u64 {sr(MSK2, 2)}, 0", f"s_cbranch_scc1 {skip}")
+    g.inline_leaf(cur["imm"] & 0xFFFF, limb0_only=True)
+    g(f"v_cndmask_b32_e64 {v(T)}, 0, {v(XC)}, {sr(MSK2, 2)}")
+    off = cur["imm"] >> 16
+    q, bit = off >> 5, off & 31
+    g(f"v_lshl_or_b32 {v(XR + q)}, {v(T)}, {bit}, {v(XR + q)}")
+    if bit > 24 and q + 1 < 8:   # a byte straddling a limb boundary
+        g(f"v_lshrrev_b32_e32 {v(T)}, {32 - bit}, {v(T)}", f"v_or_b32_e32 {v(XR + q + 1)}, {v(T)}, {v(XR + q + 1)}")
+    g.label(skip)
+    g.width(S[2]), g.canon(XR, S[2])
+    if cur["flags"] & 1:          # MW_FLAG_CHAIN: the next W_CDINS reads XR as its acc
+        g.chain_open = True
+    else:
+        g.chain_open = False
+        g.write_w(XR)
+
+
+_IMM_REG = re.compile(rf"\bs{CUR + 3}\b")
+
+
+def static_body(code, consts, leaves, forward: bool = True) -> list:
+    """The straight-line body of an assembled kernel for a validated,
+    asm-eligible program (code: its instruction words, original encoding;
+    consts and leaves: its constant pool and leaf table)."""
+    g = StaticGen(consts, leaves)
+    names = {c: n for n, c in isa.OPCODES.items()}
+    words = [int(x) for x in code]
+    out = []
+    for i in range(0, len(words), 4):
+        insn = words[i:i + 4]
+        name = names[insn[0] & 0xFF]
+        if name == "END":
+            break
+        g.set_insn(insn)
+        g.lines = []
+        if name == "W_CDINS":
+            _cdins_static(g)
+        elif name in ("LEAF_W", "LEAF_N"):
+            g.chain_open = False
+            g.summary_b = None
+            g.inline_leaf(insn[3], limb0_only=name == "LEAF_N")
+            (g.write_w if name == "LEAF_W" else g.write_n)(XC)
+        else:
+            g.chain_open = False
+            g.summary_b = None
+            g.digit_spec = None
+            HANDLERS[name](g)
+        lines = g.lines
+        if any(_IMM_REG.search(ln) for ln in lines):   # the handler reads the immediate word
+            lines = [f"s_mov_b32 {s(CUR + 3)}, {_lit(insn[3])}"] + lines
+        out.append(f"; {i // 4}: {name}")
+        out.extend(lines)
+    out.append(f"s_setpc_b64 {sr(ENDADDR, 2)}")
+    return forward_copies(out) if forward else out
+
+
+# ------------------------------------------------ copy forwarding (static bodies)
+_VREG = re.compile(r"^v(\d+)$")
+_VRANGE = re.compile(r"^v\[(\d+):(\d+)\]$")
+TEMP_LO = XA   # v136..v191: operand, result and scratch registers; v0..v127 are the files
+
+
+def _operands(line: str):
+    parts = line.split(None, 1)
+    if len(parts) == 1:
+        return parts[0], []
+    return parts[0], [o.strip() for o in parts[1].split(",")]
+
+
+def _regs(tok: str):
+    """VGPR numbers an operand names (first word of the operand only)"""
+    t = tok.split()[0] if tok else ""
+    m = _VREG.match(t)
+    if m:
+        return [int(m.group(1))]
+    m = _VRANGE.match(t)
+    if m:
+        return list(range(int(m.group(1)), int(m.group(2)) + 1))
+    return []
+
+
+def forward_copies(lines):
+    """Peephole over a straight-line body: a read of a register that is a
+    plain copy (v_mov_b32 vD, vS) of another reads the source instead, and a
+    copy into a scratch register (>= v136) whose value is then overwritten
+    before any other read is dropped.  Conservative: labels, branches, calls
+    and register-indexing regions end every copy's scope, and multi-register
+    operands are never rewritten."""
+    out = list(lines)
+    dead = set()
+    alias = {}     # D -> S
+    pending = {}   # D -> index of the copy into scratch register D
+    indexed = False
+
+    def clobber(r):
+        if r in pending:
+            dead.add(pending.pop(r))
+        alias.pop(r, None)
+        for d in [d for d, src in alias.items() if src == r]:
+            del alias[d]
+            pending.pop(d, None)   # read later in its own name: keep that copy
+
+    for i, ln in enumerate(out):
+        if not ln or ln.startswith(";"):
+            continue
+        op, ops = _operands(ln)
+        if op == "s_set_gpr_idx_on":
+            indexed = True
+        barrier = (ln.endswith(":") or indexed or op.startswith(("s_cbranch", "s_branch", "s_setpc", "s_swappc",
+                                                                    "s_call", "s_set_gpr_idx")))
+        if op == "s_set_gpr_idx_off":
+            indexed = False
+        if barrier:
+            alias.clear()
+            pending.clear()
+            continue
+        if not op.startswith(("v_", "ds_", "global_", "buffer_")):
+            continue
+        if op.startswith(("ds_write", "global_store", "global_atomic", "buffer_store")):
+            dst_n, srcs = 0, ops
+        elif op.startswith("v_cmp"):
+            dst_n, srcs = 0, ops[1:]          # writes vcc / an SGPR pair
+        else:
+            dst_n, srcs = 1, ops[1:]
+        dsts = _regs(ops[0]) if dst_n and ops else []
+        new_srcs = []
+        for o in srcs:
+            rs = _regs(o)
+            if len(rs) == 1 and rs[0] in alias and o.split()[0] == f"v{rs[0]}":
+                o = o.replace(f"v{rs[0]}", f"v{alias[rs[0]]}", 1)
+            else:
+                for r in rs:                   # read in its own name: that copy stays
+                    pending.pop(r, None)
+            new_srcs.append(o)
+        if new_srcs != srcs:
+            ln = op + " " + ", ".join(([ops[0]] if dst_n or op.startswith("v_cmp") else []) + new_srcs)
+            out[i] = ln
+        for r in dsts:
+            clobber(r)
+        if op == "v_mov_b32_e32" and dsts and len(new_srcs) == 1:
+            s_regs = _regs(new_srcs[0])
+            d = dsts[0]
+            if len(s_regs) == 1 and new_srcs[0] == f"v{s_regs[0]}":
+                if s_regs[0] == d:
+                    dead.add(i)
+                else:
+                    alias[d] = s_regs[0]
+                    if d >= TEMP_LO:
+                        pending[d] = i
+    return [ln for i, ln in enumerate(out) if i not in dead]

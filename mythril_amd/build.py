@@ -3,6 +3,8 @@
   mythril_amd/lib/libmythril_witness.so   product: gfx950 kernels + C-ABI
   build/host/libmw_host_emu.so            test-only CPU build of the same interpreter
   oracle/build/liboracle.so               test-only C restatement (built by oracle/Makefile)
+  build/asmjit/template.s                 the assembled kernels' template (gfx950 assembly,
+                                          mythril_amd/asmjit.py fills in a program's body)
 
 Usage: python -m mythril_amd.build [--force]
 """
@@ -21,7 +23,9 @@ ARCH = os.environ.get("MW_OFFLOAD_ARCH", "gfx950")
 
 DEVICE_SRCS = ["mw_kernels.hip", "mw_validate.cpp"]
 HOST_SRCS = ["mw_host_emu.cpp", "mw_validate.cpp"]
-HEADERS = ["mw_isa.h", "mw_prog.h", "mw_alu.h", "mw_interp.h", "mw_leaf.h", "mw_keccak.h", "mw_asm_interp.inc"]
+HEADERS = ["mw_isa.h", "mw_prog.h", "mw_alu.h", "mw_interp.h", "mw_leaf.h", "mw_keccak.h", "mw_asm_interp.inc",
+           "mw_asm_abi.h"]
+ASMJIT_TEMPLATE = ROOT / "build" / "asmjit" / "template.s"
 
 
 def _hipcc() -> str:
@@ -66,6 +70,18 @@ def build_host_emu(force: bool = False) -> Path:
     return HOST_EMU
 
 
+def build_asmjit_template(force: bool = False) -> Path:
+    """hipcc compiles the assembled kernels' shell to gfx950 assembly once; the
+    runtime only assembles (mythril_amd/asmjit.py)."""
+    if force or _stale(ASMJIT_TEMPLATE, ["mw_asmjit_shell.hip"]):
+        ASMJIT_TEMPLATE.parent.mkdir(parents=True, exist_ok=True)
+        tmp = ASMJIT_TEMPLATE.with_suffix(".s.tmp")
+        _run([_hipcc(), f"--offload-arch={ARCH}", "--cuda-device-only", "-S", "-O3", "-std=c++17",
+              "-Wno-inline-asm", "-Wno-unused-command-line-argument", "mw_asmjit_shell.hip", "-o", tmp])
+        os.replace(tmp, ASMJIT_TEMPLATE)
+    return ASMJIT_TEMPLATE
+
+
 def build_oracle(force: bool = False) -> None:
     mk = ROOT / "oracle" / "Makefile"
     if mk.exists():
@@ -74,6 +90,7 @@ def build_oracle(force: bool = False) -> None:
 
 def build_all(force: bool = False) -> None:
     build_device(force)
+    build_asmjit_template(force)
     build_host_emu(force)
     build_oracle(force)
 

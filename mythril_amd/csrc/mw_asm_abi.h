@@ -1,0 +1,56 @@
+// mw_asm_abi.h — launch records and kernel body shared by the two asm engines:
+// the threaded-dispatch interpreter (mw_kernels.hip mw_search_asm_kernel) and
+// the assembled kernels (mw_asmjit_shell.hip, instantiated per program by
+// mythril_amd/asmjit.py).  The asm text reads both records at fixed offsets
+// (mythril_amd/asmgen.py gen(): "AsmArgs: ..." and "ProgDev: ...").
+#pragma once
+#include "mw_alu.h"
+
+namespace mw {
+
+struct ProgDev {
+  const u32* code;     // the asm interpreter reads its predecoded copy here
+  const u32* consts;
+  const u32* leaves;
+  const u32* pool;
+  u32 n_spill;
+  u32 npool;   // pool words (staged in LDS)
+  u32 n_insn;
+  u32 pad;
+};
+
+struct AsmArgs {
+  u64 seed, begin, end;
+  u32 flags, nlds, gstride, nchunks, gdx, pad;
+  u32* spillbuf;
+  u32* verdict;   // per-candidate verdicts at cand - begin (mg_eval_generated), or null
+};
+static_assert(sizeof(AsmArgs) == 64, "AsmArgs layout (mythril_amd/asmgen.py)");
+static_assert(sizeof(ProgDev) == 48, "ProgDev layout (mythril_amd/asmgen.py)");
+
+}  // namespace mw
+
+// Kernel body: stage the program's pool in LDS after the spill words (LDS: the
+// dynamic shared array), run ASMTEXT over this block's chunks (grid x: chunk
+// stride, grid y: program), add the evals to the launch counter (stripe 0).
+#define MW_ASM_KERNEL_BODY(ASMTEXT, LDS)                                                             \
+  const mw::ProgDev* P = progs + blockIdx.y;                                                         \
+  {                                                                                                  \
+    mw::u32* dst = LDS + nlds * 256u;                                                                \
+    const mw::u32 np = P->npool;                                                                     \
+    const mw::u32* src = P->pool;                                                                    \
+    for (mw::u32 i = threadIdx.x; i < np; i += 256u) dst[i] = src[i];                                \
+    __syncthreads();                                                                                 \
+  }                                                                                                  \
+  const mw::u64 gtid = ((mw::u64)blockIdx.y * gridDim.x + blockIdx.x) * 256u + threadIdx.x;         \
+  const mw::u32 goff = (mw::u32)(gtid * 4u);                                                         \
+  const mw::u32 tid = threadIdx.x;                                                                   \
+  const mw::u32 ch0 = blockIdx.x;                                                                    \
+  mw::u64* om = out_min + blockIdx.y;                                                                \
+  mw::u64 evals;                                                                                     \
+  asm volatile(ASMTEXT                                                                               \
+               : [evals] "=s"(evals)                                                                 \
+               : [args] "s"(args), [prog] "s"(P), [outmin] "s"(om), [ch0] "s"(ch0), [tid] "v"(tid), \
+                 [goff] "v"(goff)                                                                    \
+               : MW_ASM_CLOBBERS);                                                                   \
+  if ((threadIdx.x & 63u) == 0 && evals) atomicAdd((unsigned long long*)counter, (unsigned long long)evals);

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/mythril_witness.h"
+#include "mw_asm_abi.h"
 #include "mw_asm_interp.inc"
 #include "mw_interp.h"
 #include "mw_keccak.h"
@@ -34,17 +35,6 @@ extern "C" void mw_asm_predecode(const uint32_t* code, size_t nwords, const uint
 using namespace mw;
 
 namespace {
-
-struct ProgDev {
-  const u32* code;
-  const u32* consts;
-  const u32* leaves;
-  const u32* pool;
-  u32 n_spill;
-  u32 npool;   // pool words (LDS staging, mw_search_kernel)
-  u32 n_insn;  // instructions (the asm interpreter's dispatch budget)
-  u32 pad;
-};
 
 constexpr int kBlock = 256;
 constexpr int kNCounters = 5;  // counter words: evals, then DivCount fields x lanes
@@ -247,46 +237,18 @@ __global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __r
   }
 }
 
-// Threaded-dispatch interpreter (tools/gen_asm_interp.py -> mw_asm_interp.inc):
+// Threaded-dispatch interpreter (mythril_amd/asmgen.py -> mw_asm_interp.inc):
 // the same result protocol as mw_search_kernel, for programs whose opcodes and
 // leaf kinds all have an asm handler and whose pools are staged in LDS
 // (mg_prog.asm_ok, checked on load; the launch checks the LDS fit).  The asm
 // block runs the whole chunk loop of the block (one copy of the code: a loop
 // around it gets unswitched into several copies) and reads its launch
-// arguments from an AsmArgs record in device memory.
-struct AsmArgs {
-  u64 seed, begin, end;
-  u32 flags, nlds, gstride, nchunks, gdx, pad;
-  u32* spillbuf;
-  u32* verdict;   // per-candidate verdicts at cand - begin (mg_eval_generated), or null
-};
-static_assert(sizeof(AsmArgs) == 64, "AsmArgs layout (tools/gen_asm_interp.py)");
-static_assert(sizeof(ProgDev) == 48, "ProgDev layout (tools/gen_asm_interp.py)");
-
+// arguments from an AsmArgs record in device memory (mw_asm_abi.h).
 __global__ __launch_bounds__(kBlock, 2) void mw_search_asm_kernel(const ProgDev* __restrict__ progs,
                                                                 const AsmArgs* __restrict__ args,
                                                                 u64* __restrict__ out_min,
                                                                 u64* __restrict__ counter, u32 nlds) {
-  const ProgDev* P = progs + blockIdx.y;
-  {
-    u32* dst = lds_spill + nlds * kBlock;
-    const u32 np = P->npool;
-    const u32* src = P->pool;
-    for (u32 i = threadIdx.x; i < np; i += kBlock) dst[i] = src[i];
-    __syncthreads();
-  }
-  const u64 gtid = ((u64)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x;
-  const u32 goff = (u32)(gtid * 4u);
-  const u32 tid = threadIdx.x;
-  const u32 ch0 = blockIdx.x;
-  u64* om = out_min + blockIdx.y;
-  u64 evals;
-  asm volatile(MW_ASM_BODY
-               : [evals] "=s"(evals)
-               : [args] "s"(args), [prog] "s"(P), [outmin] "s"(om), [ch0] "s"(ch0), [tid] "v"(tid),
-                 [goff] "v"(goff)
-               : MW_ASM_CLOBBERS);
-  if ((threadIdx.x & 63u) == 0 && evals) atomicAdd((unsigned long long*)counter, (unsigned long long)evals);
+  MW_ASM_KERNEL_BODY(MW_ASM_BODY, lds_spill)
 }
 
 __global__ __launch_bounds__(kBlock, 2) void mw_eval_kernel(ProgDev P, const u32* __restrict__ in,
@@ -392,7 +354,8 @@ struct mg_ctx {
   size_t alive_cap = 0;
   ProgDev* d_progs = nullptr;
   size_t nprogs_cap = 0;
-  void* d_asmargs = nullptr;  // AsmArgs of the asm interpreter's launch
+  AsmArgs* d_asmargs = nullptr;  // AsmArgs records: [0] the asm interpreter's launch, [1..] assembled kernels'
+  size_t nasmargs_cap = 0;
   std::mutex mu;
 };
 
@@ -412,6 +375,10 @@ struct mg_prog {
     hipFunction_t fe = nullptr;  // early exit (optional)
   };
   std::vector<Part> parts;
+  // assembled kernel (mg_prog_attach_asm): the asm interpreter's launch
+  // records and grid, the program as straight-line code
+  hipModule_t amod = nullptr;
+  hipFunction_t afn = nullptr;
   bool jit_ready() const {
     if (parts.empty()) return false;
     for (const Part& q : parts)
@@ -422,6 +389,9 @@ struct mg_prog {
     for (Part& q : parts)
       if (q.mod) hipModuleUnload(q.mod);
     parts.clear();
+    if (amod) hipModuleUnload(amod);
+    amod = nullptr;
+    afn = nullptr;
   }
 };
 
@@ -518,6 +488,27 @@ void destroy_prog(mg_prog* p) {
   p->unload();
   if (p->d_buf) hipFree(p->d_buf);
   delete p;
+}
+
+int ensure_asmargs(mg_ctx* c, size_t n) {
+  if (n <= c->nasmargs_cap) return 0;
+  if (c->d_asmargs) HIPCHK(hipFree(c->d_asmargs));
+  c->d_asmargs = nullptr;
+  c->nasmargs_cap = 0;
+  HIPCHK(hipMalloc(&c->d_asmargs, n * sizeof(AsmArgs)));
+  c->nasmargs_cap = n;
+  return 0;
+}
+
+// One launch of a program's assembled kernel: the asm interpreter's grid (x:
+// chunk stride, one program) and records (mw_asm_abi.h); its LDS is a fixed
+// 80 KiB array in the kernel (mw_asmjit_shell.hip).
+int launch_assembled(mg_ctx* c, const mg_prog* p, u32 gx, const ProgDev* dprog, const AsmArgs* dargs, u64* dmin,
+                     u32 nlds) {
+  u64* ctr = c->d_counter;
+  void* args[] = {&dprog, &dargs, &dmin, &ctr, &nlds};
+  HIPCHK(hipModuleLaunchKernel(p->afn, gx, 1, 1, kBlock, 1, 1, 0, c->stream, args, nullptr));
+  return 0;
 }
 
 int ensure_spill(mg_ctx* c, size_t bytes) {
@@ -797,7 +788,44 @@ int mg_prog_engine(const mg_prog* p) {
   if (!prog_live(p)) return fail(MG_E_ARG, "mg_prog_engine: not a live program");
   if (p->jit_ready()) return 2;
   u32 nlds = 0;   // the engine mg_search gives this program alone (a pool too big for LDS: compiled)
-  return p->asm_ok && asm_enabled() && asm_lds_fit(p->dev.n_spill, p->dev.npool, &nlds) ? 1 : 0;
+  if (!p->asm_ok || !asm_enabled() || !asm_lds_fit(p->dev.n_spill, p->dev.npool, &nlds)) return 0;
+  return p->afn ? 3 : 1;
+}
+
+int mg_prog_attach_asm(mg_prog* p, const void* image, size_t size, const char* name) {
+  if (!p || !image || !size || !name) return fail(MG_E_ARG, "null argument");
+  if (std::strlen(name) > 200) return fail(MG_E_ARG, "kernel name too long");
+  if (!prog_live(p)) return fail(MG_E_ARG, "mg_prog_attach_asm: not a live program");
+  if (!p->asm_ok) return fail(MG_E_PROG, "mg_prog_attach_asm: the program has opcodes the asm engines lack");
+  mg_ctx* c = p->ctx;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIPCHK(hipSetDevice(c->dev));
+  hipModule_t mod = nullptr;
+  HIPCHK(hipModuleLoadData(&mod, image));
+  const std::string base(name);
+  hipDeviceptr_t dsig = nullptr;
+  size_t nsig = 0;
+  u64 sig = 0;
+  if (hipModuleGetGlobal(&dsig, &nsig, mod, (base + "_sig").c_str()) != hipSuccess || nsig != sizeof(u64) ||
+      hipMemcpyDtoH(&sig, dsig, sizeof(u64)) != hipSuccess) {
+    (void)hipGetLastError();
+    hipModuleUnload(mod);
+    return fail(MG_E_PROG, "code object has no program signature " + base + "_sig");
+  }
+  if (sig != p->sig) {
+    hipModuleUnload(mod);
+    return fail(MG_E_PROG, "code object was assembled for another program (signature mismatch)");
+  }
+  hipFunction_t fn = nullptr;
+  if (hipModuleGetFunction(&fn, mod, base.c_str()) != hipSuccess) {
+    (void)hipGetLastError();
+    hipModuleUnload(mod);
+    return fail(MG_E_PROG, "code object lacks kernel " + base);
+  }
+  if (p->amod) hipModuleUnload(p->amod);
+  p->amod = mod;
+  p->afn = fn;
+  return 0;
 }
 
 int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uint64_t begin,
@@ -822,12 +850,18 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   // the threaded-dispatch asm interpreter for the programs it handles, one of
   // the compiled interpreter for the others.  d_min holds the asm group, then
   // the compiled group, then the specialised programs.
-  std::vector<size_t> gasm, gcpp, special;
+  // Programs with an assembled kernel (mg_prog_attach_asm) get one launch each
+  // on the asm interpreter's records, after the interpreter groups.
+  std::vector<size_t> gasm, gcpp, gasb, special;
   u64 ops = 0;
   const bool use_asm = asm_enabled();
   for (size_t i = 0; i < nprog; ++i) {
     if (!progs[i] || progs[i]->ctx != c) return fail(MG_E_ARG, "program from another context");
+    u32 n1 = 0;
     if (progs[i]->jit_ready()) special.push_back(i);
+    else if (use_asm && progs[i]->afn && count < (1ull << 40) &&
+             asm_lds_fit(progs[i]->dev.n_spill, progs[i]->dev.npool, &n1))
+      gasb.push_back(i);
     else (use_asm && progs[i]->asm_ok ? gasm : gcpp).push_back(i);
     ops += progs[i]->ops_per_eval;
   }
@@ -853,11 +887,13 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   }
   std::vector<size_t> interp(gasm);
   interp.insert(interp.end(), gcpp.begin(), gcpp.end());
+  const size_t ni = interp.size();
+  interp.insert(interp.end(), gasb.begin(), gasb.end());   // d_progs / d_min: then the assembled ones
+  const size_t nia = interp.size();
   std::vector<ProgDev> hp;
-  for (size_t j = 0; j < interp.size(); ++j)   // the asm group reads the predecoded code
+  for (size_t j = 0; j < nia; ++j)   // the asm group reads the predecoded code
     hp.push_back(j < gasm.size() ? progs[interp[j]]->adev : progs[interp[j]]->dev);
   const u64 nchunks = (count + kBlock - 1) / kBlock;
-  const size_t ni = interp.size();
   struct Group {
     size_t first, n;
     u64 gx;
@@ -878,14 +914,35 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
     G.nlds = &G == &groups[0] ? asm_nlds : std::min(max_spill, kLdsSpillWords);
     spill_need = std::max(spill_need, (size_t)(max_spill - G.nlds) * nthreads * sizeof(u32));
   }
-  if (ni) {
+  // assembled kernels: records 1.. (one program, the whole chip each)
+  const u64 agx = std::min<u64>((u64)c->ncu * 8, nchunks);
+  std::vector<AsmArgs> ha(1 + gasb.size());
+  for (size_t k = 0; k < gasb.size(); ++k) {
+    const ProgDev& d = hp[ni + k];
+    AsmArgs& r = ha[1 + k];
+    (void)asm_lds_fit(d.n_spill, d.npool, &r.nlds);
+    r.seed = seed;
+    r.begin = begin;
+    r.end = begin + count;
+    r.flags = flags;
+    r.gstride = (u32)(agx * kBlock * 4);
+    r.nchunks = (u32)nchunks;
+    r.gdx = (u32)agx;
+    r.verdict = nullptr;
+    spill_need = std::max(spill_need, (size_t)(d.n_spill - r.nlds) * agx * kBlock * sizeof(u32));
+  }
+  if (nia) {
     rc = ensure_spill(c, spill_need);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(c->d_progs, hp.data(), ni * sizeof(ProgDev), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_progs, hp.data(), nia * sizeof(ProgDev), hipMemcpyHostToDevice, c->stream));
   }
-  AsmArgs aa{};
-  if (groups[0].n) {
-    if (!c->d_asmargs) HIPCHK(hipMalloc(&c->d_asmargs, sizeof(AsmArgs)));
+  for (size_t k = 0; k < gasb.size(); ++k) ha[1 + k].spillbuf = c->d_spill;
+  if (groups[0].n || !gasb.empty()) {
+    rc = ensure_asmargs(c, ha.size());
+    if (rc) return rc;
+  }
+  AsmArgs& aa = ha[0];
+  if (groups[0].n || !gasb.empty()) {
     aa.seed = seed;
     aa.begin = begin;
     aa.end = begin + count;
@@ -896,7 +953,7 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
     aa.gdx = (u32)groups[0].gx;
     aa.spillbuf = c->d_spill;
     aa.verdict = nullptr;
-    HIPCHK(hipMemcpyAsync(c->d_asmargs, &aa, sizeof(AsmArgs), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_asmargs, ha.data(), ha.size() * sizeof(AsmArgs), hipMemcpyHostToDevice, c->stream));
   }
   std::vector<u64> init(nprog, MG_NONE);
   HIPCHK(hipMemcpyAsync(c->d_min, init.data(), nprog * sizeof(u64), hipMemcpyHostToDevice, c->stream));
@@ -928,8 +985,13 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
                          c->stream, dp, seed, begin, count, flags, dm, c->d_counter, c->d_spill, G.nlds);
     HIPCHK(hipGetLastError());
   }
+  for (size_t k = 0; k < gasb.size(); ++k) {
+    rc = launch_assembled(c, progs[gasb[k]], (u32)agx, c->d_progs + ni + k, c->d_asmargs + 1 + k,
+                          c->d_min + ni + k, ha[1 + k].nlds);
+    if (rc) return rc;
+  }
   for (size_t j = 0; j < special.size(); ++j) {
-    rc = launch_jit(c, progs[special[j]], seed, begin, count, flags, c->d_min + ni + j, nullptr);
+    rc = launch_jit(c, progs[special[j]], seed, begin, count, flags, c->d_min + nia + j, nullptr);
     if (rc) return rc;
   }
   HIPCHK(hipEventRecord(c->e1, c->stream));
@@ -943,15 +1005,15 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   for (size_t sidx = 0; sidx <= MW_CTR_STRIPES; ++sidx)
     for (int k = 0; k < kNCounters; ++k) ctr[k] += stripes[sidx * MW_CTR_STRIPE_WORDS + k];
   const u64 evals = ctr[0];
-  for (size_t j = 0; j < ni; ++j) out_min_idx[interp[j]] = mins[j];
-  for (size_t j = 0; j < special.size(); ++j) out_min_idx[special[j]] = mins[ni + j];
+  for (size_t j = 0; j < nia; ++j) out_min_idx[interp[j]] = mins[j];
+  for (size_t j = 0; j < special.size(); ++j) out_min_idx[special[j]] = mins[nia + j];
   if (st) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
     st->kernel_ms = ms;
     st->wall_ms = now_ms() - t0;
     st->evals = evals;  // summed over every program's blocks
-    st->launches = (groups[0].n ? 1 : 0) + (groups[1].n ? 1 : 0) + special.size();
+    st->launches = (groups[0].n ? 1 : 0) + (groups[1].n ? 1 : 0) + gasb.size() + special.size();
     st->ops = (double)evals / (double)nprog * (double)ops;
     st->lane_div_steps = ctr[1];
     st->lane_div_full = ctr[2];
@@ -1014,6 +1076,7 @@ int mg_eval(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncan
 // with a verdict array); 1 = not applicable (the caller uses mw_eval_kernel).
 static int eval_asm(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, size_t count, uint32_t* verdict) {
   if (!asm_enabled() || !p->asm_ok || begin + count < begin || count >= (1ull << 40)) return 1;
+  const bool assembled = p->afn != nullptr;   // its assembled kernel, else the asm interpreter
   u32 nlds = 0;
   if (!asm_lds_fit(p->dev.n_spill, p->dev.npool, &nlds)) return 1;
   const size_t lds = (size_t)nlds * kBlock * 4 + (size_t)p->dev.npool * 4;
@@ -1026,7 +1089,8 @@ static int eval_asm(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, 
   const u64 gx = std::min<u64>(nchunks, (u64)c->ncu * 8);
   rc = ensure_spill(c, std::max<size_t>(4, (size_t)(p->dev.n_spill - nlds) * gx * kBlock * sizeof(u32)));
   if (rc) return rc;
-  if (!c->d_asmargs) HIPCHK(hipMalloc(&c->d_asmargs, sizeof(AsmArgs)));
+  rc = ensure_asmargs(c, 1);
+  if (rc) return rc;
   u32* d_v = nullptr;
   if (hipMalloc(&d_v, count * 4) != hipSuccess) return fail(MG_E_NOMEM, "eval verdict alloc");
   AsmArgs aa{};
@@ -1041,11 +1105,17 @@ static int eval_asm(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, 
   aa.spillbuf = c->d_spill;
   aa.verdict = d_v;
   const u64 none = MG_NONE;
-  hipError_t e = hipMemcpyAsync(c->d_progs, &p->adev, sizeof(ProgDev), hipMemcpyHostToDevice, c->stream);
+  hipError_t e = hipMemcpyAsync(c->d_progs, assembled ? &p->dev : &p->adev, sizeof(ProgDev), hipMemcpyHostToDevice,
+                                c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_min, &none, sizeof(u64), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_asmargs, &aa, sizeof(AsmArgs), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, kCounterWords * sizeof(u64), c->stream);
-  if (e == hipSuccess) {
+  if (e == hipSuccess && assembled) {
+    if (launch_assembled(c, p, (u32)gx, c->d_progs, c->d_asmargs, c->d_min, nlds)) {
+      hipFree(d_v);
+      return MG_E_HIP;
+    }
+  } else if (e == hipSuccess) {
     hipLaunchKernelGGL(mw_search_asm_kernel, dim3((u32)gx, 1u), dim3(kBlock), lds, c->stream, c->d_progs,
                        (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, nlds);
     e = hipGetLastError();
@@ -1053,7 +1123,9 @@ static int eval_asm(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, 
   if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, count * 4, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   hipFree(d_v);
-  if (e != hipSuccess) return fail(MG_E_HIP, std::string("eval (asm interpreter): ") + hipGetErrorString(e));
+  if (e != hipSuccess)
+    return fail(MG_E_HIP, std::string(assembled ? "eval (assembled kernel): " : "eval (asm interpreter): ") +
+                              hipGetErrorString(e));
   return 0;
 }
 

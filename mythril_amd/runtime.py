@@ -65,6 +65,7 @@ SIGNATURES = {
     "mg_prog_load": (ctypes.c_int, [_P, ctypes.POINTER(MgProgDesc), ctypes.POINTER(_P)]),
     "mg_prog_free": (ctypes.c_int, [_P]),
     "mg_prog_attach_kernel": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
+    "mg_prog_attach_asm": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]),
     "mg_prog_has_kernel": (ctypes.c_int, [_P]),
     "mg_prog_engine": (ctypes.c_int, [_P]),
     "mg_search": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
@@ -132,6 +133,7 @@ class DeviceProgram:
         self.handle = handle
         self.prog = prog
         self.kernel: Optional[str] = None   # specialised kernel name, if attached
+        self.assembled: Optional[str] = None  # assembled kernel name (mythril_amd.asmjit), if attached
 
     def free(self):
         # a program never outlives its context: Device.close() frees the
@@ -186,10 +188,16 @@ class Device:
                "mg_prog_attach_kernel")
         dp.kernel = name
 
+    def attach_asm(self, dp: DeviceProgram, image: bytes, name: str) -> None:
+        """Bind an assembled code object (mythril_amd.asmjit) to a loaded program."""
+        _check(self.lib, self.lib.mg_prog_attach_asm(dp.handle, image, len(image), name.encode()),
+               "mg_prog_attach_asm")
+        dp.assembled = name
+
     def has_kernel(self, dp: DeviceProgram) -> bool:
         return bool(self.lib.mg_prog_has_kernel(dp.handle))
 
-    ENGINES = ("interp", "asm", "jit")
+    ENGINES = ("interp", "asm", "jit", "asmjit")
 
     def engine_of(self, dp: DeviceProgram) -> str:
         """Which kernel searches this program (mg_prog_engine)."""

@@ -1,0 +1,147 @@
+"""Assembled kernels (mythril_amd/asmjit.py) on gfx950: the asm interpreter's
+handlers instantiated per program as straight-line code.  Verdicts and search
+results must equal the asm interpreter's (same program, no kernel attached)
+and the oracle's:
+
+* random DAGs over every opcode the asm engines handle, Philox and pooled
+  leaves, widths 1..256;
+* every corpus program (C2-C4 solver-log queries; the LASER corpus: W_CDINS
+  chains, keccak UFs, congruence conjuncts; C3's global spill words);
+* batched searches in every mode, witnesses in every wave.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from mythril_amd import asmjit, isa
+from mythril_amd.compiler import compile_program
+from mythril_amd.engine import DEFAULT_SEED, prepare
+from mythril_amd.ir import Ctx
+from oracle import cdag
+from tests.test_gpu_asm import _corpus, _random_supported_dag
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from mythril_amd.runtime import Device
+    if not asmjit.available():
+        pytest.fail("assembled kernels unavailable (build/asmjit/template.s or llvm-mc missing)")
+    d = Device(0)
+    yield d
+    d.close()
+
+
+def pair(dev, p):
+    """(interpreter handle, assembled handle) of one program"""
+    di = dev.load(p)
+    da = dev.load(p)
+    asmjit.attach(dev, da)
+    assert dev.engine_of(di) == "asm" and dev.engine_of(da) == "asmjit"
+    return di, da
+
+
+def test_asmjit_00_smoke(dev):
+    """One small program first (a hang here stops the run early)."""
+    c = Ctx()
+    x, y = c.var("x", 256), c.var("y", 8)
+    conj = [c.app("bvult", x, c.const(1 << 255, 256)), c.app("bvugt", y, c.const(9, 8))]
+    p = compile_program(conj)
+    di, da = pair(dev, p)
+    try:
+        va, _ = dev.eval_generated(da, 7, 0, 1 << 12, trace=False)
+        vi, _ = dev.eval_generated(di, 7, 0, 1 << 12, trace=False)
+    finally:
+        di.free()
+        da.free()
+    _, _, vo = cdag.evaluate(conj, 7, 0, 1 << 12, want_verdict=True)
+    assert np.array_equal(va.astype(np.uint8), vo)
+    assert np.array_equal(va, vi)
+    assert 0 < int(va.sum()) < len(va)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_asmjit_random_dags(dev, seed):
+    c, conj = _random_supported_dag(9000 + seed)
+    for pools in (False, True):
+        q = prepare(conj, c, use_pools=pools)
+        p = q.program
+        if not isa.asm_eligible(p.code, p.leaves):
+            pytest.skip("lowered outside the asm opcode set")
+        n = 1 << 12
+        di, da = pair(dev, p)
+        try:
+            va, _ = dev.eval_generated(da, DEFAULT_SEED + seed, 1 << 20, n, trace=False)
+            vi, _ = dev.eval_generated(di, DEFAULT_SEED + seed, 1 << 20, n, trace=False)
+        finally:
+            di.free()
+            da.free()
+        assert np.array_equal(va, vi), (seed, pools, int(np.count_nonzero(va != vi)))
+        _, _, vo = cdag.evaluate(q.lowered.conjuncts, DEFAULT_SEED + seed, 1 << 20, n, want_verdict=True,
+                                 specs=cdag.program_specs(p) if pools else None)
+        assert np.array_equal(va.astype(np.uint8), vo), (seed, pools)
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    from mythril_amd.smt2 import parse_file
+    out = []
+    for f in _corpus():
+        s = parse_file(f)
+        out.append((os.path.basename(f), prepare(s.asserts, s.ctx)))
+    return out
+
+
+def test_asmjit_corpus_verdicts(dev, corpus):
+    n = 1 << 14
+    for name, q in corpus:
+        di, da = pair(dev, q.program)
+        try:
+            va, _ = dev.eval_generated(da, DEFAULT_SEED, 0, n, trace=False)
+            vi, _ = dev.eval_generated(di, DEFAULT_SEED, 0, n, trace=False)
+        finally:
+            di.free()
+            da.free()
+        assert np.array_equal(va, vi), (name, int(np.count_nonzero(va != vi)))
+
+
+def test_asmjit_corpus_search_modes(dev, corpus):
+    """Batched: assembled programs launch one by one beside the interpreter
+    group; the lowest witness per program matches the interpreter's in every
+    search mode."""
+    sub = corpus[:24]
+    dis = [dev.load(q.program) for _, q in sub]
+    das = [dev.load(q.program) for _, q in sub]
+    for da in das:
+        asmjit.attach(dev, da)
+    try:
+        for flags in (0, isa.FLAG_EARLY_EXIT, isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT):
+            fi, sti = dev.search(dis, DEFAULT_SEED, 0, 1 << 16, flags)
+            fa, sta = dev.search(das, DEFAULT_SEED, 0, 1 << 16, flags)
+            assert fa == fi, flags
+            if flags == 0:
+                assert sta["evals"] == sti["evals"] == len(sub) << 16
+            # mixed: half assembled, half interpreted, in one call
+            fm, _ = dev.search(das[::2] + dis[1::2], DEFAULT_SEED, 0, 1 << 16, flags)
+            assert fm == fi[::2] + fi[1::2], flags
+    finally:
+        for d in dis + das:
+            d.free()
+
+
+@pytest.mark.parametrize("k", range(4))
+def test_asmjit_reports_the_satisfying_lane(dev, k):
+    c = Ctx()
+    x = c.var(f"x{k}", 8)
+    p = compile_program([c.app("=", x, c.const(37 * k + 11, 8))])
+    di, da = pair(dev, p)
+    try:
+        for flags in (0, isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT):
+            (fa,), _ = dev.search([da], 3 + k, 1000 * k, 1 << 16, flags)
+            (fi,), _ = dev.search([di], 3 + k, 1000 * k, 1 << 16, flags)
+            assert fa == fi and fa is not None
+    finally:
+        di.free()
+        da.free()

@@ -105,11 +105,17 @@ def main():
                 first = [x if x is not None else y for x, y in zip(first, found)]
                 pos += SLICE
             ttfw = time.perf_counter() - t0
-            for engine in (["asm", "interp"] if a.no_jit else ["asm", "interp", "jit"]):
+            for engine in (["asm", "asmjit", "interp"] if a.no_jit else ["asm", "asmjit", "interp", "jit"]):
                 compile_s = None
                 # asm: the threaded-dispatch interpreter (the default for these
-                # programs); interp: the compiled interpreter (MYTHRIL_AMD_ASM=0)
+                # programs); asmjit: each program's assembled kernel
+                # (mythril_amd/asmjit.py, attached here, assembly time reported);
+                # interp: the compiled interpreter (MYTHRIL_AMD_ASM=0, which also
+                # turns the assembled kernels off); jit: hipcc's specialised kernel
                 os.environ["MYTHRIL_AMD_ASM"] = "0" if engine == "interp" else "1"
+                if engine == "asmjit":
+                    from mythril_amd import asmjit
+                    compile_s = sum(asmjit.attach(dev, dp, cache=False) for dp in dps)
                 if engine == "jit":
                     compile_s = jit.attach(dev, dps, variants="xe", waves=2, lds_leaves=0)
                 ran = sorted({dev.engine_of(dp) for dp in dps})

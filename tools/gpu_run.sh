@@ -18,6 +18,7 @@
 #   keccak         tools/keccak_bench.py
 #   ipmc=FILE      PMC passes on one exhaustive interpreter launch of FILE (tools/interp_once.py)
 #   jpmc=FILE      the same on FILE's cached specialised kernel
+#   apmc=FILE      the same on FILE's assembled kernel (mythril_amd/asmjit.py)
 #   opcost         tools/interp_opcost.py (+ one PMC pass: instructions per bytecode op)
 #   ablate         tools/leaf_ablate.py --run (candidate-generation ablations, C2/C2L/C4)
 #   recip          tools/exp/recip_check (device reciprocal vs u64 division; built by hand)
@@ -91,11 +92,12 @@ for step in "$@"; do
     keccak)
       run 300 "$OUT/keccak.log" python3 tools/keccak_bench.py
       tail -8 "$OUT/keccak.log" ;;
-    ipmc=*|jpmc=*)
+    ipmc=*|jpmc=*|apmc=*)
       F=${step#*=}
       J=()
       P=${step%%=*}
       [ "$P" = jpmc ] && J=(--jit)
+      [ "$P" = apmc ] && J=(--asmjit)
       i=0
       for set in "SQ_WAVES,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_SCA" \
                  "SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_SMEM,SQ_INSTS_LDS,SQ_INSTS_BRANCH,SQ_INSTS_VMEM,SQ_INST_CYCLES_SALU,SQ_INSTS_FLAT" \
