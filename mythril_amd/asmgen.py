@@ -90,6 +90,7 @@ EXECSV = 34       # s[34:35]
 VALID = 36        # s[36:37] valid lanes of the chunk
 ARGP = 36         # s[36:37] AsmArgs (prologue only; then VALID)
 PROGP = 38        # s[38:39] ProgDev (prologue only)
+HIT = 38          # after the prologue: this wave has reported a witness (chunks only grow)
 TID, LO_SREG = 165, 0
 
 NTAB = 128
@@ -803,7 +804,7 @@ def gen(mode="interp"):
       f"s_mov_b64 {sr(LEAVES, 2)}, {sr(DESC + 4, 2)}",
       f"s_lshl_b32 {s(POOLB)}, {s(NLDS)}, 10",
       f"s_mov_b32 {s(PM0)}, 0xD2511F53", f"s_mov_b32 {s(PM1)}, 0xCD9E8D57",
-      f"s_mov_b64 {sr(EVALS, 2)}, 0",
+      f"s_mov_b64 {sr(EVALS, 2)}, 0", f"s_mov_b32 {s(HIT)}, 0",
       f"v_lshlrev_b32_e32 {v(LDSOFF)}, 2, {v(T)}", f"v_mov_b32_e32 {v(TID)}, {v(T)}")
     if mode == "interp":
         # the dispatch table's address (s_getpc_b64 gives the next instruction's)
@@ -878,12 +879,16 @@ def gen(mode="interp"):
       f"s_mov_b64 exec, {sr(EXECSV, 2)}")
     g.label("Lnoverd_%=")
     g(f"s_cmp_eq_u64 {sr(MSK, 2)}, 0", "s_cbranch_scc1 Lnohit_%=",
+      # a wave that has reported a witness never reports again: its later
+      # chunks hold only larger indices (one contended atomic per wave, not
+      # one per satisfied chunk: dense programs queued them on one address)
+      f"s_cmp_lg_u32 {s(HIT)}, 0", "s_cbranch_scc1 Lnohit_%=",
       # the wave's lowest satisfying lane issues the atomic with its own candidate index
       f"s_ff1_i32_b64 {s(SX)}, {sr(MSK, 2)}", f"s_lshl_b64 {sr(JMP, 2)}, 1, {s(SX)}",
       f"s_mov_b64 {sr(EXECSV, 2)}, exec", f"s_mov_b64 exec, {sr(JMP, 2)}",
       f"v_mov_b32_e32 {v(T + 2)}, 0",
       f"global_atomic_umin_x2 {v(T + 2)}, {vr(CLO, 2)}, {sr(OUTMIN, 2)}",
-      f"s_mov_b64 exec, {sr(EXECSV, 2)}")
+      f"s_mov_b64 exec, {sr(EXECSV, 2)}", f"s_mov_b32 {s(HIT)}, 1")
     g.label("Lnohit_%=")
     g(f"s_add_u32 {s(CH)}, {s(CH)}, {s(GDX)}", "s_branch Lchunk_%=")
     # ------------------------------------------------------ subroutines
@@ -1343,6 +1348,88 @@ def _cdins_static(g):
 _IMM_REG = re.compile(rf"\bs{CUR + 3}\b")
 
 
+CDINS_BATCH = 8   # gathers in flight per batch (XB..XB+7 addresses, XC..XC+7 values)
+
+
+def _batchable(g, insn) -> bool:
+    """A W_CDINS link the batched emission handles: a small immediate index
+    and a pooled narrow leaf."""
+    o = (insn[2] >> 16) & 0x7FFF
+    idx = g.consts[o:o + 8]
+    L = g.leaves[8 * (insn[3] & 0xFFFF): 8 * (insn[3] & 0xFFFF) + 8]
+    return (not any(idx[1:]) and idx[0] < 0x4000 and L[0] < 32 and L[1] in (1, 2, 3))
+
+
+def _cdins_chain_static(g, links):
+    """A chain of W_CDINS links (MW_FLAG_CHAIN on all but the last) building one
+    word, emitted as batches: every link's pool gather issued before one wait,
+    then the random draws (only when some lane's entry says RANDOM), the range
+    selects and the inserts.  The per-link form waits for each gather and each
+    branch condition in turn (latency-bound)."""
+    g.set_insn(links[0])
+    g.field("a", S[0]), g.fetch_w(S[0], XR)
+    for start in range(0, len(links), CDINS_BATCH):
+        batch = links[start:start + CDINS_BATCH]
+        for k, insn in enumerate(batch):
+            g.set_insn(insn)
+            if g.summary_b != g.cur["b"]:     # size summary (mw: i <s size <=> i <u XA)
+                g.field("b", S[2]), g.fetch_w(S[2], XB)
+                g(f"v_or3_b32 {v(T)}, {v(XB + 1)}, {v(XB + 2)}, {v(XB + 3)}",
+                  f"v_and_b32_e32 {v(T + 1)}, 0x7fffffff, {v(XB + 7)}",
+                  f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 4)}, {v(XB + 5)}",
+                  f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 6)}, {v(T + 1)}",
+                  f"v_cmp_ne_u32_e32 vcc, 0, {v(T)}", "s_nop 1",
+                  f"v_cndmask_b32_e64 {v(XA)}, {v(XB)}, -1, vcc",
+                  f"v_cmp_gt_i32_e32 vcc, 0, {v(XB + 7)}", "s_nop 1",
+                  f"v_cndmask_b32_e64 {v(XA)}, {v(XA)}, 0, vcc")
+                g.summary_b = g.cur["b"]
+        for k, insn in enumerate(batch):      # addresses and gathers
+            li = insn[3] & 0xFFFF
+            g.leaf_digit(li)
+            poff = g.leaves[8 * li + 5]
+            g(f"s_add_u32 {s(S[6])}, {s(POOLB)}, {_lit(4 * poff)}",
+              f"v_lshl_add_u32 {v(XB + k)}, {v(T + 6)}, 2, {s(S[6])}", f"ds_read_b32 {v(XC + k)}, {v(XB + k)}")
+        g("s_waitcnt lgkmcnt(0)")
+        # random draws: only when some lane's entry in the batch says RANDOM (bit 31)
+        done = g.L("cbr")
+        n = len(batch)
+        acc = [XC + k for k in range(n)]
+        g(f"v_or_b32_e32 {v(XB)}, {v(acc[0])}, {v(acc[0])}")
+        for k in range(1, n):
+            g(f"v_or_b32_e32 {v(XB)}, {v(XB)}, {v(acc[k])}")
+        g(f"v_cmp_gt_i32_e32 vcc, 0, {v(XB)}", "s_nop 1", f"s_cbranch_vccz {done}")
+        for k, insn in enumerate(batch):
+            lid = g.leaves[8 * (insn[3] & 0xFFFF) + 2]
+            g(f"v_cmp_gt_i32_e64 {sr(MSK, 2)}, 0, {v(XC + k)}")
+            g._narrow_random(lid, T)
+            g(f"v_cndmask_b32_e64 {v(XC + k)}, {v(XC + k)}, {v(T)}, {sr(MSK, 2)}")
+        g.label(done)
+        for k, insn in enumerate(batch):      # mask, range select, insert
+            g.set_insn(insn)
+            li = insn[3] & 0xFFFF
+            w = g.leaves[8 * li]
+            i = g.consts[(insn[2] >> 16) & 0x7FFF]
+            g(f"v_and_b32_e32 {v(XC + k)}, {_lit((1 << w) - 1)}, {v(XC + k)}")
+            if i <= 64:
+                g(f"v_cmp_lt_u32_e64 {sr(MSK2, 2)}, {i}, {v(XA)}")
+            else:
+                g(f"s_mov_b32 {s(S[1])}, {i:#x}", f"v_cmp_lt_u32_e64 {sr(MSK2, 2)}, {s(S[1])}, {v(XA)}")
+            g("s_nop 1", f"v_cndmask_b32_e64 {v(T)}, 0, {v(XC + k)}, {sr(MSK2, 2)}")
+            off = insn[3] >> 16
+            q, bit = off >> 5, off & 31
+            g(f"v_lshl_or_b32 {v(XR + q)}, {v(T)}, {bit}, {v(XR + q)}")
+            if bit > 24 and q + 1 < 8:
+                g(f"v_lshrrev_b32_e32 {v(T)}, {32 - bit}, {v(T)}",
+                  f"v_or_b32_e32 {v(XR + q + 1)}, {v(T)}, {v(XR + q + 1)}")
+            w_word = g.cur["w"]
+            if w_word < 256 and g.cur["flags"] & 1:   # a chained link canonicalises its word
+                g._canon_static(XR, w_word)
+    g.set_insn(links[-1])
+    g._canon_static(XR, g.cur["w"])
+    g.chain_open = False
+    g.write_w(XR)
+
+
 def static_body(code, consts, leaves, forward: bool = True) -> list:
     """The straight-line body of an assembled kernel for a validated,
     asm-eligible program (code: its instruction words, original encoding;
@@ -1351,14 +1438,36 @@ def static_body(code, consts, leaves, forward: bool = True) -> list:
     names = {c: n for n, c in isa.OPCODES.items()}
     words = [int(x) for x in code]
     out = []
+    cdins = isa.OPCODES["W_CDINS"]
+    skip_to = 0
     for i in range(0, len(words), 4):
+        if i < skip_to:
+            continue
         insn = words[i:i + 4]
         name = names[insn[0] & 0xFF]
         if name == "END":
             break
         g.set_insn(insn)
         g.lines = []
-        if name == "W_CDINS":
+        if name == "W_CDINS" and not g.chain_open:
+            # a whole chain, batched, when every link qualifies
+            j = i
+            links = []
+            while True:
+                ln_ = words[j:j + 4]
+                links.append(ln_)
+                if not ((ln_[0] >> 8) & 1) or j + 4 >= len(words) or (words[j + 4] & 0xFF) != cdins:
+                    break
+                j += 4
+            if (len(links) > 1 and all(_batchable(g, x) for x in links) and not ((links[-1][0] >> 8) & 1)
+                    and len({x[2] & 0xFFFF for x in links}) == 1):   # one size operand: one summary
+                _cdins_chain_static(g, links)
+                skip_to = j + 4
+                name = f"W_CDINS x{len(links)}"
+            else:
+                g.set_insn(insn)
+                _cdins_static(g)
+        elif name == "W_CDINS":
             _cdins_static(g)
         elif name in ("LEAF_W", "LEAF_N"):
             g.chain_open = False

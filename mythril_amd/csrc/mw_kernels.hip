@@ -205,6 +205,7 @@ __global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __r
   const u64 gtid = ((u64)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x;
   const u32 lane = threadIdx.x & 63u;
   u64 evals = 0, lsteps = 0, lfull = 0, lshort = 0, lgen = 0;   // division paths x lanes
+  bool reported = false;   // this wave's later chunks hold only larger indices
   for (u64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const u64 base = begin + ch * kBlock;
     if (flags & MW_FLAG_STOP_AFTER_HIT) {
@@ -216,10 +217,11 @@ __global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __r
     SearchEnv<POOL_LDS> env{P.leaves, P.pool, seed, cand, spillbuf, nthreads, gtid, nlds};
     const bool ok = mw_run(P.code, P.consts, env, valid, flags);
     const u64 hit = __ballot(ok);
-    if (hit) {
+    if (hit && !reported) {
       const u32 first = (u32)__ffsll((unsigned long long)hit) - 1u;
       if (lane == first && cand < __hip_atomic_load(&out_min[blockIdx.y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
         atomicMin((unsigned long long*)&out_min[blockIdx.y], (unsigned long long)cand);
+      reported = true;
     }
     const u64 nvalid = (u64)__popcll(__ballot(valid));
     evals += nvalid;
