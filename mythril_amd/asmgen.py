@@ -1430,7 +1430,118 @@ def _cdins_chain_static(g, links):
     g.write_w(XR)
 
 
-def static_body(code, consts, leaves, forward: bool = True) -> list:
+CHECK_OPS = ("CHECK", "CHECK_IMP", "CHECK_IMPEQ")
+ACC = JMP   # s[92:93]: a check run's lane mask (free in a static body)
+
+
+def _nsrc(g, f):
+    """an N operand as a VOPC src0: its register, or its constant as a literal"""
+    if f & KBIT:
+        return _lit(g.consts[f & 0x7FFF])
+    return v(N0 + f)
+
+
+def _nreg(g, f, tmp):
+    """an N operand in a VGPR (constants moved into tmp)"""
+    if f & KBIT:
+        g(f"v_mov_b32_e32 {v(tmp)}, {_lit(g.consts[f & 0x7FFF])}")
+        return v(tmp)
+    return v(N0 + f)
+
+
+def _check_run_static(g, run):
+    """A run of CHECK / CHECK_IMP / CHECK_IMPEQ as one lane mask: each check's
+    condition is formed in SGPRs (premise false OR consequence), ANDed into
+    ACC, and ALIVE and the early-exit test are updated once at the end of the
+    run.  The SALU combine of check k is emitted after check k+1's compares,
+    so no VALU-written SGPR is read by the next instruction."""
+    g(f"s_mov_b64 {sr(ACC, 2)}, -1")
+    pending = None
+    for insn in run:
+        g.set_insn(insn)
+        op = insn[0] & 0xFF
+        a, b, c = g.cur["a"], g.cur["b"], g.cur["c"]
+        m = MSK if pending != MSK else MSK2           # alternate the mask pairs
+        if op == isa.OPCODES["CHECK"]:
+            g(f"v_cmp_ne_u32_e64 {sr(m, 2)}, 0, {_nreg(g, a, T)}")
+            combine = [f"s_and_b64 {sr(ACC, 2)}, {sr(ACC, 2)}, {sr(m, 2)}"]
+        else:
+            g(f"v_cmp_eq_u32_e64 {sr(m, 2)}, 0, {_nreg(g, a, T)}")
+            if op == isa.OPCODES["CHECK_IMP"]:
+                g(f"v_cmp_ne_u32_e32 vcc, 0, {_nreg(g, b, T + 1)}")
+            else:
+                g(f"v_cmp_eq_u32_e32 vcc, {_nsrc(g, b)}, {_nreg(g, c, T + 1)}")
+            combine = [f"s_or_b64 {sr(m, 2)}, vcc, {sr(m, 2)}", f"s_and_b64 {sr(ACC, 2)}, {sr(ACC, 2)}, {sr(m, 2)}"]
+        if pending is not None:
+            g(*pending_lines)
+        pending, pending_lines = m, combine
+    g("s_nop 1")
+    g(*pending_lines)
+    g(f"v_cndmask_b32_e64 {v(ALIVE)}, 0, {v(ALIVE)}, {sr(ACC, 2)}")
+    skip = g.L("ee")
+    g(f"s_bitcmp1_b32 {s(FLAGS)}, 0", f"s_cbranch_scc0 {skip}",
+      f"v_cmp_ne_u32_e32 vcc, 0, {v(ALIVE)}", "s_nop 1", "s_cmp_eq_u64 vcc, 0")
+    g.stop_if_scc1()
+    g.label(skip)
+
+
+LDS_SPILL_WORDS = 80   # mw_kernels.hip kLdsSpillWords
+
+
+def lds_spill_words(n_spill: int, npool: int) -> int:
+    """Spill words an assembled kernel keeps in LDS: mw_kernels.hip
+    asm_lds_fit (the pool first, the hottest spill words in what is left)."""
+    rows = (npool * 4 + 1023) // 1024
+    return max(0, min(n_spill, LDS_SPILL_WORDS - rows))
+
+
+def _spill_static(g, name, insn, nlds):
+    """SPILL/FILL with the word's place known: LDS [word][lane] below nlds,
+    else the global buffer [word][thread] (mw_kernels.hip)."""
+    wd0 = insn[3]
+    n = 8 if name.endswith("_W") else 1
+    g.set_insn(insn)
+
+    def addr(word):
+        if word < nlds:
+            if word * 1024 < 65536:
+                return "lds", v(LDSOFF), f" offset:{word * 1024}"
+            g(f"v_add_u32_e32 {v(T + 7)}, {_lit(word * 1024)}, {v(LDSOFF)}")
+            return "lds", v(T + 7), ""
+        g(f"s_mul_i32 {s(S[7])}, {s(GSTRIDE)}, {word - nlds}", f"v_add_u32_e32 {v(T + 7)}, {s(S[7])}, {v(GOFF)}")
+        return "glob", v(T + 7), ""
+
+    if name.startswith("SPILL"):
+        a = g.cur["a"]
+        if a & KBIT:
+            o = a & 0x7FFF
+            for k in range(n):
+                g(f"v_mov_b32_e32 {v(XA + k)}, {_lit(g.consts[o + k])}")
+            src = [v(XA + k) for k in range(n)]
+        else:
+            src = [v(W0 + 8 * a + k) for k in range(n)] if n == 8 else [v(N0 + a)]
+        for k in range(n):
+            kind, base, off = addr(wd0 + k)
+            if kind == "lds":
+                g(f"ds_write_b32 {base}, {src[k]}{off}")
+            else:
+                g(f"global_store_dword {base}, {src[k]}, {sr(GSP, 2)}")
+        # no wait: LDS operations of a wave execute in order, and the fill waits
+        # for its own loads (the global store is waited for below)
+        if any(wd0 + k >= nlds for k in range(n)):
+            g("s_waitcnt vmcnt(0)")
+    else:
+        for k in range(n):
+            kind, base, off = addr(wd0 + k)
+            if kind == "lds":
+                g(f"ds_read_b32 {v(XR + k)}, {base}{off}")
+            else:
+                g(f"global_load_dword {v(XR + k)}, {base}, {sr(GSP, 2)}")
+        g("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        (g.write_w if n == 8 else g.write_n)(XR)
+
+
+def static_body(code, consts, leaves, forward: bool = True, nlds: int = None) -> list:
     """The straight-line body of an assembled kernel for a validated,
     asm-eligible program (code: its instruction words, original encoding;
     consts and leaves: its constant pool and leaf table)."""
@@ -1449,7 +1560,19 @@ def static_body(code, consts, leaves, forward: bool = True) -> list:
             break
         g.set_insn(insn)
         g.lines = []
-        if name == "W_CDINS" and not g.chain_open:
+        if name in CHECK_OPS:
+            run = []
+            j = i
+            while j + 4 <= len(words) and names[words[j] & 0xFF] in CHECK_OPS:
+                run.append(words[j:j + 4])
+                j += 4
+            g.chain_open = False
+            g.summary_b = None
+            g.digit_spec = None
+            _check_run_static(g, run)
+            skip_to = j
+            name = f"{name} run x{len(run)}"
+        elif name == "W_CDINS" and not g.chain_open:
             # a whole chain, batched, when every link qualifies
             j = i
             links = []
@@ -1469,6 +1592,11 @@ def static_body(code, consts, leaves, forward: bool = True) -> list:
                 _cdins_static(g)
         elif name == "W_CDINS":
             _cdins_static(g)
+        elif name in ("SPILL_W", "SPILL_N", "FILL_W", "FILL_N") and nlds is not None:
+            g.chain_open = False
+            g.summary_b = None
+            g.digit_spec = None
+            _spill_static(g, name, insn, nlds)
         elif name in ("LEAF_W", "LEAF_N"):
             g.chain_open = False
             g.summary_b = None

@@ -81,7 +81,9 @@ def source(p: Program) -> Tuple[str, str]:
     text, num, _ = _load_template()
     name = kernel_name(p)
     body = "\n".join("\t" + ln if not ln.endswith(":") else ln
-                     for ln in asmgen.static_body(p.code, p.consts, p.leaves)).replace("%=", num)
+                     for ln in asmgen.static_body(p.code, p.consts, p.leaves,
+                                                  nlds=asmgen.lds_spill_words(p.n_spill, len(p.pool))
+                                                  )).replace("%=", num)
     out = text.replace(asmgen.MARKER, body, 1).replace(TEMPLATE_NAME, name)
     return name, out.replace(TEMPLATE_SIG, str(signature(p)), 1)
 

@@ -30,6 +30,11 @@ DEFAULT_BUDGET = 1 << 22  # candidates per query (early exit + stop-after-hit)
 # on the interpreter; a 14 000-op C3-class query gets ~600 k candidates.
 DEFAULT_OP_BUDGET = (1 << 22) * 2000
 MIN_CANDIDATES = 1 << 16
+# A launch planned at this many u32 ops or more assembles its programs first
+# (mythril_amd/asmjit.py: tens of ms per program, 2.5-6x the asm interpreter's
+# rate); below it the asm interpreter starts at once.  The default budget's
+# launches stay below it: they finish in a few ms.
+DEFAULT_ASMJIT_MIN_OPS = 1 << 36
 
 
 @dataclass
@@ -124,7 +129,7 @@ class WitnessEngine:
     """Owns one device context; everything goes through the C-ABI."""
 
     def __init__(self, device: int = 0, seed: int = DEFAULT_SEED, budget: int = DEFAULT_BUDGET, dev=None,
-                 op_budget: Optional[int] = DEFAULT_OP_BUDGET):
+                 op_budget: Optional[int] = DEFAULT_OP_BUDGET, asmjit_min_ops: Optional[int] = DEFAULT_ASMJIT_MIN_OPS):
         if dev is None:
             from .runtime import Device  # raises EngineUnavailable without the HIP library / GPU
             dev = Device(device)
@@ -132,7 +137,9 @@ class WitnessEngine:
         self.seed = seed
         self.budget = budget
         self.op_budget = op_budget
-        self.stats = {"searches": 0, "programs": 0, "hits": 0, "evals": 0, "kernel_ms": 0.0}
+        self.asmjit_min_ops = asmjit_min_ops   # None / 0: never assemble
+        self.stats = {"searches": 0, "programs": 0, "hits": 0, "evals": 0, "kernel_ms": 0.0, "assembled": 0,
+                      "assemble_s": 0.0}
 
     def close(self):
         self.dev.close()
@@ -146,6 +153,9 @@ class WitnessEngine:
         try:
             for q in queries:   # a failed load frees the programs already loaded
                 dps.append(self.dev.load(q.program))
+            if (self.asmjit_min_ops and hasattr(self.dev, "attach_asm")
+                    and count * sum(q.ops_per_eval for q in queries) >= self.asmjit_min_ops):
+                self._assemble(dps)
             found, st = self.dev.search(dps, self.seed, begin, count, flags)
         finally:
             for dp in dps:
@@ -161,6 +171,29 @@ class WitnessEngine:
                 self.stats["hits"] += 1
             out.append(w)
         return out
+
+    def _assemble(self, dps) -> None:
+        """Attach assembled kernels to the eligible programs (parallel
+        llvm-mc runs; on-disk cache).  Any failure leaves that program on the
+        asm interpreter: same results, only slower."""
+        import time
+        from concurrent.futures import ThreadPoolExecutor
+
+        from . import asmjit
+        if not asmjit.available():
+            return
+        todo = [dp for dp in dps if asmjit.eligible(dp.prog)]
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(max(1, min(8, len(todo)))) as ex:
+            futs = [(dp, ex.submit(asmjit.assemble, dp.prog)) for dp in todo]
+            for dp, f in futs:
+                try:
+                    image, name, _ = f.result()
+                    self.dev.attach_asm(dp, image, name)
+                    self.stats["assembled"] += 1
+                except Exception as e:   # noqa: BLE001 - stays on the interpreter
+                    log.warning("assembled kernel unavailable for %s: %s", getattr(dp.prog, "n_insn", "?"), e)
+        self.stats["assemble_s"] += time.perf_counter() - t0
 
     def launch_count(self, queries: Sequence[Query]) -> int:
         """Candidates per query for one launch: the candidate budget, cut so the

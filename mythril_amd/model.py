@@ -79,14 +79,16 @@ def engine():
                     from .engine import WitnessEngine
                     dev = int(os.environ.get("LOCAL_RANK", os.environ.get("MYTHRIL_AMD_DEVICE", "0")))
                     budget = int(os.environ.get("MYTHRIL_AMD_BUDGET", str(1 << 22)))
-                    from .engine import DEFAULT_OP_BUDGET
+                    from .engine import DEFAULT_ASMJIT_MIN_OPS, DEFAULT_OP_BUDGET
                     op_budget = int(os.environ.get("MYTHRIL_AMD_OP_BUDGET", str(DEFAULT_OP_BUDGET)))
+                    asm_min = int(os.environ.get("MYTHRIL_AMD_ASMJIT_MIN_OPS", str(DEFAULT_ASMJIT_MIN_OPS)))
                     ndev = int(os.environ.get("MYTHRIL_AMD_DEVICES", "1"))
                     multi = None
                     if ndev > 1:   # one process over several GPUs (multidev.py)
                         from .multidev import MultiDevice
                         multi = MultiDevice.open(range(ndev))
-                    _engine = WitnessEngine(device=dev, budget=budget, op_budget=op_budget, dev=multi)
+                    _engine = WitnessEngine(device=dev, budget=budget, op_budget=op_budget, dev=multi,
+                                            asmjit_min_ops=asm_min)
                 except Exception as e:  # EngineUnavailable / EngineError
                     log.warning("MI355X witness engine unavailable (%s); using z3 only", e)
                     _engine_failed = True

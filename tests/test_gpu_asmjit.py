@@ -145,3 +145,17 @@ def test_asmjit_reports_the_satisfying_lane(dev, k):
     finally:
         di.free()
         da.free()
+
+
+def test_engine_assembles_long_launches(dev, corpus):
+    """WitnessEngine assembles a launch's programs once it is planned above
+    asmjit_min_ops; the witnesses are the interpreter's."""
+    from mythril_amd.engine import WitnessEngine
+    qs = [q for _, q in corpus[:12]]
+    with_asm = WitnessEngine(dev=dev, budget=1 << 20, op_budget=None, asmjit_min_ops=1)
+    without = WitnessEngine(dev=dev, budget=1 << 20, op_budget=None, asmjit_min_ops=0)
+    wa = with_asm.search(qs)
+    wi = without.search(qs)
+    assert [w.index if w else None for w in wa] == [w.index if w else None for w in wi]
+    assert with_asm.stats["assembled"] == sum(asmjit.eligible(q.program) for q in qs) > 0
+    assert without.stats["assembled"] == 0
