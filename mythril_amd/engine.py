@@ -1,12 +1,15 @@
 """Witness engine: constraint sets -> batched GPU search -> concrete witnesses.
 
 ``prepare`` lowers one constraint set (Ackermannisation, width legalisation,
-candidate pools) and compiles it twice with identical leaf layouts: a search
-program (verdicts only) and a materialisation program that also traces every
-leaf and every array index / function argument.  ``WitnessEngine.search``
-launches many programs in one ``mg_search`` call (one grid row per program,
-SURVEY.md §8a row A9 batching) and turns each lowest satisfying index back
-into a :class:`Witness` by re-evaluating that single candidate on the device.
+candidate pools) and compiles its search program (verdicts only).
+``WitnessEngine.search`` launches many programs in one ``mg_search`` call (one
+grid row per program, SURVEY.md §8a row A9 batching) and turns each lowest
+satisfying index back into a :class:`Witness`: the search program re-evaluates
+that single candidate on the device (the verdict), and a witness program with
+the same leaf layout and no conjuncts - only the leaves and every array index
+/ function argument, traced - reads its values out.  The witness program is
+compiled on first use and costs a fraction of the search program (C3: ~1 ms
+against ~110 ms for a trace of the whole conjunction).
 """
 from __future__ import annotations
 
@@ -51,16 +54,16 @@ class Query:
     conjuncts: List[Node]
     lowered: Lowered
     program: Program
-    trace_build: "Callable[[], Program]"     # the materialisation program, compiled on first use
+    trace_build: "Callable[[], Program]"     # the witness program, compiled on first use
     arg_terms: List[Node]
     arg_chunks: Dict[str, List[List[Node]]] = field(default_factory=dict)
     _trace: Optional[Program] = None
 
     @property
     def trace_program(self) -> Program:
-        """Same conjuncts and leaf layout as ``program``, tracing every leaf and
-        array index / function argument.  Only a witness needs it, so it is
-        compiled lazily (half of prepare()'s cost on a miss)."""
+        """The witness program: ``program``'s leaf layout with no conjuncts,
+        tracing every leaf and array index / function argument.  Only a
+        witness needs it, so it is compiled lazily."""
         if self._trace is None:
             self._trace = self.trace_build()
         return self._trace
@@ -91,7 +94,7 @@ def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True,
     prog = compile_program(low.conjuncts, leaf_specs=specs)
     if timings is not None:
         timings.update(lower=t1 - t0, pools=t2 - t1, compile=time.perf_counter() - t2)
-    # identical leaf layout (pool fields already assigned) for the materialisation program
+    # identical leaf layout (pool fields already assigned) for the witness program
     fixed = {s.name: dataclasses.replace(s, pool=None if s.pool is None else list(s.pool))
              for s in prog.leaf_specs}
     # trace every array index / function argument (wider than 256 bits: as 256-bit chunks)
@@ -108,8 +111,9 @@ def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True,
             arg_terms.extend(parts)
         arg_chunks[al.name] = per
     traced = list(prog.leaf_nodes) + arg_terms
-    q = Query(ctx, conj, low, prog, lambda: compile_program(low.conjuncts, leaf_specs=fixed, trace=traced),
-              arg_terms)
+    # the search program's leaves lead the trace list in its order, so the witness
+    # program numbers them identically: same candidate generator, same values
+    q = Query(ctx, conj, low, prog, lambda: compile_program([], leaf_specs=fixed, trace=traced), arg_terms)
     q.arg_chunks = arg_chunks
     return q
 
@@ -157,19 +161,19 @@ class WitnessEngine:
                     and count * sum(q.ops_per_eval for q in queries) >= self.asmjit_min_ops):
                 self._assemble(dps)
             found, st = self.dev.search(dps, self.seed, begin, count, flags)
+            self.stats["searches"] += 1
+            self.stats["programs"] += len(queries)
+            self.stats["evals"] += st["evals"]
+            self.stats["kernel_ms"] += st["kernel_ms"]
+            out: List[Optional[Witness]] = []
+            for q, dp, idx in zip(queries, dps, found):
+                w = self.materialize(q, idx, dp) if idx is not None else None
+                if w is not None:
+                    self.stats["hits"] += 1
+                out.append(w)
         finally:
             for dp in dps:
                 dp.free()
-        self.stats["searches"] += 1
-        self.stats["programs"] += len(queries)
-        self.stats["evals"] += st["evals"]
-        self.stats["kernel_ms"] += st["kernel_ms"]
-        out: List[Optional[Witness]] = []
-        for q, idx in zip(queries, found):
-            w = self.materialize(q, idx) if idx is not None else None
-            if w is not None:
-                self.stats["hits"] += 1
-            out.append(w)
         return out
 
     def _assemble(self, dps) -> None:
@@ -203,17 +207,29 @@ class WitnessEngine:
         ops = max(1, sum(q.ops_per_eval for q in queries))
         return max(min(self.budget, MIN_CANDIDATES), min(self.budget, self.op_budget // ops))
 
-    def materialize(self, q: Query, index: int) -> Optional[Witness]:
+    def materialize(self, q: Query, index: int, search_dp=None) -> Optional[Witness]:
+        """The witness at candidate ``index``: its verdict re-evaluated by the
+        search program (``search_dp`` if still loaded), its values read from
+        the witness program."""
         from .runtime import unpack_trace
-        dp = self.dev.load(q.trace_program)
+        p = q.trace_program
+        if [n.name for n in p.leaf_nodes] != [n.name for n in q.program.leaf_nodes]:
+            raise RuntimeError("witness program's leaf layout differs from the search program's")
+        own = search_dp is None
+        sdp = self.dev.load(q.program) if own else search_dp
         try:
-            verdict, trace = self.dev.eval_generated(dp, self.seed, index, 1)
+            verdict, _ = self.dev.eval_generated(sdp, self.seed, index, 1)
         finally:
-            dp.free()
+            if own:
+                sdp.free()
         if int(verdict[0]) != 1:
             log.error("witness %d failed device re-evaluation; discarded", index)
             return None
-        p = q.trace_program
+        dp = self.dev.load(p)
+        try:
+            _, trace = self.dev.eval_generated(dp, self.seed, index, 1)
+        finally:
+            dp.free()
         values = {n.name: unpack_trace(p, trace, n)[0] for n in p.leaf_nodes}
         w = Witness(index, values)
         for al in q.lowered.ack.values():
