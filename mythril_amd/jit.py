@@ -49,6 +49,9 @@ SPLIT_EVERY = 48
 # how a region boundary is emitted: "branch" (JIT_SPLIT of mw_jit.h) or
 # "sched_barrier" (MW_JIT_SPLIT env: experiments)
 SPLIT_KIND = os.environ.get("MW_JIT_SPLIT", "branch")
+# experiments (tools/ab_c5.py): a workgroup barrier after every conjunct of the
+# exhaustive variant, keeping a block's waves at the same place in the code
+CHECK_SYNC = os.environ.get("MW_JIT_CHECK_SYNC", "0") == "1"
 M32 = 0xFFFFFFFF
 
 _WBIN = {"W_ADD": "w_add", "W_SUB": "w_sub", "W_MUL": "w_mul", "W_AND": "w_and", "W_OR": "w_or",
@@ -226,7 +229,9 @@ class _Gen:
         if d is not None:
             dn = f"v{d.id}" if d.cls == "W" else f"n{d.id}"
         if op == "CHECK":
-            out(f"alive = jit::check(alive, {A[0]}); if (EARLY) {{ if (jit::none(alive)) break; }} else JIT_SPLIT();")
+            sync = " JIT_SYNC();" if CHECK_SYNC else ""
+            out(f"alive = jit::check(alive, {A[0]}); if (EARLY) {{ if (jit::none(alive)) break; }} "
+                f"else {{ JIT_SPLIT();{sync} }}")
             self.since_split = 0
         elif op == "LEAF_W" and d.id in self.lds_slot:
             out(f"{{ u32 t_[8]; {self.leaf(imm, 't_')} jit::lds_put8({self.lds_slot[d.id]}u, t_); }}")
@@ -399,6 +404,9 @@ def generate(progs: Sequence[Program], names: Sequence[str], variants: str = "xe
         # multi-MiB body), the scheduler still cannot move code across them
         out += ["#if defined(__HIP_DEVICE_COMPILE__)", "#undef JIT_SPLIT",
                 "#define JIT_SPLIT() __builtin_amdgcn_sched_barrier(0)", "#endif", ""]
+    if CHECK_SYNC:
+        out += ["#if defined(__HIP_DEVICE_COMPILE__)", "#define JIT_SYNC() __syncthreads()", "#else",
+                "#define JIT_SYNC() ((void)0)", "#endif", ""]
     done = set()
     for k, (p, name) in enumerate(zip(progs, names)):
         if name in done:   # two queries that compile to the same program share one kernel

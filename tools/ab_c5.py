@@ -25,7 +25,9 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             "il2": {"EXTRA_FLAGS": [], "interleave": 2},
             "abl_knuth": {"EXTRA_FLAGS": ["-DMW_ABLATE_KNUTH"]}, "abl_fulldiv": {"EXTRA_FLAGS": ["-DMW_ABLATE_FULLDIV"]},
             # one wave per SIMD: 512 registers per lane, no leaves in LDS
-            "w1": {"EXTRA_FLAGS": [], "waves": 1, "lds": 0}}
+            "w1": {"EXTRA_FLAGS": [], "waves": 1, "lds": 0},
+            # a workgroup barrier after every conjunct (jit.CHECK_SYNC): the block's waves fetch the same code
+            "sync": {"EXTRA_FLAGS": [], "CHECK_SYNC": True}}
 
 
 def main():
