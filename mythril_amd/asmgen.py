@@ -228,6 +228,25 @@ class Gen:
     def nop_vcc(self):
         self("s_nop 1")
 
+    def static_imm(self):
+        """the instruction's immediate word when known at generation time"""
+        return None
+
+    def flip_sign_bits(self, w, t):
+        """flip bit w-1 (w: SGPR holding the width) of XA and XB; t: scratch SGPR"""
+        self(f"s_sub_u32 {s(w)}, {s(w)}, 1", f"s_lshr_b32 {s(t)}, {s(w)}, 5",
+             f"s_and_b32 {s(w)}, {s(w)}, 31", f"s_lshl_b32 {s(w)}, 1, {s(w)}",
+             f"s_set_gpr_idx_on {s(t)}, gpr_idx(SRC1,DST)", f"v_xor_b32_e32 {v(XA)}, {s(w)}, {v(XA)}",
+             "s_set_gpr_idx_off", f"s_set_gpr_idx_on {s(t)}, gpr_idx(SRC1,DST)",
+             f"v_xor_b32_e32 {v(XB)}, {s(w)}, {v(XB)}", "s_set_gpr_idx_off")
+
+    def extract_limb(self, q, r):
+        """XR = bits imm..imm+31 of XA (imm: the instruction's immediate word;
+        limb 8 reads v144, zeroed once per block); q, r: scratch SGPRs"""
+        self(f"s_lshr_b32 {s(q)}, {s(CUR + 3)}, 5", f"s_and_b32 {s(r)}, {s(CUR + 3)}, 31",
+             f"s_set_gpr_idx_on {s(q)}, gpr_idx(SRC0,SRC1)",
+             f"v_alignbit_b32 {v(XR)}, {v(XA + 1)}, {v(XA)}, {s(r)}", "s_set_gpr_idx_off")
+
     def sub_chain(self, a, b, dst=None, borrow_only=False):
         """a - b over 8 limbs (VGPR bases); borrow out in vcc"""
         for k in range(8):
@@ -461,11 +480,7 @@ def build_handlers():
             g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
             # flip bit w-1 of both (width = operand width), then compare unsigned
             g.width(S[2])
-            g(f"s_sub_u32 {s(S[2])}, {s(S[2])}, 1", f"s_lshr_b32 {s(S[3])}, {s(S[2])}, 5",
-              f"s_and_b32 {s(S[2])}, {s(S[2])}, 31", f"s_lshl_b32 {s(S[2])}, 1, {s(S[2])}",
-              f"s_set_gpr_idx_on {s(S[3])}, gpr_idx(SRC1,DST)", f"v_xor_b32_e32 {v(XA)}, {s(S[2])}, {v(XA)}",
-              "s_set_gpr_idx_off", f"s_set_gpr_idx_on {s(S[3])}, gpr_idx(SRC1,DST)",
-              f"v_xor_b32_e32 {v(XB)}, {s(S[2])}, {v(XB)}", "s_set_gpr_idx_off")
+            g.flip_sign_bits(S[2], S[3])
             if le:
                 g.sub_chain(XB, XA)
                 g.bool_from_vcc(XR, invert=True)
@@ -479,9 +494,7 @@ def build_handlers():
     def _(g):
         g.field("a", S[0]), g.fetch_w(S[0], XA)
         # (x >> imm)[0] & nmask(w): limb q = imm >> 5 and the next, funnel by imm & 31
-        g(f"s_lshr_b32 {s(S[1])}, {s(CUR + 3)}, 5", f"s_and_b32 {s(S[2])}, {s(CUR + 3)}, 31",
-          f"s_set_gpr_idx_on {s(S[1])}, gpr_idx(SRC0,SRC1)",
-          f"v_alignbit_b32 {v(XR)}, {v(XA + 1)}, {v(XA)}, {s(S[2])}", "s_set_gpr_idx_off")
+        g.extract_limb(S[1], S[2])
         g.width(S[3]), g.nmask(S[3], S[4])
         g(f"v_and_b32_e32 {v(XR)}, {s(S[4])}, {v(XR)}")
         g.write_n(XR)
@@ -551,6 +564,18 @@ def build_handlers():
         """dst..dst+7 = XA << amount (SGPR, < 256): written through a positive
         destination index (limbs past dst+7 land in the next 8 temporaries
         and are dropped); XA has zeros below it"""
+        if amount == CUR + 3 and g.static_imm() is not None:   # an assembled body: literal limbs
+            n = g.static_imm() & 255
+            q, b = n >> 5, n & 31
+            src = lambda i: v(XA + i) if i >= 0 else "0"   # noqa: E731
+            for k in range(8):
+                if k - q < 0:
+                    g(f"v_mov_b32_e32 {v(dst + k)}, 0")
+                elif b == 0:
+                    g(f"v_mov_b32_e32 {v(dst + k)}, {v(XA + k - q)}")
+                else:
+                    g(f"v_alignbit_b32 {v(dst + k)}, {src(k - q)}, {src(k - q - 1)}, {32 - b}")
+            return
         q, b = S[4], S[5]
         zb, j = g.L("z0"), g.L("sj")
         for k in range(8):
@@ -579,12 +604,20 @@ def build_handlers():
     @handler("W_LSHRI")
     def _(g):
         g.field("a", S[0]), g.fetch_w(S[0], XA)
-        q, b = S[4], S[5]
-        g(f"s_lshr_b32 {s(q)}, {s(CUR + 3)}, 5", f"s_and_b32 {s(b)}, {s(CUR + 3)}, 31",
-          f"s_set_gpr_idx_on {s(q)}, gpr_idx(SRC0,SRC1)")
-        for k in range(8):
-            g(f"v_alignbit_b32 {v(XR + k)}, {v(XA + k + 1)}, {v(XA + k)}, {s(b)}")
-        g("s_set_gpr_idx_off")
+        if g.static_imm() is not None:      # an assembled body: literal limbs
+            n = g.static_imm() & 255
+            sq, sb = n >> 5, n & 31
+            src = lambda i: v(XA + i) if i < 8 else "0"   # noqa: E731
+            for k in range(8):
+                g(f"v_alignbit_b32 {v(XR + k)}, {src(k + sq + 1)}, {src(k + sq)}, {sb}" if k + sq < 8
+                  else f"v_mov_b32_e32 {v(XR + k)}, 0")
+        else:
+            q, b = S[4], S[5]
+            g(f"s_lshr_b32 {s(q)}, {s(CUR + 3)}, 5", f"s_and_b32 {s(b)}, {s(CUR + 3)}, 31",
+              f"s_set_gpr_idx_on {s(q)}, gpr_idx(SRC0,SRC1)")
+            for k in range(8):
+                g(f"v_alignbit_b32 {v(XR + k)}, {v(XA + k + 1)}, {v(XA + k)}, {s(b)}")
+            g("s_set_gpr_idx_off")
         g.width(S[2]), g.canon(XR, S[2])
         g.write_w(XR)
 
@@ -601,9 +634,16 @@ def build_handlers():
         # r = a | (zext(N b) << imm)
         g.field("a", S[0]), g.field("b", S[1])
         g.fetch_w(S[0], XR), g.fetch_n(S[1], XA)
-        for k in range(1, 8):
-            g(f"v_mov_b32_e32 {v(XA + k)}, 0")
-        shl_imm_into_or(g, CUR + 3)
+        if g.static_imm() is not None:      # an assembled body: the two limbs it reaches
+            n = g.static_imm() & 255
+            q, b = n >> 5, n & 31
+            g(f"v_lshl_or_b32 {v(XR + q)}, {v(XA)}, {b}, {v(XR + q)}")
+            if b and q + 1 < 8:
+                g(f"v_lshrrev_b32_e32 {v(T)}, {32 - b}, {v(XA)}", f"v_or_b32_e32 {v(XR + q + 1)}, {v(XR + q + 1)}, {v(T)}")
+        else:
+            for k in range(1, 8):
+                g(f"v_mov_b32_e32 {v(XA + k)}, 0")
+            shl_imm_into_or(g, CUR + 3)
         g.width(S[2]), g.canon(XR, S[2])
         g.write_w(XR)
 
@@ -837,8 +877,11 @@ def gen(mode="interp"):
       f"v_addc_co_u32_e32 {v(CHI)}, vcc, 0, {v(T + 7)}, vcc",
       f"v_cmp_gt_u64_e32 vcc, {sr(END, 2)}, {vr(CLO, 2)}", "s_nop 1",
       f"s_mov_b64 {sr(VALID, 2)}, vcc", f"v_cndmask_b32_e64 {v(ALIVE)}, 0, 1, vcc")
-    for k in range(0, 128, 2):
-        g(f"v_mov_b64 {vr(k, 2)}, 0")
+    if mode == "interp":
+        # the register files start at zero (an assembled body zeroes the
+        # registers it reads before writing them: static_body / dead_code)
+        for k in range(0, 128, 2):
+            g(f"v_mov_b64 {vr(k, 2)}, 0")
     if mode == "template":
         g.long_addr(SX, "Lbody_%=")
         g(f"s_setpc_b64 {sr(SX, 2)}")
@@ -1157,6 +1200,23 @@ class StaticGen(Gen):
 
     def next(self):
         pass
+
+    def static_imm(self):
+        return self.cur["imm"]
+
+    def flip_sign_bits(self, w, t):
+        if w not in self.sval:
+            super().flip_sign_bits(w, t)
+            return
+        b = self.sval[w] - 1
+        q, m = b >> 5, _lit(1 << (b & 31))
+        self(f"v_xor_b32_e32 {v(XA + q)}, {m}, {v(XA + q)}", f"v_xor_b32_e32 {v(XB + q)}, {m}, {v(XB + q)}")
+
+    def extract_limb(self, q, r):
+        imm = self.cur["imm"]
+        k, sh = imm >> 5, imm & 31
+        hi = v(XA + k + 1) if k + 1 < 8 else "0"
+        self(f"v_alignbit_b32 {v(XR)}, {hi}, {v(XA + k)}, {sh}")
 
     # the body sits after the template's code and may be longer than a
     # branch reaches (simm16 words): it leaves through addresses the template
@@ -1613,7 +1673,21 @@ def static_body(code, consts, leaves, forward: bool = True, nlds: int = None) ->
         out.append(f"; {i // 4}: {name}")
         out.extend(lines)
     out.append(f"s_setpc_b64 {sr(ENDADDR, 2)}")
-    return forward_copies(out) if forward else out
+    if forward:
+        out = forward_copies(out)
+    out, live_in = dead_code(out)
+    # the files start at zero (mw_interp.h): only what the body reads before writing
+    zero = sorted(r for r in live_in if r < 128)
+    head, k = [], 0
+    while k < len(zero):
+        r = zero[k]
+        if r % 2 == 0 and k + 1 < len(zero) and zero[k + 1] == r + 1:
+            head.append(f"v_mov_b64 {vr(r, 2)}, 0")
+            k += 2
+        else:
+            head.append(f"v_mov_b32_e32 {v(r)}, 0")
+            k += 1
+    return head + out
 
 
 # ------------------------------------------------ copy forwarding (static bodies)
@@ -1710,3 +1784,93 @@ def forward_copies(lines):
                     if d >= TEMP_LO:
                         pending[d] = i
     return [ln for i, ln in enumerate(out) if i not in dead]
+
+
+# ------------------------------------------------ dead-code elimination (static bodies)
+# Registers a static body may leave dead: the W and N files and the operand /
+# result / scratch registers.  v128..v135 and v144..v151 (zeroed once per
+# block) and v160..v167 (candidate, alive, offsets) are the template's and are
+# live wherever the body leaves.
+DCE_REGS = frozenset(range(0, 128)) | frozenset(range(XA, XA + 8)) | frozenset(range(XB, XB + 8)) \
+    | frozenset(range(XR, T + 8))
+_ALL_V = frozenset(range(256))
+EXIT_LIVE = _ALL_V - DCE_REGS
+# VALU forms with no effect besides their VGPR result (no vcc / SGPR write)
+_PURE = ("v_mov_b32", "v_mov_b32_e32", "v_mov_b32_e64", "v_mov_b64", "v_cndmask_b32_e32", "v_cndmask_b32_e64",
+         "v_and_b32_e32", "v_or_b32_e32", "v_xor_b32_e32", "v_or3_b32", "v_lshl_or_b32", "v_bfe_u32",
+         "v_lshrrev_b32_e32", "v_lshlrev_b32_e32", "v_add_u32_e32", "v_sub_u32_e32", "v_not_b32_e32",
+         "v_add3_u32", "v_alignbit_b32", "v_lshl_add_u32", "v_mul_lo_u32", "v_mad_u32_u24")
+_LABEL_REF = re.compile(r"\b(L\w+_%=|L\w+_\d+)$")
+
+
+def _defs_uses(op, ops):
+    """(VGPRs written, VGPRs read) of one instruction; None when unknown"""
+    regs = [_regs(o) for o in ops]
+    if op.startswith(("ds_write", "global_store", "global_atomic", "buffer_store")):
+        return [], [r for rs in regs for r in rs]
+    if op.startswith("v_cmp"):
+        return [], [r for rs in regs[1:] for r in rs]
+    if op.startswith(("v_readfirstlane", "v_readlane")):
+        return [], [r for rs in regs[1:] for r in rs]
+    if op.startswith("v_writelane"):
+        return regs[0], [r for rs in regs for r in rs]     # a partial write: the old value stays live
+    if op.startswith(("v_", "ds_read", "global_load", "buffer_load")):
+        return (regs[0] if ops else []), [r for rs in regs[1:] for r in rs]
+    return [], []
+
+
+def dead_code(lines):
+    """Backward liveness over a straight-line body with forward skips: pure
+    VALU instructions whose result no later instruction reads are dropped.
+    Returns (lines, live_in), live_in being the body registers read before
+    any write (the body zeroes those itself).  Exits (s_setpc) leave only the
+    template's registers live; calls keep every register from v128 up live;
+    an instruction inside an s_set_gpr_idx region reads everything."""
+    live = set(EXIT_LIVE)
+    at_label = {}
+    keep = [True] * len(lines)
+    indexed = False
+    for i in range(len(lines) - 1, -1, -1):
+        ln = lines[i]
+        if not ln or ln.startswith(";"):
+            continue
+        if ln.endswith(":"):
+            at_label[ln[:-1]] = set(live)
+            continue
+        op, ops = _operands(ln)
+        if "exec" in ln:
+            raise ValueError("dead_code: a body that writes exec")
+        if op == "s_set_gpr_idx_off":
+            indexed = True            # walking backwards: the region starts here
+            live = set(_ALL_V)
+            continue
+        if op == "s_set_gpr_idx_on":
+            indexed = False
+            live = set(_ALL_V)
+            continue
+        if indexed:
+            live = set(_ALL_V)
+            continue
+        if op.startswith(("s_cbranch", "s_branch")):
+            tgt = ops[0] if ops else ""
+            out = at_label.get(tgt)
+            if out is None:
+                out = _ALL_V
+            live = set(out) if op == "s_branch" else live | out
+            continue
+        if op == "s_setpc_b64":
+            live = set(EXIT_LIVE)
+            continue
+        if op.startswith(("s_swappc", "s_call")):
+            live |= _ALL_V - frozenset(range(0, 128))
+            continue
+        if not op.startswith(("v_", "ds_", "global_", "buffer_")):
+            continue
+        defs, uses = _defs_uses(op, ops)
+        if op in _PURE and defs and all(d in DCE_REGS and d not in live for d in defs):
+            keep[i] = False
+            continue
+        live.difference_update(defs)
+        live.update(uses)
+    live_in = sorted(r for r in live if r in DCE_REGS)
+    return [ln for ln, k in zip(lines, keep) if k], live_in

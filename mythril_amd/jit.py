@@ -229,9 +229,8 @@ class _Gen:
         if d is not None:
             dn = f"v{d.id}" if d.cls == "W" else f"n{d.id}"
         if op == "CHECK":
-            sync = " JIT_SYNC();" if CHECK_SYNC else ""
-            out(f"alive = jit::check(alive, {A[0]}); if (EARLY) {{ if (jit::none(alive)) break; }} "
-                f"else {{ JIT_SPLIT();{sync} }}")
+            tail = "{ JIT_SPLIT(); JIT_SYNC(); }" if CHECK_SYNC else "JIT_SPLIT();"
+            out(f"alive = jit::check(alive, {A[0]}); if (EARLY) {{ if (jit::none(alive)) break; }} else {tail}")
             self.since_split = 0
         elif op == "LEAF_W" and d.id in self.lds_slot:
             out(f"{{ u32 t_[8]; {self.leaf(imm, 't_')} jit::lds_put8({self.lds_slot[d.id]}u, t_); }}")

@@ -22,6 +22,7 @@
 #   opcost         tools/interp_opcost.py (+ one PMC pass: instructions per bytecode op)
 #   ablate         tools/leaf_ablate.py --run (candidate-generation ablations, C2/C2L/C4)
 #   recip          tools/exp/recip_check (device reciprocal vs u64 division; built by hand)
+#   ab=V1,V2       tools/ab_c5.py: C5 code-generation variants (compiled beforehand), timed and cross-checked
 # Outputs land in gpurun_out/TAG/.
 set -o pipefail
 export TMPDIR=/tmp
@@ -92,6 +93,9 @@ for step in "$@"; do
     keccak)
       run 300 "$OUT/keccak.log" python3 tools/keccak_bench.py
       tail -8 "$OUT/keccak.log" ;;
+    ab=*)
+      run 300 "$OUT/ab_c5.log" python3 -u tools/ab_c5.py --variants "${step#ab=}" --out "$OUT/ab_c5.json" || exit 1
+      cat "$OUT/ab_c5.log" ;;
     ipmc=*|jpmc=*|apmc=*)
       F=${step#*=}
       J=()
