@@ -1067,9 +1067,10 @@ def philox_sub(g):
           f"v_mov_b32_e32 {v(c[2])}, {blk}", f"v_mov_b32_e32 {v(c[3])}, 0",
           f"s_xor_b32 {s(PK0)}, {s(SEED)}, {s(D + 2)}", f"s_mov_b32 {s(PK1)}, {s(SEED + 1)}")
         for r in range(10):
-            hi0, lo0, hi1, lo1 = XB, XB + 1, XB + 2, XB + 3
-            g(f"v_mul_hi_u32 {v(hi0)}, {v(c[0])}, {s(PM0)}", f"v_mul_lo_u32 {v(lo0)}, {v(c[0])}, {s(PM0)}",
-              f"v_mul_hi_u32 {v(hi1)}, {v(c[2])}, {s(PM1)}", f"v_mul_lo_u32 {v(lo1)}, {v(c[2])}, {s(PM1)}",
+            # one v_mad_u64_u32 per product (hi:lo in an aligned pair), not a mul_hi + mul_lo
+            lo0, hi0, lo1, hi1 = XB, XB + 1, XB + 2, XB + 3
+            g(f"v_mad_u64_u32 {vr(lo0, 2)}, {sr(SX, 2)}, {v(c[0])}, {s(PM0)}, 0",
+              f"v_mad_u64_u32 {vr(lo1, 2)}, {sr(SX, 2)}, {v(c[2])}, {s(PM1)}, 0",
               # n0 = hi1 ^ c1 ^ k0 ; n2 = hi0 ^ c3 ^ k1 ; c = (n0, lo1, n2, lo0)
               f"v_xor_b32_e32 {v(c[0])}, {s(PK0)}, {v(hi1)}", f"v_xor_b32_e32 {v(c[0])}, {v(c[0])}, {v(c[1])}",
               f"v_xor_b32_e32 {v(c[2])}, {s(PK1)}, {v(hi0)}", f"v_xor_b32_e32 {v(c[2])}, {v(c[2])}, {v(c[3])}",
