@@ -1675,7 +1675,7 @@ def static_body(code, consts, leaves, forward: bool = True, nlds: int = None) ->
         out.extend(lines)
     out.append(f"s_setpc_b64 {sr(ENDADDR, 2)}")
     if forward:
-        out = forward_copies(out)
+        out = forward_copies(const_fold(out))
     out, live_in = dead_code(out)
     # the files start at zero (mw_interp.h): only what the body reads before writing
     zero = sorted(r for r in live_in if r < 128)
@@ -1785,6 +1785,115 @@ def forward_copies(lines):
                     if d >= TEMP_LO:
                         pending[d] = i
     return [ln for i, ln in enumerate(out) if i not in dead]
+
+
+# ------------------------------------------------ constant operands (static bodies)
+_INT = re.compile(r"^-?(0x[0-9a-fA-F]+|\d+)$")
+_COMMUTE = {"v_xor_b32_e32", "v_or_b32_e32", "v_and_b32_e32", "v_add_u32_e32", "v_add_co_u32_e32",
+            "v_addc_co_u32_e32"}
+_REVERSE = {"v_sub_co_u32_e32": "v_subrev_co_u32_e32", "v_subb_co_u32_e32": "v_subbrev_co_u32_e32",
+            "v_sub_u32_e32": "v_subrev_u32_e32"}
+_CMP_SWAP = {"eq": "eq", "ne": "ne", "lt": "gt", "gt": "lt", "le": "ge", "ge": "le"}
+_FOLD = {"v_xor_b32_e32": lambda a, b: a ^ b, "v_or_b32_e32": lambda a, b: a | b,
+         "v_and_b32_e32": lambda a, b: a & b, "v_add_u32_e32": lambda a, b: a + b}
+
+
+def _imm(tok):
+    t = tok.strip()
+    if not _INT.match(t):
+        return None
+    return int(t, 0) & 0xFFFFFFFF
+
+
+def _inline(x):
+    """gfx9 inline integer constant (VOP3 operands take no literal)"""
+    return x <= 64 or x >= 0xFFFFFFF0
+
+
+def const_fold(lines):
+    """Peephole over a straight-line body: a VGPR loaded with a constant
+    (v_mov_b32 vX, imm - the static handlers' constant operands) is read as
+    that constant where the encoding allows: a VOP2 / VOPC src0 literal
+    (operands swapped or the reversed form used when the constant is src1),
+    an inline constant anywhere; operations on two constants fold and
+    identities (x ^ 0, x | 0, x & -1, x + 0) become copies.  The loads then
+    die (dead_code).  Labels, branches and calls end every constant's scope."""
+    out = list(lines)
+    const = {}
+    for i, ln in enumerate(out):
+        if not ln or ln.startswith(";"):
+            continue
+        op, ops = _operands(ln)
+        if (ln.endswith(":") or op.startswith(("s_cbranch", "s_branch", "s_setpc", "s_swappc", "s_call",
+                                               "s_set_gpr_idx")) or "exec" in ln):
+            const.clear()
+            continue
+        if not op.startswith(("v_", "ds_", "global_", "buffer_")):
+            continue
+        cv = lambda t: const.get(_regs(t)[0]) if (len(_regs(t)) == 1 and t == f"v{_regs(t)[0]}") else None  # noqa
+        new = None
+        if op in _COMMUTE or op in _REVERSE:
+            k = 2 if op.endswith("co_u32_e32") else 1          # src0's index (after dst[, vcc])
+            s0, s1 = ops[k], ops[k + 1]
+            c0, c1 = cv(s0) if _imm(s0) is None else _imm(s0), cv(s1)
+            # the constant bus: a carry-in (vcc) leaves no room for a literal, and
+            # src1 of a VOP2 must stay a VGPR
+            carry_in = op in ("v_addc_co_u32_e32", "v_subb_co_u32_e32")
+            if c1 is not None and (not _regs(s0) or (carry_in and not _inline(c1))):
+                c1 = None
+            if c0 is not None and carry_in and not _inline(c0):
+                c0 = None if _imm(s0) is None else c0
+            if op in _FOLD and c0 is not None and c1 is not None:
+                new = f"v_mov_b32_e32 {ops[0]}, {_lit(_FOLD[op](c0, c1))}"
+            elif c1 is not None and c0 is None:
+                if op in _FOLD and ((c1 == 0 and op != "v_and_b32_e32") or (c1 == 0xFFFFFFFF and op == "v_and_b32_e32")):
+                    new = f"v_mov_b32_e32 {ops[0]}, {s0}"
+                elif op == "v_and_b32_e32" and c1 == 0:
+                    new = f"v_mov_b32_e32 {ops[0]}, 0"
+                elif op in _COMMUTE:
+                    rest = ops[k + 2:]
+                    new = f"{op} " + ", ".join(ops[:k] + [_lit(c1), s0] + rest)
+                elif op in _REVERSE:
+                    rest = ops[k + 2:]
+                    new = f"{_REVERSE[op]} " + ", ".join(ops[:k] + [_lit(c1), s0] + rest)
+            elif c0 is not None and _imm(s0) is None:
+                if op in _FOLD and ((c0 == 0 and op != "v_and_b32_e32") or (c0 == 0xFFFFFFFF and op == "v_and_b32_e32")):
+                    new = f"v_mov_b32_e32 {ops[0]}, {s1}"
+                elif op == "v_and_b32_e32" and c0 == 0:
+                    new = f"v_mov_b32_e32 {ops[0]}, 0"
+                else:
+                    new = f"{op} " + ", ".join(ops[:k] + [_lit(c0)] + ops[k + 1:])
+        elif op.startswith("v_cmp_") and op.endswith("_e32") and len(ops) == 3:
+            s0, s1 = ops[1], ops[2]
+            c0, c1 = (cv(s0) if _imm(s0) is None else None), cv(s1)
+            parts = op.split("_")     # v cmp <cc> <type> e32
+            if c1 is not None and _imm(s0) is None and c0 is None and parts[2] in _CMP_SWAP and _regs(s0):
+                parts[2] = _CMP_SWAP[parts[2]]
+                new = "_".join(parts) + f" {ops[0]}, {_lit(c1)}, {s0}"
+            elif c0 is not None:
+                new = f"{op} {ops[0]}, {_lit(c0)}, {s1}"
+        elif op.startswith(("v_cndmask_b32_e64", "v_or3_b32", "v_add3_u32", "v_lshl_or_b32", "v_alignbit_b32",
+                            "v_bfe_u32", "v_mad_u32_u24", "v_lshl_add_u32")):
+            srcs = []
+            changed = False
+            for t in ops[1:]:
+                c = cv(t)
+                if c is not None and _inline(c):
+                    srcs.append(_lit(c))
+                    changed = True
+                else:
+                    srcs.append(t)
+            if changed:
+                new = f"{op} " + ", ".join([ops[0]] + srcs)
+        if new is not None:
+            out[i] = new
+            op, ops = _operands(new)
+        defs, _ = _defs_uses(op, ops)
+        for d in defs:
+            const.pop(d, None)
+        if op == "v_mov_b32_e32" and len(ops) == 2 and _imm(ops[1]) is not None and len(defs) == 1:
+            const[defs[0]] = _imm(ops[1])
+    return out
 
 
 # ------------------------------------------------ dead-code elimination (static bodies)

@@ -27,7 +27,9 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             # one wave per SIMD: 512 registers per lane, no leaves in LDS
             "w1": {"EXTRA_FLAGS": [], "waves": 1, "lds": 0},
             # a workgroup barrier after every conjunct (jit.CHECK_SYNC): the block's waves fetch the same code
-            "sync": {"EXTRA_FLAGS": [], "CHECK_SYNC": True}}
+            "sync": {"EXTRA_FLAGS": [], "CHECK_SYNC": True},
+            # the division's rare paths without branch weights (in line, as before round 3)
+            "nohint": {"EXTRA_FLAGS": ["-DMW_DIV_NO_HINTS"]}}
 
 
 def main():
