@@ -484,31 +484,60 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], DivCount
 #pragma unroll
     for (int k = 15; k >= 0; --k) u[k] = c ? (k >= m ? u[k - m] : 0u) : u[k];
   }
+  // The eight digit positions as a rolled loop over a sliding window
+  // w = u[j..j+8] (j = 7 - it), the untouched low limbs feeding it from lo[]
+  // and the digits shifting into qq[]: unrolled, this path was ~1 000
+  // instructions at each of C5's 384 division sites, most of the kernel's
+  // code, although a site runs it on every wave or on none.
+  u32 w[9], lo[7], qq[8];
 #pragma unroll
-  for (int j = 7; j >= 0; --j) {
-    q[j] = 0u;
-    if (!MW_ANY(u[j + 8] != 0u || u[j + 7] >= v[7])) continue;  // digit 0 in every lane
-    if (dc) dc->steps += 1u;
-    u32 qd = qdigit_est3(u[j + 8], u[j + 7], u[j + 6], v[7], v[6]);
-    u32 carry = 0, br = 0;
+  for (int k = 0; k < 9; ++k) w[k] = u[7 + k];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const u64 p = (u64)qd * v[k] + carry;
-      carry = (u32)(p >> 32);
-      u[j + k] = subb(u[j + k], (u32)p, br);
-    }
-    u32 hi = u[j + 8] - carry - br;  // 0, or the negative top limb when qd is too large
-    while (MW_RARE(MW_ANY(hi != 0u))) {
-      if (hi != 0u) {
-        u32 c = 0;
+  for (int k = 0; k < 7; ++k) lo[k] = u[k];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) u[j + k] = addc(u[j + k], v[k], c);
-        hi += c;
-        qd -= 1u;
+  for (int k = 0; k < 8; ++k) qq[k] = 0u;
+#pragma unroll 1
+  for (int it = 0; it < 8; ++it) {
+    u32 qd = 0u;
+    if (MW_ANY(w[8] != 0u || w[7] >= v[7])) {  // else digit 0 in every lane
+      if (dc) dc->steps += 1u;
+      qd = qdigit_est3(w[8], w[7], w[6], v[7], v[6]);
+      u32 carry = 0, br = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const u64 p = (u64)qd * v[k] + carry;
+        carry = (u32)(p >> 32);
+        w[k] = subb(w[k], (u32)p, br);
       }
+      u32 hi = w[8] - carry - br;  // 0, or the negative top limb when qd is too large
+      while (MW_RARE(MW_ANY(hi != 0u))) {
+        if (hi != 0u) {
+          u32 c = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) w[k] = addc(w[k], v[k], c);
+          hi += c;
+          qd -= 1u;
+        }
+      }
+      w[8] = 0u;
     }
-    u[j + 8] = 0u;
-    q[j] = qd;
+#pragma unroll
+    for (int k = 7; k > 0; --k) qq[k] = qq[k - 1];
+    qq[0] = qd;
+    if (it < 7) {  // the next window u[j-1 .. j+7]
+#pragma unroll
+      for (int k = 8; k > 0; --k) w[k] = w[k - 1];
+      w[0] = lo[6];
+#pragma unroll
+      for (int k = 6; k > 0; --k) lo[k] = lo[k - 1];
+      lo[0] = 0u;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    q[k] = qq[k];
+    u[k] = w[k];
+    u[k + 8] = 0u;
   }
 #pragma unroll
   for (int st = 0; st < 3; ++st) {  // r = u[0..7] >> 32n
