@@ -90,3 +90,36 @@ def test_const_fold_rules():
     assert out[7] == "v_subb_co_u32_e32 v188, vcc, 0, v177, vcc"         # inline constant: allowed
     assert out[8] == "v_cmp_gt_u32_e32 vcc, 0xaffeaffe, v176"
     assert out[9] == "v_xor_b32_e32 v189, s74, v152"                     # src0 an SGPR: no swap
+
+
+def test_dead_code_liveness():
+    """Backward liveness of asmgen.dead_code: a copy nobody reads goes, a copy
+    read after a forward skip's label stays, file registers are dead at the
+    exit while the template's (v160..v167) are live, a call keeps v128 and up
+    live, an s_set_gpr_idx region reads everything, and registers read before
+    any write come back as live-in."""
+    XA, T = asmgen.XA, asmgen.T
+    body = [
+        f"v_mov_b32_e32 v{XA}, v3",                 # dead: overwritten below before any read
+        f"v_mov_b32_e32 v{XA}, v4",
+        f"v_mov_b32_e32 v{T}, v{XA}",               # read after the label: stays
+        "s_cbranch_vccz LSx1_%=",
+        "v_mov_b32_e32 v5, 0",                      # dead at the exit (file register)
+        "LSx1_%=:",
+        f"v_add_u32_e32 v162, v{T}, v162",          # ALIVE: live at exit
+        "v_mov_b32_e32 v6, v7",                     # dead
+        "s_setpc_b64 s[40:41]",
+    ]
+    out, live_in = asmgen.dead_code(body)
+    assert f"v_mov_b32_e32 v{XA}, v3" not in out
+    assert f"v_mov_b32_e32 v{T}, v{XA}" in out and f"v_mov_b32_e32 v{XA}, v4" in out
+    assert "v_mov_b32_e32 v5, 0" not in out and "v_mov_b32_e32 v6, v7" not in out
+    assert 4 in live_in and 3 not in live_in and 7 not in live_in
+    # a call: every register from v128 up is live across it
+    out, _ = asmgen.dead_code([f"v_mov_b32_e32 v{T + 1}, 5", "s_swappc_b64 s[70:71], s[48:49]",
+                               "s_setpc_b64 s[40:41]"])
+    assert f"v_mov_b32_e32 v{T + 1}, 5" in out
+    # an indexed region reads everything
+    out, live_in = asmgen.dead_code(["v_mov_b32_e32 v9, 1", "s_set_gpr_idx_on s19, gpr_idx(SRC0)",
+                                     "v_mov_b32_e32 v136, v0", "s_set_gpr_idx_off", "s_setpc_b64 s[40:41]"])
+    assert "v_mov_b32_e32 v9, 1" in out and 0 in live_in

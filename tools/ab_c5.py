@@ -29,7 +29,10 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             # a workgroup barrier after every conjunct (jit.CHECK_SYNC): the block's waves fetch the same code
             "sync": {"EXTRA_FLAGS": [], "CHECK_SYNC": True},
             # the division's rare paths without branch weights (in line, as before round 3)
-            "nohint": {"EXTRA_FLAGS": ["-DMW_DIV_NO_HINTS"]}}
+            "nohint": {"EXTRA_FLAGS": ["-DMW_DIV_NO_HINTS"]},
+            # three waves per SIMD (170 registers per lane); LDS leaves cost 8 KiB per slot and
+            # block, so 3 blocks per CU (160 KiB) allow at most 6
+            "w3": {"EXTRA_FLAGS": [], "waves": 3, "lds": 6}, "w3l0": {"EXTRA_FLAGS": [], "waves": 3, "lds": 0}}
 
 
 def main():
