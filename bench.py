@@ -175,7 +175,7 @@ def main():
         # (the in-tree cache, warmed by __graft_entry__.build(), usually makes it 0)
         from mythril_amd import jit
         if args.jit_lds_leaves is None:  # LDS: waves/SIMD x slots x 8 KiB per CU <= 160 KiB
-            args.jit_lds_leaves = {1: 0, 2: 10, 3: 6, 4: 5}[args.jit_waves]
+            args.jit_lds_leaves = {1: 0, 2: jit.BENCH_LDS_LEAVES, 3: 6, 4: 5}[args.jit_waves]
         split = bool(args.jit_split)
         if not split and not jit.is_cached([prog], BENCH_VARIANTS, args.jit_waves, args.jit_lds_leaves,
                                            args.jit_interleave):

@@ -606,7 +606,15 @@ def bench_programs(n_nodes: int = 10000) -> Dict[int, Program]:
     return out
 
 
-def bench_warm_jobs(n_nodes: int = 10000, waves: int = 2, lds_leaves: int = 10, log=print):
+# leaves of the C5 benchmark kernel kept in LDS at 2 waves per SIMD (8 KiB per
+# slot and block). One A/B run (profiles/r3z/ab_c5.json): 10 slots 17.55 ms,
+# 8 17.39 ms, 6 18.12 ms, 12 32.5 ms (one block per CU).  8 is 1 % faster but
+# spills 100 bytes per lane instead of 12: 401 MB of scratch traffic per
+# launch against 32 MB (profiles/r3za) - 10 stays.
+BENCH_LDS_LEAVES = 10
+
+
+def bench_warm_jobs(n_nodes: int = 10000, waves: int = 2, lds_leaves: int = BENCH_LDS_LEAVES, log=print):
     """Independent compile jobs (callables) that put bench.py's C5 kernels in the
     in-tree cache: the single kernel of each density, and the benchmark
     program's split parts (bench.py falls back to them when the single
@@ -623,7 +631,7 @@ def bench_warm_jobs(n_nodes: int = 10000, waves: int = 2, lds_leaves: int = 10, 
     return [lambda: single(24), lambda: single(1), parts]
 
 
-def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 2, lds_leaves: int = 10) -> float:
+def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 2, lds_leaves: int = BENCH_LDS_LEAVES) -> float:
     """Pre-compile bench.py's C5 kernels into the in-tree cache, one job after
     the other (tools/jit_warm.py runs the same jobs in parallel)."""
     t0 = time.perf_counter()

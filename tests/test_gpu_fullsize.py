@@ -31,7 +31,7 @@ from oracle import cdag
 
 pytestmark = pytest.mark.gpu
 
-BENCH_WAVES, BENCH_LDS = 2, 10
+BENCH_WAVES, BENCH_LDS = 2, jit.BENCH_LDS_LEAVES
 SWEEP = 1 << 16
 
 

@@ -32,7 +32,10 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             "nohint": {"EXTRA_FLAGS": ["-DMW_DIV_NO_HINTS"]},
             # three waves per SIMD (170 registers per lane); LDS leaves cost 8 KiB per slot and
             # block, so 3 blocks per CU (160 KiB) allow at most 6
-            "w3": {"EXTRA_FLAGS": [], "waves": 3, "lds": 6}, "w3l0": {"EXTRA_FLAGS": [], "waves": 3, "lds": 0}}
+            "w3": {"EXTRA_FLAGS": [], "waves": 3, "lds": 6}, "w3l0": {"EXTRA_FLAGS": [], "waves": 3, "lds": 0},
+            # two waves per SIMD with fewer / more leaves in LDS than the default 10
+            "l6": {"EXTRA_FLAGS": [], "lds": 6}, "l8": {"EXTRA_FLAGS": [], "lds": 8},
+            "l12": {"EXTRA_FLAGS": [], "lds": 12}}
 
 
 def main():

@@ -16,16 +16,16 @@ from mythril_amd.synth import build_c5  # noqa: E402
 def main():
     syn = build_c5(hostemu.term_values)
     if "--compile-only" in sys.argv:
-        jit.compile_parts(compile_program(syn.conjuncts), "x", waves=2, lds_leaves=10)
+        jit.compile_parts(compile_program(syn.conjuncts), "x", waves=2, lds_leaves=jit.BENCH_LDS_LEAVES)
         return
     w = syn.witness_index
     p = compile_program(syn.conjuncts)
     dev = Device(0)
     interp = dev.load(p)
     special = dev.load(p)
-    jit.attach(dev, [special], variants="x", waves=2, lds_leaves=10)
+    jit.attach(dev, [special], variants="x", waves=2, lds_leaves=jit.BENCH_LDS_LEAVES)
     split = dev.load(p)
-    jit.attach(dev, [split], variants="x", waves=2, lds_leaves=10, split=True)
+    jit.attach(dev, [split], variants="x", waves=2, lds_leaves=jit.BENCH_LDS_LEAVES, split=True)
     vi, _ = dev.eval_generated(interp, syn.seed, w, 1, trace=False)
     vs, _ = dev.eval_generated(special, syn.seed, w, 1, trace=False)
     vp, _ = dev.eval_generated(split, syn.seed, w, 1, trace=False)
