@@ -1128,10 +1128,11 @@ def _lit(x: int) -> str:
 class StaticGen(Gen):
     """Gen for one program whose fields are known at generation time."""
 
-    def __init__(self, consts, leaves=None):
+    def __init__(self, consts, leaves=None, pool=None):
         super().__init__()
         self.consts = [int(x) for x in consts]
         self.leaves = [int(x) for x in leaves] if leaves is not None else None
+        self.pool = [int(x) for x in pool] if pool is not None else None
         self.cur = {}
         self.sval = {}          # SGPR -> value this instruction set by width() / nmask()
         self.chain_open = False  # XR holds the acc of a W_CDINS chain
@@ -1309,6 +1310,31 @@ class StaticGen(Gen):
                 for k in range(8):
                     self(f"v_mov_b32_e32 {v(XC + k)}, {v(T + k)}")
             self._canon_static(XC, w)
+            return
+        if bits == 0 and self.pool is not None:
+            # a one-entry pool: the entry is known here (mw_leaf.h leaf_value,
+            # digit 0) - a constant, or the random draw on every lane
+            e = self.pool[poff:poff + (1 if w < 32 else 9)]
+            if w < 32:
+                if e[0] & isa.POOL_NARROW_RANDOM:
+                    self._narrow_random(lid, XC)
+                else:
+                    self(f"v_mov_b32_e32 {v(XC)}, {_lit(e[0])}")
+                if upper:
+                    for k in range(1, 8):
+                        self(f"v_mov_b32_e32 {v(XC + k)}, 0")
+                    self._canon_static(XC, w)
+                else:
+                    self(f"v_and_b32_e32 {v(XC)}, {_lit((1 << w) - 1)}, {v(XC)}")
+            else:
+                if e[0] & 1:
+                    self._wide_random(w, lid)
+                    for k in range(8):
+                        self(f"v_mov_b32_e32 {v(XC + k)}, {v(T + k)}")
+                else:
+                    for k in range(8):
+                        self(f"v_mov_b32_e32 {v(XC + k)}, {_lit(e[1 + k])}")
+                self._canon_static(XC, w)
             return
         dig = T + 6
         self.leaf_digit(li)
@@ -1602,11 +1628,12 @@ def _spill_static(g, name, insn, nlds):
         (g.write_w if n == 8 else g.write_n)(XR)
 
 
-def static_body(code, consts, leaves, forward: bool = True, nlds: int = None) -> list:
+def static_body(code, consts, leaves, forward: bool = True, nlds: int = None, pool=None) -> list:
     """The straight-line body of an assembled kernel for a validated,
     asm-eligible program (code: its instruction words, original encoding;
-    consts and leaves: its constant pool and leaf table)."""
-    g = StaticGen(consts, leaves)
+    consts and leaves: its constant pool and leaf table; pool: its candidate
+    pool words, which lets one-entry pools fold to constants)."""
+    g = StaticGen(consts, leaves, pool)
     names = {c: n for n, c in isa.OPCODES.items()}
     words = [int(x) for x in code]
     out = []
@@ -1832,7 +1859,9 @@ def const_fold(lines):
             continue
         cv = lambda t: const.get(_regs(t)[0]) if (len(_regs(t)) == 1 and t == f"v{_regs(t)[0]}") else None  # noqa
         new = None
-        if op in _COMMUTE or op in _REVERSE:
+        if op == "v_mov_b32_e32" and len(ops) == 2 and cv(ops[1]) is not None:   # a copy of a constant
+            new = f"v_mov_b32_e32 {ops[0]}, {_lit(cv(ops[1]))}"
+        elif op in _COMMUTE or op in _REVERSE:
             k = 2 if op.endswith("co_u32_e32") else 1          # src0's index (after dst[, vcc])
             s0, s1 = ops[k], ops[k + 1]
             c0, c1 = cv(s0) if _imm(s0) is None else _imm(s0), cv(s1)

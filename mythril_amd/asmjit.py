@@ -82,8 +82,8 @@ def source(p: Program) -> Tuple[str, str]:
     name = kernel_name(p)
     body = "\n".join("\t" + ln if not ln.endswith(":") else ln
                      for ln in asmgen.static_body(p.code, p.consts, p.leaves,
-                                                  nlds=asmgen.lds_spill_words(p.n_spill, len(p.pool))
-                                                  )).replace("%=", num)
+                                                  nlds=asmgen.lds_spill_words(p.n_spill, len(p.pool)),
+                                                  pool=p.pool)).replace("%=", num)
     out = text.replace(asmgen.MARKER, body, 1).replace(TEMPLATE_NAME, name)
     return name, out.replace(TEMPLATE_SIG, str(signature(p)), 1)
 
@@ -95,7 +95,7 @@ def assemble(p: Program, cache: bool = True) -> Tuple[bytes, str, float]:
     _, _, thash = _load_template()
     name = kernel_name(p)
     key = hashlib.sha256((thash + name).encode() + p.code.tobytes() + p.consts.tobytes()
-                         + p.leaves.tobytes()).hexdigest()[:24]
+                         + p.leaves.tobytes() + p.pool.tobytes()).hexdigest()[:24]
     path = CACHE / f"{key}.hsaco"
     if cache and path.exists():
         return path.read_bytes(), name, 0.0
