@@ -1290,8 +1290,8 @@ class StaticGen(Gen):
                     self(f"v_lshl_or_b32 {v(dig)}, {v(T + 7)}, {b}, {v(dig)}")
         self.digit_spec = spec
 
-    def inline_leaf(self, li, limb0_only=False):
-        """XC..XC+7 = leaf li's candidate value, its descriptor folded in
+    def inline_leaf(self, li, limb0_only=False, base=XC):
+        """base..base+7 (XC, or a destination slot) = leaf li's candidate value, its descriptor folded in
         (mw_leaf.h leaf_value; the asm interpreter's Lleaf subroutine).
         limb0_only: a narrow leaf whose consumer reads XC alone (the upper
         limbs are left as they are).  The pool digit stays in T+6 for the next
@@ -1301,15 +1301,15 @@ class StaticGen(Gen):
         upper = not (limb0_only and w <= 32)
         if kind not in (1, 2, 3):
             if w <= 32:
-                self._narrow_random(lid, XC)
+                self._narrow_random(lid, base)
                 if upper:
                     for k in range(1, 8):
-                        self(f"v_mov_b32_e32 {v(XC + k)}, 0")
+                        self(f"v_mov_b32_e32 {v(base + k)}, 0")
             else:
                 self._wide_random(w, lid)
                 for k in range(8):
-                    self(f"v_mov_b32_e32 {v(XC + k)}, {v(T + k)}")
-            self._canon_static(XC, w)
+                    self(f"v_mov_b32_e32 {v(base + k)}, {v(T + k)}")
+            self._canon_static(base, w)
             return
         if bits == 0 and self.pool is not None:
             # a one-entry pool: the entry is known here (mw_leaf.h leaf_value,
@@ -1317,24 +1317,24 @@ class StaticGen(Gen):
             e = self.pool[poff:poff + (1 if w < 32 else 9)]
             if w < 32:
                 if e[0] & isa.POOL_NARROW_RANDOM:
-                    self._narrow_random(lid, XC)
+                    self._narrow_random(lid, base)
                 else:
-                    self(f"v_mov_b32_e32 {v(XC)}, {_lit(e[0])}")
+                    self(f"v_mov_b32_e32 {v(base)}, {_lit(e[0])}")
                 if upper:
                     for k in range(1, 8):
-                        self(f"v_mov_b32_e32 {v(XC + k)}, 0")
-                    self._canon_static(XC, w)
+                        self(f"v_mov_b32_e32 {v(base + k)}, 0")
+                    self._canon_static(base, w)
                 else:
-                    self(f"v_and_b32_e32 {v(XC)}, {_lit((1 << w) - 1)}, {v(XC)}")
+                    self(f"v_and_b32_e32 {v(base)}, {_lit((1 << w) - 1)}, {v(base)}")
             else:
                 if e[0] & 1:
                     self._wide_random(w, lid)
                     for k in range(8):
-                        self(f"v_mov_b32_e32 {v(XC + k)}, {v(T + k)}")
+                        self(f"v_mov_b32_e32 {v(base + k)}, {v(T + k)}")
                 else:
                     for k in range(8):
-                        self(f"v_mov_b32_e32 {v(XC + k)}, {_lit(e[1 + k])}")
-                self._canon_static(XC, w)
+                        self(f"v_mov_b32_e32 {v(base + k)}, {_lit(e[1 + k])}")
+                self._canon_static(base, w)
             return
         dig = T + 6
         self.leaf_digit(li)
@@ -1343,34 +1343,34 @@ class StaticGen(Gen):
         rnd = self.L("lr")
         done = self.L("ld")
         if w < 32:
-            self(f"v_lshl_add_u32 {v(T + 5)}, {v(dig)}, 2, {s(S[6])}", f"ds_read_b32 {v(XC)}, {v(T + 5)}")
+            self(f"v_lshl_add_u32 {v(T + 5)}, {v(dig)}, 2, {s(S[6])}", f"ds_read_b32 {v(base)}, {v(T + 5)}")
             if upper:
                 for k in range(1, 8):
-                    self(f"v_mov_b32_e32 {v(XC + k)}, 0")
+                    self(f"v_mov_b32_e32 {v(base + k)}, 0")
             # the random draw only when a lane's entry says RANDOM (bit 31): with
             # interleaved digits most waves pick one entry for all their lanes
-            self("s_waitcnt lgkmcnt(0)", f"v_cmp_gt_i32_e32 vcc, 0, {v(XC)}", "s_nop 1",
+            self("s_waitcnt lgkmcnt(0)", f"v_cmp_gt_i32_e32 vcc, 0, {v(base)}", "s_nop 1",
                  f"s_cbranch_vccz {done}", f"s_mov_b64 {sr(MSK, 2)}, vcc")
             self._narrow_random(lid, T)
-            self(f"v_cndmask_b32_e64 {v(XC)}, {v(XC)}, {v(T)}, {sr(MSK, 2)}")
+            self(f"v_cndmask_b32_e64 {v(base)}, {v(base)}, {v(T)}, {sr(MSK, 2)}")
         else:
             self(f"v_mov_b32_e32 {v(T + 5)}, 36", f"v_mad_u32_u24 {v(T + 5)}, {v(dig)}, {v(T + 5)}, {s(S[6])}",
                  f"ds_read_b32 {v(T + 4)}, {v(T + 5)}")
             for k in range(4):
-                self(f"ds_read2_b32 {vr(XC + 2 * k, 2)}, {v(T + 5)} offset0:{1 + 2 * k} offset1:{2 + 2 * k}")
+                self(f"ds_read2_b32 {vr(base + 2 * k, 2)}, {v(T + 5)} offset0:{1 + 2 * k} offset1:{2 + 2 * k}")
             self("s_waitcnt lgkmcnt(0)", f"v_and_b32_e32 {v(T + 4)}, 1, {v(T + 4)}",
                  f"v_cmp_ne_u32_e32 vcc, 0, {v(T + 4)}", "s_nop 1", f"s_cbranch_vccz {done}",
                  f"s_mov_b64 {sr(MSK, 2)}, vcc")
             self._wide_random(w, lid)
             self("s_nop 1")
             for k in range(8):
-                self(f"v_cndmask_b32_e64 {v(XC + k)}, {v(XC + k)}, {v(T + k)}, {sr(MSK, 2)}")
+                self(f"v_cndmask_b32_e64 {v(base + k)}, {v(base + k)}, {v(T + k)}, {sr(MSK, 2)}")
         self.label(done)
         del rnd
         if upper:
-            self._canon_static(XC, w)
+            self._canon_static(base, w)
         elif w < 32:
-            self(f"v_and_b32_e32 {v(XC)}, {_lit((1 << w) - 1)}, {v(XC)}")
+            self(f"v_and_b32_e32 {v(base)}, {_lit((1 << w) - 1)}, {v(base)}")
 
     def _canon_static(self, base, wv):
         if wv >= 256:
@@ -1688,8 +1688,11 @@ def static_body(code, consts, leaves, forward: bool = True, nlds: int = None, po
         elif name in ("LEAF_W", "LEAF_N"):
             g.chain_open = False
             g.summary_b = None
-            g.inline_leaf(insn[3], limb0_only=name == "LEAF_N")
-            (g.write_w if name == "LEAF_W" else g.write_n)(XC)
+            if name == "LEAF_W":   # straight into the destination slot: no copy
+                g.inline_leaf(insn[3], base=W0 + 8 * g._dst()[0])
+            else:
+                g.inline_leaf(insn[3], limb0_only=True)
+                g.write_n(XC)
         else:
             g.chain_open = False
             g.summary_b = None
