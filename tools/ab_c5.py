@@ -35,7 +35,11 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             "w3": {"EXTRA_FLAGS": [], "waves": 3, "lds": 6}, "w3l0": {"EXTRA_FLAGS": [], "waves": 3, "lds": 0},
             # two waves per SIMD with fewer / more leaves in LDS than the default 10
             "l6": {"EXTRA_FLAGS": [], "lds": 6}, "l8": {"EXTRA_FLAGS": [], "lds": 8},
-            "l12": {"EXTRA_FLAGS": [], "lds": 12}}
+            "l12": {"EXTRA_FLAGS": [], "lds": 12},
+            # LLVM scheduler choices
+            "ilp": {"EXTRA_FLAGS": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]},
+            "bias0": {"EXTRA_FLAGS": ["-mllvm", "-amdgpu-schedule-metric-bias=0"]},
+            "trackers": {"EXTRA_FLAGS": ["-mllvm", "-amdgpu-use-amdgpu-trackers"]}}
 
 
 def main():
