@@ -1937,6 +1937,7 @@ DCE_REGS = frozenset(range(0, 128)) | frozenset(range(XA, XA + 8)) | frozenset(r
     | frozenset(range(XR, T + 8))
 _ALL_V = frozenset(range(256))
 EXIT_LIVE = _ALL_V - DCE_REGS
+_PHILOX_DEFS = frozenset(range(T, T + 8))
 # VALU forms with no effect besides their VGPR result (no vcc / SGPR write)
 _PURE = ("v_mov_b32", "v_mov_b32_e32", "v_mov_b32_e64", "v_mov_b64", "v_cndmask_b32_e32", "v_cndmask_b32_e64",
          "v_and_b32_e32", "v_or_b32_e32", "v_xor_b32_e32", "v_or3_b32", "v_lshl_or_b32", "v_bfe_u32",
@@ -2002,6 +2003,12 @@ def dead_code(lines):
             continue
         if op == "s_setpc_b64":
             live = set(EXIT_LIVE)
+            continue
+        if op == "s_swappc_b64" and ops[1:] == [sr(PHILOXADDR, 2)]:
+            # Lphilox (philox_sub): writes T..T+7 on every path, reads the
+            # candidate index (CLO, CHI) and the template's registers
+            live.difference_update(_PHILOX_DEFS)
+            live |= EXIT_LIVE
             continue
         if op.startswith(("s_swappc", "s_call")):
             live |= _ALL_V - frozenset(range(0, 128))

@@ -115,10 +115,16 @@ def test_dead_code_liveness():
     assert f"v_mov_b32_e32 v{T}, v{XA}" in out and f"v_mov_b32_e32 v{XA}, v4" in out
     assert "v_mov_b32_e32 v5, 0" not in out and "v_mov_b32_e32 v6, v7" not in out
     assert 4 in live_in and 3 not in live_in and 7 not in live_in
-    # a call: every register from v128 up is live across it
-    out, _ = asmgen.dead_code([f"v_mov_b32_e32 v{T + 1}, 5", "s_swappc_b64 s[70:71], s[48:49]",
+    # an unknown call: every register from v128 up is live across it
+    out, _ = asmgen.dead_code([f"v_mov_b32_e32 v{T + 1}, 5", "s_swappc_b64 s[68:69], s[44:45]",
                                "s_setpc_b64 s[40:41]"])
     assert f"v_mov_b32_e32 v{T + 1}, 5" in out
+    # the Philox subroutine writes T..T+7 and reads only the candidate index
+    out, _ = asmgen.dead_code([f"v_mov_b32_e32 v{T + 1}, 5", f"v_mov_b32_e32 v{XA}, 5",
+                               "s_swappc_b64 s[70:71], s[48:49]", f"v_mov_b32_e32 v{T + 2}, v{XA}",
+                               f"v_add_u32_e32 v162, v{T + 2}, v162", "s_setpc_b64 s[40:41]"])
+    assert f"v_mov_b32_e32 v{T + 1}, 5" not in out      # overwritten by the subroutine
+    assert f"v_mov_b32_e32 v{XA}, 5" in out             # read after the call
     # an indexed region reads everything
     out, live_in = asmgen.dead_code(["v_mov_b32_e32 v9, 1", "s_set_gpr_idx_on s19, gpr_idx(SRC0)",
                                      "v_mov_b32_e32 v136, v0", "s_set_gpr_idx_off", "s_setpc_b64 s[40:41]"])
