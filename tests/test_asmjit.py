@@ -129,3 +129,18 @@ def test_dead_code_liveness():
     out, live_in = asmgen.dead_code(["v_mov_b32_e32 v9, 1", "s_set_gpr_idx_on s19, gpr_idx(SRC0)",
                                      "v_mov_b32_e32 v136, v0", "s_set_gpr_idx_off", "s_setpc_b64 s[40:41]"])
     assert "v_mov_b32_e32 v9, 1" in out and 0 in live_in
+
+
+def test_one_entry_pool_leaves_fold():
+    """C4's calldata bytes have one-entry pools: with the pool words in hand
+    the static body reads no pool entry for them and loads the constant."""
+    from mythril_amd.engine import prepare
+    from mythril_amd.smt2 import parse_file
+    s = parse_file(os.path.join(ROOT, "tests", "golden", "solver_log", "c4_wallet_onlyowner.smt2"))
+    p = prepare(s.asserts, s.ctx).program
+    nl = asmgen.lds_spill_words(p.n_spill, len(p.pool))
+    without = asmgen.static_body(p.code, p.consts, p.leaves, nlds=nl)
+    folded = asmgen.static_body(p.code, p.consts, p.leaves, nlds=nl, pool=p.pool)
+    reads = lambda body: sum(1 for ln in body if ln.startswith("ds_read"))   # noqa: E731
+    assert reads(folded) < reads(without)
+    assert sum(1 for ln in folded if ln.startswith("v_")) < sum(1 for ln in without if ln.startswith("v_"))
