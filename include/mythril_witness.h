@@ -17,12 +17,15 @@
  * Conventions: every call returns 0 on success or a negative MG_E* code; the
  * message for the calling thread is in mg_last_error().  The caller owns all
  * host buffers (copied in/out); program handles are library-owned until
- * mg_prog_free.  Nothing throws across the ABI.  A context serialises its
- * calls.  Lifetimes: the library keeps a registry of live contexts and
- * programs.  mg_free also frees every program still loaded in that context;
- * mg_prog_free / mg_free of a handle that is not live (already freed, freed
- * with its context, or never returned by the library) return MG_E_ARG without
- * touching it, and mg_search / mg_eval reject such program handles.  Programs are validated on load (slot ranges, constant offsets,
+ * mg_prog_free.  Nothing throws across the ABI.
+ * Lifetimes and threads (mythril_amd/csrc/mw_handles.h): a handle is an opaque
+ * id, never an address, and ids are never reused.  Calls on one context are
+ * serialised; calls may come from any thread.  mg_free also frees every
+ * program still loaded in that context, after the call in flight on it (from
+ * another thread) has finished.  A handle that is not live (already freed,
+ * freed with its context, never returned by the library) is refused with
+ * MG_E_ARG by every entry point, also when it is freed by another thread
+ * while the call waits for the context.  Programs are validated on load (slot ranges, constant offsets,
  * opcodes) so a malformed program can never be launched.
  */
 #ifndef MYTHRIL_WITNESS_H
@@ -75,7 +78,7 @@ typedef struct {
   /* Wide divisions (mw_alu.h udivrem8) take one of three paths per wave; each
    * count is (events per wave) x (valid lanes of that wave), summed.  bench.py
    * and compiler.Program.executed_ops price the executed division work from
-   * them (tests/test_gpu_divcount.py checks them against oracle/c). */
+   * them (tests/test_gpu_fullsize.py and tests/test_divcount.py check them against oracle/c). */
   uint64_t lane_div_steps;    /* schoolbook digit positions run (some lane's digit nonzero) */
   uint64_t lane_div_full;     /* one-digit path: every lane's divisor full width */
   uint64_t lane_div_short;    /* short division: every lane's divisor one limb */

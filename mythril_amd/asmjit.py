@@ -6,7 +6,7 @@ kernel with the program itself in place of the dispatch loop: every
 instruction is its handler instantiated with literal registers and constants
 (mythril_amd/asmgen.py static_body).  The template - prologue, chunk loop,
 result protocol, leaf subroutines - is compiled once by hipcc at build time
-(csrc/mw_asmjit_shell.hip -> build/asmjit/template.s); here the program's body
+(csrc/mw_asmjit_shell.hip -> lib/asmjit_template.s, package data); here the program's body
 replaces its marker line and llvm-mc + ld.lld turn the text into a code
 object, about 1 ms per hundred instructions, where hipcc's specialised
 kernels (mythril_amd/jit.py) take seconds to minutes.  Results are the
@@ -31,14 +31,40 @@ from . import asmgen, isa
 from .compiler import Program
 from .jit import signature
 
-ROOT = Path(__file__).resolve().parent.parent
-TEMPLATE = ROOT / "build" / "asmjit" / "template.s"
-CACHE = ROOT / "build" / "asmjit" / "cache"
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+# shipped with the package (setup.py package_data), beside the product library
+TEMPLATE = PKG / "lib" / "asmjit_template.s"
+# in a source tree: build/asmjit/cache; installed: the user's cache directory
+CACHE = Path(os.environ.get("MYTHRIL_AMD_ASMJIT_CACHE") or (
+    ROOT / "build" / "asmjit" / "cache" if (ROOT / "setup.py").exists()
+    else Path.home() / ".cache" / "mythril_amd" / "asmjit"))
 LLVM_BIN = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / "llvm" / "bin"
 TEMPLATE_NAME = "mwa_TEMPLATE"
 TEMPLATE_SIG = str(0x0123456789ABCDEF)   # the shell's placeholder signature, as the .s prints it
 
 _template: Optional[Tuple[str, str, str]] = None   # (text, asm-statement number, hash)
+_generator: Optional[str] = None
+
+
+def generator_hash() -> str:
+    """Hash of everything that turns a program into assembly text besides the
+    template: the body generator's sources and the assembler's version.  Part
+    of the on-disk cache key, so a changed generator never reuses a stale
+    code object."""
+    global _generator
+    if _generator is None:
+        h = hashlib.sha256()
+        here = Path(__file__).resolve().parent
+        for f in ("asmgen.py", "asmjit.py", "isa.py"):
+            h.update((here / f).read_bytes())
+        try:
+            r = subprocess.run([str(LLVM_BIN / "llvm-mc"), "--version"], capture_output=True, text=True)
+            h.update(r.stdout.encode())
+        except OSError:
+            pass
+        _generator = h.hexdigest()[:16]
+    return _generator
 
 
 class Unavailable(RuntimeError):
@@ -60,12 +86,21 @@ def _load_template() -> Tuple[str, str, str]:
     return _template
 
 
-def available() -> bool:
+def why_unavailable() -> Optional[str]:
+    """None when programs can be assembled, else the reason they stay on the
+    asm interpreter (missing template or assembler)."""
     try:
         _load_template()
-    except Unavailable:
-        return False
-    return (LLVM_BIN / "llvm-mc").exists() and (LLVM_BIN / "ld.lld").exists()
+    except Unavailable as e:
+        return str(e)
+    for tool in ("llvm-mc", "ld.lld"):
+        if not (LLVM_BIN / tool).exists():
+            return f"{LLVM_BIN / tool} missing (ROCm's LLVM tools)"
+    return None
+
+
+def available() -> bool:
+    return why_unavailable() is None
 
 
 def eligible(p: Program) -> bool:
@@ -94,7 +129,7 @@ def assemble(p: Program, cache: bool = True) -> Tuple[bytes, str, float]:
         raise Unavailable("program has opcodes or leaf kinds the asm engines lack")
     _, _, thash = _load_template()
     name = kernel_name(p)
-    key = hashlib.sha256((thash + name).encode() + p.code.tobytes() + p.consts.tobytes()
+    key = hashlib.sha256((thash + generator_hash() + name).encode() + p.code.tobytes() + p.consts.tobytes()
                          + p.leaves.tobytes() + p.pool.tobytes()).hexdigest()[:24]
     path = CACHE / f"{key}.hsaco"
     if cache and path.exists():

@@ -3,7 +3,7 @@
   mythril_amd/lib/libmythril_witness.so   product: gfx950 kernels + C-ABI
   build/host/libmw_host_emu.so            test-only CPU build of the same interpreter
   oracle/build/liboracle.so               test-only C restatement (built by oracle/Makefile)
-  build/asmjit/template.s                 the assembled kernels' template (gfx950 assembly,
+  mythril_amd/lib/asmjit_template.s       the assembled kernels' template (gfx950 assembly,
                                           mythril_amd/asmjit.py fills in a program's body)
 
 Usage: python -m mythril_amd.build [--force]
@@ -24,8 +24,8 @@ ARCH = os.environ.get("MW_OFFLOAD_ARCH", "gfx950")
 DEVICE_SRCS = ["mw_kernels.hip", "mw_validate.cpp"]
 HOST_SRCS = ["mw_host_emu.cpp", "mw_validate.cpp"]
 HEADERS = ["mw_isa.h", "mw_prog.h", "mw_alu.h", "mw_interp.h", "mw_leaf.h", "mw_keccak.h", "mw_asm_interp.inc",
-           "mw_asm_abi.h"]
-ASMJIT_TEMPLATE = ROOT / "build" / "asmjit" / "template.s"
+           "mw_asm_abi.h", "mw_handles.h"]
+ASMJIT_TEMPLATE = ROOT / "mythril_amd" / "lib" / "asmjit_template.s"   # package data
 
 
 def _hipcc() -> str:

@@ -17,12 +17,12 @@
 #include <cstring>
 #include <mutex>
 #include <string>
-#include <unordered_set>
 #include <vector>
 
 #include "../../include/mythril_witness.h"
 #include "mw_asm_abi.h"
 #include "mw_asm_interp.inc"
+#include "mw_handles.h"
 #include "mw_interp.h"
 #include "mw_keccak.h"
 #include "mw_leaf.h"
@@ -342,7 +342,7 @@ double now_ms() {
 
 }  // namespace
 
-struct mg_ctx {
+struct Ctx {
   int dev = 0;
   int ncu = 256;
   hipStream_t stream = nullptr;
@@ -358,11 +358,13 @@ struct mg_ctx {
   size_t nprogs_cap = 0;
   AsmArgs* d_asmargs = nullptr;  // AsmArgs records: [0] the asm interpreter's launch, [1..] assembled kernels'
   size_t nasmargs_cap = 0;
-  std::mutex mu;
+  std::mutex mu;                 // serialises the calls on this context (mw_handles.h)
+  bool dead = false;             // freed by mg_free (guarded by mu)
 };
 
-struct mg_prog {
-  mg_ctx* ctx = nullptr;
+struct Prog {
+  std::shared_ptr<Ctx> ctx;     // keeps the context's record alive while this program's is
+  bool dead = false;            // resources released (guarded by ctx->mu)
   u32* d_buf = nullptr;
   ProgDev dev{};
   mg_prog_desc desc{};
@@ -423,9 +425,9 @@ u64 prog_signature(const mg_prog_desc* d) {
 // passing alive bits through c->d_alive.
 constexpr u64 kAliveSlice = 1ull << 24;
 
-int launch_part(mg_ctx* c, const mg_prog* p, size_t k, u64 seed, u64 begin, u64 count, u32 flags, u64* d_min,
+int launch_part(Ctx* c, const Prog* p, size_t k, u64 seed, u64 begin, u64 count, u32 flags, u64* d_min,
                 u32* d_verdict, u32 stage) {
-  const mg_prog::Part& q = p->parts[k];
+  const Prog::Part& q = p->parts[k];
   hipFunction_t f = ((flags & MW_FLAG_EARLY_EXIT) && q.fe) ? q.fe : q.fx;
   const u64 nchunks = (count + kBlock - 1) / kBlock;
   const u64 kMaxBlocks = 1ull << 30;
@@ -444,7 +446,7 @@ int launch_part(mg_ctx* c, const mg_prog* p, size_t k, u64 seed, u64 begin, u64 
   return 0;
 }
 
-int launch_jit(mg_ctx* c, const mg_prog* p, u64 seed, u64 begin, u64 count, u32 flags, u64* d_min,
+int launch_jit(Ctx* c, const Prog* p, u64 seed, u64 begin, u64 count, u32 flags, u64* d_min,
                u32* d_verdict) {
   const size_t np = p->parts.size();
   if (np == 1) return launch_part(c, p, 0, seed, begin, count, flags, d_min, d_verdict, 3u);
@@ -467,32 +469,47 @@ int launch_jit(mg_ctx* c, const mg_prog* p, u64 seed, u64 begin, u64 count, u32 
   return 0;
 }
 
-// Registry of live handles (include/mythril_witness.h, "Lifetimes"): a handle
-// is dereferenced only while it is registered, so freeing in the wrong order or
-// twice is an MG_E_ARG, never a use-after-free.
-std::mutex g_reg_mu;
-std::unordered_set<const mg_ctx*> g_ctxs;
-std::unordered_set<const mg_prog*> g_progs;
+// Live handles (include/mythril_witness.h, "Lifetimes"; the protocol is
+// mw_handles.h): handles are ids that are never reused, resolved to
+// reference-counted records, and every call re-checks them under the
+// context's lock, so freeing in the wrong order, twice, or while another
+// thread uses the handle is an MG_E_ARG, never a use-after-free.
+mw::Registry<Ctx, Prog> g_reg;
+using CallG = mw::Call<Ctx, Prog>;
 
-bool ctx_live(const mg_ctx* c) {
-  std::lock_guard<std::mutex> lk(g_reg_mu);
-  return c && g_ctxs.count(c) != 0;
+inline u64 hid(const void* h) { return (u64)(uintptr_t)h; }
+
+// the device resources of a program (its context's mu held)
+void release_prog(Prog& p) {
+  hipSetDevice(p.ctx->dev);
+  p.unload();
+  if (p.d_buf) hipFree(p.d_buf);
+  p.d_buf = nullptr;
 }
 
-bool prog_live(const mg_prog* p) {
-  std::lock_guard<std::mutex> lk(g_reg_mu);
-  return p && g_progs.count(p) != 0;
+void release_ctx(Ctx& c) {
+  hipSetDevice(c.dev);
+  if (c.stream) hipStreamSynchronize(c.stream);
+  if (c.d_spill) hipFree(c.d_spill);
+  if (c.d_min) hipFree(c.d_min);
+  if (c.d_progs) hipFree(c.d_progs);
+  if (c.d_asmargs) hipFree(c.d_asmargs);
+  if (c.d_counter) hipFree(c.d_counter);
+  if (c.d_alive) hipFree(c.d_alive);
+  if (c.e0) hipEventDestroy(c.e0);
+  if (c.e1) hipEventDestroy(c.e1);
+  if (c.stream) hipStreamDestroy(c.stream);
+  c.d_spill = nullptr;
+  c.d_min = nullptr;
+  c.d_progs = nullptr;
+  c.d_asmargs = nullptr;
+  c.d_counter = nullptr;
+  c.d_alive = nullptr;
+  c.e0 = c.e1 = nullptr;
+  c.stream = nullptr;
 }
 
-// frees a program that has already left the registry
-void destroy_prog(mg_prog* p) {
-  hipSetDevice(p->ctx->dev);
-  p->unload();
-  if (p->d_buf) hipFree(p->d_buf);
-  delete p;
-}
-
-int ensure_asmargs(mg_ctx* c, size_t n) {
+int ensure_asmargs(Ctx* c, size_t n) {
   if (n <= c->nasmargs_cap) return 0;
   if (c->d_asmargs) HIPCHK(hipFree(c->d_asmargs));
   c->d_asmargs = nullptr;
@@ -505,7 +522,7 @@ int ensure_asmargs(mg_ctx* c, size_t n) {
 // One launch of a program's assembled kernel: the asm interpreter's grid (x:
 // chunk stride, one program) and records (mw_asm_abi.h); its LDS is a fixed
 // 80 KiB array in the kernel (mw_asmjit_shell.hip).
-int launch_assembled(mg_ctx* c, const mg_prog* p, u32 gx, const ProgDev* dprog, const AsmArgs* dargs, u64* dmin,
+int launch_assembled(Ctx* c, const Prog* p, u32 gx, const ProgDev* dprog, const AsmArgs* dargs, u64* dmin,
                      u32 nlds) {
   u64* ctr = c->d_counter;
   void* args[] = {&dprog, &dargs, &dmin, &ctr, &nlds};
@@ -513,7 +530,7 @@ int launch_assembled(mg_ctx* c, const mg_prog* p, u32 gx, const ProgDev* dprog, 
   return 0;
 }
 
-int ensure_spill(mg_ctx* c, size_t bytes) {
+int ensure_spill(Ctx* c, size_t bytes) {
   if (bytes <= c->spill_bytes) return 0;
   if (c->d_spill) HIPCHK(hipFree(c->d_spill));
   c->d_spill = nullptr;
@@ -523,7 +540,7 @@ int ensure_spill(mg_ctx* c, size_t bytes) {
   return 0;
 }
 
-int ensure_min(mg_ctx* c, size_t n) {
+int ensure_min(Ctx* c, size_t n) {
   if (n <= c->nmin) return 0;
   if (c->d_min) HIPCHK(hipFree(c->d_min));
   if (c->d_progs) HIPCHK(hipFree(c->d_progs));
@@ -590,7 +607,7 @@ int mg_init(int device, mg_ctx** out) {
   HIPCHK(hipGetDeviceCount(&n));
   if (device < 0 || device >= n) return fail(MG_E_ARG, "no such device");
   HIPCHK(hipSetDevice(device));
-  mg_ctx* c = new mg_ctx();
+  auto c = std::make_shared<Ctx>();
   c->dev = device;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -598,7 +615,7 @@ int mg_init(int device, mg_ctx** out) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
       hipMalloc(&c->d_counter, kCounterWords * sizeof(u64)) != hipSuccess) {
-    delete c;
+    release_ctx(*c);
     return fail(MG_E_HIP, "context setup failed");
   }
   // allow the LDS spill area (up to kLdsSpillWords x 1 KiB) beyond the 64 KiB default
@@ -613,54 +630,28 @@ int mg_init(int device, mg_ctx** out) {
           hipSuccess) {
     (void)hipGetLastError();  // older runtimes: the default limit already covers it
   }
-  {
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    g_ctxs.insert(c);
-  }
-  *out = c;
+  *out = (mg_ctx*)(uintptr_t)g_reg.add_ctx(std::move(c));
   return 0;
 }
 
-int mg_free(mg_ctx* c) {
-  if (!c) return 0;
-  std::vector<mg_prog*> orphans;  // programs still loaded in this context: freed with it
-  {
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    if (!g_ctxs.erase(c)) return fail(MG_E_ARG, "mg_free: not a live context");
-    for (auto it = g_progs.begin(); it != g_progs.end();) {
-      if ((*it)->ctx == c) {
-        orphans.push_back(const_cast<mg_prog*>(*it));
-        it = g_progs.erase(it);
-      } else {
-        ++it;
-      }
-    }
-  }
-  hipSetDevice(c->dev);
-  if (c->stream) hipStreamSynchronize(c->stream);
-  for (mg_prog* p : orphans) destroy_prog(p);
-  hipSetDevice(c->dev);
-  if (c->stream) hipStreamSynchronize(c->stream);
-  if (c->d_spill) hipFree(c->d_spill);
-  if (c->d_min) hipFree(c->d_min);
-  if (c->d_progs) hipFree(c->d_progs);
-  if (c->d_asmargs) hipFree(c->d_asmargs);
-  if (c->d_counter) hipFree(c->d_counter);
-  if (c->d_alive) hipFree(c->d_alive);
-  if (c->e0) hipEventDestroy(c->e0);
-  if (c->e1) hipEventDestroy(c->e1);
-  if (c->stream) hipStreamDestroy(c->stream);
-  delete c;
+int mg_free(mg_ctx* h) {
+  if (!h) return 0;
+  // programs still loaded in this context are freed with it; a call in flight
+  // on another thread finishes first (mw_handles.h free_ctx)
+  if (!mw::free_ctx(g_reg, hid(h), release_prog, release_ctx)) return fail(MG_E_ARG, "mg_free: not a live context");
   return 0;
 }
 
-int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
-  if (!c || !d || !out) return fail(MG_E_ARG, "null argument");
+int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
+  if (!h || !d || !out) return fail(MG_E_ARG, "null argument");
   *out = nullptr;
-  if (!ctx_live(c)) return fail(MG_E_ARG, "mg_prog_load: not a live context");
+  std::shared_ptr<Ctx> cref = g_reg.ctx(hid(h));
+  if (!cref) return fail(MG_E_ARG, "mg_prog_load: not a live context");
   int rc = mg_validate_desc(d);
   if (rc) return rc;
+  Ctx* c = cref.get();
   std::lock_guard<std::mutex> lk(c->mu);
+  if (c->dead) return fail(MG_E_ARG, "mg_prog_load: the context was freed during the call");
   HIPCHK(hipSetDevice(c->dev));
   // constants padded to >= MW_KPAD words: the interpreter's branch-free narrow
   // operand fetch reads cpool[slot] (slot < 64) before selecting the register
@@ -669,24 +660,23 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
   const bool asm_ok = asm_eligible(d);
   const size_t na = asm_ok ? nc + 8 : 0;   // + the block after END the dispatch prefetches
   const size_t total = nc + nk + nl + np + na;
-  mg_prog* p = new mg_prog();
-  p->ctx = c;
+  auto p = std::make_shared<Prog>();
+  p->ctx = cref;
   p->desc = *d;
   p->ops_per_eval = d->ops_per_eval;
   p->sig = prog_signature(d);
   if (hipMalloc(&p->d_buf, total * sizeof(u32)) != hipSuccess) {
-    delete p;
+    p->d_buf = nullptr;
     return fail(MG_E_NOMEM, "program upload allocation failed");
   }
-  std::vector<u32> h(total, 0u);
-  std::memcpy(h.data(), d->code, nc * 4);
-  if (d->nconst_words) std::memcpy(h.data() + nc, d->consts, d->nconst_words * 4);
-  if (d->nleaves) std::memcpy(h.data() + nc + nk, d->leaves, d->nleaves * MW_LEAF_WORDS * 4);
-  if (d->npool_words) std::memcpy(h.data() + nc + nk + nl, d->pool, d->npool_words * 4);
-  if (asm_ok) mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, h.data() + nc + nk + nl + np);
-  if (hipMemcpy(p->d_buf, h.data(), total * 4, hipMemcpyHostToDevice) != hipSuccess) {
-    hipFree(p->d_buf);
-    delete p;
+  std::vector<u32> hbuf(total, 0u);
+  std::memcpy(hbuf.data(), d->code, nc * 4);
+  if (d->nconst_words) std::memcpy(hbuf.data() + nc, d->consts, d->nconst_words * 4);
+  if (d->nleaves) std::memcpy(hbuf.data() + nc + nk, d->leaves, d->nleaves * MW_LEAF_WORDS * 4);
+  if (d->npool_words) std::memcpy(hbuf.data() + nc + nk + nl, d->pool, d->npool_words * 4);
+  if (asm_ok) mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, hbuf.data() + nc + nk + nl + np);
+  if (hipMemcpy(p->d_buf, hbuf.data(), total * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    release_prog(*p);
     return fail(MG_E_HIP, "program upload copy failed");
   }
   p->dev.code = p->d_buf;
@@ -704,31 +694,24 @@ int mg_prog_load(mg_ctx* c, const mg_prog_desc* d, mg_prog** out) {
   p->desc.consts = nullptr;
   p->desc.leaves = nullptr;
   p->desc.pool = nullptr;
-  {
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    g_progs.insert(p);
-  }
-  *out = p;
+  *out = (mg_prog*)(uintptr_t)g_reg.add_prog(std::move(p));   // published under c->mu (mw_handles.h)
   return 0;
 }
 
-int mg_prog_free(mg_prog* p) {
-  if (!p) return 0;
-  {
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    if (!g_progs.erase(p)) return fail(MG_E_ARG, "mg_prog_free: not a live program (already freed, or freed with its context)");
-  }
-  std::lock_guard<std::mutex> lk(p->ctx->mu);
-  destroy_prog(p);
+int mg_prog_free(mg_prog* h) {
+  if (!h) return 0;
+  if (!mw::free_prog(g_reg, hid(h), release_prog))
+    return fail(MG_E_ARG, "mg_prog_free: not a live program (already freed, or freed with its context)");
   return 0;
 }
 
-int mg_prog_attach_kernel(mg_prog* p, const void* image, size_t size, const char* name) {
-  if (!p || !image || !size || !name) return fail(MG_E_ARG, "null argument");
+int mg_prog_attach_kernel(mg_prog* h, const void* image, size_t size, const char* name) {
+  if (!h || !image || !size || !name) return fail(MG_E_ARG, "null argument");
   if (std::strlen(name) > 200) return fail(MG_E_ARG, "kernel name too long");
-  if (!prog_live(p)) return fail(MG_E_ARG, "mg_prog_attach_kernel: not a live program");
-  mg_ctx* c = p->ctx;
-  std::lock_guard<std::mutex> lk(c->mu);
+  CallG call;
+  if (const char* why = mw::enter_prog(g_reg, hid(h), call)) return fail(MG_E_ARG, std::string("mg_prog_attach_kernel: ") + why);
+  Ctx* c = call.c.get();
+  Prog* p = call.ps[0].get();
   HIPCHK(hipSetDevice(c->dev));
   hipModule_t mod = nullptr;
   HIPCHK(hipModuleLoadData(&mod, image));
@@ -776,7 +759,7 @@ int mg_prog_attach_kernel(mg_prog* p, const void* image, size_t size, const char
     p->unload();
     p->parts.resize(nparts);
   }
-  mg_prog::Part& q = p->parts[part];
+  Prog::Part& q = p->parts[part];
   if (q.mod) hipModuleUnload(q.mod);
   q.mod = mod;
   q.fx = fx;
@@ -784,23 +767,30 @@ int mg_prog_attach_kernel(mg_prog* p, const void* image, size_t size, const char
   return 0;
 }
 
-int mg_prog_has_kernel(const mg_prog* p) { return prog_live(p) && p->jit_ready() ? 1 : 0; }
+int mg_prog_has_kernel(const mg_prog* h) {
+  CallG call;
+  if (mw::enter_prog(g_reg, hid(h), call)) return 0;
+  return call.ps[0]->jit_ready() ? 1 : 0;
+}
 
-int mg_prog_engine(const mg_prog* p) {
-  if (!prog_live(p)) return fail(MG_E_ARG, "mg_prog_engine: not a live program");
+int mg_prog_engine(const mg_prog* h) {
+  CallG call;
+  if (const char* why = mw::enter_prog(g_reg, hid(h), call)) return fail(MG_E_ARG, std::string("mg_prog_engine: ") + why);
+  const Prog* p = call.ps[0].get();
   if (p->jit_ready()) return 2;
   u32 nlds = 0;   // the engine mg_search gives this program alone (a pool too big for LDS: compiled)
   if (!p->asm_ok || !asm_enabled() || !asm_lds_fit(p->dev.n_spill, p->dev.npool, &nlds)) return 0;
   return p->afn ? 3 : 1;
 }
 
-int mg_prog_attach_asm(mg_prog* p, const void* image, size_t size, const char* name) {
-  if (!p || !image || !size || !name) return fail(MG_E_ARG, "null argument");
+int mg_prog_attach_asm(mg_prog* h, const void* image, size_t size, const char* name) {
+  if (!h || !image || !size || !name) return fail(MG_E_ARG, "null argument");
   if (std::strlen(name) > 200) return fail(MG_E_ARG, "kernel name too long");
-  if (!prog_live(p)) return fail(MG_E_ARG, "mg_prog_attach_asm: not a live program");
+  CallG call;
+  if (const char* why = mw::enter_prog(g_reg, hid(h), call)) return fail(MG_E_ARG, std::string("mg_prog_attach_asm: ") + why);
+  Ctx* c = call.c.get();
+  Prog* p = call.ps[0].get();
   if (!p->asm_ok) return fail(MG_E_PROG, "mg_prog_attach_asm: the program has opcodes the asm engines lack");
-  mg_ctx* c = p->ctx;
-  std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
   hipModule_t mod = nullptr;
   HIPCHK(hipModuleLoadData(&mod, image));
@@ -830,18 +820,18 @@ int mg_prog_attach_asm(mg_prog* p, const void* image, size_t size, const char* n
   return 0;
 }
 
-int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uint64_t begin,
+int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, uint64_t begin,
               uint64_t count, uint32_t flags, uint64_t* out_min_idx, mg_stats* st) {
-  if (!c || !progs || !out_min_idx || nprog == 0) return fail(MG_E_ARG, "null argument");
+  if (!h || !hprogs || !out_min_idx || nprog == 0) return fail(MG_E_ARG, "null argument");
   if (nprog > 65535) return fail(MG_E_ARG, "too many programs per launch");
   if (count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad candidate range");
-  {
-    std::lock_guard<std::mutex> rl(g_reg_mu);
-    if (!g_ctxs.count(c)) return fail(MG_E_ARG, "mg_search: not a live context");
-    for (size_t i = 0; i < nprog; ++i)
-      if (!g_progs.count(progs[i])) return fail(MG_E_ARG, "mg_search: program " + std::to_string(i) + " is not live");
-  }
-  std::lock_guard<std::mutex> lk(c->mu);
+  std::vector<u64> ids(nprog);
+  for (size_t i = 0; i < nprog; ++i) ids[i] = hid(hprogs[i]);
+  CallG call;   // resolved, reference-held and locked for the whole call (mw_handles.h)
+  if (const char* why = mw::enter(g_reg, hid(h), ids.data(), nprog, call)) return fail(MG_E_ARG, std::string("mg_search: ") + why);
+  Ctx* c = call.c.get();
+  std::vector<const Prog*> progs(nprog);
+  for (size_t i = 0; i < nprog; ++i) progs[i] = call.ps[i].get();
   const double t0 = now_ms();
   HIPCHK(hipSetDevice(c->dev));
   (void)hipGetLastError();  // start from a clean error state: launch errors are read back below
@@ -858,7 +848,6 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   u64 ops = 0;
   const bool use_asm = asm_enabled();
   for (size_t i = 0; i < nprog; ++i) {
-    if (!progs[i] || progs[i]->ctx != c) return fail(MG_E_ARG, "program from another context");
     u32 n1 = 0;
     if (progs[i]->jit_ready()) special.push_back(i);
     else if (use_asm && progs[i]->afn && count < (1ull << 40) &&
@@ -1025,11 +1014,10 @@ int mg_search(mg_ctx* c, mg_prog* const* progs, size_t nprog, uint64_t seed, uin
   return 0;
 }
 
-static int eval_common(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncand, uint64_t seed,
+// The eval paths below run inside a call (the context's mu held, handles live).
+static int eval_common(Ctx* c, const Prog* p, const uint32_t* leaves_soa, size_t ncand, uint64_t seed,
                        uint64_t begin, uint32_t* verdict, uint32_t* trace) {
-  if (!c || !p || !verdict || ncand == 0) return fail(MG_E_ARG, "null argument");
-  if (!ctx_live(c) || !prog_live(p) || p->ctx != c) return fail(MG_E_ARG, "eval: not a live context/program pair");
-  std::lock_guard<std::mutex> lk(c->mu);
+  if (!verdict || ncand == 0) return fail(MG_E_ARG, "null argument");
   HIPCHK(hipSetDevice(c->dev));
   (void)hipGetLastError();  // clean error state before the launch below
   const u64 nchunks = (ncand + kBlock - 1) / kBlock;
@@ -1064,25 +1052,28 @@ static int eval_common(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, 
   return 0;
 }
 
-int mg_eval(mg_ctx* c, const mg_prog* p, const uint32_t* leaves_soa, size_t ncand, uint32_t* verdict,
+int mg_eval(mg_ctx* h, const mg_prog* hp, const uint32_t* leaves_soa, size_t ncand, uint32_t* verdict,
             uint32_t* trace) {
-  if (p && !prog_live(p)) return fail(MG_E_ARG, "mg_eval: not a live program");
-  if (p && p->desc.nleaves && p->desc.n_input_rows && !leaves_soa) return fail(MG_E_ARG, "leaves_soa required");
-  if (p && p->desc.nleaves && !p->desc.n_input_rows) return fail(MG_E_ARG, "program has no input rows");
+  if (!h || !hp) return fail(MG_E_ARG, "null argument");
+  const u64 id = hid(hp);
+  CallG call;
+  if (const char* why = mw::enter(g_reg, hid(h), &id, 1, call)) return fail(MG_E_ARG, std::string("mg_eval: ") + why);
+  const Prog* p = call.ps[0].get();
+  if (p->desc.nleaves && p->desc.n_input_rows && !leaves_soa) return fail(MG_E_ARG, "leaves_soa required");
+  if (p->desc.nleaves && !p->desc.n_input_rows) return fail(MG_E_ARG, "program has no input rows");
   static const u32 dummy = 0;
-  return eval_common(c, p, leaves_soa ? leaves_soa : (p && p->desc.nleaves ? nullptr : &dummy), ncand, 0, 0,
+  return eval_common(call.c.get(), p, leaves_soa ? leaves_soa : (p->desc.nleaves ? nullptr : &dummy), ncand, 0, 0,
                      verdict, trace);
 }
 
 // Verdicts of generated candidates on the asm interpreter (mw_search_asm_kernel
 // with a verdict array); 1 = not applicable (the caller uses mw_eval_kernel).
-static int eval_asm(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, size_t count, uint32_t* verdict) {
+static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t count, uint32_t* verdict) {
   if (!asm_enabled() || !p->asm_ok || begin + count < begin || count >= (1ull << 40)) return 1;
   const bool assembled = p->afn != nullptr;   // its assembled kernel, else the asm interpreter
   u32 nlds = 0;
   if (!asm_lds_fit(p->dev.n_spill, p->dev.npool, &nlds)) return 1;
   const size_t lds = (size_t)nlds * kBlock * 4 + (size_t)p->dev.npool * 4;
-  std::lock_guard<std::mutex> lk(c->mu);
   HIPCHK(hipSetDevice(c->dev));
   (void)hipGetLastError();
   int rc = ensure_min(c, 1);
@@ -1131,18 +1122,22 @@ static int eval_asm(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, 
   return 0;
 }
 
-int mg_eval_generated(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin, size_t count,
+int mg_eval_generated(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t begin, size_t count,
                       uint32_t* verdict, uint32_t* trace) {
-  if (p && prog_live(p) && c && ctx_live(c) && p->ctx == c && !p->jit_ready() && !trace && verdict && count) {
+  if (!h || !hp) return fail(MG_E_ARG, "null argument");
+  const u64 id = hid(hp);
+  CallG call;
+  if (const char* why = mw::enter(g_reg, hid(h), &id, 1, call))
+    return fail(MG_E_ARG, std::string("mg_eval_generated: ") + why);
+  Ctx* c = call.c.get();
+  const Prog* p = call.ps[0].get();
+  if (!p->jit_ready() && !trace && verdict && count) {
     const int rc = eval_asm(c, p, seed, begin, count, verdict);
     if (rc != 1) return rc;
   }
-  if (!p || !prog_live(p) || !p->jit_ready() || trace)
-    return eval_common(c, p, nullptr, count, seed, begin, verdict, trace);  // rejects dead handles
+  if (!p->jit_ready() || trace) return eval_common(c, p, nullptr, count, seed, begin, verdict, trace);
   // verdicts only, on the program's specialised kernel
-  if (!c || !verdict || count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad argument");
-  if (!ctx_live(c) || p->ctx != c) return fail(MG_E_ARG, "eval: not a live context/program pair");
-  std::lock_guard<std::mutex> lk(c->mu);
+  if (!verdict || count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad argument");
   HIPCHK(hipSetDevice(c->dev));
   int rc = ensure_min(c, 1);
   if (rc) return rc;
@@ -1165,10 +1160,11 @@ int mg_eval_generated(mg_ctx* c, const mg_prog* p, uint64_t seed, uint64_t begin
   return 0;
 }
 
-int mg_valu_peak(mg_ctx* c, uint32_t mul, double* ops_per_s, double* kernel_ms) {
-  if (!c || !ops_per_s) return fail(MG_E_ARG, "null argument");
-  if (!ctx_live(c)) return fail(MG_E_ARG, "not a live context");
-  std::lock_guard<std::mutex> lk(c->mu);
+int mg_valu_peak(mg_ctx* h, uint32_t mul, double* ops_per_s, double* kernel_ms) {
+  if (!h || !ops_per_s) return fail(MG_E_ARG, "null argument");
+  CallG call;
+  if (const char* why = mw::enter(g_reg, hid(h), nullptr, 0, call)) return fail(MG_E_ARG, std::string("mg_valu_peak: ") + why);
+  Ctx* c = call.c.get();
   HIPCHK(hipSetDevice(c->dev));
   const u32 blocks = (u32)c->ncu * 8, iters = 4096;
   u32* d = nullptr;
@@ -1186,11 +1182,12 @@ int mg_valu_peak(mg_ctx* c, uint32_t mul, double* ops_per_s, double* kernel_ms) 
   return 0;
 }
 
-int mg_keccak256_device(mg_ctx* c, const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len, size_t n,
+int mg_keccak256_device(mg_ctx* h, const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len, size_t n,
                         uint8_t* d_out32, mg_stats* st) {
-  if (!c || (!n)) return fail(MG_E_ARG, "bad argument");
-  if (!ctx_live(c)) return fail(MG_E_ARG, "not a live context");
-  std::lock_guard<std::mutex> lk(c->mu);
+  if (!h || (!n)) return fail(MG_E_ARG, "bad argument");
+  CallG call;
+  if (const char* why = mw::enter(g_reg, hid(h), nullptr, 0, call)) return fail(MG_E_ARG, std::string("mg_keccak256: ") + why);
+  Ctx* c = call.c.get();
   HIPCHK(hipSetDevice(c->dev));
   const double t0 = now_ms();
   const u64 gx = std::min<u64>((n + kBlock - 1) / kBlock, (u64)c->ncu * 16);
@@ -1214,10 +1211,12 @@ int mg_keccak256_device(mg_ctx* c, const uint8_t* d_data, const uint64_t* d_off,
   return 0;
 }
 
-int mg_keccak256(mg_ctx* c, const uint8_t* data, size_t ndata, const uint64_t* off, const uint32_t* len, size_t n,
+int mg_keccak256(mg_ctx* h, const uint8_t* data, size_t ndata, const uint64_t* off, const uint32_t* len, size_t n,
                  uint8_t* out32, mg_stats* st) {
-  if (!c || !off || !len || !out32) return fail(MG_E_ARG, "null argument");
-  if (!ctx_live(c)) return fail(MG_E_ARG, "not a live context");
+  if (!h || !off || !len || !out32) return fail(MG_E_ARG, "null argument");
+  std::shared_ptr<Ctx> cref = g_reg.ctx(hid(h));   // its device, for the staging buffers
+  if (!cref) return fail(MG_E_ARG, "mg_keccak256: not a live context");
+  const Ctx* c = cref.get();
   if (n == 0) return 0;
   for (size_t i = 0; i < n; ++i)
     if (off[i] + len[i] > ndata) return fail(MG_E_ARG, "message out of range");
@@ -1244,7 +1243,7 @@ int mg_keccak256(mg_ctx* c, const uint8_t* data, size_t ndata, const uint64_t* o
     cleanup();
     return fail(MG_E_HIP, "keccak copy-in");
   }
-  int rc = mg_keccak256_device(c, dd, doff, dlen, n, dout, st);
+  int rc = mg_keccak256_device(h, dd, doff, dlen, n, dout, st);   // the call proper (locked)
   if (rc == 0 && hipMemcpy(out32, dout, 32 * n, hipMemcpyDeviceToHost) != hipSuccess) rc = fail(MG_E_HIP, "keccak copy-out");
   cleanup();
   return rc;

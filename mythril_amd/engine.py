@@ -211,10 +211,11 @@ class WitnessEngine:
         """The witness at candidate ``index``: its verdict re-evaluated by the
         search program (``search_dp`` if still loaded), its values read from
         the witness program."""
-        from .runtime import unpack_trace
+        from .runtime import EngineError, unpack_trace
         p = q.trace_program
         if [n.name for n in p.leaf_nodes] != [n.name for n in q.program.leaf_nodes]:
-            raise RuntimeError("witness program's leaf layout differs from the search program's")
+            # an EngineError, so get_model's handler sends the query to z3 (ADVICE r3)
+            raise EngineError("witness program's leaf layout differs from the search program's")
         own = search_dp is None
         sdp = self.dev.load(q.program) if own else search_dp
         try:

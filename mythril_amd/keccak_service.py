@@ -92,10 +92,12 @@ class KeccakService:
 
     # -- the reference's entry points, same arguments and results ----------
     def sha3(self, value) -> bytes:
-        """support_utils.py:50-59: ``0x``-hex strings are decoded, other strings
-        UTF-8 encoded, bytes hashed as they are."""
+        """support_utils.py:50-59: strings starting ``0x`` go to ``bytes.fromhex``
+        WHOLE (``:53-54``), so they raise ``ValueError`` on the ``x`` exactly
+        as the reference does; other strings are UTF-8 encoded, bytes hashed as
+        they are."""
         if type(value) == str:
-            value = bytes.fromhex(value[2:]) if value[:2] == "0x" else value.encode()
+            value = bytes.fromhex(value) if value[:2] == "0x" else value.encode()
         return self.digest(bytes(value))
 
     def get_code_hash(self, code) -> str:

@@ -251,12 +251,22 @@ def _minimize_hint(constraints, minimize, timeout):
     name = z3bridge.var_name(obj.raw)
     if name is None:
         return None
+    def confirmed(w) -> bool:
+        # the bound becomes a hard constraint of z3's Optimize: a value the
+        # reference solver does not confirm on the unextended set is never used
+        # (the verdict and the values come from different programs)
+        try:
+            return z3bridge.model_from_witness(raws, script, w, timeout) is not None
+        except Exception as e:   # noqa: BLE001 - fail closed: no hint
+            log.warning("witness engine: z3 re-check of a minimize hint failed (%s)", e)
+            return False
+
     try:
         script = z3bridge.to_ir(raws)
         from .engine import prepare
         q = prepare(script.asserts, script.ctx)
         w = eng.search([q])[0]
-        if w is None or name not in w.values:
+        if w is None or name not in w.values or not confirmed(w):
             return None
         best = w.values[name]
         # descent: search again below the best value so far, aiming at half of
@@ -270,7 +280,7 @@ def _minimize_hint(constraints, minimize, timeout):
             target = lo + (best - lo) // 2
             extra = script.ctx.app("bvule", var, script.ctx.const(target, var.width))
             w2 = eng.search([prepare(list(script.asserts) + [extra], script.ctx)])[0]
-            if w2 is not None and name in w2.values and w2.values[name] <= target:
+            if w2 is not None and name in w2.values and w2.values[name] <= target and confirmed(w2):
                 best = w2.values[name]
             else:
                 lo = target + 1
@@ -347,24 +357,34 @@ def prefetch(constraint_sets) -> int:
             items.append((key, raws, script, prepare(script.asserts, script.ctx)))
         except (Unsupported, RecursionError, ValueError, KeyError):
             STATS["unsupported"] += 1
+        except Exception as e:   # noqa: BLE001 - z3 printing/parsing trouble: that set goes to z3
+            STATS["unsupported"] += 1
+            log.warning("witness engine: could not translate a batched query (%s)", e)
     if not items:
         return 0
+    qs = [q for *_, q in items]
     try:
-        found = eng.search([q for *_, q in items])
+        found = eng.search(qs)
     except EngineError as e:
         STATS["device_errors"] = STATS.get("device_errors", 0) + 1
         log.warning("witness engine: device error in batched prefetch (%s)", e)
         return 0
+    # a batch splits the op budget over its programs, so each got at most the
+    # candidates get_model's own launch would give it
+    count_of = getattr(eng, "launch_count", None)
+    batch_count = count_of(qs) if count_of else None
     n = 0
-    for (key, raws, script, _), w in zip(items, found):
+    for (key, raws, script, q), w in zip(items, found):
         if w is not None:
             if len(_memo) >= MEMO_MAX:
                 _memo.clear()
             _memo[key] = (raws, w, script)
             n += 1
-        else:
-            # searched with the same budget get_model would use: its is_possible
-            # goes straight to the reference instead of searching again
+        elif batch_count is not None and batch_count >= count_of([q]):
+            # searched with the budget get_model would use: its is_possible
+            # goes straight to the reference instead of searching again.  A
+            # miss on a shortened budget is not recorded: get_model searches
+            # that set again with its full budget.
             _record_miss(raws, key)
     return n
 

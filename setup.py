@@ -10,7 +10,9 @@ setup(
     version="0.1.0",
     description="MI355X constraint-witness engine behind Mythril's get_model",
     packages=["mythril_amd"],
-    package_data={"mythril_amd": ["lib/*.so", "csrc/*.h", "csrc/*.hip", "csrc/*.cpp"]},
+    # lib/asmjit_template.s: the assembled kernels' template (mythril_amd/asmjit.py);
+    # csrc/*.inc: the generated asm interpreter the sources include
+    package_data={"mythril_amd": ["lib/*.so", "lib/*.s", "csrc/*.h", "csrc/*.hip", "csrc/*.cpp", "csrc/*.inc"]},
     python_requires=">=3.8",
     install_requires=["numpy"],
     entry_points={"mythril.plugins": ["mi355x-witness-engine = mythril_amd.mythril_plugin:MI355XWitnessEngine"]},

@@ -388,3 +388,59 @@ def test_minimize_hint_bounds_only_the_first_objective(mythril, monkeypatch):
     assert bound.op == "bvuge" and bound.args[1] is X and 200 < bound.args[0].val < 203
     assert dropin.STATS["minimize_hints"] >= 1
     monkeypatch.setattr(dropin, "_reference", ref)
+
+
+def test_prefetch_miss_on_a_shortened_budget_is_searched_again(mythril, monkeypatch):
+    """a batch divides the op budget over its programs, so a miss in
+    it is recorded (and later skipped by get_model) only when the batch gave the
+    set at least the candidates get_model's own launch would."""
+    from mythril_amd import engine as engine_mod
+    monkeypatch.setattr(engine_mod, "MIN_CANDIDATES", 16)
+    eng = dropin._engine
+    unsat2 = (fb(CTX.app("bvugt", X, CTX.const(240, 8))), fb(CTX.app("bvult", X, CTX.const(10, 8))))
+    q = engine_mod.prepare([c.raw.node for c in UNSAT], CTX)
+    monkeypatch.setattr(eng, "op_budget", q.ops_per_eval * eng.budget)   # one set alone: the full budget
+    dropin._misses.clear()
+    assert dropin.prefetch([UNSAT, unsat2]) == 0
+    assert not dropin._misses                           # each got about half: nothing recorded
+    s0 = eng.stats["searches"]
+    with pytest.raises(UnsatError):
+        dropin.get_model(UNSAT)
+    assert eng.stats["searches"] == s0 + 1              # searched again, on its own budget
+    monkeypatch.setattr(eng, "op_budget", None)         # every launch gets the full budget
+    dropin._misses.clear()
+    assert dropin.prefetch([UNSAT, unsat2]) == 0
+    assert len(dropin._misses) == 2
+
+
+def test_minimize_hint_needs_a_confirmed_witness(mythril, monkeypatch):
+    """the hint becomes a hard bound, so a witness the reference
+    solver does not confirm gives no hint at all."""
+    Y = CTX.var("y", 8)
+
+    class BV:
+        def __init__(self, node):
+            self.raw = FakeRaw(node)
+            self.node = node
+
+        def size(self):
+            return self.node.width
+    monkeypatch.setattr(z3bridge, "var_name", lambda raw: raw.node.name)
+    monkeypatch.setattr(z3bridge, "model_from_witness", lambda *a, **k: None)
+    assert dropin._minimize_hint(SAT, (BV(X), BV(Y)), 2000) is None
+
+
+def test_witness_layout_mismatch_falls_back_to_reference(mythril, monkeypatch):
+    """materialize's layout check raises EngineError, which get_model
+    turns into a z3 answer instead of an exception in LASER."""
+    from mythril_amd import engine as engine_mod
+    from mythril_amd.compiler import compile_program
+    real = engine_mod.prepare
+
+    def broken(conj, ctx, **kw):
+        q = real(conj, ctx, **kw)
+        q._trace = compile_program([], leaf_specs={})     # no leaves: layout differs
+        return q
+    monkeypatch.setattr(engine_mod, "prepare", broken)
+    assert dropin.get_model(SAT).raw[0] == "ref"
+    assert dropin.STATS["device_errors"] >= 1

@@ -28,7 +28,7 @@ pytestmark = pytest.mark.gpu
 def dev():
     from mythril_amd.runtime import Device
     if not asmjit.available():
-        pytest.fail("assembled kernels unavailable (build/asmjit/template.s or llvm-mc missing)")
+        pytest.fail(f"assembled kernels unavailable: {asmjit.why_unavailable()}")
     d = Device(0)
     yield d
     d.close()

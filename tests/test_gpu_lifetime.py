@@ -56,3 +56,69 @@ def test_close_frees_loaded_programs():
     for h, dp in zip(handles, dps):
         assert lib.mg_prog_free(h) == -1
         dp.handle = None
+
+
+def test_stale_handle_refused_after_a_new_load():
+    """Handles are ids that are never reused: a freed program's
+    handle stays refused after later loads, which may get its memory."""
+    import ctypes
+
+    from mythril_amd.runtime import Device
+    dev = Device(0)
+    try:
+        lib = dev.lib
+        dp = dev.load(_prog())
+        old = dp.handle
+        dp.free()
+        fresh = [dev.load(_prog()) for _ in range(8)]
+        assert old not in [d.handle for d in fresh]
+        assert lib.mg_prog_free(old) == -1
+        out = (ctypes.c_uint64 * 1)()
+        assert lib.mg_search(dev.handle, (ctypes.c_void_p * 1)(old), 1, 1, 0, 256, 0, out, None) == -1
+        (found,), _ = dev.search([fresh[0]], 1, 0, 1 << 12, 0)
+        assert found is not None
+        for d in fresh:
+            d.free()
+    finally:
+        dev.close()
+
+
+def test_context_freed_while_other_threads_search():
+    """mg_free waits for the call in flight on another thread and frees the
+    programs with the context; later calls with those handles are refused."""
+    import ctypes
+    import threading
+
+    from mythril_amd.runtime import Device
+    dev = Device(0)
+    lib = dev.lib
+    dps = [dev.load(_prog()) for _ in range(4)]
+    ctx = dev.handle
+    handles = [dp.handle for dp in dps]
+    rcs = []
+
+    def searcher(h):
+        out = (ctypes.c_uint64 * 1)()
+        for _ in range(20):
+            rcs.append(lib.mg_search(ctx, (ctypes.c_void_p * 1)(h), 1, 1, 0, 1 << 16, 0, out, None))
+
+    ts = [threading.Thread(target=searcher, args=(h,)) for h in handles]
+    for t in ts:
+        t.start()
+    assert lib.mg_free(ctx) == 0
+    for t in ts:
+        t.join()
+    dev.handle = None
+    for dp in dps:
+        dp.handle = None
+    assert rcs and set(rcs) <= {0, -1}
+    for h in handles:
+        assert lib.mg_prog_free(h) == -1
+    dev2 = Device(0)                      # the device is still usable
+    try:
+        dp2 = dev2.load(_prog())
+        (found,), _ = dev2.search([dp2], 1, 0, 1 << 12, 0)
+        assert found is not None
+        dp2.free()
+    finally:
+        dev2.close()

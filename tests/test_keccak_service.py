@@ -33,8 +33,14 @@ def test_sha3_argument_forms_match_reference():
     ref, _ = _reference_counter()
     svc = KeccakService(device=FakeDevice(), reference=ref, min_batch=1)
     assert svc.sha3(b"").hex() == EMPTY
-    assert svc.sha3("0x").hex() == EMPTY
-    assert svc.sha3("0x0000000000") == keccak256(b"\0" * 5)
+    # support_utils.py:53-54 hands "0x..." strings to bytes.fromhex whole: the
+    # reference raises ValueError on the "x", and so does the service
+    for s in ("0x", "0x0000000000", "0xab"):
+        with pytest.raises(ValueError):
+            svc.sha3(s)
+        with pytest.raises(ValueError):
+            bytes.fromhex(s)            # the reference's own operation
+    assert svc.sha3("0000000000") == keccak256(b"0000000000")   # no prefix: UTF-8 text, as the reference
     # text is UTF-8 encoded: the selector of transfer(address,uint256)
     assert svc.sha3("transfer(address,uint256)")[:4].hex() == "a9059cbb"
     assert svc.sha3(bytearray(b"abc")) == keccak256(b"abc")
@@ -218,7 +224,9 @@ def test_install_rebinds_reference_sites(monkeypatch):
     h = KFM.find_concrete_keccak(BitVecVal(5, 256))
     assert h.value == int.from_bytes(keccak256((5).to_bytes(32, "big")), "big") and h.size() == 256
     kmod = mods["mythril.laser.ethereum.function_managers.keccak_function_manager"]
-    assert kmod.sha3("0x") .hex() == EMPTY
+    assert kmod.sha3(b"").hex() == EMPTY
+    with pytest.raises(ValueError):
+        kmod.sha3("0x")
     txs = [{"input": "0x" + "a9059cbb" + "%064x" % placeholder + "%064x" % 7}]
     mods["mythril.analysis.solver"]._replace_with_actual_sha(txs, Z3Model())
     assert txs[0]["input"] == "0x" + "a9059cbb" + keccak256(preimage.to_bytes(32, "big")).hex() + "%064x" % 7
