@@ -228,6 +228,14 @@ class Gen:
     def nop_vcc(self):
         self("s_nop 1")
 
+    def bit_at(self, base, w, dst):
+        """v(dst) = bit w (SGPR) of the limbs at VGPR base (limb w >> 5 read
+        through the index register)"""
+        q, r = S[3], S[4]
+        self(f"s_lshr_b32 {s(q)}, {s(w)}, 5", f"s_and_b32 {s(r)}, {s(w)}, 31",
+             f"s_set_gpr_idx_on {s(q)}, gpr_idx(SRC1)", f"v_lshrrev_b32_e64 {v(dst)}, {s(r)}, {v(base)}",
+             "s_set_gpr_idx_off", f"v_and_b32_e32 {v(dst)}, 1, {v(dst)}")
+
     def static_imm(self):
         """the instruction's immediate word when known at generation time"""
         return None
@@ -518,6 +526,69 @@ def build_handlers():
           f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 4)}, {v(XB + 5)}", f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 6)}, {v(XB + 7)}",
           f"v_cmp_eq_u32_e32 vcc, 0, {v(T)}")
         g.bool_from_vcc(XR)
+        g.write_n(XR)
+
+    def udivrem(g):
+        """XR = XA / XB, XC = XA % XB over 256 bits (canonical operands, so the
+        w-bit results follow): restoring division, one quotient bit per step,
+        most significant first, a uniform 256 steps.  A zero divisor gives all
+        ones and the dividend: bvudiv / bvurem's definition (SMT-LIB, z3)."""
+        for k in range(8):
+            g(f"v_mov_b32_e32 {v(XC + k)}, 0", f"v_mov_b32_e32 {v(XR + k)}, {v(XA + k)}")
+        g(f"s_movk_i32 {s(S[5])}, 0x100")
+        top = g.L("dv")
+        g.label(top)
+        # (R:Q) <<= 1: funnel each limb with the top bit of the one below
+        for k in range(7, 0, -1):
+            g(f"v_alignbit_b32 {v(XC + k)}, {v(XC + k)}, {v(XC + k - 1)}, 31")
+        g(f"v_alignbit_b32 {v(XC)}, {v(XC)}, {v(XR + 7)}, 31")
+        for k in range(7, 0, -1):
+            g(f"v_alignbit_b32 {v(XR + k)}, {v(XR + k)}, {v(XR + k - 1)}, 31")
+        g(f"v_lshlrev_b32_e32 {v(XR)}, 1, {v(XR)}")
+        g.sub_chain(XC, XB, T)                   # borrow (vcc): R < B
+        g.nop_vcc()
+        for k in range(8):
+            g(f"v_cndmask_b32_e32 {v(XC + k)}, {v(T + k)}, {v(XC + k)}, vcc")
+        g(f"v_cndmask_b32_e64 {v(T)}, 1, 0, vcc")
+        g(f"v_or_b32_e32 {v(XR)}, {v(XR)}, {v(T)}")
+        g(f"s_sub_u32 {s(S[5])}, {s(S[5])}, 1", f"s_cmp_lg_u32 {s(S[5])}, 0", f"s_cbranch_scc1 {top}")
+
+    @handler("W_UDIV")
+    def _(g):
+        g.field("a", S[0]), g.field("b", S[1])
+        g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
+        udivrem(g)
+        g.width(S[2]), g.canon(XR, S[2])
+        g.write_w(XR)
+
+    @handler("W_UREM")
+    def _(g):
+        g.field("a", S[0]), g.field("b", S[1])
+        g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
+        udivrem(g)
+        g.write_w(XC)
+
+    @handler("N_ADDC")
+    def _(g):
+        # carry out of the w-bit add a + b of canonical operands: bit w of the
+        # 257-bit sum (lower.py's bvaddc: BVAddNoOverflow's 257-bit add)
+        g.field("a", S[0]), g.field("b", S[1])
+        g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
+        g.add_chain(XA, XB, XR)
+        g.bool_from_vcc(XR + 8)                 # bit 256 (XR + 8 is XC)
+        g.width(S[2])
+        g.bit_at(XR, S[2], T)
+        g.write_n(T)
+
+    @handler("N_ADDCN")
+    def _(g):
+        # ((a + b) >> w) & 1 for w <= 32: the 33-bit sum in T+2 (low), T+3 (carry)
+        g.field("a", S[0]), g.field("b", S[1])
+        g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
+        g(f"v_add_co_u32_e32 {v(T + 2)}, vcc, {v(T)}, {v(T + 1)}")
+        g.bool_from_vcc(T + 3)
+        g.width(S[2])
+        g.bit_at(T + 2, S[2], XR)
         g.write_n(XR)
 
     # -------------------------------------------------------- wide
@@ -1101,6 +1172,7 @@ def render_interp() -> str:
            "// template of the assembled kernels (mw_asmjit_shell.hip, mythril_amd/asmjit.py).",
            "#pragma once",
            f"#define MW_ASM_NOPS {len(ASM_OPCODES)}",
+           f"#define MW_ASM_MAX_DIV {isa.ASM_MAX_DIV}u",
            "#define MW_ASM_OPCODES " + ", ".join(f"MW_{n}" for n in ASM_OPCODES),
            "#define MW_ASM_LEAF_KINDS " + ", ".join(str(k) for k in ASM_LEAF_KINDS)]
     out += _inc(gen("interp"), "MW_ASM_BODY")
@@ -1213,6 +1285,13 @@ class StaticGen(Gen):
         b = self.sval[w] - 1
         q, m = b >> 5, _lit(1 << (b & 31))
         self(f"v_xor_b32_e32 {v(XA + q)}, {m}, {v(XA + q)}", f"v_xor_b32_e32 {v(XB + q)}, {m}, {v(XB + q)}")
+
+    def bit_at(self, base, w, dst):
+        if w not in self.sval:
+            super().bit_at(base, w, dst)
+            return
+        b = self.sval[w]
+        self(f"v_bfe_u32 {v(dst)}, {v(base + (b >> 5))}, {b & 31}, 1")
 
     def extract_limb(self, q, r):
         imm = self.cur["imm"]

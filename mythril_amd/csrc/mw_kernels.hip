@@ -559,8 +559,13 @@ bool asm_eligible(const mg_prog_desc* d) {
   static const u32 kinds[] = {MW_ASM_LEAF_KINDS};
   bool ok_op[256] = {false};
   for (u32 o : ops) ok_op[o & 0xffu] = true;
-  for (size_t i = 0; i < d->ncode_words / 4; ++i)
-    if (!ok_op[d->code[4 * i] & 0xffu]) return false;
+  u32 ndiv = 0;   // bit-serial wide divisions (asmgen.py udivrem): a few at most (isa.ASM_MAX_DIV)
+  for (size_t i = 0; i < d->ncode_words / 4; ++i) {
+    const u32 op = d->code[4 * i] & 0xffu;
+    if (!ok_op[op]) return false;
+    ndiv += (op == MW_W_UDIV || op == MW_W_UREM) ? 1u : 0u;
+  }
+  if (ndiv > MW_ASM_MAX_DIV) return false;
   for (size_t l = 0; l < d->nleaves; ++l) {
     const u32 kind = d->leaves[l * MW_LEAF_WORDS + MW_LEAF_KIND];
     bool ok = false;

@@ -6,8 +6,14 @@ formula, mixed with RANDOM entries (Philox draws):
 
 * values implied by comparisons against constants, projected through
   ``concat`` / ``extract`` / ``zero_extend`` / ``+K`` / ``-K`` / ``^K`` / ``ite``
-  down to the leaves (e.g. ``extract(255,224, concat(cd[0..31])) == 0xa9059cbb``
-  proposes ``cd[0]=0xa9 .. cd[3]=0xbb``), plus the constant +-1 for orderings;
+  / ``udiv K`` / ``urem K`` down to the leaves (e.g. ``extract(255,224,
+  concat(cd[0..31])) == 0xa9059cbb`` proposes ``cd[0]=0xa9 .. cd[3]=0xbb``),
+  plus the constant +-1 for orderings;
+* packed-array indexing: a term compared through both ``t / K == c`` and
+  ``t % K == r`` (Solidity's packed ``bool[]``/``uint8[]`` reads: slot
+  ``i / 32``, byte ``i % 32``, the byte offset reaching ``EXP`` / the ``Power``
+  UF of ``exponent_function_manager.py``) gets the combined values ``c*K + r``
+  first;
 * the three LASER actors for 256-bit address-like leaves
   (``mythril/laser/ethereum/transaction/symbolic.py:29-40``: CREATOR
   0xAFFE.., ATTACKER 0xDEADBEEF.., SOMEGUY 0xAAAA..; the
@@ -98,6 +104,102 @@ def _project(e: Node, value: int, out: Dict[str, List[int]], depth: int = 0,
     elif op == "ite":
         _project(e.args[1], value, out, depth + 1, words)
         _project(e.args[2], value, out, depth + 1, words)
+    elif op in ("bvudiv", "bvurem") and e.args[1].op == "const" and e.args[1].val > 1:
+        # x / K == v: the interval's start v*K; x % K == v: v itself
+        _project(e.args[0], value * e.args[1].val if op == "bvudiv" else value, out, depth + 1, words)
+    elif op in ("bvor", "bvand") and len(e.args) == 2:
+        # a masked merge (an address written over a storage word's other bits):
+        # either side may carry the value's bits
+        for x in e.args:
+            if x.op != "const":
+                _project(x, value, out, depth + 1, words)
+
+
+def _bare_leaf(t: Node) -> Optional[Node]:
+    """The leaf under zero padding, low-bit extracts and constant masks, else None."""
+    for _ in range(6):
+        if t.op == "var":
+            return t
+        if t.op == "concat" and len(t.args) == 2 and t.args[0].op == "const" and t.args[0].val == 0:
+            t = t.args[1]
+        elif t.op == "zero_extend" or (t.op == "extract" and t.params[1] == 0):
+            t = t.args[0]
+        elif t.op == "bvand" and len(t.args) == 2 and (t.args[0].op == "const") != (t.args[1].op == "const"):
+            t = t.args[1] if t.args[0].op == "const" else t.args[0]
+        else:
+            return None
+    return None
+
+
+def _assign(e: Node, value: int, lo: int, hi: int, out: Dict[str, List[int]], depth: int = 0) -> None:
+    """Bits lo..hi of term e equal those bits of `value`: record, per leaf, the
+    mask of bits this fixes and their values (partial fixes too, unlike
+    ``_force``)."""
+    if depth > 32 or e.width == BOOL or lo > hi:
+        return
+    op = e.op
+    if op == "var":
+        m = ((1 << (hi + 1)) - 1) ^ ((1 << lo) - 1)
+        rec = out.setdefault(e.name, [0, 0, e.width])
+        rec[0] |= m
+        rec[1] = (rec[1] & ~m) | (value & m)
+    elif op == "concat":
+        off = e.width
+        for a in e.args:
+            off -= a.width
+            a_lo, a_hi = max(lo, off), min(hi, off + a.width - 1)
+            if a_lo <= a_hi:
+                _assign(a, value >> off, a_lo - off, a_hi - off, out, depth + 1)
+    elif op == "extract":
+        _, l = e.params
+        _assign(e.args[0], value << l, lo + l, hi + l, out, depth + 1)
+    elif op == "zero_extend":
+        x = e.args[0]
+        _assign(x, value, lo, min(hi, x.width - 1), out, depth + 1)
+    elif op == "ite":
+        _, x, y = e.args
+        for v, k in ((x, y), (y, x)):
+            if k.op == "const" and v.op != "const":
+                _assign(v, value, lo, hi, out, depth + 1)
+                return
+    elif op in ("bvudiv", "bvurem") and e.args[1].op == "const" and e.args[1].val > 1 and lo == 0 \
+            and hi == e.width - 1 and e.args[1].val & (e.args[1].val - 1) == 0:
+        k = e.args[1].val.bit_length() - 1       # powers of two: a bit field of the dividend
+        x = e.args[0]
+        if op == "bvudiv":
+            _assign(x, value << k, k, x.width - 1, out, depth + 1)
+        else:
+            _assign(x, value, 0, k - 1, out, depth + 1)
+
+
+def _combine_partial(facts: List[Dict[str, List[int]]]) -> List[Dict[str, int]]:
+    """Packed-array indexing (module doc): pairs of facts that each fix only
+    some bits of a shared leaf, fix disjoint bits of it and agree elsewhere,
+    merged into one assignment of full leaf values (unfixed bits 0)."""
+    partial = facts
+    by_leaf: Dict[str, List[int]] = {}
+    for i, f in enumerate(partial):
+        for name in f:
+            by_leaf.setdefault(name, []).append(i)
+    out, seen = [], set()
+    for name, idx in by_leaf.items():
+        idx = idx[:96]
+        for ii, i in enumerate(idx):
+            for j in idx[ii + 1:]:
+                if (i, j) in seen:
+                    continue
+                seen.add((i, j))
+                a, b = partial[i], partial[j]
+                if a[name][0] & b[name][0] or a[name][0] | b[name][0] == a[name][0] or \
+                        a[name][0] | b[name][0] == b[name][0]:
+                    continue          # the same bits of the shared leaf: not complementary
+                ok = all((a[n][0] & b[n][0] & (a[n][1] ^ b[n][1])) == 0 for n in a if n in b)
+                if ok:
+                    merged = {n: a.get(n, [0, 0])[1] | b.get(n, [0, 0])[1] for n in set(a) | set(b)}
+                    out.append(merged)
+                if len(out) >= 256:
+                    return out
+    return out
 
 
 def _force(e: Node, value: int, lo: int, hi: int, out: Dict[str, int], depth: int = 0) -> None:
@@ -170,6 +272,7 @@ def domains(conjuncts: List[Node]):
     exact: Dict[str, List[int]] = {}
     interval: Dict[str, List[int]] = {}
     align: Dict[str, int] = {}
+    below: List[tuple] = []          # (x, y, strict): leaf x <=u / <u leaf y
 
     def facts(n: Node, neg: bool = False):
         if n.op == "not":
@@ -237,6 +340,9 @@ def domains(conjuncts: List[Node]):
         # pools (every candidate is still checked exactly)
         upper, strict = _UPPER[op]   # bvult/bvule: a is below b
         lo_t, hi_t = (b, a) if upper else (a, b)
+        xl, xh = _bare_leaf(lo_t), _bare_leaf(hi_t)
+        if xl is not None and xh is not None and xl is not xh:
+            below.append((xl.name, xh.name, strict == -1))   # lo_t is the smaller side
         sl, sh = _shifted(lo_t), _shifted(hi_t)
         if sl is not None and hi_t.op == "const":       # x + d <(=) K
             x, d = sl
@@ -253,6 +359,7 @@ def domains(conjuncts: List[Node]):
 
     for c in conjuncts:
         facts(c)
+    domains.below = below
     return exact, interval, align
 
 
@@ -314,8 +421,26 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
     nodes = topo(conjuncts)
     exact, interval, dom_align = domains(conjuncts) if restrict else ({}, {}, {})
     proposals: Dict[str, List[int]] = {}
+    # orderings between two leaves (INVEST_MIN < msg.value < INVEST_MAX with
+    # symbolic storage): each leaf leads with its rank in the order, so the
+    # first candidates already respect it (0 < 1 < 2 ...)
+    ranks: Dict[str, int] = {}
+    below = getattr(domains, "below", []) if restrict else []
+    for _ in range(8):
+        changed = False
+        for small, big, strict in below:
+            r = ranks.get(small, 0) + (1 if strict else 0)
+            if ranks.get(big, 0) < r:
+                ranks[big] = r
+                changed = True
+            ranks.setdefault(small, 0)
+        if not changed:
+            break
+    for name, r in ranks.items():
+        proposals[name] = [r]
     word_props: Dict[int, List[int]] = {}
     consts = []
+    dm: List[Dict[str, List[int]]] = []
     for n in nodes:
         if n.op == "const" and n.width != BOOL:
             consts.append(n.val)
@@ -326,6 +451,13 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
                     deltas = (0,) if n.op in ("=", "distinct") else (0, 1, -1)
                     for d in deltas:
                         _project(x, k.val + d, proposals, words=word_props)
+                    if n.op == "=" and x.width != BOOL:
+                        f: Dict[str, List[int]] = {}
+                        _assign(x, k.val, 0, x.width - 1, f)
+                        if any(m != (1 << w) - 1 for m, _, w in f.values()):
+                            dm.append(f)      # fixes only part of some leaf's bits
+    # packed-array indexing: t / K == c and t % K == r -> t = c*K + r, tried first
+    combos = _combine_partial(dm)
     # alignment facts: (= (bvurem x K) 0)  ->  x should be a multiple of K
     align: Dict[str, int] = {}
     for n in nodes:
@@ -352,11 +484,15 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
         return x
 
     for n in nodes:
-        if n.op == "=" and len(n.args) == 2 and all(a.op == "var" for a in n.args) \
-                and n.args[0].width == n.args[1].width:
-            ra, rb = find(n.args[0].name), find(n.args[1].name)
-            if ra != rb:
-                parent[ra] = rb
+        if n.op == "=" and len(n.args) == 2:
+            # x = y, also through the masks and zero-padding of an address
+            # compare (concat(0, extract(159, 0, x)), bvand(mask, x)): a stored
+            # owner equated with msg.sender gets the actors
+            xa, xb = _bare_leaf(n.args[0]), _bare_leaf(n.args[1])
+            if xa is not None and xb is not None and xa.width == xb.width and xa is not xb:
+                ra, rb = find(xa.name), find(xb.name)
+                if ra != rb:
+                    parent[ra] = rb
     groups: Dict[str, List[int]] = {}
     for name, props in list(proposals.items()):
         groups.setdefault(find(name), []).extend(props)
@@ -384,7 +520,7 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
         pool: List[Optional[int]] = []
         seen = set()
         nfixed = max(1, int(pool_size * (1 - random_share)))
-        for v in cand:
+        for v in itertools.chain((c[leaf.name] for c in combos if leaf.name in c), cand) if combos else cand:
             v &= m
             if v not in seen:
                 seen.add(v)
@@ -400,7 +536,7 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
                 pool = _restrict(pool, leaf.name, w, exact, interval, dom_align, pool_size,
                                  proposals.get(leaf.name, ()))
         specs[leaf.name] = LeafSpec(leaf.name, w, pool=pool)
-    _tie_words(nodes, specs, word_props, set(exact), uniq_consts, pool_size, random_share)
+    _tie_words(nodes, specs, word_props, set(exact), uniq_consts, pool_size, random_share, combos)
     return specs
 
 
@@ -421,7 +557,7 @@ def _byte_leaf(a: Node) -> Optional[Node]:
     return None
 
 
-def _tie_words(nodes, specs, word_props, exact_names, uniq_consts, pool_size, random_share):
+def _tie_words(nodes, specs, word_props, exact_names, uniq_consts, pool_size, random_share, combos=()):
     """Bytes of one word (a concat of byte leaves: an ABI argument read from
     calldata, ``calldata.py:218-231``) draw one word-level pool entry together:
     the pool holds whole-word proposals split into bytes, and every byte after
@@ -452,6 +588,13 @@ def _tie_words(nodes, specs, word_props, exact_names, uniq_consts, pool_size, ra
         m = (1 << W) - 1
         generic = {0, 1, 2, m, m - 1, 1 << (W - 1)}
         props = [v for v in dict.fromkeys(v & m for v in word_props.get(n.id, [])) if v not in generic]
+        # merged partial facts (packed-array indexing) that reach this word come first
+        nb_ = len(bl)
+        lead_combos = []
+        for cmb in combos:
+            if any(b.name in cmb for _, b in fb):
+                lead_combos.append(sum(cmb.get(b.name, 0) << (8 * (nb_ - 1 - i)) for i, b in enumerate(bl)))
+        props = list(dict.fromkeys(lead_combos + props))
         abi = ABI_WORDS if any("calldata" in b.name for _, b in fb) else []
         # Pool order is search order (Morton digits try low entries first), so
         # the first few proposals, an ABI offset and the extreme values come

@@ -28,7 +28,26 @@ constraint set LASER would hold at every JUMPI:
   prunes each successor with ``is_possible`` (``svm.py:287-292``), so both
   successor sets are feasibility queries;
 * keccak of symbolic memory is the UF ``keccak256_N`` with the manager's
-  conditions appended by ``get_all_constraints`` (tests/mythril_shapes.py).
+  conditions appended by ``get_all_constraints`` (tests/mythril_shapes.py);
+* contract creation (``transaction_models.py:195-260``): the init code runs
+  with a concrete CREATOR, storage ``K(256, 256, 0)`` (``account.py:26-29``),
+  the new account's balance set to 0 (``world_state.py:145-166``); its RETURN
+  data becomes the runtime code of the later message calls;
+* the environment leaves of ``global_state.py:126-136`` /
+  ``environment.py:47-48``: ``{tx}_timestamp``, ``block_number``,
+  ``{tx}_coinbase``, ``{tx}_block_difficulty``, ``chain_id``, ``{tx}_gas``,
+  ``{tx}_returndatasize``; ORIGIN is the transaction's ``sender_{tx}``;
+* EXP through the ``Power`` UF with the exponent manager's conditions
+  (``exponent_function_manager.py:21-58``, ``instructions.py:623-636``);
+* CALL / CALLCODE / DELEGATECALL / STATICCALL to a symbolic callee: an ether
+  transfer (``instructions.py:1960-2000``, ``transfer_ether :72-93``) and a
+  fresh ``{tx}_retval_{pc}``;
+* the detection modules' own ``get_model`` queries (``Query.kind``):
+  EtherThief's balance increase after CALL/STATICCALL (``ether_thief.py:60-76``),
+  StateChangeAfterCall's external-call and balance-change checks
+  (``state_change_external_calls.py:119-140,183-197``), and the integer
+  module's overflow checks at the end of a transaction (``integer.py:140-160,
+  245-277``, annotations propagated as ``smt/bitvec.py`` unions them).
 
 The concrete model satisfies every constraint set on the path it follows
 (checked with the oracle when the corpus is made), so the taken-branch
@@ -68,6 +87,9 @@ class TxInput:
     sender: int = ACTORS["ATTACKER"]
     value: int = 0
     gas_price: int = 1
+    retvals: Dict[int, int] = field(default_factory=dict)   # CALL pc (-1: any) -> {tx}_retval_{pc} (default 1)
+    env: Dict[str, int] = field(default_factory=dict)       # timestamp, block_number, gas, ... (model values)
+    creation: bool = False                                  # contract creation: the code is init code
 
 
 @dataclass
@@ -79,6 +101,7 @@ class Query:
     constraints: List[Node]        # world-state constraints + keccak conditions
     sat: Optional[bool]            # True for the followed successor; None = unknown
     keccak_cond: Optional[Node] = None   # the manager's conditions: the last element of constraints
+    kind: str = "jumpi"            # "jumpi", or the detection module whose get_model asks it
 
 
 @dataclass
@@ -100,10 +123,22 @@ class ConcolicLaser:
         stor_name = f"Storage[{CONTRACT}]"
         self.storage = self.c.array(stor_name, 256, 256)
         self.balance = self.c.array("balance", 256, 256)
+        self.balance0 = self.balance               # world_state.starting_balances (world_state.py:33-34)
         self.model: Dict = {stor_name: ArrayVal(dict(storage or {}), 0),
-                            "balance": ArrayVal(dict(balances or {}), 0)}
+                            "balance": ArrayVal(dict(balances or {}), 0),
+                            "Power": ({}, 0)}
         self.vals: Dict[int, object] = {}
         self.run_log = Run()
+        # analysis/symbolic.py:100-117: the actor accounts in the world state
+        # (CREATOR only when there is creation code), then the contract
+        self.accounts: List[int] = [ACTORS["ATTACKER"], CONTRACT]
+        self.power_sent = False                    # exponent_function_manager.concrete_constraints_sent
+        # integer module (integer.py): node id -> annotation indices, and the
+        # annotations (kind, tx, pc, constraints at the operation, overflow condition)
+        self.ann: Dict[int, frozenset] = {}
+        self.annotations: List[Tuple[str, int, int, List[Node], Node]] = []
+        self.tx_anns: set = set()
+        self.tx = 0
 
     # ---------------------------------------------------------------- terms
     @staticmethod
@@ -135,8 +170,19 @@ class ConcolicLaser:
         return _eval1(m, [self.vals[a.id] for a in m.args], self.model)
 
     def app(self, op: str, *args: Node, params=()) -> Node:
-        """Build a term, folding what z3's simplify folds: constant operands, and
-        the concat of a term's own byte slices (memory word round trips)."""
+        """Build a term, folding what z3's simplify folds (constant operands, the
+        concat of a term's own byte slices, select over a store chain with
+        constant keys, x+0, x>=u 0, x=x), and carrying the integer module's
+        annotations from the operands to the result as smt/bitvec.py does
+        (not through array reads: BaseArray.__getitem__ starts a fresh BitVec)."""
+        r = self._app(op, *args, params=params)
+        if self.ann and op not in ("select", "store", "apply"):
+            u = frozenset().union(*[self.ann.get(a.id, frozenset()) for a in args])
+            if u:
+                self.ann[r.id] = self.ann.get(r.id, frozenset()) | u
+        return r
+
+    def _app(self, op: str, *args: Node, params=()) -> Node:
         c = self.c
         if op == "concat":
             args = _merge_slices(c, list(args))
@@ -146,6 +192,25 @@ class ConcolicLaser:
             t = c.app(op, *args, params=params)
             v = _eval1(t, [a.val for a in args], {})
             return c.const(v, t.width)
+        if op == "select":
+            arr, key = args
+            while arr.op == "store" and key.op == "const" and arr.args[1].op == "const":
+                if arr.args[1].val == key.val:
+                    return arr.args[2]
+                arr = arr.args[0]
+            if arr.op == "const_array":
+                return arr.args[0]
+            return c.app("select", arr, key)
+        if op == "store" and args[0].op == "store" and args[1].op == "const" and args[0].args[1] is args[1]:
+            return c.app("store", args[0].args[0], args[1], args[2])     # store(store(a,k,_),k,v)
+        if op in ("bvadd", "bvsub") and args[1].op == "const" and args[1].val == 0:
+            return args[0]
+        if op == "bvadd" and args[0].op == "const" and args[0].val == 0:
+            return args[1]
+        if op == "bvuge" and args[1].op == "const" and args[1].val == 0:
+            return c.true()
+        if op == "=" and args[0] is args[1]:
+            return c.true()
         if op == "extract" and args[0].op == "concat":
             # slice of a concat that falls inside one operand
             hi, lo = params
@@ -172,7 +237,7 @@ class ConcolicLaser:
         return x
 
     def leaf(self, name: str, value: int, w: int = 256) -> Node:
-        self.model[name] = value
+        self.model.setdefault(name, value)
         return self.c.var(name, w)
 
     # ---------------------------------------------------------------- keccak
@@ -185,7 +250,13 @@ class ConcolicLaser:
             # LASER hashes concrete data on the spot (find_concrete_keccak): logged
             # with its position among the queries for tests/laser_replay.py
             self.run_log.keccaks.append((self.tx, len(self.run_log.queries), data.width, data.val))
-            return self.km.create_keccak(data)
+            h = self.km.create_keccak(data)
+            # the manager's concrete-hash conditions (keccak256_N(data) == h, and the
+            # inverse) hold in the model too
+            n = data.width
+            self.model.setdefault(f"keccak256_{n}", ({}, 0))[0][(data.val,)] = h.val
+            self.model.setdefault(f"keccak256_{n}-1", ({}, 0))[0][(h.val,)] = data.val
+            return h
         n = data.width
         fx = self.km.create_keccak(data)
         x = self.val(data)
@@ -202,37 +273,147 @@ class ConcolicLaser:
         self.vals.pop(fx.id, None)
         return fx
 
-    def query_set(self) -> List[Node]:
-        """Constraints.get_all_constraints(): the world constraints + keccak conditions."""
+    # ---------------------------------------------------------------- EXP
+    def power(self, b: Node, e: Node) -> Node:
+        """exponent_function_manager.create_condition (``:34-58``): the result is
+        the UF application Power(b, e); the condition goes to the world state."""
+        c = self.c
+        fx = c.apply("Power", 256, b, e)
+        tab = self.model["Power"][0]
+        bv, ev = self.val(b), self.val(e)
+        if b.op == "const" and e.op == "const":
+            v = pow(b.val, e.val, 1 << 256)
+            tab[(bv, ev)] = v
+            self.vals.pop(fx.id, None)
+            self.constraints.append(self.app("=", self.k(v), fx))
+            return self.k(v)
+        conds = [self.app("bvsgt", fx, self.k(0))]
+        if not self.power_sent:
+            for i in range(32):
+                conds.append(self.app("=", c.apply("Power", 256, self.k(256), self.k(i)), self.k(256 ** i)))
+                tab[(256, i)] = 256 ** i
+            self.power_sent = True
+        if b.op == "const" and b.val == 256:
+            conds.append(self.app("=", c.apply("Power", 256, b, self.app("bvurem", e, self.k(32))), fx))
+            tab[(256, ev % 32)] = 256 ** (ev % 32)
+            tab[(bv, ev)] = 256 ** (ev % 32)          # the UF the conditions pin down
+        else:
+            tab[(bv, ev)] = pow(bv, ev, 1 << 256)
+        self.vals.clear()
+        self.constraints.append(conds[0] if len(conds) == 1 else self.app("and", *conds))
+        return fx
+
+    # ---------------------------------------------------------------- queries
+    def query_set(self, extra=()) -> List[Node]:
+        """Constraints.get_all_constraints(): the world constraints (+ a module's
+        extra conjuncts) + keccak conditions."""
         cond = self.km.create_conditions()
-        extra = [] if (cond.op == "const" and cond.val) else [cond]
-        return [x for x in self.constraints if not (x.op == "const" and x.val)] + extra
+        tail = [] if (cond.op == "const" and cond.val) else [cond]
+        body = [x for x in list(self.constraints) + list(extra) if not (x.op == "const" and x.val)]
+        return body + tail
+
+    def module_query(self, kind: str, extra, base: Optional[List[Node]] = None) -> None:
+        """A detection module's get_model(constraints + extra): recorded with
+        status sat when the concrete model satisfies it, else unknown."""
+        saved = self.constraints
+        if base is not None:
+            self.constraints = base
+        try:
+            extra = [self.bv(x) if x.width != BOOL else x for x in extra]
+            qset = self.query_set(extra)
+        finally:
+            self.constraints = saved
+        if any(x.op == "const" and not x.val for x in qset):
+            return                    # folded to False: nothing to ask
+        kc = qset[-1] if self.km.create_conditions().op != "const" else None
+        ok = check_model(qset, self.model)
+        self.run_log.queries.append(Query(self.tx, self.pc, True, qset, True if ok else None, kc, kind))
+
+    def annotate(self, kind: str, op0: Node, res: Node, cond: Node) -> None:
+        """integer.py:_handle_add/_mul/_sub: the overflow condition annotates
+        the first operand (a constant operand: the result)."""
+        if cond.op == "const":
+            return
+        idx = len(self.annotations)
+        self.annotations.append((kind, self.tx, self.pc, list(self.constraints), cond))
+        tgt = op0 if op0.op != "const" else res
+        self.ann[tgt.id] = self.ann.get(tgt.id, frozenset()) | {idx}
+        if tgt is not res:
+            self.ann[res.id] = self.ann.get(res.id, frozenset()) | {idx}
+
+    def collect(self, x: Node) -> None:
+        """integer.py:_handle_sstore/_jumpi/_call/_return: annotations reaching a sink."""
+        self.tx_anns |= self.ann.get(x.id, frozenset())
+
+    def tx_end_queries(self) -> None:
+        """integer.py:_handle_transaction_end (``:245-277``): for each collected
+        annotation, get_model(ostate constraints + [condition])."""
+        for idx in sorted(self.tx_anns):
+            kind, _, _, ostate, cond = self.annotations[idx]
+            self.module_query(f"IntegerArithmetics/{kind}", [cond], base=ostate)
+        self.tx_anns = set()
 
     # ---------------------------------------------------------------- transactions
-    def message_call(self, tx: int, inp: TxInput, max_steps: int = 20000) -> str:
+    def _setup_tx(self, tx: int, inp: TxInput, sender: Node, me: Node) -> None:
         c = self.c
-        sender = self.leaf(f"sender_{tx}", inp.sender)
         value = self.leaf(f"call_value{tx}", inp.value)
         self.leaf(f"gas_price{tx}", inp.gas_price)
         size = self.leaf(f"{tx}_calldatasize", len(inp.calldata))
         self.model[f"{tx}_calldata"] = ArrayVal(dict(enumerate(inp.calldata)), 0)
+        for name, v in inp.env.items():
+            self.model[name if name in ("block_number", "chain_id") else f"{tx}_{name}"] = v
         self.cd = c.array(f"{tx}_calldata", 256, 8)
         self.cdsize = size
-        self.sender, self.value, self.tx = sender, value, tx
+        self.sender, self.value, self.tx, self.inp = sender, value, tx, inp
+        self.returndata = None
+        self.tx_anns = set()
         # transaction_models.py:139-143 then transaction/symbolic.py:210-212
         self.constraints.append(self.app("bvuge", self.app("select", self.balance, sender), value))
-        me = self.k(CONTRACT)
         self.balance = self.app("store", self.balance, me, self.app("bvadd", self.app("select", self.balance, me), value))
         self.balance = self.app("store", self.balance, sender,
                                 self.app("bvsub", self.app("select", self.balance, sender), value))
-        self.constraints.append(c.app("or", *[c.app("=", sender, self.k(a)) for a in ACTORS.values()]))
+        orc = c.app("or", *[self.app("=", sender, self.k(a)) for a in ACTORS.values()]) \
+            if sender.op != "const" else c.true()
+        if not (orc.op == "const" and orc.val):
+            self.constraints.append(orc)
         self.vals.clear()
-        for key in ("balance",):
-            pass
+
+    def message_call(self, tx: int, inp: TxInput, max_steps: int = 20000) -> str:
+        sender = self.leaf(f"sender_{tx}", inp.sender)
+        self._setup_tx(tx, inp, sender, self.k(CONTRACT))
         return self._exec(max_steps)
+
+    def contract_creation(self, tx: int, inp: TxInput, max_steps: int = 20000) -> str:
+        """ContractCreationTransaction (transaction_models.py:195-245): CREATOR
+        calls the init code; the new account has concrete storage K(256,256,0)
+        and balance 0; the RETURN data becomes the runtime code."""
+        if ACTORS["CREATOR"] not in self.accounts:
+            self.accounts.insert(0, ACTORS["CREATOR"])
+        self.storage = self.c.const_array(256, self.k(0))
+        self.balance = self.app("store", self.balance, self.k(CONTRACT), self.k(0))
+        self._setup_tx(tx, inp, self.k(inp.sender), self.k(CONTRACT))
+        res = self._exec(max_steps)
+        if res == "RETURN":
+            self.code = self.returned
+            self.jumpdests = self._jumpdests(self.code)
+        return res
 
     def _calldata_byte(self, i: Node) -> Node:
         return self.app("ite", self.app("bvslt", i, self.cdsize), self.app("select", self.cd, i), self.k(0, 8))
+
+    def _env_leaf(self, name: str, default: int) -> Node:
+        """global_state.new_bitvec (global_state.py:126-136): '{tx}_{name}'."""
+        full = f"{self.tx}_{name}"
+        return self.leaf(full, self.model.get(full, default))
+
+    def _transfer(self, sender: Node, receiver: Node, value: Node) -> None:
+        """instructions.py:72-93 transfer_ether."""
+        self.constraints.append(self.app("bvuge", self.app("select", self.balance, sender), value))
+        self.balance = self.app("store", self.balance, receiver,
+                                self.app("bvadd", self.app("select", self.balance, receiver), value))
+        self.balance = self.app("store", self.balance, sender,
+                                self.app("bvsub", self.app("select", self.balance, sender), value))
+        self.vals.clear()
 
     def _exec(self, max_steps: int) -> str:
         code, stack, mem = self.code, [], {}
@@ -260,33 +441,42 @@ class ConcolicLaser:
             for i in range(32):
                 mem[off + i] = self.app("extract", v, params=(255 - 8 * i, 248 - 8 * i))
 
+        def arith(name, kind, cond_of):
+            x, y = popbv(), popbv()
+            r = self.app(name, x, y)
+            if cond_of is not None:
+                self.annotate(kind, x, r, cond_of(x, y))
+            stack.append(r)
+
         while True:
             steps += 1
             if steps > max_steps:
                 raise Unsupported("step limit")
             if pc >= len(code):
+                self.tx_end_queries()
                 return "STOP"
             op = code[pc]
+            self.pc = pc
             pc += 1
             a = self.app
             if op == 0x00:
+                self.tx_end_queries()
                 return "STOP"
-            elif op == 0x01:
-                stack.append(a("bvadd", popbv(), popbv()))
-            elif op == 0x02:
-                stack.append(a("bvmul", popbv(), popbv()))
-            elif op == 0x03:
-                x, y = popbv(), popbv()
-                stack.append(a("bvsub", x, y))
+            elif op == 0x01:   # integer.py:140-145 Not(BVAddNoOverflow(op0, op1, False))
+                arith("bvadd", "addition", lambda x, y: a("not", a("=", a(
+                    "extract", a("bvadd", a("zero_extend", x, params=(1,)), a("zero_extend", y, params=(1,))),
+                    params=(256, 256)), self.k(0, 1))))
+            elif op == 0x02:   # :147-151 Not(BVMulNoOverflow(op0, op1, False))
+                arith("bvmul", "multiplication", lambda x, y: a("not", a("bvumul_noovfl", x, y)))
+            elif op == 0x03:   # :153-157 Not(BVSubNoUnderflow(op0, op1, False)) = Not(op1 <=u op0)
+                arith("bvsub", "subtraction", lambda x, y: a("not", a("bvule", y, x)))
             elif op in (0x04, 0x05, 0x06, 0x07):   # DIV SDIV MOD SMOD: concrete-zero divisor -> 0
                 x, y = popbv(), popbv()
                 name = {0x04: "bvudiv", 0x05: "bvsdiv", 0x06: "bvurem", 0x07: "bvsrem"}[op]
                 stack.append(self.k(0) if (y.op == "const" and y.val == 0) else a(name, x, y))
-            elif op == 0x0A:   # EXP: concrete only (exponent_function_manager.py:39-49)
+            elif op == 0x0A:   # EXP: the Power UF (exponent_function_manager.py)
                 b, e = popbv(), popbv()
-                if b.op != "const" or e.op != "const":
-                    raise Unsupported("symbolic EXP")
-                stack.append(self.k(pow(b.val, e.val, 1 << 256)))
+                stack.append(self.power(b, e))
             elif op == 0x10:
                 stack.append(a("bvult", popbv(), popbv()))
             elif op == 0x11:
@@ -322,9 +512,18 @@ class ConcolicLaser:
                 stack.append(self.sha3(data) if ln else self.k(0xC5D2460186F7233C927E7DB2DCC703C0E500B653CA82273B7BFAD8045D85A470))
             elif op == 0x30:
                 stack.append(self.k(CONTRACT))
-            elif op == 0x31:
-                stack.append(a("select", self.balance, popbv()))
-            elif op in (0x32, 0x33):
+            elif op == 0x31:   # BALANCE (instructions.py:903-920)
+                addr = popbv()
+                if addr.op == "const":
+                    if addr.val not in self.accounts:
+                        raise Unsupported("BALANCE of an account outside the world state")
+                    stack.append(a("select", self.balance, addr))
+                else:
+                    bal = self.k(0)
+                    for acct in self.accounts:
+                        bal = a("ite", a("=", addr, self.k(acct)), a("select", self.balance, self.k(acct)), bal)
+                    stack.append(bal)
+            elif op in (0x32, 0x33):   # ORIGIN, CALLER: the transaction's sender (transaction/symbolic.py:121-131)
                 stack.append(self.sender)
             elif op == 0x34:
                 stack.append(self.value)
@@ -340,10 +539,33 @@ class ConcolicLaser:
                     mem[dst + i] = self._calldata_byte(a("bvadd", src, self.k(i)) if i else src)
             elif op == 0x38:
                 stack.append(self.k(len(code)))
+            elif op == 0x39:   # CODECOPY (instructions.py:1065-1130; concrete operands)
+                dst, src, ln = conc(pop()), conc(pop()), conc(pop())
+                for i in range(ln):
+                    mem[dst + i] = self.k(code[src + i] if src + i < len(code) else 0, 8)
             elif op == 0x3A:
                 stack.append(self.c.var(f"gas_price{self.tx}", 256))
-            elif op in (0x42, 0x43):   # TIMESTAMP, NUMBER: fresh symbols (global_state.py:126-136)
-                stack.append(self.leaf("timestamp" if op == 0x42 else "block_number", 1_600_000_000))
+            elif op == 0x3D:   # RETURNDATASIZE, no call returned data (instructions.py:1350-1365)
+                stack.append(self._env_leaf("returndatasize", 0) if self.returndata is None
+                             else self.k(len(self.returndata)))
+            elif op == 0x3E:   # RETURNDATACOPY with no return data: a no-op (:1336-1337)
+                dst, src, ln = pop(), pop(), pop()
+                if self.returndata is not None:
+                    raise Unsupported("RETURNDATACOPY of real return data")
+            elif op == 0x41:
+                stack.append(self._env_leaf("coinbase", 0))
+            elif op == 0x42:   # TIMESTAMP (instructions.py:1393-1400)
+                stack.append(self._env_leaf("timestamp", 1_600_000_000))
+            elif op == 0x43:   # NUMBER: environment.block_number (environment.py:47)
+                stack.append(self.leaf("block_number", 10_000_000))
+            elif op == 0x44:
+                stack.append(self._env_leaf("block_difficulty", 0))
+            elif op == 0x45:   # GASLIMIT: the transaction's concrete gas limit
+                stack.append(self.k(8_000_000))
+            elif op == 0x46:
+                stack.append(self.leaf("chain_id", 1))
+            elif op == 0x47:   # SELFBALANCE (instructions.py:959-967)
+                stack.append(a("select", self.balance, self.k(CONTRACT)))
             elif op == 0x50:
                 pop()
             elif op == 0x51:
@@ -358,6 +580,7 @@ class ConcolicLaser:
                 stack.append(a("select", self.storage, popbv()))
             elif op == 0x55:
                 key, v = popbv(), popbv()
+                self.collect(v)
                 self.storage = a("store", self.storage, key, v)
             elif op == 0x56:
                 dest = conc(pop())
@@ -366,6 +589,7 @@ class ConcolicLaser:
                 pc = dest
             elif op == 0x57:
                 dest, cond = conc(pop()), pop()
+                self.collect(cond)
                 if cond.width == BOOL:
                     pos, neg = cond, a("not", cond)
                 else:
@@ -391,10 +615,12 @@ class ConcolicLaser:
                 stack.append(self.k(pc - 1))
             elif op == 0x59:
                 stack.append(self.k((max(mem) + 32) // 32 * 32 if mem else 0))
-            elif op == 0x5A:
-                stack.append(self.k(8_000_000 - steps))
+            elif op == 0x5A:   # GAS: a fresh symbol (instructions.py:1697-1705)
+                stack.append(self._env_leaf("gas", 2_000_000))
             elif op == 0x5B:
                 pass
+            elif op == 0x5F:
+                stack.append(self.k(0))
             elif 0x60 <= op <= 0x7F:
                 n = op - 0x5F
                 stack.append(self.k(int.from_bytes(code[pc:pc + n].ljust(n, b"\0"), "big")))
@@ -413,7 +639,18 @@ class ConcolicLaser:
                 pop(), pop()
                 for _ in range(op - 0xA0):
                     pop()
+            elif op in (0xF1, 0xF2, 0xF4, 0xFA):
+                self._call(op, stack, pop, popbv)
             elif op == 0xF3:
+                off, ln = conc(pop()), conc(pop())
+                data = [mbyte(off + i) for i in range(ln)]
+                for x in data:
+                    self.collect(x)
+                self.tx_end_queries()
+                if all(x.op == "const" for x in data):
+                    self.returned = bytes(x.val for x in data)
+                elif self.inp.creation:
+                    raise Unsupported("symbolic runtime code")
                 return "RETURN"
             elif op == 0xFD:
                 return "REVERT"
@@ -424,6 +661,40 @@ class ConcolicLaser:
                 return "SELFDESTRUCT"
             else:
                 raise Unsupported(f"opcode 0x{op:02x} at {pc - 1}")
+
+    def _call(self, op: int, stack, pop, popbv) -> None:
+        """CALL (0xF1), CALLCODE (0xF2), DELEGATECALL (0xF4), STATICCALL (0xFA)
+        to a symbolic callee: an account with no code, so an ether transfer and
+        a fresh return value (instructions.py:1960-2000, 2194-2237, 2335-2379;
+        call.py:140-143).  The detection modules' hooks run around it."""
+        if len(stack) < (7 if op in (0xF1, 0xF2) else 6):
+            raise Halt("stack underflow")
+        a = self.app
+        gas, to = self.bv(stack[-1]), self.bv(stack[-2])
+        if op in (0xF1, 0xF4, 0xF2):
+            # StateChangeAfterCall pre hook (state_change_external_calls.py:183-197, 119-140)
+            v3 = self.bv(stack[-3])
+            if v3.op != "const":
+                self.module_query("StateChangeAfterCall/balance_change", [a("bvsgt", v3, self.k(0))])
+            self.module_query("StateChangeAfterCall/external_call", [
+                a("bvugt", gas, self.k(2300)), a("or", a("bvsgt", to, self.k(16)), a("=", to, self.k(0)))])
+            self.module_query("StateChangeAfterCall/attacker_callee", [a("=", to, self.k(ACTORS["ATTACKER"]))])
+        if op == 0xF1:
+            self.collect(self.bv(stack[-3]))      # integer.py:_handle_call
+        pop(), pop()
+        value = popbv() if op in (0xF1, 0xF2) else self.k(0)
+        for _ in range(4):
+            pop()
+        if to.op == "const":
+            raise Unsupported("call to a concrete address")
+        self._transfer(self.k(CONTRACT), to, value)
+        stack.append(self._env_leaf(f"retval_{self.pc}", self.inp.retvals.get(self.pc, self.inp.retvals.get(-1, 1))))
+        if op in (0xF1, 0xFA):
+            # EtherThief post hook (ether_thief.py:60-76)
+            att = self.k(ACTORS["ATTACKER"])
+            self.module_query("EtherThief", [
+                a("bvugt", a("select", self.balance, att), a("select", self.balance0, att)),
+                a("=", self.sender, att), self.c.true()])
 
 
 def _postorder(root: Node, done: Dict[int, object]) -> List[Node]:
@@ -476,13 +747,13 @@ def run_sequence(code: bytes, txs: List[TxInput], storage=None, balances=None) -
     for t, inp in enumerate(txs, start=1):
         # a reverted transaction leaves no open state (svm.py _execute_transactions):
         # the next one starts from the world state before it
-        snap = (list(m.constraints), m.storage, m.balance)
+        snap = (list(m.constraints), m.storage, m.balance, m.code, m.jumpdests)
         try:
-            res = m.message_call(t, inp)
+            res = m.contract_creation(t, inp) if inp.creation else m.message_call(t, inp)
         except Halt as e:
             res = f"halt: {e}"
         if res not in ("STOP", "RETURN", "SELFDESTRUCT"):
-            m.constraints, m.storage, m.balance = snap
+            m.constraints, m.storage, m.balance, m.code, m.jumpdests = snap
         m.run_log.halts.append(res)
     m.run_log.model = m.model
     return m, m.run_log

@@ -99,7 +99,7 @@ class ReplayVM:
         self.laser_hooks: Dict[str, list] = {}
         self.post_hooks: Dict[str, list] = {}
         self.open_states: list = []
-        self.counts = {"is_possible": 0, "tx_prunes": 0, "jumpi_prunes": 0, "keccaks": 0}
+        self.counts = {"is_possible": 0, "tx_prunes": 0, "jumpi_prunes": 0, "keccaks": 0, "module_queries": 0}
 
     def register_laser_hooks(self, kind, hook):
         self.laser_hooks.setdefault(kind, []).append(hook)
@@ -116,6 +116,14 @@ class ReplayVM:
     def _possible(self, cons: Constraints) -> bool:
         self.counts["is_possible"] += 1
         return cons.is_possible
+
+    def _module(self, cons: Constraints) -> bool:
+        solver = sys.modules["mythril.analysis.solver"]
+        try:
+            solver.get_model(cons)
+            return True
+        except UnsatError:
+            return False
 
     def replay(self, runs, keccak=None) -> List[bool]:
         """Play every run (one concolic transaction sequence each) in LASER's
@@ -137,9 +145,19 @@ class ReplayVM:
                 qs = [(i, q) for i, q in enumerate(run.queries) if q.tx == tx]
                 j = 0
                 while j < len(qs):
+                    if qs[j][1].kind != "jumpi":
+                        # a detection module's own query: analysis.solver.get_model
+                        # on the state's Constraints plus its conditions
+                        while kk and kk[0][0] == tx and kk[0][1] <= qs[j][0]:
+                            self._keccak(keccak, kk.pop(0))
+                        self.counts["module_queries"] += 1
+                        answers.append(self._module(_state(qs[j][1]).world_state.constraints))
+                        j += 1
+                        continue
                     # one JUMPI: its successor sets are recorded consecutively
                     grp = [qs[j]]
-                    while j + len(grp) < len(qs) and qs[j + len(grp)][1].pc == qs[j][1].pc and len(grp) < 2:
+                    while j + len(grp) < len(qs) and qs[j + len(grp)][1].pc == qs[j][1].pc and len(grp) < 2 \
+                            and qs[j + len(grp)][1].kind == "jumpi":
                         grp.append(qs[j + len(grp)])
                     # concrete SHA3s executed before this JUMPI
                     while kk and kk[0][0] == tx and kk[0][1] <= grp[0][0]:
@@ -258,7 +276,9 @@ def concolic_runs(contracts=None):
         if contracts and contract not in contracts:
             continue
         code = load_code(contract)
-        for name, txs in scenarios:
-            m, run = run_sequence(code, txs, balances={x: 10 ** 18 for x in ACTORS.values()})
+        for name, txs, *opt in scenarios:
+            opts = opt[0] if opt else {}
+            bal = opts.get("balances", 10 ** 18)
+            m, run = run_sequence(code, txs, storage=opts.get("storage"), balances={x: bal for x in ACTORS.values()})
             out.append((f"{contract}/{name}", m, run, len(txs)))
     return out

@@ -30,6 +30,7 @@ def test_replay_on_device(name, monkeypatch, device):
     for q, got, exp in zip(run.queries, answers, expect):
         if q.sat or exp:
             assert got, q.pc
-    # one launch per JUMPI pair, plus one per transaction-boundary prefetch
-    assert rec["launches"] * 2 <= rec["jumpi_prunes"] + 1 + 2 * rec["tx_prunes"]
+    # one launch per JUMPI pair, plus one per transaction-boundary prefetch and
+    # per detection-module query
+    assert rec["launches"] * 2 <= rec["jumpi_prunes"] + 1 + 2 * rec["tx_prunes"] + 2 * rec["module_queries"]
     assert rec["z3_confirmed"] == rec["gpu_witnesses"]

@@ -53,7 +53,8 @@ def replay(name, monkeypatch, dev, budget):
            "programs_searched": eng.stats["programs"], "memo_hits": dropin.STATS["memo_hits"],
            "gpu_witnesses": dropin.STATS["gpu_witnesses"], "z3_confirmed": dropin.STATS["z3_confirmed"],
            "reference_calls": calls["reference"], "batched_prefetches": dropin.STATS.get("batched_prefetches", 0),
-           "keccak_requests": vm.counts["keccaks"], "keccak_stats": dict(svc.stats)}
+           "keccak_requests": vm.counts["keccaks"], "keccak_stats": dict(svc.stats),
+           "module_queries": vm.counts["module_queries"]}
     return answers, expect, rec
 
 
@@ -64,7 +65,7 @@ def test_replay_in_laser_order(name, monkeypatch):
     # JUMPI successor answers: the followed successor is always possible; the
     # drop-in never says "possible" where the reference (model check) says no
     m, run, _ = RUNS[name]
-    assert len(answers) == len(run.queries) == rec["jumpi_prunes"]
+    assert len(answers) == len(run.queries) == rec["jumpi_prunes"] + rec["module_queries"]
     for q, got, exp in zip(run.queries, answers, expect):
         if q.sat or exp:
             assert got
@@ -72,7 +73,7 @@ def test_replay_in_laser_order(name, monkeypatch):
         # witness the stand-in reference, which only knows the concolic
         # model, does not have
     # every successor set is searched at most once; a JUMPI pair in one launch
-    assert rec["launches"] <= rec["is_possible"]
-    assert rec["programs_searched"] <= rec["is_possible"] + rec["tx_prunes"]
+    assert rec["launches"] <= rec["is_possible"] + rec["module_queries"]
+    assert rec["programs_searched"] <= rec["is_possible"] + rec["tx_prunes"] + rec["module_queries"]
     assert rec["memo_hits"] + rec["reference_calls"] + rec["gpu_witnesses"] >= rec["jumpi_prunes"] // 2
     assert rec["keccak_stats"]["requests"] >= rec["keccak_requests"]

@@ -2,18 +2,30 @@
 """Write tests/golden/laser/: LASER-shaped feasibility queries derived from the
 reference's own runtime bytecode.
 
-Source bytecode: the reference's runtime-bytecode fixtures (data), copied to
+Source bytecode: the reference's bytecode fixtures (data), copied to
 tests/golden/laser_bytecode.json (or read from a checkout with --ref):
 tests/testdata/inputs/
   underflow.sol.o  = solidity_examples/token.sol (transfer renamed sendeth) — C2's contract
   overflow.sol.o, metacoin.sol.o — the same mapping/arithmetic shapes
   suicide.sol.o    = C1's contract (suicide.sol, kill(address))
+  flag_array.sol.o — CREATION code; extractMoney's EtherThief query, pinned by the
+                     reference's expected calldata (tests/integration_tests/analysis_tests.py:9-19)
+  origin.sol.o, calls.sol.o, kinds_of_calls.sol.o, returnvalue.sol.o, ether_send.sol.o
+                   — ORIGIN, the four CALL kinds to symbolic callees ({tx}_retval_{pc}),
+                     BALANCE, the call-site module queries
+  exceptions_0.8.0.sol.o — creation code, Panic paths, the Power UF (EXP)
+  environments.sol.o — batchTransfer(address[],uint256): the BECToken shape of C3
+tests/laser/evm_testsuite/VMTests/vmIOandFlowOperations/DynamicJumpJD_DependsOnJumps{0,1}.json
+                   — NUMBER in a JUMPI condition (block_number)
 
-Each contract runs a 2-3 transaction sequence under tests/laser_concolic.py
+Each contract runs a 1-3 transaction sequence under tests/laser_concolic.py
 (symbolic calldata, caller, callvalue; a concrete path chosen by the listed
 inputs); every JUMPI contributes both successor sets (LASER prunes each with
 is_possible, svm.py:287-292).  The followed successor is SAT and its model is
-verified here with the oracle; the other successor's status is unknown.
+verified here with the oracle; the other successor's status is unknown.  The
+detection modules' own get_model queries along the path are recorded too
+(``kind``: EtherThief, StateChangeAfterCall/*, IntegerArithmetics/*), SAT when
+the concrete model satisfies them, else unknown.
 Output: one ``--solver-log``-format file per query (z3 Optimize.sexpr shape,
 mythril/support/model.py:45-56), gzip-compressed, starting with
 ``; expect: sat|unknown``, plus
@@ -79,6 +91,76 @@ SCENARIOS = {
             TxInput(abi_call(sel("kill(address)"), C), sender=C, value=5),
             TxInput(abi_call(sel("kill(address)"), S), sender=A)]),
     ],
+    # creation code: tx 1 is CREATOR's creation with 0.1 ether (the constructor's
+    # require), tx 2 the reference's EtherThief test case (analysis_tests.py:9-19)
+    "flag_array": [
+        ("t2_extract_money", [
+            TxInput(b"", sender=C, value=10 ** 17, creation=True),
+            TxInput(abi_call(sel("extractMoney(uint256)"), 1234), sender=A)]),
+        ("t2_unflagged_index", [
+            TxInput(b"", sender=C, value=10 ** 17, creation=True),
+            TxInput(abi_call(sel("extractMoney(uint256)"), 77), sender=A)]),
+    ],
+    "origin": [   # the runtime code's storage is symbolic: the model's owner (slot 0) decides the ORIGIN check
+        ("t2_transfer_ownership", [
+            TxInput(abi_call(sel("transferOwnership(address)"), S), sender=A),
+            TxInput(abi_call(sel("owner()")), sender=C)], {"storage": {0: A}}),
+        ("t1_origin_check_fails", [
+            TxInput(abi_call(sel("transferOwnership(address)"), S), sender=A)]),
+    ],
+    "calls": [
+        ("t3_stored_and_user_address", [
+            TxInput(abi_call(sel("setstoredaddress(address)"), A), sender=A),
+            TxInput(abi_call(sel("callstoredaddress()")), sender=A),
+            TxInput(abi_call(sel("calluseraddress(address)"), S), sender=S)]),
+        ("t2_fixed_address", [
+            TxInput(abi_call(sel("thisisfine()")), sender=A),
+            TxInput(abi_call(sel("reentrancy()")), sender=C, retvals={-1: 0})]),
+    ],
+    "kinds_of_calls": [
+        ("t3_call_kinds", [
+            TxInput(abi_call(sel("callSetN(address,uint256)"), A, 5), sender=A),
+            TxInput(abi_call(sel("callcodeSetN(address,uint256)"), S, 1), sender=S),
+            TxInput(abi_call(sel("delegatecallSetN(address,uint256)"), A, 2), sender=A)]),
+    ],
+    "returnvalue": [
+        ("t2_checked_unchecked", [
+            TxInput(abi_call(sel("callnotchecked()")), sender=A, retvals={-1: 0}),
+            TxInput(abi_call(sel("callchecked()")), sender=S)]),
+        ("t1_failed_checked_call", [
+            TxInput(abi_call(sel("callchecked()")), sender=A, retvals={-1: 0})]),
+    ],
+    "ether_send": [
+        ("t3_crowdfund_invest_withdraw", [
+            TxInput(abi_call(sel("crowdfunding()")), sender=A),
+            TxInput(abi_call(sel("invest()")), sender=S, value=2 * 10 ** 18),
+            TxInput(abi_call(sel("withdrawfunds()")), sender=A)],
+         {"balances": 10 ** 20, "storage": {2: 10 ** 18, 3: 10 * 10 ** 18}}),   # INVEST_MIN, INVEST_MAX
+    ],
+    "exceptions_0.8.0": [
+        ("t2_assert_fails", [
+            TxInput(b"", sender=C, creation=True),
+            TxInput(abi_call(sel("assert1()")), sender=A)]),
+        ("t3_change_then_fail", [
+            TxInput(b"", sender=C, creation=True),
+            TxInput(abi_call(sel("change_val()")), sender=A),
+            TxInput(abi_call(sel("fail()")), sender=S)]),
+    ],
+    # BECToken's batchTransfer (C3's shape) in the reference's own bytecode: the
+    # receivers array is ABI-encoded (offset 0x40, length, addresses)
+    "environments": [
+        ("t1_batch_transfer", [
+            TxInput(abi_call(sel("batchTransfer(address[],uint256)"), 0x40, 5, 2, A, S), sender=A)]),
+        ("t1_batch_transfer_overflow", [
+            TxInput(abi_call(sel("batchTransfer(address[],uint256)"), 0x40, 1 << 255, 2, A, S), sender=S)]),
+    ],
+    "vm:vmIOandFlowOperations/DynamicJumpJD_DependsOnJumps0": [
+        ("t1_number_branch", [TxInput(b"", sender=A, env={"block_number": 1})]),
+        ("t1_number_zero", [TxInput(b"", sender=A, env={"block_number": 0})]),
+    ],
+    "vm:vmIOandFlowOperations/DynamicJumpJD_DependsOnJumps1": [
+        ("t1_number_branch", [TxInput(b"", sender=A, env={"block_number": 5})]),
+    ],
 }
 
 
@@ -88,16 +170,38 @@ def main():
                     "instead of tests/golden/laser_bytecode.json")
     ap.add_argument("--out", default=OUT)
     ap.add_argument("--only", default=None, help="contract/scenario to (re)generate")
+    ap.add_argument("--import-bytecode", action="store_true", help="copy the fixtures from --ref into "
+                    "tests/golden/laser_bytecode.json first")
     a = ap.parse_args()
+    if a.import_bytecode:
+        import_bytecode(a.ref)
     write(a.out, a.ref, a.only)
 
 
 def load_code(contract: str, ref=None) -> bytes:
+    """The bytecode of a fixture: ``name`` is tests/testdata/inputs/name.sol.o,
+    ``vm:category/test`` the ``exec.code`` of a VMTests json."""
     if ref:
+        if contract.startswith("vm:"):
+            path = os.path.join(ref, "tests", "laser", "evm_testsuite", "VMTests", contract[3:] + ".json")
+            d = json.load(open(path))
+            return bytes.fromhex(next(iter(d.values()))["exec"]["code"][2:])
         path = os.path.join(ref, "tests", "testdata", "inputs", f"{contract}.sol.o")
         return bytes.fromhex(open(path).read().strip())
     d = json.load(open(os.path.join(ROOT, "tests", "golden", "laser_bytecode.json")))
     return bytes.fromhex(d["bytecode"][contract])
+
+
+def import_bytecode(ref: str) -> None:
+    """Copy every fixture SCENARIOS names from a reference checkout into
+    tests/golden/laser_bytecode.json (data: hex strings)."""
+    path = os.path.join(ROOT, "tests", "golden", "laser_bytecode.json")
+    d = json.load(open(path))
+    for contract in SCENARIOS:
+        d["bytecode"][contract] = load_code(contract, ref).hex()
+    d["source"] = ("runtime / creation bytecode of /root/reference/tests/testdata/inputs/*.sol.o and exec.code "
+                   "of tests/laser/evm_testsuite/VMTests/*/*.json (reference test data)")
+    json.dump(d, open(path, "w"), indent=1)
 
 
 def write(out_dir: str, ref=None, only=None):
@@ -108,24 +212,35 @@ def write(out_dir: str, ref=None, only=None):
     manifest = []
     for contract, scenarios in SCENARIOS.items():
         code = load_code(contract, ref)
-        for name, txs in scenarios:
+        for name, txs, *opt in scenarios:
             if only is not None and only != f"{contract}/{name}":
                 continue
-            m, run = run_sequence(code, txs, balances={x: 10 ** 18 for x in ACTORS.values()})
+            opts = opt[0] if opt else {}
+            bal = opts.get("balances", 10 ** 18)
+            m, run = run_sequence(code, txs, storage=opts.get("storage"), balances={x: bal for x in ACTORS.values()})
             for qi, q in enumerate(run.queries):
                 if q.sat:
                     assert check_model(q.constraints, run.model), (contract, name, qi)
-                fn = f"{contract}_{name}_q{qi:02d}_{'sat' if q.sat else 'unknown'}.smt2.gz"
+                tag = contract.replace("vm:", "vm_").replace("/", "_")
+                kt = "" if q.kind == "jumpi" else q.kind.replace("/", "-") + "_"
+                fn = f"{tag}_{name}_q{qi:02d}_{kt}{'sat' if q.sat else 'unknown'}.smt2.gz"
                 with io.TextIOWrapper(gzip.GzipFile(os.path.join(out_dir, fn), "wb", 9, mtime=0)) as fh:
                     fh.write(f"; expect: {'sat' if q.sat else 'unknown'}\n")
-                    fh.write(f"; source: reference tests/testdata/inputs/{contract}.sol.o, tx {q.tx}, "
-                             f"JUMPI at pc {q.pc}, {'followed' if q.taken else 'other'} successor\n")
+                    src = (f"tests/laser/evm_testsuite/VMTests/{contract[3:]}.json" if contract.startswith("vm:")
+                           else f"tests/testdata/inputs/{contract}.sol.o")
+                    where = (f"JUMPI at pc {q.pc}, {'followed' if q.taken else 'other'} successor" if q.kind == "jumpi"
+                             else f"{q.kind} get_model at pc {q.pc}")
+                    fh.write(f"; source: reference {src}, tx {q.tx}, {where}\n")
                     fh.write(to_smt2(q.constraints))
                 scalars = {k: hex(v) for k, v in run.model.items() if isinstance(v, int)}
                 manifest.append({"file": fn, "contract": contract, "scenario": name, "tx": q.tx, "pc": q.pc,
-                                 "status": "sat" if q.sat else "unknown", "conjuncts": len(q.constraints),
+                                 "kind": q.kind, "status": "sat" if q.sat else "unknown",
+                                 "conjuncts": len(q.constraints),
                                  "model_scalars": scalars if q.sat else None})
-            print(f"{contract}/{name}: {len(run.queries)} queries, tx results {run.halts}")
+            kinds = {}
+            for q in run.queries:
+                kinds[q.kind] = kinds.get(q.kind, 0) + 1
+            print(f"{contract}/{name}: {len(run.queries)} queries {kinds}, tx results {run.halts}")
     if only is None:
         json.dump(manifest, open(os.path.join(out_dir, "manifest.json"), "w"), indent=1)
     print(f"{len(manifest)} queries -> {out_dir}")
