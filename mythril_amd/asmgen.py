@@ -1598,6 +1598,7 @@ def _cdins_chain_static(g, links):
 
 CHECK_OPS = ("CHECK", "CHECK_IMP", "CHECK_IMPEQ")
 ACC = JMP   # s[92:93]: a check run's lane mask (free in a static body)
+CMSK, CMSK2 = S[0], S[2]   # s[72:73], s[74:75]: a check's consequence mask (scratch in a static body)
 
 
 def _nsrc(g, f):
@@ -1620,24 +1621,28 @@ def _check_run_static(g, run):
     condition is formed in SGPRs (premise false OR consequence), ANDed into
     ACC, and ALIVE and the early-exit test are updated once at the end of the
     run.  The SALU combine of check k is emitted after check k+1's compares,
-    so no VALU-written SGPR is read by the next instruction."""
+    so no VALU-written SGPR is read by the next instruction.  Each check
+    writes its own pair of mask pairs (premise, consequence), alternating
+    between two sets: the consequence must not go through vcc, which the next
+    check's compare would overwrite before the deferred combine reads it."""
     g(f"s_mov_b64 {sr(ACC, 2)}, -1")
     pending = None
     for insn in run:
         g.set_insn(insn)
         op = insn[0] & 0xFF
         a, b, c = g.cur["a"], g.cur["b"], g.cur["c"]
-        m = MSK if pending != MSK else MSK2           # alternate the mask pairs
+        m, mc = (MSK, CMSK) if pending != MSK else (MSK2, CMSK2)   # alternate the mask pairs
         if op == isa.OPCODES["CHECK"]:
             g(f"v_cmp_ne_u32_e64 {sr(m, 2)}, 0, {_nreg(g, a, T)}")
             combine = [f"s_and_b64 {sr(ACC, 2)}, {sr(ACC, 2)}, {sr(m, 2)}"]
         else:
             g(f"v_cmp_eq_u32_e64 {sr(m, 2)}, 0, {_nreg(g, a, T)}")
             if op == isa.OPCODES["CHECK_IMP"]:
-                g(f"v_cmp_ne_u32_e32 vcc, 0, {_nreg(g, b, T + 1)}")
+                g(f"v_cmp_ne_u32_e64 {sr(mc, 2)}, 0, {_nreg(g, b, T + 1)}")
             else:
-                g(f"v_cmp_eq_u32_e32 vcc, {_nsrc(g, b)}, {_nreg(g, c, T + 1)}")
-            combine = [f"s_or_b64 {sr(m, 2)}, vcc, {sr(m, 2)}", f"s_and_b64 {sr(ACC, 2)}, {sr(ACC, 2)}, {sr(m, 2)}"]
+                g(f"v_cmp_eq_u32_e64 {sr(mc, 2)}, {_nreg(g, b, T + 2)}, {_nreg(g, c, T + 1)}")   # VOP3: no literal
+            combine = [f"s_or_b64 {sr(m, 2)}, {sr(mc, 2)}, {sr(m, 2)}",
+                       f"s_and_b64 {sr(ACC, 2)}, {sr(ACC, 2)}, {sr(m, 2)}"]
         if pending is not None:
             g(*pending_lines)
         pending, pending_lines = m, combine

@@ -159,3 +159,31 @@ def test_engine_assembles_long_launches(dev, corpus):
     assert [w.index if w else None for w in wa] == [w.index if w else None for w in wi]
     assert with_asm.stats["assembled"] == sum(asmjit.eligible(q.program) for q in qs) > 0
     assert without.stats["assembled"] == 0
+
+
+def test_check_runs_with_true_premises(dev):
+    """A run of CHECK_IMPEQ whose premises hold for some lanes: each check's
+    consequence must be its own.  Round 4 found the assembled run reading the
+    NEXT check's consequence through vcc: environments.sol.o's congruence
+    conjuncts (calldata reads at symbolic offsets, runs of up to 8 checks
+    between fills), found by tools/asmjit_bisect.py."""
+    f = os.path.join(os.path.dirname(__file__), "golden", "laser",
+                     "environments_t1_batch_transfer_q09_unknown.smt2.gz")
+    s = parse_file(f)
+    q = prepare(s.asserts, s.ctx)
+    p = q.program
+    ops = [int(w) & 0xFF for w in p.code[0::4]]
+    imp = isa.OPCODES["CHECK_IMPEQ"]
+    assert any(a == b == imp for a, b in zip(ops, ops[1:])), "no run of CHECK_IMPEQ"
+    n = 1 << 14
+    di, da = pair(dev, p)
+    try:
+        va, _ = dev.eval_generated(da, DEFAULT_SEED, 0, n, trace=False)
+        vi, _ = dev.eval_generated(di, DEFAULT_SEED, 0, n, trace=False)
+    finally:
+        di.free()
+        da.free()
+    _, _, vo = cdag.evaluate(q.lowered.conjuncts, DEFAULT_SEED, 0, n, want_verdict=True,
+                             specs=cdag.program_specs(p))
+    assert np.array_equal(vi.astype(np.uint8), vo)
+    assert np.array_equal(va.astype(np.uint8), vo), int(np.count_nonzero(va.astype(np.uint8) != vo))
