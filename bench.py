@@ -403,22 +403,38 @@ def valu_issue_frac(prog, batch, kernel, kernel_s, n_cu=256, clock_hz=2.4e9):
 
 
 def cpu_baseline(syn, prog, budget_s, dev, dp):
-    """Oracle on the host cores over a bounded sample of the same candidate
-    indices; its verdict vector is compared with the GPU's on those indices
-    (a full-size parity check of the benchmarked kernel)."""
+    """Two CPU legs over bounded samples of the same candidate indices 0..:
+    the product's interpreter and ALU built for the host with OpenMP
+    (mythril_amd/host_baseline.py; the reported ``value``, SURVEY §8(d)'s
+    "build CPU restatement"), and the independent C oracle (oracle/c, bit-serial
+    division; ``checker``).  Each leg's verdict vector is compared with the
+    GPU's on its indices, and the two legs with each other on their overlap (a
+    full-size parity check of the benchmarked kernel)."""
     import numpy as np
     from oracle import cbaseline
-    rec, vo = cbaseline.run(syn, prog, budget_s, verdicts=True)
-    if vo is not None:
-        vg, _ = dev.eval_generated(dp, syn.seed, 0, len(vo), trace=False)
-        bad = int(np.count_nonzero(vg.astype(np.uint8) != vo))
-        rec["verdicts_compared"] = int(len(vo))
-        rec["verdict_mismatches_vs_gpu"] = bad
-        if bad:
-            print(f"[bench] PARITY FAILURE: {bad} of {len(vo)} CPU-baseline verdicts differ from the GPU's",
-                  file=sys.stderr)
-    return rec
+    rec, vf = None, None
+    from mythril_amd import host_baseline
+    if host_baseline.available():
+        rec, vf = host_baseline.baseline(prog, syn.seed, budget_s, verdicts=True)
+    orc, vo = cbaseline.run(syn, prog, budget_s / 2 if rec else budget_s, verdicts=True)
 
+    def vs_gpu(v):
+        vg, _ = dev.eval_generated(dp, syn.seed, 0, len(v), trace=False)
+        return int(np.count_nonzero(vg.astype(np.uint8) != v))
+    for r, v in ((rec, vf), (orc, vo)):
+        if r is not None and v is not None:
+            r["verdicts_compared"] = int(len(v))
+            r["verdict_mismatches_vs_gpu"] = vs_gpu(v)
+            if r["verdict_mismatches_vs_gpu"]:
+                print(f"[bench] PARITY FAILURE: {r['verdict_mismatches_vs_gpu']} of {len(v)} CPU verdicts "
+                      f"({r['sample'][:40]}...) differ from the GPU's", file=sys.stderr)
+    if rec is None:
+        return orc
+    if vo is not None:
+        k = min(len(vo), len(vf))
+        orc["verdict_mismatches_vs_host_build"] = int(np.count_nonzero(vo[:k] != vf[:k]))
+    rec["checker"] = orc
+    return rec
 
 if __name__ == "__main__":
     main()

@@ -64,8 +64,9 @@ def build_host_emu(force: bool = False) -> Path:
         HOST_EMU.parent.mkdir(parents=True, exist_ok=True)
         tmp = HOST_EMU.with_suffix(".so.tmp")
         # host-only compile of the same headers (no device code in these TUs)
-        _run([_hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__",
-              *HOST_SRCS, "-o", tmp])
+        # OpenMP: mwh_count_omp, bench.py's CPU baseline on the product's ALU
+        _run([_hipcc(), "-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__", "-fopenmp",
+              *HOST_SRCS, "-o", tmp, "-Wl,-rpath,/opt/rocm/llvm/lib"])
         os.replace(tmp, HOST_EMU)
     return HOST_EMU
 

@@ -1,8 +1,12 @@
 // mw_host_emu.cpp — CPU build of the *same* interpreter/ALU/leaf code that runs
 // on gfx950 (mw_interp.h, mw_alu.h, mw_leaf.h, mw_keccak.h), one candidate at a
 // time.  TEST/DEVELOPMENT ONLY: lets tests/ check compiler + bytecode + ALU
-// semantics against the oracle on a machine without a GPU.  The product path
-// (mythril_amd.runtime) never loads this library.
+// semantics against the oracle on a machine without a GPU, and is bench.py's
+// fast CPU baseline (mwh_count_omp: the product's ALU on every host core,
+// SURVEY §8(d) "build CPU restatement").  The product path (mythril_amd.runtime)
+// never loads this library.
+#include <omp.h>
+
 #include <cstring>
 #include <vector>
 
@@ -93,6 +97,35 @@ int mwh_div_counts(const mg_prog_desc* d, uint64_t seed, uint64_t begin, size_t 
   }
   return 0;
 }
+
+// Satisfied candidates among generated candidates [begin, begin+ncand) on
+// nthreads OpenMP threads (0: the OpenMP default), each with its own spill
+// area; verdict (optional) receives the per-candidate bits.
+long long mwh_count_omp(const mg_prog_desc* d, uint64_t seed, uint64_t begin, size_t ncand, uint32_t flags,
+                        uint8_t* verdict, int nthreads) {
+  int rc = mg_validate_desc(d);
+  if (rc) return rc;
+  std::vector<u32> consts(d->nconst_words + MW_KPAD, 0u);
+  if (d->nconst_words) std::memcpy(consts.data(), d->consts, d->nconst_words * 4);
+  std::vector<u32> code(d->ncode_words + 32, 0u);
+  std::memcpy(code.data(), d->code, d->ncode_words * 4);
+  if (nthreads <= 0) nthreads = omp_get_max_threads();
+  long long sat = 0;
+#pragma omp parallel num_threads(nthreads) reduction(+ : sat)
+  {
+    std::vector<u32> spill;
+#pragma omp for schedule(dynamic, 256)
+    for (long long i = 0; i < (long long)ncand; ++i) {
+      HostEnv env{d->leaves, d->pool, nullptr, nullptr, (u64)ncand, (u64)i, seed, begin + (u64)i, &spill};
+      const bool ok = mw_run(code.data(), consts.data(), env, true, flags);
+      if (verdict) verdict[i] = ok ? 1 : 0;
+      sat += ok ? 1 : 0;
+    }
+  }
+  return sat;
+}
+
+int mwh_max_threads(void) { return omp_get_max_threads(); }
 
 int mwh_keccak256(const uint8_t* data, const uint64_t* off, const uint32_t* len, size_t n, uint8_t* out32) {
   for (size_t i = 0; i < n; ++i) {

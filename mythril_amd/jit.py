@@ -513,12 +513,45 @@ def compile_device(progs: Sequence[Program], variants: str = "xe", fence_first: 
     return path.read_bytes(), names, dt
 
 
+HOST_OMP_FLAGS = ["-fopenmp", "-Wl,-rpath,/opt/rocm/llvm/lib"]
+
+
+def _omp_entries(names: Sequence[str]) -> str:
+    """<name>_host_omp: the exhaustive verdicts of candidates [begin,
+    begin+count) on every host core (OpenMP), for bench.py's CPU baseline."""
+    out = []
+    for name in dict.fromkeys(names):
+        out += [f'extern "C" int {name}_host_omp(const mw::u32* pool, mw::u64 seed, mw::u64 begin, mw::u64 count,',
+                "                               mw::u32* verdict) {",
+                "#pragma omp parallel for schedule(dynamic, 64)",
+                "  for (long long i = 0; i < (long long)count; ++i) {",
+                "    mw::DivCount ds;",
+                f"    verdict[i] = {name}_body<false>(pool, seed, begin + (mw::u64)i, true, 0u, nullptr, count,",
+                "                                    (mw::u64)i, ds) ? 1u : 0u;",
+                "  }",
+                "  return 0;",
+                "}"]
+    return "\n".join(out) + "\n"
+
+
+def is_host_cached(progs: Sequence[Program], openmp: bool = True) -> bool:
+    """Whether compile_host(progs, openmp=...) would be a cache hit."""
+    names = [kernel_name(p) for p in progs]
+    src = generate(progs, names, "") + (_omp_entries(names) if openmp else "")
+    return (_cache_dir() / f"{_key(src, HOST_FLAGS + (HOST_OMP_FLAGS if openmp else []))}.so").exists()
+
+
 def compile_host(progs: Sequence[Program], lds_leaves: int = 0,
-                 part_weight: Optional[int] = None) -> Tuple[Path, List[str]]:
+                 part_weight: Optional[int] = None, openmp: bool = False) -> Tuple[Path, List[str]]:
     """TEST ONLY: x86 build of the same generated source (verdicts + trace rows).
     With part_weight, every part of every program gets a host entry
-    (<name>_p<k>_host; the program's verdict is the AND over its parts)."""
+    (<name>_p<k>_host; the program's verdict is the AND over its parts).
+    openmp: the candidate loop on every host core (bench.py's CPU baseline)."""
     names = [kernel_name(p) for p in progs]
+    if openmp:
+        src = generate(progs, names, "", lds_leaves=lds_leaves) + _omp_entries(names)
+        path, _ = _compile(src, HOST_FLAGS + HOST_OMP_FLAGS, ".so", ".cpp")
+        return path, names
     if part_weight is not None:
         allp, alln, spec = [], [], []
         for p, name in zip(progs, names):
@@ -628,7 +661,14 @@ def bench_warm_jobs(n_nodes: int = 10000, waves: int = 2, lds_leaves: int = BENC
     def parts():
         objs, dt = compile_parts(progs[24], "x", waves=waves, lds_leaves=lds_leaves)
         log(f"[jit] C5 split kernels ({len(objs)} parts): {'compiled in %.0f s' % dt if dt else 'cached'}")
-    return [lambda: single(24), lambda: single(1), parts]
+
+    def host():   # bench.py's CPU baseline (mythril_amd/host_baseline.py)
+        cached = is_host_cached([progs[24]], openmp=True)
+        t0 = time.perf_counter()
+        compile_host([progs[24]], openmp=True)
+        log(f"[jit] C5 x86 OpenMP build (CPU baseline): "
+            f"{'cached' if cached else 'compiled in %.0f s' % (time.perf_counter() - t0)}")
+    return [lambda: single(24), lambda: single(1), parts, host]
 
 
 def warm_bench_cache(n_nodes: int = 10000, log=print, waves: int = 2, lds_leaves: int = BENCH_LDS_LEAVES) -> float:

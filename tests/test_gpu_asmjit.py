@@ -18,6 +18,7 @@ from mythril_amd import asmjit, isa
 from mythril_amd.compiler import compile_program
 from mythril_amd.engine import DEFAULT_SEED, prepare
 from mythril_amd.ir import Ctx
+from mythril_amd.smt2 import parse_file
 from oracle import cdag
 from tests.test_gpu_asm import _corpus, _random_supported_dag
 
