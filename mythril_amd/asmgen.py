@@ -47,7 +47,7 @@ CLO, CHI, ALIVE, LDSOFF, GOFF = 160, 161, 162, 163, 164
 CUR = 40          # s40..s43 current instruction words w0..w3
 NXT = 44          # s44..s47 next instruction (prefetched)
 SOFF = 48         # byte offset of the next instruction from CODE0
-TABLO = 49        # address of the dispatch table (Ltab), low / high word
+TABLO = 49        # address of the handlers' base (Lpc0), low / high word
 TABHI = 58
 SIDX = 19         # register-file index of an operand / write-back
 # assembled kernels (template mode): addresses the straight-line body leaves
@@ -94,6 +94,8 @@ HIT = 38          # after the prologue: this wave has reported a witness (chunks
 TID, LO_SREG = 165, 0
 
 NTAB = 128
+CHAIN_BIT = 15     # predecoded word 0: W_CDINS's FLAG_CHAIN (mw_asm_predecode)
+INTROSPECT_FLAG = 7   # AsmArgs.flags bit: report the handler offsets and exit
 
 
 def v(i):
@@ -295,11 +297,14 @@ class Gen:
         """dispatch the next instruction (each handler ends in its own copy:
         no jump back to a shared dispatch block).  It was prefetched one ahead;
         the stream ends in a validated END and no instruction jumps, so the
-        offset only grows to it."""
+        offset only grows to it.  The predecoded word 0 holds the handler's
+        word offset from Lpc0 in bits [14:0] (mw_asm_predecode, from the
+        offsets the kernel reports in its introspection mode): one jump, no
+        table."""
         self("s_waitcnt lgkmcnt(0)", f"s_mov_b64 {sr(CUR, 2)}, {sr(NXT, 2)}",
              f"s_mov_b64 {sr(CUR + 2, 2)}, {sr(NXT + 2, 2)}",
              f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, {s(SOFF)}",
-             f"s_and_b32 {s(JMP)}, {s(CUR)}, 0x7f", f"s_lshl2_add_u32 {s(SX)}, {s(JMP)}, {s(TABLO)}",
+             f"s_and_b32 {s(JMP)}, {s(CUR)}, 0x7fff", f"s_lshl2_add_u32 {s(SX)}, {s(JMP)}, {s(TABLO)}",
              f"s_addc_u32 {s(SX + 1)}, {s(TABHI)}, 0", f"s_setpc_b64 {sr(SX, 2)}")
 
 
@@ -780,7 +785,7 @@ def build_handlers():
         g.label(nos)
         # chained: consume the next instruction (a W_CDINS whose acc is this word)
         last = g.L("cdlast")
-        g(f"s_bitcmp1_b32 {s(CUR)}, 8", f"s_cbranch_scc0 {last}")
+        g(f"s_bitcmp1_b32 {s(CUR)}, {CHAIN_BIT}", f"s_cbranch_scc0 {last}")
         g.width(S[2]), g.canon(XR, S[2])
         consume_next(g)
         g(f"s_branch {top}")
@@ -918,10 +923,24 @@ def gen(mode="interp"):
       f"s_mov_b64 {sr(EVALS, 2)}, 0", f"s_mov_b32 {s(HIT)}, 0",
       f"v_lshlrev_b32_e32 {v(LDSOFF)}, 2, {v(T)}", f"v_mov_b32_e32 {v(TID)}, {v(T)}")
     if mode == "interp":
-        # the dispatch table's address (s_getpc_b64 gives the next instruction's)
-        g(f"s_getpc_b64 {sr(SX, 2)}")
+        # the handlers' base address (s_getpc_b64 gives the next instruction's)
+        g(f"s_getpc_b64 {sr(TABLO, 2) if TABHI == TABLO + 1 else sr(SX, 2)}")
         g.label("Lpc0_%=")
-        g(f"s_add_u32 {s(TABLO)}, {s(SX)}, (Ltab_%= - Lpc0_%=)", f"s_addc_u32 {s(TABHI)}, {s(SX + 1)}, 0")
+        if TABHI != TABLO + 1:
+            g(f"s_mov_b32 {s(TABLO)}, {s(SX)}", f"s_mov_b32 {s(TABHI)}, {s(SX + 1)}")
+        # introspection (AsmArgs.flags bit 7): lane 0 writes the word offset of
+        # every opcode's handler from Lpc0 to the verdict pointer and the kernel
+        # exits; mg_init reads them once for mw_asm_predecode
+        names = {c: n for n, c in isa.OPCODES.items()}
+        g(f"s_bitcmp1_b32 {s(FLAGS)}, {INTROSPECT_FLAG}", "s_cbranch_scc0 Lnointro_%=",
+          f"s_mov_b64 {sr(EXECSV, 2)}, exec", "s_mov_b64 exec, 1")
+        for code in range(NTAB):
+            n = names.get(code)
+            tgt = f"Lh_{n}_%=" if (n in handlers or n == "END") else "Lunsup_%="
+            g(f"v_mov_b32_e32 {v(T)}, (({tgt} - Lpc0_%=) >> 2)", f"v_mov_b32_e32 {v(T + 1)}, {4 * code}",
+              f"global_store_dword {v(T + 1)}, {v(T)}, {sr(VERD, 2)}")
+        g(f"s_mov_b64 exec, {sr(EXECSV, 2)}", "s_branch Lexit_%=")
+        g.label("Lnointro_%=")
     else:
         for reg, lab in ((LEAFADDR, "Lleaf_%="), (STOPADDR, "Lstop_%="), (ENDADDR, "Lh_END_%="),
                          (PHILOXADDR, "Lphilox_%=")):
@@ -961,11 +980,6 @@ def gen(mode="interp"):
         # ---- dispatch
         g.label("Ldisp_%=")
         g.next()
-        g.label("Ltab_%=")
-        names = {c: n for n, c in isa.OPCODES.items()}
-        for code in range(NTAB):
-            n = names.get(code)
-            g(f"s_branch Lh_{n}_%=" if n in handlers or n == "END" else "s_branch Lunsup_%=")
         # handlers
         for n in ASM_OPCODES:
             if n == "END":

@@ -30,7 +30,7 @@
 extern "C" int mw_fail(int code, const char* msg);
 extern "C" int mg_validate_desc(const mg_prog_desc* d);
 extern "C" void mw_asm_predecode(const uint32_t* code, size_t nwords, const uint32_t* consts, size_t nconst,
-                                 uint32_t* out);
+                                 const uint32_t* hoff, uint32_t* out);
 
 using namespace mw;
 
@@ -593,6 +593,58 @@ bool asm_enabled() {
   return !(e && e[0] == '0');
 }
 
+// The asm interpreter's handler word offsets per opcode, as the kernel itself
+// reports them (AsmArgs.flags bit 7, mythril_amd/asmgen.py gen "introspection"):
+// mw_asm_predecode writes them into the instructions so the dispatch is one
+// jump.  Read once per process on the first context's device (every device
+// runs the same code object); until then, or if it fails, no program is
+// asm-eligible (the compiled interpreter runs them: same results).
+std::mutex g_hoff_mu;
+bool g_hoff_ready = false;
+u32 g_hoff[128];
+
+int asm_handler_offsets(int dev, hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_hoff_mu);
+  if (g_hoff_ready) return 0;
+  HIPCHK(hipSetDevice(dev));
+  void* buf = nullptr;
+  const size_t bytes = sizeof(ProgDev) + sizeof(AsmArgs) + 128 * sizeof(u32) + 2 * sizeof(u64);
+  HIPCHK(hipMalloc(&buf, bytes));
+  char* b = (char*)buf;
+  ProgDev* dp = (ProgDev*)b;
+  AsmArgs* da = (AsmArgs*)(b + sizeof(ProgDev));
+  u32* dout = (u32*)(b + sizeof(ProgDev) + sizeof(AsmArgs));
+  u64* dmin = (u64*)(dout + 128);
+  ProgDev hp{};
+  AsmArgs ha{};
+  ha.flags = 1u << 7;
+  ha.verdict = dout;
+  hipError_t e = hipMemsetAsync(buf, 0, bytes, stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(dp, &hp, sizeof hp, hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(da, &ha, sizeof ha, hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(mw_search_asm_kernel, dim3(1u, 1u), dim3(kBlock), 0, stream, (const ProgDev*)dp,
+                       (const AsmArgs*)da, dmin, dmin + 1, 0u);
+    e = hipGetLastError();
+  }
+  u32 h[128];
+  if (e == hipSuccess) e = hipMemcpyAsync(h, dout, sizeof h, hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  hipFree(buf);
+  if (e != hipSuccess) return fail(MG_E_HIP, std::string("asm handler offsets: ") + hipGetErrorString(e));
+  for (int k = 0; k < 128; ++k) {
+    if (h[k] == 0 || h[k] > 0x7fffu) return fail(MG_E_HIP, "asm handler offsets out of range");
+    g_hoff[k] = h[k];
+  }
+  g_hoff_ready = true;
+  return 0;
+}
+
+bool asm_offsets_ready() {
+  std::lock_guard<std::mutex> lk(g_hoff_mu);
+  return g_hoff_ready;
+}
+
 }  // namespace
 
 extern "C" {
@@ -635,6 +687,10 @@ int mg_init(int device, mg_ctx** out) {
           hipSuccess) {
     (void)hipGetLastError();  // older runtimes: the default limit already covers it
   }
+  if (asm_enabled() && asm_handler_offsets(c->dev, c->stream) != 0) {
+    (void)hipGetLastError();  // the asm interpreter stays off: the compiled interpreter runs every program
+    std::fprintf(stderr, "[mythril_amd] asm interpreter disabled: %s\n", mg_last_error());
+  }
   *out = (mg_ctx*)(uintptr_t)g_reg.add_ctx(std::move(c));
   return 0;
 }
@@ -662,7 +718,7 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   // operand fetch reads cpool[slot] (slot < 64) before selecting the register
   const size_t nc = d->ncode_words, nk = (d->nconst_words + 8 > MW_KPAD ? d->nconst_words + 8 : MW_KPAD), nl = d->nleaves * MW_LEAF_WORDS + 8,
                np = d->npool_words + 8;
-  const bool asm_ok = asm_eligible(d);
+  const bool asm_ok = asm_offsets_ready() && asm_eligible(d);
   const size_t na = asm_ok ? nc + 8 : 0;   // + the block after END the dispatch prefetches
   const size_t total = nc + nk + nl + np + na;
   auto p = std::make_shared<Prog>();
@@ -679,7 +735,7 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   if (d->nconst_words) std::memcpy(hbuf.data() + nc, d->consts, d->nconst_words * 4);
   if (d->nleaves) std::memcpy(hbuf.data() + nc + nk, d->leaves, d->nleaves * MW_LEAF_WORDS * 4);
   if (d->npool_words) std::memcpy(hbuf.data() + nc + nk + nl, d->pool, d->npool_words * 4);
-  if (asm_ok) mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, hbuf.data() + nc + nk + nl + np);
+  if (asm_ok) mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, g_hoff, hbuf.data() + nc + nk + nl + np);
   if (hipMemcpy(p->d_buf, hbuf.data(), total * 4, hipMemcpyHostToDevice) != hipSuccess) {
     release_prog(*p);
     return fail(MG_E_HIP, "program upload copy failed");

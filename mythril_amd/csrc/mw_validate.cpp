@@ -201,7 +201,12 @@ int mg_validate_desc(const mg_prog_desc* d) {
 // W_CDINS byte index (always a constant) below 0x4000, which becomes
 // 0x4000 | index (the handler then compares it with one 32-bit summary of the
 // size instead of a signed 256-bit subtraction).
-void mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t nconst, u32* out) {
+// hoff: the asm interpreter's handler word offsets per opcode (128 entries,
+// reported by the kernel itself, mw_kernels.hip asm_handler_offsets); word 0
+// becomes width [31:16] | FLAG_CHAIN [15] | handler offset [14:0], so the
+// dispatch is one jump (mythril_amd/asmgen.py Gen.next).
+void mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t nconst, const u32* hoff,
+                      u32* out) {
   for (size_t i = 0; i + 3 < nwords; i += 4) {
     const u32* I = code + i;
     u32* O = out + i;
@@ -212,7 +217,7 @@ void mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t 
     if (sh.dst == 4) d2 = MW_DST_NLO(dst) != MW_N_RESERVED ? MW_DST_NLO(dst) : 32u + MW_DST_NHI(dst);
     else if (sh.dst == 3) d2 = (MW_DST_W(dst) * 8u) << 8;
     auto opnd = [](int kind, u32 f) { return (kind == 1 && !(f & MW_KBIT)) ? f * 8u : f; };
-    O[0] = I[0];
+    O[0] = (I[0] & 0xffff0000u) | ((I[0] >> 8) & MW_FLAG_CHAIN ? 0x8000u : 0u) | (hoff[I[0] & 0x7fu] & 0x7fffu);
     O[1] = d2 | (opnd(sh.a, a) << 16);
     u32 c2 = opnd(sh.c, c);
     if ((I[0] & 0xffu) == MW_W_CDINS && (c & MW_KBIT)) {

@@ -26,10 +26,12 @@ def test_opcode_lists_agree():
     assert [o[3:] for o in ops] == isa.ASM_OPCODES
     kinds = [int(k) for k in re.search(r"#define MW_ASM_LEAF_KINDS (.*)", txt).group(1).split(", ")]
     assert kinds == isa.ASM_LEAF_KINDS
-    # every listed opcode has a handler label, and the dispatch table has 128 entries
+    # every listed opcode has a handler label, and the introspection block
+    # reports an offset for all 128 opcodes (handler or Lunsup)
     for o in isa.ASM_OPCODES:
         assert f"Lh_{o}_%=:" in txt, o
-    assert txt.count("s_branch Lh_") + txt.count("s_branch Lunsup_%=") >= 128
+    assert txt.count("- Lpc0_%=) >> 2)") == 128
+    assert "s_branch Lh_" not in txt          # one jump per dispatch: no table of branches
 
 
 def _corpus_programs():
@@ -62,18 +64,25 @@ def _predecode(code, consts):
     lib = ctypes.CDLL(LIB_PATH)
     f = lib.mw_asm_predecode
     f.restype = None
-    f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                  ctypes.c_void_p]
     code = np.ascontiguousarray(code, dtype=np.uint32)
     consts = np.ascontiguousarray(consts, dtype=np.uint32)
     out = np.zeros_like(code)
-    f(code.ctypes.data, code.size, consts.ctypes.data, consts.size, out.ctypes.data)
+    f(code.ctypes.data, code.size, consts.ctypes.data, consts.size, HOFF.ctypes.data, out.ctypes.data)
     return out.reshape(-1, 4)
 
 
+# stand-in handler word offsets (the kernel reports the real ones at mg_init)
+HOFF = __import__("numpy").arange(1000, 1000 + 128 * 7, 7, dtype="uint32")
+
+
 def test_predecode_operand_layout():
-    """The asm engine's copy of the code: N dst -> slot in [5:0], W dst -> slot
-    x 8 in [13:8], W register operands -> slot x 8, constants and N operands
-    unchanged, a W_CDINS index constant below 0x4000 -> 0x4000 | index."""
+    """The asm engine's copy of the code: word 0 -> width | FLAG_CHAIN at bit 15
+    | the opcode's handler word offset (one-jump dispatch), N dst -> slot in
+    [5:0], W dst -> slot x 8 in [13:8], W register operands -> slot x 8,
+    constants and N operands unchanged, a W_CDINS index constant below 0x4000
+    -> 0x4000 | index."""
     e = isa.encode
     consts = [0] * 16
     consts[0], consts[8] = 0x24, 0x5000   # two 256-bit constants (limbs 1..7 zero)
@@ -86,7 +95,8 @@ def test_predecode_operand_layout():
             + e("END", 0, isa.encode_dst(None)))
     o = _predecode(code, consts)
     src = __import__("numpy").asarray(code, dtype="uint32").reshape(-1, 4)
-    assert (o[:, 0] == src[:, 0]).all() and (o[:, 3] == src[:, 3]).all()
+    want0 = (src[:, 0] & 0xFFFF0000) | HOFF[src[:, 0] & 0x7F] | (((src[:, 0] >> 8) & isa.FLAG_CHAIN) << 15)
+    assert (o[:, 0] == want0).all() and (o[:, 3] == src[:, 3]).all()
     assert o[0, 1] == 37 | (3 << 16) and o[0, 2] == isa.KBIT | 8
     assert o[1, 1] == (40 << 8) | (16 << 16) and o[1, 2] == isa.KBIT | 0
     assert o[2, 1] == 4 | (48 << 16) and o[2, 2] == 8
