@@ -109,6 +109,13 @@ int mg_eval(mg_ctx* ctx, const mg_prog* prog, const uint32_t* leaves_soa, size_t
 int mg_eval_generated(mg_ctx* ctx, const mg_prog* prog, uint64_t seed, uint64_t begin,
                       size_t count, uint32_t* verdict, uint32_t* trace);
 
+/* The values of every leaf (free variable) of a loaded program at candidate
+ * `index`: out receives nleaves x 8 u32 limbs, leaf by leaf in the program's
+ * leaf-table order, as the search kernels generate them (the witness values
+ * of an index mg_search returned).  Replaces z3's Optimize.model()
+ * (mythril/laser/smt/solver/solver.py:68-77) for the free symbols. */
+int mg_witness_leaves(mg_ctx* ctx, const mg_prog* prog, uint64_t seed, uint64_t index, uint32_t* out);
+
 /* Attach a specialised kernel to a loaded program: `image` is a gfx950 code
  * object generated from this program's own IR by mythril_amd/jit.py (one
  * straight-line kernel per program, csrc/mw_jit.h).  It must export

@@ -380,11 +380,43 @@ MW_HD void udivrem8_full(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
 // the normalised divisor; the remainder stays one limb throughout.  C5 divides
 // by such values (quotients of earlier divisions) in 42 of its 384 divisions,
 // where the general loop ran all eight steps.
+// The eight steps run as a rolled loop over a sliding window (w[7] the current
+// limb, w[6] the next lower one), the digits shifting into qq: unrolled, the
+// steps were ~160 instructions at each of C5's 384 division sites, which run
+// this path on a few waves only (18 of 384 per candidate); MW_SHORT_UNROLLED
+// restores the unrolled form (tools/ab_c5.py variant "shortunroll").
 MW_HD void udivrem8_short(const u32 x[8], u32 y0, u32 q[8], u32 r[8]) {
   const u32 s = clz32(y0);
   const u32 d = y0 << s;
   const u32 v = recip32(d);
   u32 rem = fshl32(0u, x[7], s);  // < 2^s <= d
+#if !defined(MW_SHORT_UNROLLED)
+  u32 w[8], qq[8];
+  copy8(w, x);
+  zero8(qq);
+#pragma unroll 1
+  for (int it = 0; it < 8; ++it) {
+    const u32 u0 = fshl32(w[7], w[6], s);   // it == 7: x[0] << s (w[6] is 0 by then)
+    const u64 qp = (u64)v * rem + ((((u64)rem) << 32) | u0);
+    u32 q1 = (u32)(qp >> 32) + 1u;
+    const u32 q0 = (u32)qp;
+    u32 rr = u0 - q1 * d;
+    const bool adj1 = rr > q0;
+    q1 = adj1 ? q1 - 1u : q1;
+    rr = adj1 ? rr + d : rr;
+    const bool adj2 = rr >= d;  // unlikely
+    q1 = adj2 ? q1 + 1u : q1;
+    rr = adj2 ? rr - d : rr;
+#pragma unroll
+    for (int k = 7; k > 0; --k) qq[k] = qq[k - 1];
+    qq[0] = q1;
+#pragma unroll
+    for (int k = 7; k > 0; --k) w[k] = w[k - 1];
+    w[0] = 0u;
+    rem = rr;
+  }
+  copy8(q, qq);
+#else
 #pragma unroll
   for (int k = 7; k >= 0; --k) {
     const u32 u0 = k > 0 ? fshl32(x[k], x[k - 1], s) : (x[0] << s);
@@ -401,6 +433,7 @@ MW_HD void udivrem8_short(const u32 x[8], u32 y0, u32 q[8], u32 r[8]) {
     q[k] = q1;
     rem = rr;
   }
+#endif
   r[0] = rem >> s;
 #pragma unroll
   for (int k = 1; k < 8; ++k) r[k] = 0u;
@@ -467,7 +500,6 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], DivCount
   // round 2, needed bit normalisation and cost about 1.5x as much per digit;
   // tools/ab_c5.py put those 25 of C5's 384 divisions at 13 % of the kernel.)
   if (dc) dc->gen += 1u;
-  const u32 n = y[7] ? 0u : y[6] ? 1u : y[5] ? 2u : y[4] ? 3u : y[3] ? 4u : y[2] ? 5u : y[1] ? 6u : 7u;
   u32 v[8], u[16];
   copy8(v, y);
 #pragma unroll
@@ -475,6 +507,26 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], DivCount
     u[k] = x[k];
     u[k + 8] = 0u;
   }
+#if !defined(MW_GEN_SELECT_STAGES)
+  // v <<= 32n, u <<= 32n (n: the lane's zero top limbs of y) as a rolled loop
+  // of one-limb moves under selects, run as often as the wave's largest n:
+  // three unrolled select stages were ~80 instructions at each of C5's 384
+  // division sites (MW_GEN_SELECT_STAGES restores them; tools/ab_c5.py "genstages")
+  u32 n = 0u;
+#pragma unroll 1
+  for (int st = 0; st < 7; ++st) {
+    const bool c = v[7] == 0u;
+    if (!MW_ANY(c)) break;
+    n += c ? 1u : 0u;
+#pragma unroll
+    for (int k = 7; k > 0; --k) v[k] = c ? v[k - 1] : v[k];
+    v[0] = c ? 0u : v[0];
+#pragma unroll
+    for (int k = 15; k > 0; --k) u[k] = c ? u[k - 1] : u[k];
+    u[0] = c ? 0u : u[0];
+  }
+#else
+  const u32 n = y[7] ? 0u : y[6] ? 1u : y[5] ? 2u : y[4] ? 3u : y[3] ? 4u : y[2] ? 5u : y[1] ? 6u : 7u;
 #pragma unroll
   for (int st = 0; st < 3; ++st) {  // v <<= 32n, u <<= 32n (limb moves under selects)
     const int m = 1 << st;
@@ -484,6 +536,7 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], DivCount
 #pragma unroll
     for (int k = 15; k >= 0; --k) u[k] = c ? (k >= m ? u[k - m] : 0u) : u[k];
   }
+#endif
   // The eight digit positions as a rolled loop over a sliding window
   // w = u[j..j+8] (j = 7 - it), the untouched low limbs feeding it from lo[]
   // and the digits shifting into qq[]: unrolled, this path was ~1 000
@@ -539,6 +592,16 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], DivCount
     u[k] = w[k];
     u[k + 8] = 0u;
   }
+#if !defined(MW_GEN_SELECT_STAGES)
+#pragma unroll 1
+  for (int st = 0; st < 7; ++st) {  // r = u[0..7] >> 32n, one limb per pass
+    const bool c = n > (u32)st;
+    if (!MW_ANY(c)) break;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) u[k] = c ? u[k + 1] : u[k];
+    u[7] = c ? 0u : u[7];
+  }
+#else
 #pragma unroll
   for (int st = 0; st < 3; ++st) {  // r = u[0..7] >> 32n
     const int m = 1 << st;
@@ -546,6 +609,7 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], DivCount
 #pragma unroll
     for (int k = 0; k < 8; ++k) u[k] = c ? (k + m < 16 ? u[k + m] : 0u) : u[k];
   }
+#endif
   copy8(r, u);
 }
 

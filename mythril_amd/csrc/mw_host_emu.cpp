@@ -127,6 +127,14 @@ long long mwh_count_omp(const mg_prog_desc* d, uint64_t seed, uint64_t begin, si
 
 int mwh_max_threads(void) { return omp_get_max_threads(); }
 
+// Leaf values of candidate `cand` (the host twin of mg_witness_leaves).
+int mwh_leaf_values(const mg_prog_desc* d, uint64_t seed, uint64_t cand, uint32_t* out) {
+  int rc = mg_validate_desc(d);
+  if (rc) return rc;
+  for (size_t l = 0; l < d->nleaves; ++l) leaf_value(d->leaves + l * MW_LEAF_WORDS, d->pool, seed, cand, out + 8 * l);
+  return 0;
+}
+
 int mwh_keccak256(const uint8_t* data, const uint64_t* off, const uint32_t* len, size_t n, uint8_t* out32) {
   for (size_t i = 0; i < n; ++i) {
     u64 h[4];

@@ -271,6 +271,18 @@ __global__ __launch_bounds__(kBlock, 2) void mw_eval_kernel(ProgDev P, const u32
   }
 }
 
+// The leaf values of one candidate: one thread per leaf, the candidate
+// generator of every search engine (mw_leaf.h leaf_value), for mg_witness_leaves.
+__global__ __launch_bounds__(kBlock) void mw_leaf_kernel(const u32* __restrict__ leaves, const u32* __restrict__ pool,
+                                                         u32 nleaves, u64 seed, u64 cand, u32* __restrict__ out) {
+  const u32 l = blockIdx.x * kBlock + threadIdx.x;
+  if (l >= nleaves) return;
+  u32 v[8];
+  leaf_value(leaves + (u64)l * MW_LEAF_WORDS, pool, seed, cand, v);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[(u64)l * 8 + k] = v[k];
+}
+
 __global__ __launch_bounds__(kBlock) void mw_keccak_kernel(const uint8_t* __restrict__ data,
                                                            const u64* __restrict__ off,
                                                            const u32* __restrict__ len, u64 n,
@@ -1218,6 +1230,30 @@ int mg_eval_generated(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t begi
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   hipFree(d_v);
   if (e != hipSuccess) return fail(MG_E_HIP, std::string("eval (specialised): ") + hipGetErrorString(e));
+  return 0;
+}
+
+int mg_witness_leaves(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t index, uint32_t* out) {
+  if (!h || !hp || !out) return fail(MG_E_ARG, "null argument");
+  const u64 id = hid(hp);
+  CallG call;
+  if (const char* why = mw::enter(g_reg, hid(h), &id, 1, call))
+    return fail(MG_E_ARG, std::string("mg_witness_leaves: ") + why);
+  Ctx* c = call.c.get();
+  const Prog* p = call.ps[0].get();
+  const u32 nl = (u32)p->desc.nleaves;
+  if (nl == 0) return 0;
+  HIPCHK(hipSetDevice(c->dev));
+  (void)hipGetLastError();
+  u32* d = nullptr;
+  if (hipMalloc(&d, (size_t)nl * 8 * sizeof(u32)) != hipSuccess) return fail(MG_E_NOMEM, "witness leaf buffer");
+  hipLaunchKernelGGL(mw_leaf_kernel, dim3((nl + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, p->dev.leaves,
+                     p->dev.pool, nl, seed, index, d);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d, (size_t)nl * 8 * sizeof(u32), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(d);
+  if (e != hipSuccess) return fail(MG_E_HIP, std::string("witness leaves: ") + hipGetErrorString(e));
   return 0;
 }
 

@@ -208,9 +208,43 @@ class WitnessEngine:
         return max(min(self.budget, MIN_CANDIDATES), min(self.budget, self.op_budget // ops))
 
     def materialize(self, q: Query, index: int, search_dp=None) -> Optional[Witness]:
-        """The witness at candidate ``index``: its verdict re-evaluated by the
-        search program (``search_dp`` if still loaded), its values read from
-        the witness program."""
+        """The witness at candidate ``index``.  When every array index and
+        function argument is a constant (each such cell is then a leaf of its
+        own), the leaf values are all of it: one mg_witness_leaves launch on
+        the still-loaded search program.  Otherwise the verdict is re-evaluated
+        by the search program and the values are read from the witness
+        program (leaves plus the traced argument terms)."""
+        if (search_dp is not None and getattr(self.dev, "witness_leaves", None) is not None
+                and all(t.op == "const" for t in q.arg_terms)):
+            return self._from_leaves(q, index, self.dev.witness_leaves(search_dp, self.seed, index))
+        return self._materialize_traced(q, index, search_dp)
+
+    def _from_leaves(self, q: Query, index: int, leaf_values) -> Witness:
+        values = {n.name: v for n, v in zip(q.program.leaf_nodes, leaf_values)}
+        w = Witness(index, values)
+        self._ack_cells(q, w, values, lambda t: t.val)
+        return w
+
+    @staticmethod
+    def _ack_cells(q: Query, w: Witness, values: Dict[str, int], term_value) -> None:
+        for al in q.lowered.ack.values():
+            args = []
+            for parts in q.arg_chunks[al.name]:
+                v = 0
+                for k, t in enumerate(parts):
+                    v |= term_value(t) << (256 * k)
+                args.append(v)
+            if al.value is not None:
+                val = args.pop()  # defined value (keccak inverse = hashed input)
+            else:
+                val = _combine_chunks(values, al.name, al.width)
+            args = tuple(args)
+            if al.kind == "select":
+                w.arrays.setdefault(al.base, {})[args[0]] = val
+            else:
+                w.functions.setdefault(al.base, {})[args] = val
+
+    def _materialize_traced(self, q: Query, index: int, search_dp=None) -> Optional[Witness]:
         from .runtime import EngineError, unpack_trace
         p = q.trace_program
         if [n.name for n in p.leaf_nodes] != [n.name for n in q.program.leaf_nodes]:
@@ -233,20 +267,5 @@ class WitnessEngine:
             dp.free()
         values = {n.name: unpack_trace(p, trace, n)[0] for n in p.leaf_nodes}
         w = Witness(index, values)
-        for al in q.lowered.ack.values():
-            args = []
-            for parts in q.arg_chunks[al.name]:
-                v = 0
-                for k, t in enumerate(parts):
-                    v |= (t.val if t.op == "const" else unpack_trace(p, trace, t)[0]) << (256 * k)
-                args.append(v)
-            if al.value is not None:
-                val = args.pop()  # defined value (keccak inverse = hashed input)
-            else:
-                val = _combine_chunks(values, al.name, al.width)
-            args = tuple(args)
-            if al.kind == "select":
-                w.arrays.setdefault(al.base, {})[args[0]] = val
-            else:
-                w.functions.setdefault(al.base, {})[args] = val
+        self._ack_cells(q, w, values, lambda t: t.val if t.op == "const" else unpack_trace(p, trace, t)[0])
         return w

@@ -73,6 +73,7 @@ SIGNATURES = {
                                  ctypes.POINTER(MgStats)]),
     "mg_eval": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t, _P, _P]),
     "mg_eval_generated": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, _P, _P]),
+    "mg_witness_leaves": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, _P]),
     "mg_keccak256": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _P, _P, ctypes.c_size_t, _P, ctypes.POINTER(MgStats)]),
     "mg_keccak256_device": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_size_t, _P, ctypes.POINTER(MgStats)]),
     "mg_validate_desc": (ctypes.c_int, [ctypes.POINTER(MgProgDesc)]),
@@ -233,6 +234,23 @@ class Device:
                                                     v.ctypes.data, _ptr(t) if t is not None else None),
                "mg_eval_generated")
         return v, (t.reshape(dp.prog.n_trace_rows, count) if t is not None else None)
+
+    def witness_leaves(self, dp: DeviceProgram, seed: int, index: int) -> List[int]:
+        """The value of every leaf of dp's program at candidate index, in
+        leaf-table order (mg_witness_leaves), masked to the leaf's width."""
+        p = dp.prog
+        n = len(p.leaf_nodes)
+        out = np.zeros(max(1, n) * 8, dtype=np.uint32)
+        _check(self.lib, self.lib.mg_witness_leaves(self.handle, dp.handle, seed & ((1 << 64) - 1), index,
+                                                    out.ctypes.data), "mg_witness_leaves")
+        vals = []
+        for i, node in enumerate(p.leaf_nodes):
+            v = 0
+            for k in range(8):
+                v |= int(out[8 * i + k]) << (32 * k)
+            w = 1 if node.width == 0 else node.width
+            vals.append(v & ((1 << w) - 1))
+        return vals
 
     def keccak256(self, msgs: Sequence[bytes]) -> Tuple[List[bytes], dict]:
         n = len(msgs)

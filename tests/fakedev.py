@@ -43,6 +43,28 @@ class FakeDevice:
     def eval_generated(self, dp, seed, begin, count, trace=True):
         return emu_eval(dp.prog, None, count, seed=seed, begin=begin)
 
+    def witness_leaves(self, dp, seed, index):
+        """Device.witness_leaves (mg_witness_leaves) on the host build of the
+        same leaf generator (mw_leaf.h, mwh_leaf_values)."""
+        import ctypes
+
+        from mythril_amd.runtime import make_desc
+        from tests.helpers import host_emu
+        p = dp.prog
+        d, keep = make_desc(p)
+        out = np.zeros(max(1, len(p.leaf_nodes)) * 8, dtype=np.uint32)
+        f = host_emu().mwh_leaf_values
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+        rc = f(ctypes.byref(d), seed & ((1 << 64) - 1), index, out.ctypes.data)
+        assert rc == 0
+        self.witness_leaf_calls = getattr(self, "witness_leaf_calls", 0) + 1
+        vals = []
+        for i, node in enumerate(p.leaf_nodes):
+            v = sum(int(out[8 * i + k]) << (32 * k) for k in range(8))
+            vals.append(v & ((1 << (1 if node.width == 0 else node.width)) - 1))
+        return vals
+
     def keccak256(self, msgs):
         """Device.keccak256 on the host build of the same Keccak source."""
         from tests.helpers import host_emu

@@ -436,6 +436,7 @@ def test_witness_layout_mismatch_falls_back_to_reference(mythril, monkeypatch):
     from mythril_amd import engine as engine_mod
     from mythril_amd.compiler import compile_program
     real = engine_mod.prepare
+    monkeypatch.setattr(FakeDevice, "witness_leaves", None)   # the traced path (witness program)
 
     def broken(conj, ctx, **kw):
         q = real(conj, ctx, **kw)
@@ -444,3 +445,13 @@ def test_witness_layout_mismatch_falls_back_to_reference(mythril, monkeypatch):
     monkeypatch.setattr(engine_mod, "prepare", broken)
     assert dropin.get_model(SAT).raw[0] == "ref"
     assert dropin.STATS["device_errors"] >= 1
+
+
+def test_constant_cells_materialise_from_leaves(mythril):
+    """A witness whose array cells all have constant indices is read from the
+    search program's leaves (mg_witness_leaves), without a witness program."""
+    dev = dropin._engine.dev
+    n0 = getattr(dev, "witness_leaf_calls", 0)
+    res = dropin.get_model(SAT)
+    assert res.raw[0][0] == "z3"
+    assert getattr(dev, "witness_leaf_calls", 0) == n0 + 1
