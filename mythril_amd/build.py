@@ -1,6 +1,6 @@
 """Build the native libraries in-tree (hipcc cross-compiles gfx950 without a GPU).
 
-  mythril_amd/lib/libmythril_witness.so   product: gfx950 kernels + C-ABI
+  mythril_amd/lib/libmythril_witness.so   product: gfx950 kernels + C-ABI + the host compiler
   build/host/libmw_host_emu.so            test-only CPU build of the same interpreter
   oracle/build/liboracle.so               test-only C restatement (built by oracle/Makefile)
   mythril_amd/lib/asmjit_template.s       the assembled kernels' template (gfx950 assembly,
@@ -21,7 +21,7 @@ LIB = ROOT / "mythril_amd" / "lib" / "libmythril_witness.so"
 HOST_EMU = ROOT / "build" / "host" / "libmw_host_emu.so"
 ARCH = os.environ.get("MW_OFFLOAD_ARCH", "gfx950")
 
-DEVICE_SRCS = ["mw_kernels.hip", "mw_validate.cpp"]
+DEVICE_SRCS = ["mw_kernels.hip", "mw_validate.cpp", "mw_compile.cpp"]
 HOST_SRCS = ["mw_host_emu.cpp", "mw_validate.cpp"]
 HEADERS = ["mw_isa.h", "mw_prog.h", "mw_alu.h", "mw_interp.h", "mw_leaf.h", "mw_keccak.h", "mw_asm_interp.inc",
            "mw_asm_abi.h", "mw_handles.h"]
@@ -39,7 +39,8 @@ def _stale(target: Path, srcs) -> bool:
     if not target.exists():
         return True
     t = target.stat().st_mtime
-    deps = [CSRC / s for s in srcs] + [CSRC / h for h in HEADERS] + [ROOT / "include" / "mythril_witness.h"]
+    deps = [CSRC / s for s in srcs] + [CSRC / h for h in HEADERS] + [ROOT / "include" / h for h in
+                                                                     ("mythril_witness.h", "mythril_compile.h")]
     return any(d.stat().st_mtime > t for d in deps if d.exists())
 
 

@@ -24,7 +24,7 @@ from __future__ import annotations
 import math
 import zlib
 from dataclasses import dataclass, field
-from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -121,6 +121,14 @@ class Program:
     n_conjuncts: int
     stats: Dict[str, int] = field(default_factory=dict)
     ssa: List[MInsn] = field(default_factory=list)   # machine IR before slot allocation (jit.py)
+    # natively compiled programs (ccompile.py) carry no machine IR; this builds it on first use
+    ssa_build: Optional[Callable[[], List[MInsn]]] = None
+
+    def machine_ir(self) -> List[MInsn]:
+        """The SSA machine IR the specialised kernels are generated from (jit.py)."""
+        if not self.ssa and self.ssa_build is not None:
+            self.ssa = self.ssa_build()
+        return self.ssa
 
     def executed_ops(self, evals: int, st: Optional[dict] = None) -> float:
         """Algorithmic u32 ops a search of `evals` candidates executed: ops_per_eval

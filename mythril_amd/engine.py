@@ -1,7 +1,8 @@
 """Witness engine: constraint sets -> batched GPU search -> concrete witnesses.
 
 ``prepare`` lowers one constraint set (Ackermannisation, width legalisation,
-candidate pools) and compiles its search program (verdicts only).
+candidate pools) and compiles its search program (verdicts only; the native
+compiler, ccompile.py).
 ``WitnessEngine.search`` launches many programs in one ``mg_search`` call (one
 grid row per program, SURVEY.md §8a row A9 batching) and turns each lowest
 satisfying index back into a :class:`Witness`: the search program re-evaluates
@@ -19,7 +20,8 @@ from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 from . import isa
-from .compiler import LeafSpec, Program, Unsupported, compile_program
+from .ccompile import compile_query
+from .compiler import LeafSpec, Program, Unsupported
 from .ir import BOOL, Ctx, Node
 from .lower import Lowered, lower_constraints, needs_lowering
 from .pools import harvest
@@ -91,7 +93,7 @@ def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True,
             leaves.append(n)
     specs = harvest(low.conjuncts, leaves) if use_pools else {}
     t2 = time.perf_counter()
-    prog = compile_program(low.conjuncts, leaf_specs=specs)
+    prog = compile_query(low.conjuncts, leaf_specs=specs)
     if timings is not None:
         timings.update(lower=t1 - t0, pools=t2 - t1, compile=time.perf_counter() - t2)
     # identical leaf layout (pool fields already assigned) for the witness program
@@ -113,7 +115,7 @@ def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True,
     traced = list(prog.leaf_nodes) + arg_terms
     # the search program's leaves lead the trace list in its order, so the witness
     # program numbers them identically: same candidate generator, same values
-    q = Query(ctx, conj, low, prog, lambda: compile_program([], leaf_specs=fixed, trace=traced), arg_terms)
+    q = Query(ctx, conj, low, prog, lambda: compile_query([], leaf_specs=fixed, trace=traced), arg_terms)
     q.arg_chunks = arg_chunks
     return q
 

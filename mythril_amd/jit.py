@@ -5,7 +5,7 @@ bytecode instruction it pays a scalar dispatch and indexed register-file
 moves (``s_set_gpr_idx``) around a handful of VALU ops.  On the C5 workload
 that overhead is about two thirds of the kernel time (performance
 log).  For long searches the program is instead emitted as HIP source: one
-straight-line function over the compiler's SSA machine IR (``Program.ssa``),
+straight-line function over the compiler's SSA machine IR (``Program.machine_ir()``),
 every value a register array, every constant a literal, every leaf
 descriptor folded into the generator call.  hipcc compiles it for gfx950 into
 a code object, and ``mg_prog_attach_kernel`` binds it to the loaded program;
@@ -148,7 +148,7 @@ class _Gen:
                  insns: Optional[List[MInsn]] = None, interleave: int = 1):
         self.fence_first = fence_first  # diagnostics (tools/opbench.py): no folding across nodes
         self.p = p
-        self.insns = interleave_conjuncts(p.ssa if insns is None else insns, interleave)
+        self.insns = interleave_conjuncts(p.machine_ir() if insns is None else insns, interleave)
         # the lds_leaves most-used wide leaves live in LDS (mw_jit.h lds_put8/lds_get8)
         uses: Dict[int, int] = {}
         defs: Dict[int, int] = {}
@@ -340,11 +340,11 @@ def insn_weight(ins: MInsn) -> int:
 
 def split_ssa(p: Program, part_weight: int = PART_WEIGHT) -> List[List[MInsn]]:
     """Instruction lists of the program's parts (one list when it is small)."""
-    ssa = [i for i in p.ssa if i.op != "END"]
+    ssa = [i for i in p.machine_ir() if i.op != "END"]
     n = len(ssa)
     total = sum(insn_weight(i) for i in ssa)
     if total <= part_weight * 1.25 or n < 2:
-        return [p.ssa]
+        return [p.machine_ir()]
     defs: Dict[int, int] = {}
     last: Dict[int, int] = {}
     for i, ins in enumerate(ssa):
@@ -370,7 +370,7 @@ def split_ssa(p: Program, part_weight: int = PART_WEIGHT) -> List[List[MInsn]]:
             cuts.append(b)
             acc = 0
     if not cuts:
-        return [p.ssa]
+        return [p.machine_ir()]
     bounds = [0] + cuts + [n]
     parts = []
     for a, b in zip(bounds, bounds[1:]):
@@ -411,7 +411,7 @@ def generate(progs: Sequence[Program], names: Sequence[str], variants: str = "xe
         if name in done:   # two queries that compile to the same program share one kernel
             continue
         done.add(name)
-        if not p.ssa:
+        if not p.machine_ir():
             raise ValueError("program has no SSA machine IR (compiled by an older compiler?)")
         part = parts[k] if parts else None
         out.append(f"// program {name}: {p.n_insn} bytecode insns, {p.ops_per_eval} u32 ops/eval"

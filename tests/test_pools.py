@@ -125,7 +125,7 @@ def test_congruence_conjuncts_fuse_to_one_check():
         ops.count(isa.OPCODES["CHECK_IMPEQW"])
     assert fused >= 2000
     assert ops.count(isa.OPCODES["CHECK_IMPEQ"]) >= 2000   # (i = j) => (v = w): one dispatch
-    assert all(not i.op.startswith("CHECK_IMP") for i in q.program.ssa)
+    assert all(not i.op.startswith("CHECK_IMP") for i in q.program.machine_ir())
 
 
 def test_check_imp_verdicts_all_input_combinations():

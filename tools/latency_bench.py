@@ -11,8 +11,10 @@ bytecode) it reports, in ms:
   compile    bytecode + register allocation (compiler.py)
   search     one mg_search launch, early exit + stop-after-hit, the engine's
              default per-query budget (device; wall time of the call)
-  materialise  trace program compile + single-candidate re-evaluation (only
-             on a witness)
+  materialise  the witness values of the found index with the search program
+             still loaded (only on a witness): one mg_witness_leaves launch when
+             every array index / function argument is constant, else the
+             trace program compile + single-candidate re-evaluation
 and the medians per corpus.  Without a GPU (--no-device) only the host
 phases are timed.
 
@@ -54,14 +56,19 @@ def main():
             if eng is not None:
                 t1 = time.perf_counter()
                 dp = eng.dev.load(q.program)
-                (idx,), st = eng.dev.search([dp], eng.seed, 0, eng.launch_count([q]), 3)
-                dp.free()
-                row["search"] = (time.perf_counter() - t1) * 1e3
-                row["kernel"] = st["kernel_ms"]
-                if idx is not None:
-                    t2 = time.perf_counter()
-                    eng.materialize(q, idx)
-                    row["materialise"] = (time.perf_counter() - t2) * 1e3
+                try:
+                    (idx,), st = eng.dev.search([dp], eng.seed, 0, eng.launch_count([q]), 3)
+                    row["search"] = (time.perf_counter() - t1) * 1e3
+                    row["kernel"] = st["kernel_ms"]
+                    if idx is not None:
+                        # as WitnessEngine.search does: the search program is still
+                        # loaded (mg_witness_leaves when every cell index is constant)
+                        t2 = time.perf_counter()
+                        eng.materialize(q, idx, dp)
+                        row["materialise"] = (time.perf_counter() - t2) * 1e3
+                        row["leaf_path"] = all(t.op == "const" for t in q.arg_terms)
+                finally:
+                    dp.free()
                 row["witness"] = idx is not None
             rows.append(row)
             print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in row.items()}), flush=True)
