@@ -93,12 +93,13 @@ def why_unavailable() -> Optional[str]:
     return _why
 
 
-def serialize(conj: Sequence[Node], trace: Sequence[Node]):
+def serialize(conj: Sequence[Node], trace: Sequence[Node], nodes: Optional[List[Node]] = None):
     """(records, number of nodes, constant bytes, roots, nodes): the DAG below
     the (flattened) conjuncts and traced terms in the mythril_compile.h
     format, operand-first (``topo`` order, the node set compile_program
-    counts ops over)."""
-    nodes = topo(list(conj) + list(trace))
+    counts ops over; `nodes` when the caller has that walk already)."""
+    if nodes is None:
+        nodes = topo(list(conj) + list(trace))
     idx: Dict[int, int] = {}
     recs: List[int] = []
     kb = bytearray()
@@ -134,16 +135,22 @@ def _addr(buf) -> int:
 
 
 def compile_native(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, LeafSpec]] = None,
-                   trace: Sequence[Node] = (), pools: Optional[Dict[str, List[Optional[int]]]] = None
-                   ) -> Program:
-    """compile_program(conjuncts, leaf_specs, trace, pools), natively."""
+                   trace: Sequence[Node] = (), pools: Optional[Dict[str, List[Optional[int]]]] = None,
+                   reach=None) -> Program:
+    """compile_program(conjuncts, leaf_specs, trace, pools), natively.
+    reach: (flattened conjuncts, their topo) when the caller has them and
+    nothing is traced (prepare: Lowered.flat, Lowered.nodes)."""
     fns = _bind()
     if fns is None:
         raise RuntimeError(f"native compiler unavailable: {_why}")
     lib, c_compile, c_take, c_free = fns
-    conj = _flatten(conjuncts)
     trace = list(trace)
-    recs, nn, kb, nk, roots, nodes = serialize(conj, trace)
+    if reach is not None and not trace:
+        conj, nodes = reach
+        recs, nn, kb, nk, roots, nodes = serialize(conj, trace, nodes)
+    else:
+        conj = _flatten(conjuncts)
+        recs, nn, kb, nk, roots, nodes = serialize(conj, trace)
     kbuf = ctypes.create_string_buffer(kb, len(kb)) if kb else None
     h = _P()
     info = MwCompileInfo()
@@ -171,7 +178,7 @@ def compile_native(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
              "div_nominal_ops": int(info.div_nominal_ops), "wide_divisions": int(info.n_div)}
     return Program(code=code, consts=consts if consts.size else np.zeros(1, dtype=np.uint32),
                    leaves=np.asarray(leaf_words, dtype=np.uint32),
-                   pool=np.asarray(pool_words if pool_words else [0], dtype=np.uint32),
+                   pool=pool_words if pool_words.size else np.zeros(1, dtype=np.uint32),
                    n_spill=int(info.n_spill), n_trace_rows=int(info.n_trace_rows), n_input_rows=in_row,
                    ops_per_eval=int(info.ops_per_eval), leaf_specs=specs, leaf_nodes=leaf_nodes,
                    trace_map=trace_map, n_insn=n_insn, n_conjuncts=len(conj), stats=stats,
@@ -182,9 +189,9 @@ USE_PYTHON = os.environ.get("MYTHRIL_AMD_PY_COMPILE", "0") == "1"
 
 
 def compile_query(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, LeafSpec]] = None,
-                  trace: Sequence[Node] = (), pools=None) -> Program:
+                  trace: Sequence[Node] = (), pools=None, reach=None) -> Program:
     """The product's compiler: native when the library is built (always, on
     a GPU box: the device path needs the same library), else compiler.py."""
     if not USE_PYTHON and available():
-        return compile_native(conjuncts, leaf_specs, trace, pools)
+        return compile_native(conjuncts, leaf_specs, trace, pools, reach)
     return compile_program(conjuncts, leaf_specs=leaf_specs, trace=trace, pools=pools)

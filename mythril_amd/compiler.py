@@ -848,6 +848,9 @@ LDS_SPILL_WORDS = 80   # mw_kernels.hip kLdsSpillWords
 
 
 # --------------------------------------------------------------------------- encode
+_POOL_RANDOM_W = (1).to_bytes(4, "little") + bytes(32)   # a RANDOM entry of a wide leaf
+
+
 def _limbs(v: int) -> List[int]:
     return [(v >> (32 * k)) & 0xFFFFFFFF for k in range(8)]
 
@@ -864,7 +867,7 @@ def layout_leaves(leaf_nodes: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
     whose leaf set grows (incremental.py) re-lays its table with this."""
     specs: List[LeafSpec] = []
     leaf_words: List[int] = []
-    pool_words: List[int] = []
+    pool_words = bytearray()   # u32 words, little-endian
     in_row = 0
     user = dict(leaf_specs or {})
     resolved: List[LeafSpec] = []
@@ -925,22 +928,22 @@ def layout_leaves(leaf_nodes: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
                 kind = 1
                 if spec.bits == 0 and spec.shift == 0:
                     spec.bits = nb
-            pshift, pbits, poff, pstride = spec.shift, spec.bits, len(pool_words), spec.stride
+            pshift, pbits, poff, pstride = spec.shift, spec.bits, len(pool_words) // 4, spec.stride
             bit = max(bit, spec.shift + (spec.bits - 1) * max(spec.stride, 1) + 1 if spec.bits else 0)
-            for e in spec.pool:
-                if w < 32:   # one word per entry (mw_isa.h MW_POOL_NARROW_RANDOM)
-                    pool_words.append(isa.POOL_NARROW_RANDOM if e is None else e & ((1 << w) - 1))
-                elif e is None:
-                    pool_words.extend([1] + [0] * 8)
-                else:
-                    pool_words.extend([0] + _limbs(e & ((1 << w) - 1)))
+            m = (1 << w) - 1
+            if w < 32:   # one word per entry (mw_isa.h MW_POOL_NARROW_RANDOM)
+                for e in spec.pool:
+                    pool_words += (isa.POOL_NARROW_RANDOM if e is None else e & m).to_bytes(4, "little")
+            else:        # flags word + 8 limbs, little-endian
+                for e in spec.pool:
+                    pool_words += _POOL_RANDOM_W if e is None else b"\0\0\0\0" + (e & m).to_bytes(32, "little")
         leaf_words.extend([w, kind, spec.key_salt(), pshift, pbits, poff, in_row, pstride])
         in_row += (w + 31) // 32
         specs.append(spec)
     if bit > 63:
         raise Unsupported("pool digit fields exceed the 64-bit candidate index")
 
-    return specs, leaf_words, pool_words, in_row
+    return specs, leaf_words, np.frombuffer(bytes(pool_words), dtype="<u4").astype(np.uint32), in_row
 
 
 def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, LeafSpec]] = None,
@@ -1027,7 +1030,8 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
              "fills": sum(1 for i in insns if i.op.startswith("FILL")),
              "div_nominal_ops": div_nominal_ops, "wide_divisions": n_div}
     return Program(code=np.asarray(code, dtype=np.uint32), consts=arr(consts),
-                   leaves=np.asarray(leaf_words, dtype=np.uint32), pool=arr(pool_words),
+                   leaves=np.asarray(leaf_words, dtype=np.uint32),
+                   pool=pool_words if pool_words.size else arr([]),
                    n_spill=n_spill, n_trace_rows=rows, n_input_rows=in_row, ops_per_eval=ops,
                    leaf_specs=specs, leaf_nodes=list(lw.leaf_nodes), trace_map=trace_map,
                    n_insn=len(code) // 4, n_conjuncts=checks, stats=stats, ssa=list(lw.insns))

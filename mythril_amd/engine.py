@@ -86,19 +86,15 @@ def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True,
     t1 = time.perf_counter()
     leaves = []
     seen = set()
-    from .ir import topo
-    for n in topo(low.conjuncts):
+    for n in low.nodes:   # topo of the flattened conjuncts, computed once by lower_constraints
         if n.op == "var" and n.name not in seen:
             seen.add(n.name)
             leaves.append(n)
-    specs = harvest(low.conjuncts, leaves) if use_pools else {}
+    specs = harvest(low.conjuncts, leaves, nodes=low.nodes) if use_pools else {}
     t2 = time.perf_counter()
-    prog = compile_query(low.conjuncts, leaf_specs=specs)
+    prog = compile_query(low.conjuncts, leaf_specs=specs, reach=(low.flat, low.nodes))
     if timings is not None:
         timings.update(lower=t1 - t0, pools=t2 - t1, compile=time.perf_counter() - t2)
-    # identical leaf layout (pool fields already assigned) for the witness program
-    fixed = {s.name: dataclasses.replace(s, pool=None if s.pool is None else list(s.pool))
-             for s in prog.leaf_specs}
     # trace every array index / function argument (wider than 256 bits: as 256-bit chunks)
     from .lower import _Rewriter
     chunker = _Rewriter(ctx)
@@ -115,9 +111,18 @@ def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True,
     traced = list(prog.leaf_nodes) + arg_terms
     # the search program's leaves lead the trace list in its order, so the witness
     # program numbers them identically: same candidate generator, same values
-    q = Query(ctx, conj, low, prog, lambda: compile_query([], leaf_specs=fixed, trace=traced), arg_terms)
+    q = Query(ctx, conj, low, prog, lambda: _witness_program(prog, traced), arg_terms)
     q.arg_chunks = arg_chunks
     return q
+
+
+def _witness_program(prog: Program, traced: List[Node]) -> Program:
+    """The witness program of `prog`: its leaf layout (pool fields already
+    assigned; copies, layout_leaves updates the specs it is given), no
+    conjuncts, the leaves and cell indices traced."""
+    fixed = {s.name: dataclasses.replace(s, pool=None if s.pool is None else list(s.pool))
+             for s in prog.leaf_specs}
+    return compile_query([], leaf_specs=fixed, trace=traced)
 
 
 def _combine_chunks(values: Dict[str, int], name: str, width: int) -> int:

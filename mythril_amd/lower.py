@@ -41,9 +41,10 @@ for (:class:`AckLeaf`) so a witness can be turned back into a model.
 from __future__ import annotations
 
 from dataclasses import dataclass, field
+from operator import attrgetter
 from typing import Dict, List, Optional, Tuple
 
-from .compiler import Unsupported
+from .compiler import Unsupported, _flatten
 from .ir import BOOL, Ctx, Node, topo
 
 MAXW = 256
@@ -64,13 +65,14 @@ class Lowered:
     conjuncts: List[Node]
     ack: Dict[str, AckLeaf] = field(default_factory=dict)
     congruence: int = 0
+    flat: List[Node] = field(default_factory=list)    # conjuncts with top-level `and` flattened, `true` dropped
+    nodes: List[Node] = field(default_factory=list)   # topo(flat): every node the search program evaluates
 
 
 class _Rewriter:
     def __init__(self, ctx: Ctx):
         self.ctx = ctx
         self.memo: Dict[int, Node] = {}
-        self._visited: set = set()   # node ids rw() has walked (topo skips them)
         self.ack: Dict[str, AckLeaf] = {}
         self.by_base: Dict[str, List[AckLeaf]] = {}
         self.leaf_of_key: Dict[tuple, Node] = {}
@@ -300,6 +302,9 @@ class _Rewriter:
 
     # -- leaves for array reads / UF applications ---------------------------------
     def _key_name(self, base: str, args: Tuple[Node, ...]) -> Tuple[tuple, str]:
+        if len(args) == 1 and args[0].op == "const":   # a cell at a concrete index (calldata bytes)
+            a = args[0]
+            return (base, (a.width, a.val)), f"{base}@{a.val:x}"
         if all(a.op == "const" for a in args):
             key = (base,) + tuple((a.width, a.val) for a in args)
             nm = f"{base}@" + ",".join(f"{a.val:x}" for a in args)
@@ -364,11 +369,32 @@ class _Rewriter:
 
     # -- main rewrite --------------------------------------------------------------
     def rw(self, root: Node) -> Node:
-        for n in topo([root], self._visited):
-            if n.id in self.memo:
+        """The rewrite of root: operands first, each node once per rewriter
+        (the walk of ir.topo with the memo as its visited set, so _rw1 runs in
+        topo order: leaf names and congruence pairs do not depend on it)."""
+        memo = self.memo
+        got = memo.get(root.id)
+        if got is not None:
+            return got
+        rw1 = self._rw1
+        stack = [root]
+        push, pop = stack.append, stack.pop
+        while stack:
+            n = stack[-1]
+            if n.id in memo:
+                pop()
                 continue
-            self.memo[n.id] = self._rw1(n)
-        return self.memo[root.id]
+            pending = False
+            for a in reversed(n.args):
+                if a.id not in memo:
+                    push(a)
+                    pending = True
+            if not pending:
+                pop()
+                op = n.op
+                # constants, arrays and leaves up to 256 bits rewrite to themselves (_rw1)
+                memo[n.id] = n if (op == "const" or op == "array" or (op == "var" and n.width <= MAXW)) else rw1(n)
+        return memo[root.id]
 
     def _rw1(self, n: Node) -> Node:
         c = self.ctx
@@ -378,8 +404,14 @@ class _Rewriter:
             return self.wide_var(n.name, n.width) if n.width > MAXW else n
         if n.op == "array":
             return n  # only reachable through select/store, handled there
-        args = [self.memo[a.id] for a in n.args]
+        memo = self.memo
+        args = [memo[a.id] for a in n.args]
         op = n.op
+        # unchanged operands and nothing to rewrite at this node: hash-consing
+        # would return n itself (most nodes of a LASER query)
+        if (op not in _REWRITE and n.width <= MAXW and n.dom is None and tuple(args) == n.args
+                and (op not in _WIDE_ARG_OPS or max(map(_width, args)) <= MAXW)):
+            return n
         if op == "select":
             return self.select(args[0], args[1])
         if op in ("store", "const_array"):
@@ -410,7 +442,8 @@ class _Rewriter:
             return leaf
         if op in ("=", "distinct") and args and args[0].is_array:
             raise Unsupported("array equality")
-        wide_args = any(a.width > MAXW and not a.is_array for a in args)
+        wide_args = bool(args) and max(map(_width, args)) > MAXW and any(
+            a.width > MAXW and not a.is_array for a in args)
         if op == "=" and wide_args:
             eqs = [self.eq(args[0], b) for b in args[1:]]
             return c.app("and", *eqs) if len(eqs) > 1 else eqs[0]
@@ -436,7 +469,9 @@ class _Rewriter:
                       "bvsmul_noovfl", "bvsmul_noudfl"):
                 raise Unsupported(f"{op} on {max(a.width for a in args)} bits")
             return c._mk(op, n.width, tuple(args), n.params)
-        return c.app(op, *args, params=n.params) if op not in ("ite",) else c.app("ite", *args)
+        # what c.app(op, *args, params=n.params) builds: every rewrite keeps its
+        # node's width, so the result width is n's
+        return c._mk(op, n.width, tuple(args), n.params)
 
     def _pow2(self, op: str, args: List[Node], w: int) -> Optional[Node]:
         """z3 ``simplify`` rewrites (bv_rewriter) that turn arithmetic by a power
@@ -527,6 +562,12 @@ class _Rewriter:
 
 
 _POW2_OPS = frozenset({"bvudiv", "bvurem", "bvmul", "bvand", "bvshl", "bvlshr"})
+# ops _rw1 may rewrite even when their operands are unchanged
+_REWRITE = _POW2_OPS | {"select", "store", "const_array", "apply", "extract", "=", "not", "distinct", "bvcomp"}
+# narrow results that may read wide operands (every other op's result is as wide as its operands)
+_WIDE_ARG_OPS = frozenset({"bvult", "bvugt", "bvule", "bvuge", "bvslt", "bvsgt", "bvsle", "bvsge",
+                           "bvumul_noovfl", "bvsmul_noovfl", "bvsmul_noudfl", "bvaddc"})
+_width = attrgetter("width")
 
 # wide orderings: op -> (signedness, swap operands, strict)
 _ORDER = {"bvult": ("u", False, True), "bvugt": ("u", True, True), "bvule": ("u", False, False),
@@ -594,10 +635,12 @@ def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
     rw = _Rewriter(ctx)
     out = [rw.rw(cj) for cj in conjuncts]
     cong = rw.congruence()
-    for n in topo(out + cong):
+    flat = _flatten(out + cong)
+    nodes = topo(flat)
+    for n in nodes:
         if n.width > MAXW:   # every consumer chunks its wide operands; none may remain
             raise Unsupported(f"{n.width}-bit {n.op} outside the legalised vocabulary")
-    return Lowered(out + cong, rw.ack, len(cong))
+    return Lowered(out + cong, rw.ack, len(cong), flat, nodes)
 
 
 def needs_lowering(conjuncts: List[Node]) -> bool:

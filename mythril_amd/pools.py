@@ -417,8 +417,12 @@ def _const_props(consts, m: int, split_bytes: bool):
 
 
 def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
-            random_share: float = 0.25, restrict: bool = True) -> Dict[str, LeafSpec]:
-    nodes = topo(conjuncts)
+            random_share: float = 0.25, restrict: bool = True,
+            nodes: Optional[List[Node]] = None) -> Dict[str, LeafSpec]:
+    """nodes: topo(conjuncts) when the caller has it (prepare: Lowered.nodes,
+    the same walk without the top-level `and` nodes, which no rule reads)."""
+    if nodes is None:
+        nodes = topo(conjuncts)
     exact, interval, dom_align = domains(conjuncts) if restrict else ({}, {}, {})
     proposals: Dict[str, List[int]] = {}
     # orderings between two leaves (INVEST_MIN < msg.value < INVEST_MAX with
@@ -441,17 +445,27 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
     word_props: Dict[int, List[int]] = {}
     consts = []
     dm: List[Dict[str, List[int]]] = []
+    eq2: List[Node] = []      # binary equalities (alignment, leaf unions), in walk order
+    concats: List[Node] = []  # word candidates (_tie_words)
     for n in nodes:
-        if n.op == "const" and n.width != BOOL:
-            consts.append(n.val)
-        if n.op in _CMP and len(n.args) == 2:
+        op = n.op
+        if op == "const":
+            if n.width != BOOL:
+                consts.append(n.val)
+            continue
+        if op == "concat":
+            concats.append(n)
+            continue
+        if op in _CMP and len(n.args) == 2:
+            if op == "=":
+                eq2.append(n)
             a, b = n.args
             for x, k in ((a, b), (b, a)):
                 if k.op == "const" and x.op != "const":
-                    deltas = (0,) if n.op in ("=", "distinct") else (0, 1, -1)
+                    deltas = (0,) if op in ("=", "distinct") else (0, 1, -1)
                     for d in deltas:
                         _project(x, k.val + d, proposals, words=word_props)
-                    if n.op == "=" and x.width != BOOL:
+                    if op == "=" and x.width != BOOL:
                         f: Dict[str, List[int]] = {}
                         _assign(x, k.val, 0, x.width - 1, f)
                         if any(m != (1 << w) - 1 for m, _, w in f.values()):
@@ -460,13 +474,12 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
     combos = _combine_partial(dm)
     # alignment facts: (= (bvurem x K) 0)  ->  x should be a multiple of K
     align: Dict[str, int] = {}
-    for n in nodes:
-        if n.op == "=" and len(n.args) == 2:
-            a, b = n.args
-            for x, k in ((a, b), (b, a)):
-                al = _align_of(x) if (k.op == "const" and k.val == 0) else None
-                if al is not None:
-                    align[al[0]] = al[1]
+    for n in eq2:
+        a, b = n.args
+        for x, k in ((a, b), (b, a)):
+            al = _align_of(x) if (k.op == "const" and k.val == 0) else None
+            if al is not None:
+                align[al[0]] = al[1]
     for name, K in align.items():
         props = proposals.get(name, [])
         aligned = []
@@ -483,16 +496,15 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
             x = parent[x]
         return x
 
-    for n in nodes:
-        if n.op == "=" and len(n.args) == 2:
-            # x = y, also through the masks and zero-padding of an address
-            # compare (concat(0, extract(159, 0, x)), bvand(mask, x)): a stored
-            # owner equated with msg.sender gets the actors
-            xa, xb = _bare_leaf(n.args[0]), _bare_leaf(n.args[1])
-            if xa is not None and xb is not None and xa.width == xb.width and xa is not xb:
-                ra, rb = find(xa.name), find(xb.name)
-                if ra != rb:
-                    parent[ra] = rb
+    for n in eq2:
+        # x = y, also through the masks and zero-padding of an address
+        # compare (concat(0, extract(159, 0, x)), bvand(mask, x)): a stored
+        # owner equated with msg.sender gets the actors
+        xa, xb = _bare_leaf(n.args[0]), _bare_leaf(n.args[1])
+        if xa is not None and xb is not None and xa.width == xb.width and xa is not xb:
+            ra, rb = find(xa.name), find(xb.name)
+            if ra != rb:
+                parent[ra] = rb
     groups: Dict[str, List[int]] = {}
     for name, props in list(proposals.items()):
         groups.setdefault(find(name), []).extend(props)
@@ -503,6 +515,7 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
     specs: Dict[str, LeafSpec] = {}
     uniq_consts = list(dict.fromkeys(consts))[:256]
     tails: Dict[int, List[int]] = {}   # width -> the constants' proposals, deduplicated
+    nfixed = max(1, int(pool_size * (1 - random_share)))
     for leaf in leaves:
         if leaf.op != "var":
             continue
@@ -519,14 +532,15 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
         cand = itertools.chain(proposals.get(leaf.name, ()), actors, (0, 1, 2, m, 1 << (w - 1), m - 1), tail)
         pool: List[Optional[int]] = []
         seen = set()
-        nfixed = max(1, int(pool_size * (1 - random_share)))
+        add, put, k = seen.add, pool.append, 0
         for v in itertools.chain((c[leaf.name] for c in combos if leaf.name in c), cand) if combos else cand:
             v &= m
             if v not in seen:
-                seen.add(v)
-                pool.append(v)
-            if len(pool) >= nfixed:
-                break
+                add(v)
+                put(v)
+                k += 1
+                if k >= nfixed:
+                    break
         if w == 1:
             pool = [0, 1]
         else:
@@ -536,7 +550,7 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
                 pool = _restrict(pool, leaf.name, w, exact, interval, dom_align, pool_size,
                                  proposals.get(leaf.name, ()))
         specs[leaf.name] = LeafSpec(leaf.name, w, pool=pool)
-    _tie_words(nodes, specs, word_props, set(exact), uniq_consts, pool_size, random_share, combos)
+    _tie_words(concats, specs, word_props, set(exact), uniq_consts, pool_size, random_share, combos)
     return specs
 
 
