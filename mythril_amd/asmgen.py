@@ -3,11 +3,11 @@
 * the threaded-dispatch interpreter core (``render_interp`` ->
   csrc/mw_asm_interp.inc, written by tools/gen_asm_interp.py): one inline-asm
   block that runs any eligible program.  Every handler ends in its own copy
-  of the dispatch, which loads the next instruction (prefetched one ahead
-  with s_load_dwordx4), indexes a table of s_branch entries and jumps with
-  s_setpc_b64.  The register files live in fixed VGPRs and are indexed with
-  s_set_gpr_idx_on; operands come predecoded (mw_validate.cpp
-  mw_asm_predecode);
+  of the dispatch, which takes the next instruction (prefetched one ahead
+  with s_load_dwordx4) and jumps with s_setpc_b64 to the handler offset
+  predecoded into its word 0.  The register files live in fixed VGPRs and are
+  indexed with s_set_gpr_idx_on; operands come predecoded (mw_validate.cpp
+  mw_asm_predecode), narrow constants as registers of their own (NK0);
 * assembled kernels (``render_template`` + ``static_body``, used by
   mythril_amd/asmjit.py): the same prologue, chunk loop, result protocol and
   leaf subroutines, with the program itself emitted as straight-line code -
@@ -29,6 +29,7 @@ Registers (per lane; all clobbered by the block):
   v160/v161 candidate index lo/hi  v162 alive (0/1)  v163 LDS lane byte offset
   v164 global-spill lane byte offset  v165 thread id  v168..v175 XR (result)
   v176..v183 XC (third operand / Philox output)  v184..v191 temporaries
+  v240..v255  the program's narrow constants (interpreter)
   s16..s95    chunk loop and interpreter state (see the constants below)
 """
 import re
@@ -95,6 +96,12 @@ TID, LO_SREG = 165, 0
 
 NTAB = 128
 CHAIN_BIT = 15     # predecoded word 0: W_CDINS's FLAG_CHAIN (mw_asm_predecode)
+# narrow constants: v240..v255, filled once per block from the table after the
+# predecoded code; a constant N operand is predecoded as index NK0 - N0 + k
+# (mw_isa.h MW_ASM_NK / MW_ASM_NK_INDEX)
+NK0 = 240
+NK_INDEX = NK0 - N0
+assert NK_INDEX == 176 and NK0 + isa.ASM_NK == 256
 INTROSPECT_FLAG = 7   # AsmArgs.flags bit: report the handler offsets and exit
 
 
@@ -159,18 +166,12 @@ class Gen:
         self(f"s_bitcmp1_b32 {s(wd)}, {31 if half == 'hi' else 15}", f"s_cbranch_scc1 {label}")
 
     def fetch_n(self, f, dst):
-        """N/K operand bound to f -> VGPR dst"""
+        """N operand bound to f -> VGPR dst: one indexed move, registers and
+        constants alike (a constant is predecoded as its VGPR above the N
+        file, NK0)"""
         which = self.bound[f]
-        lk, lr = self.L("kn"), self.L("rn")
-        self._is_const(which, lk)
         self._index(which, s(SIDX))
         self(f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(SRC0)", f"v_mov_b32_e32 {v(dst)}, {v(N0)}", "s_set_gpr_idx_off")
-        self.label(lr)
-        wd, half = self.WORD[which]
-        off = f"s_lshr_b32 {s(SX)}, {s(wd)}, 16" if half == "hi" else f"s_and_b32 {s(SX)}, {s(wd)}, 0x7fff"
-        self.tail += [f"{lk}:", off, f"s_and_b32 {s(SX)}, {s(SX)}, 0x7fff", f"s_lshl_b32 {s(SX)}, {s(SX)}, 2",
-                      f"s_load_dword {s(SX)}, {sr(CPOOL, 2)}, {s(SX)}", "s_waitcnt lgkmcnt(0)",
-                      f"v_mov_b32_e32 {v(dst)}, {s(SX)}", f"s_branch {lr}"]
 
     def fetch_w(self, f, dst):
         """W/K operand bound to f -> VGPRs dst..dst+7"""
@@ -198,6 +199,11 @@ class Gen:
         the 64-bit field mask (dst must start an aligned SGPR pair)"""
         assert dst % 2 == 0
         self(f"s_bfm_b64 {sr(dst, 2)}, {s(w)}, 0")
+
+    def insn_mask(self, dst):
+        """the SGPR holding this instruction's result mask: word 3, where
+        mw_asm_predecode puts it for N_ADD / N_SUB / N_MUL / N_NOT (no code)"""
+        return s(CUR + 3)
 
     def write_n(self, src):
         """N result in VGPR src -> the N slot of the predecoded dst field [5:0]"""
@@ -330,8 +336,7 @@ def build_handlers():
             g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
             g(expr.format(d=v(XR), a=v(T), b=v(T + 1)))
             if masked:
-                g.width(S[2]), g.nmask(S[2], S[4])
-                g(f"v_and_b32_e32 {v(XR)}, {s(S[4])}, {v(XR)}")
+                g(f"v_and_b32_e32 {v(XR)}, {g.insn_mask(S[4])}, {v(XR)}")
             g.write_n(XR)
         handlers[name] = h
 
@@ -340,8 +345,7 @@ def build_handlers():
         g.field("a", S[0]), g.field("b", S[1])
         g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
         g(f"v_mul_lo_u32 {v(XR)}, {v(T)}, {v(T + 1)}")
-        g.width(S[2]), g.nmask(S[2], S[4])
-        g(f"v_and_b32_e32 {v(XR)}, {s(S[4])}, {v(XR)}")
+        g(f"v_and_b32_e32 {v(XR)}, {g.insn_mask(S[4])}, {v(XR)}")
         g.write_n(XR)
 
     for name, cmp in (("N_SLTN", "v_cmp_lt_u32_e32"), ("N_SLEN", "v_cmp_le_u32_e32")):
@@ -372,8 +376,7 @@ def build_handlers():
     @handler("N_NOT")
     def _(g):
         g.field("a", S[0]), g.fetch_n(S[0], T)
-        g.width(S[2]), g.nmask(S[2], S[4])
-        g(f"v_xor_b32_e32 {v(XR)}, {s(S[4])}, {v(T)}")      # ~a & m == a ^ m (a canonical)
+        g(f"v_xor_b32_e32 {v(XR)}, {g.insn_mask(S[4])}, {v(T)}")      # ~a & m == a ^ m (a canonical)
         g.write_n(XR)
 
     for name, cmp in (("N_EQN", "v_cmp_eq_u32_e32"), ("N_ULTN", "v_cmp_lt_u32_e32"), ("N_ULEN", "v_cmp_le_u32_e32")):
@@ -941,6 +944,12 @@ def gen(mode="interp"):
               f"global_store_dword {v(T + 1)}, {v(T)}, {sr(VERD, 2)}")
         g(f"s_mov_b64 exec, {sr(EXECSV, 2)}", "s_branch Lexit_%=")
         g.label("Lnointro_%=")
+        # the program's narrow constants (mw_asm_predecode: after the predecoded
+        # code and the 8 words the dispatch prefetches past END) -> v240..v255
+        g(f"s_lshl_b32 {s(74)}, {s(74)}, 4", f"s_add_u32 {s(74)}, {s(74)}, 32",
+          f"s_load_dwordx16 {sr(DESC, 16)}, {sr(CODE0, 2)}, {s(74)}", "s_waitcnt lgkmcnt(0)")
+        for k in range(isa.ASM_NK):
+            g(f"v_mov_b32_e32 {v(NK0 + k)}, {s(DESC + k)}")
     else:
         for reg, lab in ((LEAFADDR, "Lleaf_%="), (STOPADDR, "Lstop_%="), (ENDADDR, "Lh_END_%="),
                          (PHILOXADDR, "Lphilox_%=")):
@@ -1165,7 +1174,8 @@ def philox_sub(g):
     g(f"s_setpc_b64 {sr(PRET, 2)}")
 
 
-CLOBBERS = (", ".join(f'"v{i}"' for i in range(192)) + ", " + ", ".join(f'"s{i}"' for i in range(16, 96))
+CLOBBERS = (", ".join(f'"v{i}"' for i in list(range(192)) + list(range(NK0, 256))) + ", "
+            + ", ".join(f'"s{i}"' for i in range(16, 96))
             + ', "vcc", "scc", "m0", "memory"')
 
 
@@ -1279,6 +1289,13 @@ class StaticGen(Gen):
             self.sval[dst] = m
         else:
             super().nmask(w, dst)
+
+    def insn_mask(self, dst):
+        w = self.cur["w"]
+        m = 0xFFFFFFFF if w >= 32 else (1 << w) - 1
+        self(f"s_mov_b32 {s(dst)}, {_lit(m)}")
+        self.sval[dst] = m
+        return s(dst)
 
     def canon(self, base, w):
         if w not in self.sval:

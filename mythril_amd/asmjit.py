@@ -104,7 +104,7 @@ def available() -> bool:
 
 
 def eligible(p: Program) -> bool:
-    return isa.asm_eligible(p.code, p.leaves)
+    return isa.asm_eligible(p.code, p.leaves, p.consts)
 
 
 def kernel_name(p: Program) -> str:

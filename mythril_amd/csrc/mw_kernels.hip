@@ -29,8 +29,8 @@
 
 extern "C" int mw_fail(int code, const char* msg);
 extern "C" int mg_validate_desc(const mg_prog_desc* d);
-extern "C" void mw_asm_predecode(const uint32_t* code, size_t nwords, const uint32_t* consts, size_t nconst,
-                                 const uint32_t* hoff, uint32_t* out);
+extern "C" int mw_asm_predecode(const uint32_t* code, size_t nwords, const uint32_t* consts, size_t nconst,
+                                const uint32_t* hoff, uint32_t* out, uint32_t* nk);
 
 using namespace mw;
 
@@ -730,8 +730,10 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   // operand fetch reads cpool[slot] (slot < 64) before selecting the register
   const size_t nc = d->ncode_words, nk = (d->nconst_words + 8 > MW_KPAD ? d->nconst_words + 8 : MW_KPAD), nl = d->nleaves * MW_LEAF_WORDS + 8,
                np = d->npool_words + 8;
-  const bool asm_ok = asm_offsets_ready() && asm_eligible(d);
-  const size_t na = asm_ok ? nc + 8 : 0;   // + the block after END the dispatch prefetches
+  bool asm_ok = asm_offsets_ready() && asm_eligible(d);
+  // predecoded copy + the block after END the dispatch prefetches + the narrow
+  // constants the kernel loads into VGPRs (MW_ASM_NK words)
+  const size_t na = asm_ok ? nc + 8 + MW_ASM_NK : 0;
   const size_t total = nc + nk + nl + np + na;
   auto p = std::make_shared<Prog>();
   p->ctx = cref;
@@ -747,7 +749,11 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   if (d->nconst_words) std::memcpy(hbuf.data() + nc, d->consts, d->nconst_words * 4);
   if (d->nleaves) std::memcpy(hbuf.data() + nc + nk, d->leaves, d->nleaves * MW_LEAF_WORDS * 4);
   if (d->npool_words) std::memcpy(hbuf.data() + nc + nk + nl, d->pool, d->npool_words * 4);
-  if (asm_ok) mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, g_hoff, hbuf.data() + nc + nk + nl + np);
+  if (asm_ok) {
+    u32* pre = hbuf.data() + nc + nk + nl + np;
+    // more distinct narrow constants than MW_ASM_NK: the compiled interpreter runs it
+    asm_ok = mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, g_hoff, pre, pre + nc + 8) == 0;
+  }
   if (hipMemcpy(p->d_buf, hbuf.data(), total * 4, hipMemcpyHostToDevice) != hipSuccess) {
     release_prog(*p);
     return fail(MG_E_HIP, "program upload copy failed");

@@ -197,7 +197,7 @@ int mg_validate_desc(const mg_prog_desc* d) {
 // operands without decoding them): w0 and w3 unchanged; the dst field becomes
 // the written N slot (0..63) in [5:0] and the written W slot x 8 in [13:8]; a
 // W register operand becomes its slot x 8 (the VGPR offset of its limb 0 in
-// the W file), N register operands and constants stay as they are, except a
+// the W file), N register operands and W constants stay as they are, except a
 // W_CDINS byte index (always a constant) below 0x4000, which becomes
 // 0x4000 | index (the handler then compares it with one 32-bit summary of the
 // size instead of a signed 256-bit subtraction).
@@ -205,8 +205,32 @@ int mg_validate_desc(const mg_prog_desc* d) {
 // reported by the kernel itself, mw_kernels.hip asm_handler_offsets); word 0
 // becomes width [31:16] | FLAG_CHAIN [15] | handler offset [14:0], so the
 // dispatch is one jump (mythril_amd/asmgen.py Gen.next).
-void mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t nconst, const u32* hoff,
-                      u32* out) {
+// Narrow constants: every N-class constant operand becomes a register operand
+// naming one of MW_ASM_NK VGPRs above the N file (index MW_ASM_NK_INDEX + k
+// from its base), which the kernel fills once per block from nk[0..MW_ASM_NK)
+// (the distinct values, in first-use order): the operand fetch is then the
+// same indexed move for registers and constants, with no constant test and
+// no scalar load.  Returns -1 (nothing usable written) when the program has
+// more distinct narrow constants than that (it then runs on the compiled
+// interpreter; the corpora have at most 3).
+// Width masks: N_ADD / N_SUB / N_MUL / N_NOT, which have no immediate, get
+// their result mask (width < 32 ? 2^width - 1 : ~0) in word 3.
+int mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t nconst, const u32* hoff,
+                     u32* out, u32* nk) {
+  u32 nnk = 0;
+  for (u32 k = 0; k < MW_ASM_NK; ++k) nk[k] = 0;
+  auto narrow = [&](int kind, u32 f, u32* dst) -> bool {   // dst: the predecoded field
+    if (kind != 2 || !(f & MW_KBIT)) return true;
+    const u32 val = consts[f & 0x7fffu];
+    u32 k = 0;
+    while (k < nnk && nk[k] != val) ++k;
+    if (k == nnk) {
+      if (nnk == MW_ASM_NK) return false;
+      nk[nnk++] = val;
+    }
+    *dst = MW_ASM_NK_INDEX + k;
+    return true;
+  };
   for (size_t i = 0; i + 3 < nwords; i += 4) {
     const u32* I = code + i;
     u32* O = out + i;
@@ -217,18 +241,23 @@ void mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t 
     if (sh.dst == 4) d2 = MW_DST_NLO(dst) != MW_N_RESERVED ? MW_DST_NLO(dst) : 32u + MW_DST_NHI(dst);
     else if (sh.dst == 3) d2 = (MW_DST_W(dst) * 8u) << 8;
     auto opnd = [](int kind, u32 f) { return (kind == 1 && !(f & MW_KBIT)) ? f * 8u : f; };
-    O[0] = (I[0] & 0xffff0000u) | ((I[0] >> 8) & MW_FLAG_CHAIN ? 0x8000u : 0u) | (hoff[I[0] & 0x7fu] & 0x7fffu);
-    O[1] = d2 | (opnd(sh.a, a) << 16);
-    u32 c2 = opnd(sh.c, c);
-    if ((I[0] & 0xffu) == MW_W_CDINS && (c & MW_KBIT)) {
+    const u32 op = I[0] & 0xffu, w = I[0] >> 16;
+    u32 a2 = opnd(sh.a, a), b2 = opnd(sh.b, b), c2 = opnd(sh.c, c);
+    if (op == MW_W_CDINS && (c & MW_KBIT)) {
       const size_t o = c & 0x7fffu;   // validated: o + 8 <= nconst
       bool small = o + 8 <= nconst && consts[o] < 0x4000u;
       for (int k = 1; k < 8 && small; ++k) small = consts[o + k] == 0u;
       if (small) c2 = 0x4000u | consts[o];
     }
-    O[2] = opnd(sh.b, b) | (c2 << 16);
+    if (!narrow(sh.a, a, &a2) || !narrow(sh.b, b, &b2) || !narrow(sh.c, c, &c2)) return -1;
+    O[0] = (I[0] & 0xffff0000u) | ((I[0] >> 8) & MW_FLAG_CHAIN ? 0x8000u : 0u) | (hoff[op & 0x7fu] & 0x7fffu);
+    O[1] = d2 | (a2 << 16);
+    O[2] = b2 | (c2 << 16);
     O[3] = I[3];
+    if (op == MW_N_ADD || op == MW_N_SUB || op == MW_N_MUL || op == MW_N_NOT)
+      O[3] = w >= 32u ? 0xffffffffu : (1u << w) - 1u;
   }
+  return 0;
 }
 
 }  // extern "C"

@@ -49,7 +49,7 @@ def _corpus_programs():
 
 def test_mythril_corpora_are_asm_eligible():
     progs = _corpus_programs()
-    bad = [f for f, p in progs if not isa.asm_eligible(p.code, p.leaves)]
+    bad = [f for f, p in progs if not isa.asm_eligible(p.code, p.leaves, p.consts)]
     assert not bad, bad
     assert len(progs) >= 170
 
@@ -63,14 +63,16 @@ def _predecode(code, consts):
     from mythril_amd.runtime import LIB_PATH
     lib = ctypes.CDLL(LIB_PATH)
     f = lib.mw_asm_predecode
-    f.restype = None
+    f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
-                  ctypes.c_void_p]
+                  ctypes.c_void_p, ctypes.c_void_p]
     code = np.ascontiguousarray(code, dtype=np.uint32)
     consts = np.ascontiguousarray(consts, dtype=np.uint32)
     out = np.zeros_like(code)
-    f(code.ctypes.data, code.size, consts.ctypes.data, consts.size, HOFF.ctypes.data, out.ctypes.data)
-    return out.reshape(-1, 4)
+    nk = np.full(isa.ASM_NK, 0xDEAD, dtype=np.uint32)
+    rc = f(code.ctypes.data, code.size, consts.ctypes.data, consts.size, HOFF.ctypes.data, out.ctypes.data,
+           nk.ctypes.data)
+    return (out.reshape(-1, 4), nk) if rc == 0 else (None, None)
 
 
 # stand-in handler word offsets (the kernel reports the real ones at mg_init)
@@ -81,25 +83,50 @@ def test_predecode_operand_layout():
     """The asm engine's copy of the code: word 0 -> width | FLAG_CHAIN at bit 15
     | the opcode's handler word offset (one-jump dispatch), N dst -> slot in
     [5:0], W dst -> slot x 8 in [13:8], W register operands -> slot x 8,
-    constants and N operands unchanged, a W_CDINS index constant below 0x4000
-    -> 0x4000 | index."""
+    N register operands and W constants unchanged, N constants -> the index
+    of their VGPR above the N file (176 + k, the value in table slot k), a
+    W_CDINS index constant below 0x4000 -> 0x4000 | index, and N_ADD's word 3
+    -> its width mask."""
     e = isa.encode
-    consts = [0] * 16
-    consts[0], consts[8] = 0x24, 0x5000   # two 256-bit constants (limbs 1..7 zero)
-    code = (e("N_ADD", 8, isa.encode_dst("N", 37), 3, isa.KBIT | 8)
+    consts = [0] * 17
+    consts[0], consts[8], consts[16] = 0x24, 0x5000, 0x77   # two 256-bit constants, one narrow
+    code = (e("N_ADD", 8, isa.encode_dst("N", 37), 3, isa.KBIT | 16)
             + e("W_ADD", 256, isa.encode_dst("W", 5), 2, isa.KBIT | 0)
             + e("N_ULT", 256, isa.encode_dst("N", 4), 6, 1)
             + e("W_ITE", 256, isa.encode_dst("W", 1), 3, 4, 9)
             + e("W_CDINS", 256, isa.encode_dst("W", 2), 2, 1, isa.KBIT | 0, imm=7 | (8 << 16))
             + e("W_CDINS", 256, isa.encode_dst("W", 2), 2, 1, isa.KBIT | 8, imm=7)
+            + e("N_EQN", 8, isa.encode_dst("N", 5), isa.KBIT | 0, isa.KBIT | 16)
             + e("END", 0, isa.encode_dst(None)))
-    o = _predecode(code, consts)
+    o, nk = _predecode(code, consts)
     src = __import__("numpy").asarray(code, dtype="uint32").reshape(-1, 4)
     want0 = (src[:, 0] & 0xFFFF0000) | HOFF[src[:, 0] & 0x7F] | (((src[:, 0] >> 8) & isa.FLAG_CHAIN) << 15)
-    assert (o[:, 0] == want0).all() and (o[:, 3] == src[:, 3]).all()
-    assert o[0, 1] == 37 | (3 << 16) and o[0, 2] == isa.KBIT | 8
+    assert (o[:, 0] == want0).all()
+    assert o[0, 3] == 0xFF and (o[1:, 3] == src[1:, 3]).all()       # N_ADD: the 8-bit mask
+    assert o[0, 1] == 37 | (3 << 16) and o[0, 2] == 176 + 0          # narrow constant 0x77 -> NK slot 0
+    assert list(nk[:2]) == [0x77, 0x24] and not nk[2:].any()
+    assert o[6, 1] == 5 | ((176 + 1) << 16) and o[6, 2] == 176 + 0  # 0x24 (narrow use) -> slot 1, 0x77 reused
     assert o[1, 1] == (40 << 8) | (16 << 16) and o[1, 2] == isa.KBIT | 0
     assert o[2, 1] == 4 | (48 << 16) and o[2, 2] == 8
     assert o[3, 1] == (8 << 8) | (24 << 16) and o[3, 2] == 32 | (9 << 16)   # c is the N condition
     assert o[4, 2] == 8 | ((0x4000 | 0x24) << 16)
     assert o[5, 2] == 8 | ((isa.KBIT | 8) << 16)                          # 0x5000: stays a constant
+
+
+def test_predecode_narrow_constant_bound():
+    """More distinct narrow constants than the asm interpreter's VGPRs hold:
+    predecode refuses (the program runs on the compiled interpreter) and the
+    host mirror agrees."""
+    e = isa.encode
+    n = isa.ASM_NK + 1
+    consts = list(range(100, 100 + n))
+    code = []
+    for k in range(n):
+        code += e("N_ADD", 16, isa.encode_dst("N", k % 30), k % 30, isa.KBIT | k)
+    code += e("END", 0, isa.encode_dst(None))
+    o, _ = _predecode(code, consts)
+    assert o is None
+    leaves = []
+    assert not isa.asm_eligible(code, leaves, consts)
+    assert isa.asm_eligible(code[:-8 * 4] + e("END", 0, isa.encode_dst(None)), leaves, consts)
+    assert len(isa.asm_narrow_constants(code, consts)) == n

@@ -67,7 +67,7 @@ def test_random_programs_assemble():
         c, conj = _random_supported_dag(seed)
         for pools in (False, True):
             p = prepare(conj, c, use_pools=pools).program
-            if not isa.asm_eligible(p.code, p.leaves):
+            if not isa.asm_eligible(p.code, p.leaves, p.consts):
                 continue
             image, name, _ = asmjit.assemble(p, cache=False)
             assert image[:4] == b"\x7fELF" and name == asmjit.kernel_name(p)

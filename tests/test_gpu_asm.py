@@ -135,7 +135,7 @@ def test_asm_random_dags(dev, seed):
     for pools in (False, True):
         q = prepare(conj, c, use_pools=pools)
         p = q.program
-        if not isa.asm_eligible(p.code, p.leaves):
+        if not isa.asm_eligible(p.code, p.leaves, p.consts):
             pytest.skip("lowered outside the asm opcode set")
         n = 1 << 12
         va, vi = both(dev, p, DEFAULT_SEED + seed, 1 << 20, n)

@@ -69,7 +69,7 @@ def test_asmjit_random_dags(dev, seed):
     for pools in (False, True):
         q = prepare(conj, c, use_pools=pools)
         p = q.program
-        if not isa.asm_eligible(p.code, p.leaves):
+        if not isa.asm_eligible(p.code, p.leaves, p.consts):
             pytest.skip("lowered outside the asm opcode set")
         n = 1 << 12
         di, da = pair(dev, p)
