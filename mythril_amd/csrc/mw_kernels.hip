@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -372,12 +373,17 @@ struct Ctx {
   size_t nasmargs_cap = 0;
   std::mutex mu;                 // serialises the calls on this context (mw_handles.h)
   bool dead = false;             // freed by mg_free (guarded by mu)
+  // device buffers returned by freed programs and finished calls, by size
+  // class (pool_get / pool_put below; guarded by mu)
+  std::map<size_t, std::vector<void*>> pool;
+  size_t pool_cached = 0;
 };
 
 struct Prog {
   std::shared_ptr<Ctx> ctx;     // keeps the context's record alive while this program's is
   bool dead = false;            // resources released (guarded by ctx->mu)
   u32* d_buf = nullptr;
+  size_t buf_cls = 0;           // d_buf's size class in the context's pool
   ProgDev dev{};
   mg_prog_desc desc{};
   u64 ops_per_eval = 0;
@@ -492,16 +498,86 @@ using CallG = mw::Call<Ctx, Prog>;
 inline u64 hid(const void* h) { return (u64)(uintptr_t)h; }
 
 // the device resources of a program (its context's mu held)
+// Device memory of one context is reused across calls: program buffers and
+// per-call scratch come from power-of-two size classes (from 4 KiB) and go
+// back there, instead of a hipMalloc and a hipFree per call (hipFree waits for
+// the whole device; on the get_model path a query loads, searches and frees a
+// program, and a witness loads and frees another).  Up to kPoolCacheBytes stay
+// cached per context; mg_free releases them.  Every call synchronises its
+// stream before it returns a buffer, so a reused buffer has no work pending.
+constexpr size_t kPoolCacheBytes = size_t(512) << 20;
+
+size_t pool_class(size_t bytes) {
+  size_t k = 4096;
+  while (k < bytes) k <<= 1;
+  return k;
+}
+
+void pool_drain(Ctx* c) {
+  for (auto& kv : c->pool)
+    for (void* q : kv.second) hipFree(q);
+  c->pool.clear();
+  c->pool_cached = 0;
+}
+
+void* pool_get(Ctx* c, size_t bytes, size_t* cls) {
+  const size_t k = pool_class(bytes);
+  *cls = k;
+  auto it = c->pool.find(k);
+  if (it != c->pool.end() && !it->second.empty()) {
+    void* q = it->second.back();
+    it->second.pop_back();
+    c->pool_cached -= k;
+    return q;
+  }
+  void* q = nullptr;
+  if (hipMalloc(&q, k) == hipSuccess) return q;
+  (void)hipGetLastError();
+  pool_drain(c);   // memory pressure: give the cached buffers back and try once more
+  if (hipMalloc(&q, k) == hipSuccess) return q;
+  (void)hipGetLastError();
+  return nullptr;
+}
+
+void pool_put(Ctx* c, void* q, size_t cls) {
+  if (!q) return;
+  if (c->pool_cached + cls > kPoolCacheBytes) {
+    hipFree(q);
+    return;
+  }
+  c->pool[cls].push_back(q);
+  c->pool_cached += cls;
+}
+
+// A scratch buffer for one call: back to the pool when the call returns (after
+// a stream synchronisation if the call did not reach its own).
+struct Scratch {
+  Ctx* c;
+  void* p = nullptr;
+  size_t cls = 0;
+  bool synced = false;
+  Scratch(Ctx* ctx, size_t bytes) : c(ctx) { if (bytes) p = pool_get(c, bytes, &cls); }
+  ~Scratch() {
+    if (!p) return;
+    if (!synced) hipStreamSynchronize(c->stream);
+    pool_put(c, p, cls);
+  }
+  u32* u() const { return (u32*)p; }
+};
+
 void release_prog(Prog& p) {
   hipSetDevice(p.ctx->dev);
   p.unload();
-  if (p.d_buf) hipFree(p.d_buf);
+  // every call on the context synchronises before it returns (and this runs
+  // under the context's mu): no kernel still reads the buffer
+  if (p.d_buf) pool_put(p.ctx.get(), p.d_buf, p.buf_cls);
   p.d_buf = nullptr;
 }
 
 void release_ctx(Ctx& c) {
   hipSetDevice(c.dev);
   if (c.stream) hipStreamSynchronize(c.stream);
+  pool_drain(&c);
   if (c.d_spill) hipFree(c.d_spill);
   if (c.d_min) hipFree(c.d_min);
   if (c.d_progs) hipFree(c.d_progs);
@@ -740,10 +816,8 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   p->desc = *d;
   p->ops_per_eval = d->ops_per_eval;
   p->sig = prog_signature(d);
-  if (hipMalloc(&p->d_buf, total * sizeof(u32)) != hipSuccess) {
-    p->d_buf = nullptr;
-    return fail(MG_E_NOMEM, "program upload allocation failed");
-  }
+  p->d_buf = (u32*)pool_get(c, total * sizeof(u32), &p->buf_cls);
+  if (!p->d_buf) return fail(MG_E_NOMEM, "program upload allocation failed");
   std::vector<u32> hbuf(total, 0u);
   std::memcpy(hbuf.data(), d->code, nc * 4);
   if (d->nconst_words) std::memcpy(hbuf.data() + nc, d->consts, d->nconst_words * 4);
@@ -1105,20 +1179,13 @@ static int eval_common(Ctx* c, const Prog* p, const uint32_t* leaves_soa, size_t
   const u32 nlds = std::min(p->dev.n_spill, kLdsSpillWords);
   int rc = ensure_spill(c, std::max<size_t>(4, (size_t)(p->dev.n_spill - nlds) * nthreads * sizeof(u32)));
   if (rc) return rc;
-  u32 *d_in = nullptr, *d_v = nullptr, *d_t = nullptr;
   const size_t nin = leaves_soa ? (size_t)p->desc.n_input_rows * ncand : 0;
   const size_t ntr = trace ? (size_t)p->desc.n_trace_rows * ncand : 0;
-  auto cleanup = [&]() {
-    if (d_in) hipFree(d_in);
-    if (d_v) hipFree(d_v);
-    if (d_t) hipFree(d_t);
-  };
-  if (nin && hipMalloc(&d_in, nin * 4) != hipSuccess) { cleanup(); return fail(MG_E_NOMEM, "eval input alloc"); }
-  if (hipMalloc(&d_v, ncand * 4) != hipSuccess) { cleanup(); return fail(MG_E_NOMEM, "eval verdict alloc"); }
-  if (ntr && hipMalloc(&d_t, ntr * 4) != hipSuccess) { cleanup(); return fail(MG_E_NOMEM, "eval trace alloc"); }
-  if (nin && hipMemcpyAsync(d_in, leaves_soa, nin * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
-    cleanup(); return fail(MG_E_HIP, "eval input copy");
-  }
+  Scratch s_in(c, nin * 4), s_v(c, ncand * 4), s_t(c, ntr * 4);
+  if ((nin && !s_in.p) || !s_v.p || (ntr && !s_t.p)) return fail(MG_E_NOMEM, "eval buffers");
+  u32 *d_in = s_in.u(), *d_v = s_v.u(), *d_t = s_t.u();
+  if (nin && hipMemcpyAsync(d_in, leaves_soa, nin * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    return fail(MG_E_HIP, "eval input copy");
   if (ntr) hipMemsetAsync(d_t, 0, ntr * 4, c->stream);
   hipLaunchKernelGGL(mw_eval_kernel, dim3((u32)gx), dim3(kBlock), (size_t)nlds * kBlock * 4, c->stream,
                      p->dev, (const u32*)d_in, (u64)ncand, seed, begin, d_v, d_t, c->d_spill, nlds);
@@ -1126,7 +1193,7 @@ static int eval_common(Ctx* c, const Prog* p, const uint32_t* leaves_soa, size_t
   if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, ncand * 4, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess && ntr) e = hipMemcpyAsync(trace, d_t, ntr * 4, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  cleanup();
+  s_in.synced = s_v.synced = s_t.synced = e == hipSuccess;
   if (e != hipSuccess) return fail(MG_E_HIP, std::string("eval: ") + hipGetErrorString(e));
   return 0;
 }
@@ -1163,8 +1230,9 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
   if (rc) return rc;
   rc = ensure_asmargs(c, 1);
   if (rc) return rc;
-  u32* d_v = nullptr;
-  if (hipMalloc(&d_v, count * 4) != hipSuccess) return fail(MG_E_NOMEM, "eval verdict alloc");
+  Scratch s_v(c, count * 4);
+  if (!s_v.p) return fail(MG_E_NOMEM, "eval verdict alloc");
+  u32* d_v = s_v.u();
   AsmArgs aa{};
   aa.seed = seed;
   aa.begin = begin;
@@ -1183,10 +1251,7 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
   if (e == hipSuccess) e = hipMemcpyAsync(c->d_asmargs, &aa, sizeof(AsmArgs), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, kCounterWords * sizeof(u64), c->stream);
   if (e == hipSuccess && assembled) {
-    if (launch_assembled(c, p, (u32)gx, c->d_progs, c->d_asmargs, c->d_min, nlds)) {
-      hipFree(d_v);
-      return MG_E_HIP;
-    }
+    if (launch_assembled(c, p, (u32)gx, c->d_progs, c->d_asmargs, c->d_min, nlds)) return MG_E_HIP;
   } else if (e == hipSuccess) {
     hipLaunchKernelGGL(mw_search_asm_kernel, dim3((u32)gx, 1u), dim3(kBlock), lds, c->stream, c->d_progs,
                        (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, nlds);
@@ -1194,7 +1259,7 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
   }
   if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, count * 4, hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  hipFree(d_v);
+  s_v.synced = e == hipSuccess;
   if (e != hipSuccess)
     return fail(MG_E_HIP, std::string(assembled ? "eval (assembled kernel): " : "eval (asm interpreter): ") +
                               hipGetErrorString(e));
@@ -1220,21 +1285,19 @@ int mg_eval_generated(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t begi
   HIPCHK(hipSetDevice(c->dev));
   int rc = ensure_min(c, 1);
   if (rc) return rc;
-  u32* d_v = nullptr;
-  if (hipMalloc(&d_v, count * 4) != hipSuccess) return fail(MG_E_NOMEM, "eval verdict alloc");
+  Scratch s_v(c, count * 4);
+  if (!s_v.p) return fail(MG_E_NOMEM, "eval verdict alloc");
+  u32* d_v = s_v.u();
   const u64 none = MG_NONE;
   hipError_t e = hipMemcpyAsync(c->d_min, &none, sizeof(u64), hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, kCounterWords * sizeof(u64), c->stream);
   if (e == hipSuccess) {
     rc = launch_jit(c, p, seed, begin, count, 0u, c->d_min, d_v);
-    if (rc) {
-      hipFree(d_v);
-      return rc;
-    }
+    if (rc) return rc;
     e = hipMemcpyAsync(verdict, d_v, count * 4, hipMemcpyDeviceToHost, c->stream);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  hipFree(d_v);
+  s_v.synced = e == hipSuccess;
   if (e != hipSuccess) return fail(MG_E_HIP, std::string("eval (specialised): ") + hipGetErrorString(e));
   return 0;
 }
@@ -1251,14 +1314,15 @@ int mg_witness_leaves(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t inde
   if (nl == 0) return 0;
   HIPCHK(hipSetDevice(c->dev));
   (void)hipGetLastError();
-  u32* d = nullptr;
-  if (hipMalloc(&d, (size_t)nl * 8 * sizeof(u32)) != hipSuccess) return fail(MG_E_NOMEM, "witness leaf buffer");
+  Scratch s_d(c, (size_t)nl * 8 * sizeof(u32));
+  if (!s_d.p) return fail(MG_E_NOMEM, "witness leaf buffer");
+  u32* d = s_d.u();
   hipLaunchKernelGGL(mw_leaf_kernel, dim3((nl + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, p->dev.leaves,
                      p->dev.pool, nl, seed, index, d);
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipMemcpyAsync(out, d, (size_t)nl * 8 * sizeof(u32), hipMemcpyDeviceToHost, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  hipFree(d);
+  s_d.synced = e == hipSuccess;
   if (e != hipSuccess) return fail(MG_E_HIP, std::string("witness leaves: ") + hipGetErrorString(e));
   return 0;
 }
