@@ -380,17 +380,16 @@ MW_HD void udivrem8_full(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8]) {
 // the normalised divisor; the remainder stays one limb throughout.  C5 divides
 // by such values (quotients of earlier divisions) in 42 of its 384 divisions,
 // where the general loop ran all eight steps.
-// The eight steps run as a rolled loop over a sliding window (w[7] the current
-// limb, w[6] the next lower one), the digits shifting into qq: unrolled, the
-// steps were ~160 instructions at each of C5's 384 division sites, which run
-// this path on a few waves only (18 of 384 per candidate); MW_SHORT_UNROLLED
-// restores the unrolled form (tools/ab_c5.py variant "shortunroll").
+// The eight steps are unrolled.  MW_SHORT_ROLLED runs them as a rolled loop
+// over a sliding window (w[7] the current limb, w[6] the next lower one), the
+// digits shifting into qq: 90 KB less code over C5's 384 division sites, but
+// 0.2 ms slower per 2^22 launch (tools/ab_c5.py "shortroll", profiles/r4h).
 MW_HD void udivrem8_short(const u32 x[8], u32 y0, u32 q[8], u32 r[8]) {
   const u32 s = clz32(y0);
   const u32 d = y0 << s;
   const u32 v = recip32(d);
   u32 rem = fshl32(0u, x[7], s);  // < 2^s <= d
-#if !defined(MW_SHORT_UNROLLED)
+#if defined(MW_SHORT_ROLLED)
   u32 w[8], qq[8];
   copy8(w, x);
   zero8(qq);
@@ -507,11 +506,12 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], DivCount
     u[k] = x[k];
     u[k + 8] = 0u;
   }
-#if !defined(MW_GEN_SELECT_STAGES)
+#if defined(MW_GEN_ROLLED_SHIFT)
   // v <<= 32n, u <<= 32n (n: the lane's zero top limbs of y) as a rolled loop
   // of one-limb moves under selects, run as often as the wave's largest n:
-  // three unrolled select stages were ~80 instructions at each of C5's 384
-  // division sites (MW_GEN_SELECT_STAGES restores them; tools/ab_c5.py "genstages")
+  // 90 KB less code than the three select stages below, but 1.8 ms slower per
+  // 2^22 C5 launch (tools/ab_c5.py "genroll", profiles/r4h): the loop's exit
+  // test and its serial chain run at every division site a wave reaches
   u32 n = 0u;
 #pragma unroll 1
   for (int st = 0; st < 7; ++st) {
@@ -592,7 +592,7 @@ MW_HD void udivrem8(const u32 x[8], const u32 y[8], u32 q[8], u32 r[8], DivCount
     u[k] = w[k];
     u[k + 8] = 0u;
   }
-#if !defined(MW_GEN_SELECT_STAGES)
+#if defined(MW_GEN_ROLLED_SHIFT)
 #pragma unroll 1
   for (int st = 0; st < 7; ++st) {  // r = u[0..7] >> 32n, one limb per pass
     const bool c = n > (u32)st;

@@ -35,11 +35,6 @@
 // words per pool entry of a width-w leaf
 #define MW_POOL_ENTRY_WORDS_OF(w) ((w) < 32u ? 1u : (uint32_t)MW_POOL_ENTRY_WORDS)
 #define MW_MAX_WIDTH 256
-// asm interpreter: narrow constants live in MW_ASM_NK VGPRs starting
-// MW_ASM_NK_INDEX registers above the N file's base (v64 + 176 = v240;
-// mw_validate.cpp mw_asm_predecode, mythril_amd/asmgen.py NK0)
-#define MW_ASM_NK 16u
-#define MW_ASM_NK_INDEX 176u
 
 // leaf table entry (MW_LEAF_WORDS u32 per leaf)
 #define MW_LEAF_WIDTH 0

@@ -17,3 +17,9 @@
 #define MW_DST_NLO(d) (((d) >> 3) & 31u)
 #define MW_DST_NHI(d) (((d) >> 8) & 31u)
 #define MW_DST_SCRATCH (MW_W_RESERVED | (MW_N_RESERVED << 3) | (MW_N_RESERVED << 8))
+
+// asm interpreter: narrow constants live in MW_ASM_NK VGPRs starting
+// MW_ASM_NK_INDEX registers above the N file's base (v64 + 176 = v240), filled
+// once per block (mw_validate.cpp mw_asm_predecode, mythril_amd/asmgen.py NK0)
+#define MW_ASM_NK 16u
+#define MW_ASM_NK_INDEX 176u

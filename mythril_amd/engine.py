@@ -5,12 +5,11 @@ candidate pools) and compiles its search program (verdicts only; the native
 compiler, ccompile.py).
 ``WitnessEngine.search`` launches many programs in one ``mg_search`` call (one
 grid row per program, SURVEY.md §8a row A9 batching) and turns each lowest
-satisfying index back into a :class:`Witness`: the search program re-evaluates
-that single candidate on the device (the verdict), and a witness program with
-the same leaf layout and no conjuncts - only the leaves and every array index
-/ function argument, traced - reads its values out.  The witness program is
-compiled on first use and costs a fraction of the search program (C3: ~1 ms
-against ~110 ms for a trace of the whole conjunction).
+satisfying index back into a :class:`Witness`: the leaf values come from the
+still-loaded search program (``mg_witness_leaves``) when every array index /
+function argument is constant, else from a witness program with the same leaf
+layout and no conjuncts - only the leaves and every array index / function
+argument, traced - compiled on first use.
 """
 from __future__ import annotations
 
@@ -218,9 +217,13 @@ class WitnessEngine:
         """The witness at candidate ``index``.  When every array index and
         function argument is a constant (each such cell is then a leaf of its
         own), the leaf values are all of it: one mg_witness_leaves launch on
-        the still-loaded search program.  Otherwise the verdict is re-evaluated
-        by the search program and the values are read from the witness
-        program (leaves plus the traced argument terms)."""
+        the still-loaded search program.  Otherwise the values are read from
+        the witness program (leaves plus the traced argument terms), one
+        mg_eval_generated launch.  Neither re-evaluates the verdict on the
+        device: the search launch found the index satisfying, and every
+        witness is re-checked against the original constraints before it is
+        used (z3 in the drop-in, model.py / z3bridge.model_from_witness; the
+        oracle in the tests)."""
         if (search_dp is not None and getattr(self.dev, "witness_leaves", None) is not None
                 and all(t.op == "const" for t in q.arg_terms)):
             return self._from_leaves(q, index, self.dev.witness_leaves(search_dp, self.seed, index))
@@ -257,16 +260,6 @@ class WitnessEngine:
         if [n.name for n in p.leaf_nodes] != [n.name for n in q.program.leaf_nodes]:
             # an EngineError, so get_model's handler sends the query to z3
             raise EngineError("witness program's leaf layout differs from the search program's")
-        own = search_dp is None
-        sdp = self.dev.load(q.program) if own else search_dp
-        try:
-            verdict, _ = self.dev.eval_generated(sdp, self.seed, index, 1)
-        finally:
-            if own:
-                sdp.free()
-        if int(verdict[0]) != 1:
-            log.error("witness %d failed device re-evaluation; discarded", index)
-            return None
         dp = self.dev.load(p)
         try:
             _, trace = self.dev.eval_generated(dp, self.seed, index, 1)

@@ -61,7 +61,8 @@ ACTORS = [0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE,
           0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF,
           0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA]
 
-_CMP = ("=", "distinct", "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge")
+_CMP = frozenset(("=", "distinct", "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge"))
+_ADDRESS_WORDS = ("sender", "caller", "origin", "creator", "address")
 
 
 def _project(e: Node, value: int, out: Dict[str, List[int]], depth: int = 0,
@@ -521,9 +522,7 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
             continue
         w = 1 if leaf.width == BOOL else leaf.width
         m = (1 << w) - 1
-        lname = leaf.name.lower()
-        actors = ACTORS if w >= 160 and any(t in lname for t in ("sender", "caller", "origin", "creator",
-                                                                  "address")) else ()
+        actors = ACTORS if w >= 160 and any(t in leaf.name.lower() for t in _ADDRESS_WORDS) else ()
         # lazily: the pool fills after a few dozen values, and the byte split of
         # 256 constants for every calldata byte leaf was most of prepare()'s time
         tail = tails.get(w)

@@ -30,11 +30,11 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             "sync": {"EXTRA_FLAGS": [], "CHECK_SYNC": True},
             # the division's rare paths without branch weights (in line, as before round 3)
             "nohint": {"EXTRA_FLAGS": ["-DMW_DIV_NO_HINTS"]},
-            # the short division's eight steps unrolled at every site (before round 4)
-            "shortunroll": {"EXTRA_FLAGS": ["-DMW_SHORT_UNROLLED"]},
-            # the limb-aligned division's shift as three unrolled select stages (before round 4)
-            "genstages": {"EXTRA_FLAGS": ["-DMW_GEN_SELECT_STAGES"]},
-            "r3div": {"EXTRA_FLAGS": ["-DMW_SHORT_UNROLLED", "-DMW_GEN_SELECT_STAGES"]},
+            # round 4's smaller division code, measured slower (profiles/r4h): the short
+            # division's steps as a rolled loop, the limb-aligned path's limb shifts as one
+            "shortroll": {"EXTRA_FLAGS": ["-DMW_SHORT_ROLLED"]},
+            "genroll": {"EXTRA_FLAGS": ["-DMW_GEN_ROLLED_SHIFT"]},
+            "r4roll": {"EXTRA_FLAGS": ["-DMW_SHORT_ROLLED", "-DMW_GEN_ROLLED_SHIFT"]},
             # three waves per SIMD (170 registers per lane); LDS leaves cost 8 KiB per slot and
             # block, so 3 blocks per CU (160 KiB) allow at most 6
             "w3": {"EXTRA_FLAGS": [], "waves": 3, "lds": 6}, "w3l0": {"EXTRA_FLAGS": [], "waves": 3, "lds": 0},
