@@ -637,9 +637,9 @@ def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
     cong = rw.congruence()
     flat = _flatten(out + cong)
     nodes = topo(flat)
-    for n in nodes:
-        if n.width > MAXW:   # every consumer chunks its wide operands; none may remain
-            raise Unsupported(f"{n.width}-bit {n.op} outside the legalised vocabulary")
+    if nodes and max(map(_width, nodes)) > MAXW:   # every consumer chunks its wide operands; none may remain
+        n = next(n for n in nodes if n.width > MAXW)
+        raise Unsupported(f"{n.width}-bit {n.op} outside the legalised vocabulary")
     return Lowered(out + cong, rw.ack, len(cong), flat, nodes)
 
 
