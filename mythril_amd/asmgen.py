@@ -1052,11 +1052,19 @@ def leaf(g):
     g.label("Lleaf_%=")
     g(f"s_lshl_b32 {s(S[7])}, {s(S67)}, 5", f"s_load_dwordx8 {sr(D, 8)}, {sr(LEAVES, 2)}, {s(S[7])}",
       "s_waitcnt lgkmcnt(0)",
-      f"s_cmp_eq_u32 {s(D + 1)}, 1", "s_cbranch_scc1 Lk1_%=",
+      # kind 3 first: the bit-interleaved digits of every pooled leaf that fits the 40 index bits
       f"s_cmp_eq_u32 {s(D + 1)}, 3", "s_cbranch_scc1 Lk3_%=",
+      f"s_cmp_eq_u32 {s(D + 1)}, 1", "s_cbranch_scc1 Lk1_%=",
       f"s_cmp_eq_u32 {s(D + 1)}, 2", "s_cbranch_scc1 Lk2_%=",
       # kind 0 (or anything else: the host never launches other kinds here): Philox
-      f"s_call_b64 {sr(PRET, 2)}, Lphilox_%=")
+      f"s_call_b64 {sr(PRET, 2)}, Lphilox_%=",
+      # w < 32: the draw's low word masked to w bits is the canonical value
+      f"s_cmp_lt_u32 {s(D)}, 32", "s_cbranch_scc0 Lk0_wide_%=",
+      f"s_bfm_b64 {sr(S[6], 2)}, {s(D)}, 0", f"v_and_b32_e32 {v(XC)}, {s(S[6])}, {v(T)}")
+    for k in range(1, 8):
+        g(f"v_mov_b32_e32 {v(XC + k)}, 0")
+    g(f"s_setpc_b64 {sr(LRET, 2)}")
+    g.label("Lk0_wide_%=")
     for k in range(8):
         g(f"v_mov_b32_e32 {v(XC + k)}, {v(T + k)}")
     g("s_branch Lleaf_canon_%=")
@@ -1096,11 +1104,20 @@ def leaf(g):
     for k in range(4):
         g(f"ds_read2_b32 {vr(XC + 2 * k, 2)}, {v(T + 5)} offset0:{1 + 2 * k} offset1:{2 + 2 * k}")
     g("s_waitcnt lgkmcnt(0)", f"v_and_b32_e32 {v(T + 4)}, 1, {v(T + 4)}", "s_branch Lg_flag_%=")
+    # w < 32: pool values are canonical already (masked when the pool is laid
+    # out); only RANDOM lanes draw, and their value is the draw's low word
+    # masked to w bits (no 8-limb select, no generic canonicalisation)
     g.label("Lg_narrow_%=")
     g(f"v_lshl_add_u32 {v(T + 5)}, {v(T + 6)}, 2, {s(S[6])}", f"ds_read_b32 {v(XC)}, {v(T + 5)}")
     for k in range(1, 8):
         g(f"v_mov_b32_e32 {v(XC + k)}, 0")
-    g("s_waitcnt lgkmcnt(0)", f"v_lshrrev_b32_e32 {v(T + 4)}, 31, {v(XC)}")
+    g("s_waitcnt lgkmcnt(0)", f"v_lshrrev_b32_e32 {v(T + 4)}, 31, {v(XC)}",
+      f"v_cmp_ne_u32_e32 vcc, 0, {v(T + 4)}", "s_nop 1", "s_cmp_eq_u64 vcc, 0", "s_cbranch_scc1 Lleaf_ret_%=",
+      f"s_mov_b64 {sr(MSK, 2)}, vcc", f"s_call_b64 {sr(PRET, 2)}, Lphilox_%=", "s_nop 1",
+      f"v_cndmask_b32_e64 {v(XC)}, {v(XC)}, {v(T)}, {sr(MSK, 2)}",
+      f"s_bfm_b64 {sr(S[6], 2)}, {s(D)}, 0", f"v_and_b32_e32 {v(XC)}, {s(S[6])}, {v(XC)}")
+    g.label("Lleaf_ret_%=")
+    g(f"s_setpc_b64 {sr(LRET, 2)}")
     g.label("Lg_flag_%=")
     g(f"v_cmp_ne_u32_e32 vcc, 0, {v(T + 4)}",
       "s_nop 1", "s_cmp_eq_u64 vcc, 0", "s_cbranch_scc1 Lleaf_canon_%=",

@@ -15,6 +15,8 @@ from __future__ import annotations
 
 import dataclasses
 import logging
+import threading
+import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -59,14 +61,20 @@ class Query:
     arg_terms: List[Node]
     arg_chunks: Dict[str, List[List[Node]]] = field(default_factory=dict)
     _trace: Optional[Program] = None
+    _trace_future: Optional[object] = None   # a queued compile (_prebuild_witness_programs)
 
     @property
     def trace_program(self) -> Program:
         """The witness program: ``program``'s leaf layout with no conjuncts,
         tracing every leaf and array index / function argument.  Only a
-        witness needs it, so it is compiled lazily."""
+        witness needs it, so it is compiled lazily (or on the host thread
+        while the search runs)."""
         if self._trace is None:
-            self._trace = self.trace_build()
+            f, self._trace_future = self._trace_future, None
+            if f is not None and not f.cancel():
+                f.result()           # running or done on the host thread
+            if self._trace is None:
+                self._trace = self.trace_build()
         return self._trace
 
     @property
@@ -113,6 +121,45 @@ def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True,
     q = Query(ctx, conj, low, prog, lambda: _witness_program(prog, traced), arg_terms)
     q.arg_chunks = arg_chunks
     return q
+
+
+_PREBUILD = None   # one host thread for witness-program compiles (_prebuild_witness_programs)
+_PREBUILD_LOCK = threading.Lock()
+
+
+def _build_witness_program(q: "Query") -> None:
+    try:
+        q._trace = q.trace_build()
+    except Exception:   # noqa: BLE001 - trace_program compiles it again and reports the error
+        pass
+    time.sleep(0)   # hand the GIL back between queries (the search caller waits for it)
+
+
+# Larger witness programs compile in materialize: their Python part (record
+# stream, leaf table) would hold the GIL the returning search call waits for.
+PREBUILD_MAX_TERMS = 512
+
+
+def _prebuild_witness_programs(queries) -> None:
+    """Queue the witness programs a search may need on a host thread, which
+    compiles them while the device searches (the search call releases the
+    GIL): those of queries whose cells have a non-constant index (the rest
+    read their leaves from the search program, mg_witness_leaves).
+    Query.trace_program takes a finished one, waits for a running one and
+    compiles a not yet started one itself, so nothing is compiled twice and
+    no search waits for the compiles of queries that found nothing."""
+    todo = [q for q in queries if q._trace is None and q._trace_future is None
+            and len(q.arg_terms) <= PREBUILD_MAX_TERMS and not all(t.op == "const" for t in q.arg_terms)]
+    if not todo:
+        return
+    global _PREBUILD
+    if _PREBUILD is None:
+        with _PREBUILD_LOCK:
+            if _PREBUILD is None:
+                from concurrent.futures import ThreadPoolExecutor
+                _PREBUILD = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mw-witness-program")
+    for q in todo:
+        q._trace_future = _PREBUILD.submit(_build_witness_program, q)
 
 
 def _witness_program(prog: Program, traced: List[Node]) -> Program:
@@ -166,6 +213,10 @@ class WitnessEngine:
             if (self.asmjit_min_ops and hasattr(self.dev, "attach_asm")
                     and count * sum(q.ops_per_eval for q in queries) >= self.asmjit_min_ops):
                 self._assemble(dps)
+            # the witness programs compile on a host thread while the device
+            # searches (the search call releases the GIL): a witness then costs
+            # one upload and one launch (materialize)
+            _prebuild_witness_programs(queries)
             found, st = self.dev.search(dps, self.seed, begin, count, flags)
             self.stats["searches"] += 1
             self.stats["programs"] += len(queries)

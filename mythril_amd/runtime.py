@@ -297,13 +297,9 @@ def pack_inputs(p: Program, assignments: Sequence[dict]) -> np.ndarray:
 
 
 def unpack_trace(p: Program, trace: np.ndarray, node) -> List[int]:
+    """The traced values of node, one per candidate (trace rows are u32 limbs,
+    least significant first)."""
     row, cls = p.trace_map[node.id]
-    n = trace.shape[1]
     nl = 8 if cls == "W" else 1
-    out = []
-    for j in range(n):
-        v = 0
-        for k in range(nl):
-            v |= int(trace[row + k, j]) << (32 * k)
-        out.append(v)
-    return out
+    rows = np.ascontiguousarray(trace[row:row + nl].T, dtype="<u4")   # candidate-major
+    return [int.from_bytes(rows[j].tobytes(), "little") for j in range(rows.shape[0])]

@@ -13,8 +13,9 @@ bytecode) it reports, in ms:
              default per-query budget (device; wall time of the call)
   materialise  the witness values of the found index with the search program
              still loaded (only on a witness): one mg_witness_leaves launch when
-             every array index / function argument is constant, else the
-             trace program compile + single-candidate re-evaluation
+             every array index / function argument is constant, else one
+             launch of the witness program (compiled on a host thread during
+             the search, as WitnessEngine.search does)
 and the medians per corpus.  Without a GPU (--no-device) only the host
 phases are timed.
 
@@ -37,7 +38,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-device", action="store_true")
     a = ap.parse_args()
-    from mythril_amd.engine import WitnessEngine, prepare
+    from mythril_amd.engine import WitnessEngine, _prebuild_witness_programs, prepare
     from mythril_amd.smt2 import parse_file
     eng = None if a.no_device else WitnessEngine(device=0)
     rows = []
@@ -57,6 +58,9 @@ def main():
                 t1 = time.perf_counter()
                 dp = eng.dev.load(q.program)
                 try:
+                    # as WitnessEngine.search: the witness program compiles on the
+                    # host thread while the device searches
+                    _prebuild_witness_programs([q])
                     (idx,), st = eng.dev.search([dp], eng.seed, 0, eng.launch_count([q]), 3)
                     row["search"] = (time.perf_counter() - t1) * 1e3
                     row["kernel"] = st["kernel_ms"]
