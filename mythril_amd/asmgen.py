@@ -145,21 +145,26 @@ class Gen:
     # ------------------------------------------------------------ operands
     # Operands come from the asm engine's predecoded copy of the program
     # (mw_validate.cpp mw_asm_predecode): a register operand field holds the
-    # N slot (0..63) or the W slot x 8, so it is the VGPR index relative to the
-    # file's base as it stands; bit 15 flags a constant (word offset).
+    # N slot (0..63), the W slot x 8 or a narrow constant's VGPR (NK0), so it
+    # is the VGPR index relative to the file's base as it stands; bit 15 flags
+    # a W constant (word offset).  Word 1 is a [15:0] | dst [31:16], word 2
+    # b [15:0] | c [31:16].  s_set_gpr_idx_on reads only bits [7:0] of its
+    # SGPR (tools/exp/gpridx_probe.hip), so a and b index straight from their
+    # word; c and dst take one shift.
     # field() only binds an operand to a name; fetch_n / fetch_w read it.
-    WORD = {"a": (CUR + 1, "hi"), "b": (CUR + 2, "lo"), "c": (CUR + 2, "hi")}
+    WORD = {"a": (CUR + 1, "lo"), "b": (CUR + 2, "lo"), "c": (CUR + 2, "hi")}
 
     def field(self, which, dst):
         """bind operand field a/b/c to the name dst (no code)"""
         self.bound[dst] = which
 
-    def _index(self, which, dst_sgpr):
+    def _index(self, which):
+        """the SGPR to hand s_set_gpr_idx_on for operand field `which`"""
         wd, half = self.WORD[which]
         if half == "hi":
-            self(f"s_lshr_b32 {dst_sgpr}, {s(wd)}, 16")
-        else:
-            self(f"s_and_b32 {dst_sgpr}, {s(wd)}, 0xffff")
+            self(f"s_lshr_b32 {s(SIDX)}, {s(wd)}, 16")
+            return s(SIDX)
+        return s(wd)
 
     def _is_const(self, which, label):
         wd, half = self.WORD[which]
@@ -169,24 +174,23 @@ class Gen:
         """N operand bound to f -> VGPR dst: one indexed move, registers and
         constants alike (a constant is predecoded as its VGPR above the N
         file, NK0)"""
-        which = self.bound[f]
-        self._index(which, s(SIDX))
-        self(f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(SRC0)", f"v_mov_b32_e32 {v(dst)}, {v(N0)}", "s_set_gpr_idx_off")
+        idx = self._index(self.bound[f])
+        self(f"s_set_gpr_idx_on {idx}, gpr_idx(SRC0)", f"v_mov_b32_e32 {v(dst)}, {v(N0)}", "s_set_gpr_idx_off")
 
     def fetch_w(self, f, dst):
         """W/K operand bound to f -> VGPRs dst..dst+7"""
         which = self.bound[f]
         lk, lr = self.L("kw"), self.L("rw")
         self._is_const(which, lk)
-        self._index(which, s(SIDX))
-        self(f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(SRC0)")
+        idx = self._index(which)
+        self(f"s_set_gpr_idx_on {idx}, gpr_idx(SRC0)")
         for k in range(8):
             self(f"v_mov_b32_e32 {v(dst + k)}, {v(W0 + k)}")
         self("s_set_gpr_idx_off")
         self.label(lr)
         wd, half = self.WORD[which]
-        off = f"s_lshr_b32 {s(SX)}, {s(wd)}, 16" if half == "hi" else f"s_and_b32 {s(SX)}, {s(wd)}, 0x7fff"
-        t = [f"{lk}:", off, f"s_and_b32 {s(SX)}, {s(SX)}, 0x7fff", f"s_lshl_b32 {s(SX)}, {s(SX)}, 2",
+        off = f"s_bfe_u32 {s(SX)}, {s(wd)}, {(15 << 16) | (16 if half == 'hi' else 0):#x}"   # the word offset
+        t = [f"{lk}:", off, f"s_lshl_b32 {s(SX)}, {s(SX)}, 2",
              f"s_load_dwordx8 {sr(DESC, 8)}, {sr(CPOOL, 2)}, {s(SX)}", "s_waitcnt lgkmcnt(0)"]
         t += [f"v_mov_b32_e32 {v(dst + k)}, {s(DESC + k)}" for k in range(8)]
         self.tail += t + [f"s_branch {lr}"]
@@ -206,13 +210,13 @@ class Gen:
         return s(CUR + 3)
 
     def write_n(self, src):
-        """N result in VGPR src -> the N slot of the predecoded dst field [5:0]"""
-        self(f"s_and_b32 {s(SIDX)}, {s(CUR + 1)}, 0x3f", f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(DST)",
+        """N result in VGPR src -> the N slot in the predecoded dst field (word 1 [31:16])"""
+        self(f"s_lshr_b32 {s(SIDX)}, {s(CUR + 1)}, 16", f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(DST)",
              f"v_mov_b32_e32 {v(N0)}, {v(src)}", "s_set_gpr_idx_off")
 
     def write_w(self, src):
-        """W result in VGPRs src.. -> the W slot x 8 of the predecoded dst field [13:8]"""
-        self(f"s_bfe_u32 {s(SIDX)}, {s(CUR + 1)}, 0x60008", f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(DST)")
+        """W result in VGPRs src.. -> the W slot x 8 in the predecoded dst field (word 1 [31:16])"""
+        self(f"s_lshr_b32 {s(SIDX)}, {s(CUR + 1)}, 16", f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(DST)")
         for k in range(8):
             self(f"v_mov_b32_e32 {v(W0 + k)}, {v(src + k)}")
         self("s_set_gpr_idx_off")

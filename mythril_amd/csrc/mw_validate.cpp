@@ -194,10 +194,11 @@ int mg_validate_desc(const mg_prog_desc* d) {
 }
 
 // The asm interpreter's copy of a validated program (mw_asm_interp.inc reads
-// operands without decoding them): w0 and w3 unchanged; the dst field becomes
-// the written N slot (0..63) in [5:0] and the written W slot x 8 in [13:8]; a
-// W register operand becomes its slot x 8 (the VGPR offset of its limb 0 in
-// the W file), N register operands and W constants stay as they are, except a
+// operands without decoding them): word 1 becomes a [15:0] | dst [31:16] (a
+// first: s_set_gpr_idx_on takes the index from bits [7:0] of the word), the
+// dst field the written register's index in its file (N slot 0..63, or W
+// slot x 8); a W register operand becomes its slot x 8 (the VGPR offset of
+// its limb 0 in the W file), N register operands and W constants stay as they are, except a
 // W_CDINS byte index (always a constant) below 0x4000, which becomes
 // 0x4000 | index (the handler then compares it with one 32-bit summary of the
 // size instead of a signed 256-bit subtraction).
@@ -237,9 +238,9 @@ int mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t n
     OpShape sh;
     (void)op_shape(I[0] & 0xffu, sh);   // validated: every opcode is known
     const u32 dst = I[1] & 0xffffu, a = I[1] >> 16, b = I[2] & 0xffffu, c = I[2] >> 16;
-    u32 d2 = 0;
+    u32 d2 = 0;   // the written register's index in its file: N slot, or W slot x 8
     if (sh.dst == 4) d2 = MW_DST_NLO(dst) != MW_N_RESERVED ? MW_DST_NLO(dst) : 32u + MW_DST_NHI(dst);
-    else if (sh.dst == 3) d2 = (MW_DST_W(dst) * 8u) << 8;
+    else if (sh.dst == 3) d2 = MW_DST_W(dst) * 8u;
     auto opnd = [](int kind, u32 f) { return (kind == 1 && !(f & MW_KBIT)) ? f * 8u : f; };
     const u32 op = I[0] & 0xffu, w = I[0] >> 16;
     u32 a2 = opnd(sh.a, a), b2 = opnd(sh.b, b), c2 = opnd(sh.c, c);
@@ -251,7 +252,7 @@ int mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t n
     }
     if (!narrow(sh.a, a, &a2) || !narrow(sh.b, b, &b2) || !narrow(sh.c, c, &c2)) return -1;
     O[0] = (I[0] & 0xffff0000u) | ((I[0] >> 8) & MW_FLAG_CHAIN ? 0x8000u : 0u) | (hoff[op & 0x7fu] & 0x7fffu);
-    O[1] = d2 | (a2 << 16);
+    O[1] = a2 | (d2 << 16);   // s_set_gpr_idx_on reads bits [7:0]: a indexes from the word as it is
     O[2] = b2 | (c2 << 16);
     O[3] = I[3];
     if (op == MW_N_ADD || op == MW_N_SUB || op == MW_N_MUL || op == MW_N_NOT)

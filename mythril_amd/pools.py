@@ -517,8 +517,15 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
     uniq_consts = list(dict.fromkeys(consts))[:256]
     tails: Dict[int, List[int]] = {}   # width -> the constants' proposals, deduplicated
     nfixed = max(1, int(pool_size * (1 - random_share)))
+    # word ties first: their bytes' pools are the word's (no pool of their own to build)
+    tied = _tie_words(concats, {lf.name for lf in leaves if lf.op == "var"}, word_props, set(exact), uniq_consts,
+                      pool_size, random_share, combos)
     for leaf in leaves:
         if leaf.op != "var":
+            continue
+        t = tied.get(leaf.name)
+        if t is not None:
+            specs[leaf.name] = t
             continue
         w = 1 if leaf.width == BOOL else leaf.width
         m = (1 << w) - 1
@@ -549,7 +556,6 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
                 pool = _restrict(pool, leaf.name, w, exact, interval, dom_align, pool_size,
                                  proposals.get(leaf.name, ()))
         specs[leaf.name] = LeafSpec(leaf.name, w, pool=pool)
-    _tie_words(concats, specs, word_props, set(exact), uniq_consts, pool_size, random_share, combos)
     return specs
 
 
@@ -570,14 +576,16 @@ def _byte_leaf(a: Node) -> Optional[Node]:
     return None
 
 
-def _tie_words(nodes, specs, word_props, exact_names, uniq_consts, pool_size, random_share, combos=()):
+def _tie_words(nodes, names, word_props, exact_names, uniq_consts, pool_size, random_share, combos=()):
     """Bytes of one word (a concat of byte leaves: an ABI argument read from
     calldata, ``calldata.py:218-231``) draw one word-level pool entry together:
     the pool holds whole-word proposals split into bytes, and every byte after
     the first copies the first's digit (LeafSpec.tie).  Without this each byte
     picks its own entry and a proposed word value (an array offset, a count) is
     hit with probability |pool|^-31.  Bytes already fixed by a domain fact stay
-    singletons; a byte joins at most one word, the one with most free bytes."""
+    singletons; a byte joins at most one word, the one with most free bytes.
+    names: the leaves that get a spec; returns {byte leaf name: its spec}."""
+    specs: Dict[str, LeafSpec] = {}
     words = []
     for n in nodes:
         if n.op == "concat" and len(n.args) >= 2:
@@ -589,7 +597,7 @@ def _tie_words(nodes, specs, word_props, exact_names, uniq_consts, pool_size, ra
     while words:
         scored = []
         for n, bl in words:
-            f = [(i, b) for i, b in enumerate(bl) if b.name not in taken and b.name in specs]
+            f = [(i, b) for i, b in enumerate(bl) if b.name not in taken and b.name in names]
             if len(f) >= 2:   # a word with fewer free bytes never regains them
                 scored.append(((len(f), len(word_props.get(n.id, ()))), n, bl, f))
         if not scored:
@@ -624,3 +632,4 @@ def _tie_words(nodes, specs, word_props, exact_names, uniq_consts, pool_size, ra
             specs[b.name] = LeafSpec(b.name, 8, pool=[None if v is None else (v >> sh) & 0xFF for v in pool],
                                      tie=None if b.name == lead else lead)
             taken.add(b.name)
+    return specs

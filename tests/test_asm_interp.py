@@ -81,12 +81,12 @@ HOFF = __import__("numpy").arange(1000, 1000 + 128 * 7, 7, dtype="uint32")
 
 def test_predecode_operand_layout():
     """The asm engine's copy of the code: word 0 -> width | FLAG_CHAIN at bit 15
-    | the opcode's handler word offset (one-jump dispatch), N dst -> slot in
-    [5:0], W dst -> slot x 8 in [13:8], W register operands -> slot x 8,
-    N register operands and W constants unchanged, N constants -> the index
-    of their VGPR above the N file (176 + k, the value in table slot k), a
-    W_CDINS index constant below 0x4000 -> 0x4000 | index, and N_ADD's word 3
-    -> its width mask."""
+    | the opcode's handler word offset (one-jump dispatch), word 1 -> a [15:0]
+    | dst [31:16] with dst the written register's index (N slot, W slot x 8),
+    W register operands -> slot x 8, N register operands and W constants
+    unchanged, N constants -> the index of their VGPR above the N file
+    (176 + k, the value in table slot k), a W_CDINS index constant below
+    0x4000 -> 0x4000 | index, and N_ADD's word 3 -> its width mask."""
     e = isa.encode
     consts = [0] * 17
     consts[0], consts[8], consts[16] = 0x24, 0x5000, 0x77   # two 256-bit constants, one narrow
@@ -103,12 +103,12 @@ def test_predecode_operand_layout():
     want0 = (src[:, 0] & 0xFFFF0000) | HOFF[src[:, 0] & 0x7F] | (((src[:, 0] >> 8) & isa.FLAG_CHAIN) << 15)
     assert (o[:, 0] == want0).all()
     assert o[0, 3] == 0xFF and (o[1:, 3] == src[1:, 3]).all()       # N_ADD: the 8-bit mask
-    assert o[0, 1] == 37 | (3 << 16) and o[0, 2] == 176 + 0          # narrow constant 0x77 -> NK slot 0
+    assert o[0, 1] == 3 | (37 << 16) and o[0, 2] == 176 + 0          # narrow constant 0x77 -> NK slot 0
     assert list(nk[:2]) == [0x77, 0x24] and not nk[2:].any()
-    assert o[6, 1] == 5 | ((176 + 1) << 16) and o[6, 2] == 176 + 0  # 0x24 (narrow use) -> slot 1, 0x77 reused
-    assert o[1, 1] == (40 << 8) | (16 << 16) and o[1, 2] == isa.KBIT | 0
-    assert o[2, 1] == 4 | (48 << 16) and o[2, 2] == 8
-    assert o[3, 1] == (8 << 8) | (24 << 16) and o[3, 2] == 32 | (9 << 16)   # c is the N condition
+    assert o[6, 1] == (176 + 1) | (5 << 16) and o[6, 2] == 176 + 0  # 0x24 (narrow use) -> slot 1, 0x77 reused
+    assert o[1, 1] == 16 | (40 << 16) and o[1, 2] == isa.KBIT | 0
+    assert o[2, 1] == 48 | (4 << 16) and o[2, 2] == 8
+    assert o[3, 1] == 24 | (8 << 16) and o[3, 2] == 32 | (9 << 16)   # c is the N condition
     assert o[4, 2] == 8 | ((0x4000 | 0x24) << 16)
     assert o[5, 2] == 8 | ((isa.KBIT | 8) << 16)                          # 0x5000: stays a constant
 
