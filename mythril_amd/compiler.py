@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import math
 import zlib
+from array import array
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
@@ -932,8 +933,7 @@ def layout_leaves(leaf_nodes: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
             bit = max(bit, spec.shift + (spec.bits - 1) * max(spec.stride, 1) + 1 if spec.bits else 0)
             m = (1 << w) - 1
             if w < 32:   # one word per entry (mw_isa.h MW_POOL_NARROW_RANDOM)
-                for e in spec.pool:
-                    pool_words += (isa.POOL_NARROW_RANDOM if e is None else e & m).to_bytes(4, "little")
+                pool_words += array("I", [isa.POOL_NARROW_RANDOM if e is None else e & m for e in spec.pool]).tobytes()
             else:        # flags word + 8 limbs, little-endian
                 for e in spec.pool:
                     pool_words += _POOL_RANDOM_W if e is None else b"\0\0\0\0" + (e & m).to_bytes(32, "little")
