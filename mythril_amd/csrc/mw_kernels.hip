@@ -11,6 +11,7 @@
 // program upload with full validation, thread-local error strings.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -362,15 +363,21 @@ struct Ctx {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   u32* d_spill = nullptr;
   size_t spill_bytes = 0;
+  // One call's launch records, in one device block mirrored by a pinned host
+  // block (stage_upload / stage_readback): counters, d_min, ProgDev records,
+  // AsmArgs records.  A call uploads them with one copy and reads counters and
+  // d_min back with one copy.
+  uint8_t* d_blk = nullptr;
+  uint8_t* h_blk = nullptr;
+  size_t off_min = 0, off_progs = 0, off_args = 0;
+  u64* d_counter = nullptr;   // [0] evals, [1..4] division steps/full/short/general x lanes (mg_stats)
   u64* d_min = nullptr;
   size_t nmin = 0;
-  u64* d_counter = nullptr;   // [0] evals, [1..4] division steps/full/short/general x lanes (mg_stats)
-  u32* d_alive = nullptr;     // per-candidate alive bits between the parts of a split program
-  size_t alive_cap = 0;
-  ProgDev* d_progs = nullptr;
-  size_t nprogs_cap = 0;
+  ProgDev* d_progs = nullptr; // nmin records
   AsmArgs* d_asmargs = nullptr;  // AsmArgs records: [0] the asm interpreter's launch, [1..] assembled kernels'
   size_t nasmargs_cap = 0;
+  u32* d_alive = nullptr;     // per-candidate alive bits between the parts of a split program
+  size_t alive_cap = 0;
   std::mutex mu;                 // serialises the calls on this context (mw_handles.h)
   bool dead = false;             // freed by mg_free (guarded by mu)
   // device buffers returned by freed programs and finished calls, by size
@@ -579,32 +586,81 @@ void release_ctx(Ctx& c) {
   if (c.stream) hipStreamSynchronize(c.stream);
   pool_drain(&c);
   if (c.d_spill) hipFree(c.d_spill);
-  if (c.d_min) hipFree(c.d_min);
-  if (c.d_progs) hipFree(c.d_progs);
-  if (c.d_asmargs) hipFree(c.d_asmargs);
-  if (c.d_counter) hipFree(c.d_counter);
+  if (c.d_blk) hipFree(c.d_blk);
+  if (c.h_blk) hipHostFree(c.h_blk);
   if (c.d_alive) hipFree(c.d_alive);
   if (c.e0) hipEventDestroy(c.e0);
   if (c.e1) hipEventDestroy(c.e1);
   if (c.stream) hipStreamDestroy(c.stream);
   c.d_spill = nullptr;
+  c.d_blk = c.h_blk = nullptr;
   c.d_min = nullptr;
   c.d_progs = nullptr;
   c.d_asmargs = nullptr;
   c.d_counter = nullptr;
+  c.nmin = c.nasmargs_cap = 0;
   c.d_alive = nullptr;
   c.e0 = c.e1 = nullptr;
   c.stream = nullptr;
 }
 
-int ensure_asmargs(Ctx* c, size_t n) {
-  if (n <= c->nasmargs_cap) return 0;
-  if (c->d_asmargs) HIPCHK(hipFree(c->d_asmargs));
+// Room for nmin d_min words and ProgDev records and nargs AsmArgs records in
+// the launch block.  Runs before a call enqueues anything (the previous call on
+// the context synchronised before it returned).
+int ensure_launch(Ctx* c, size_t nmin, size_t nargs) {
+  if (c->d_blk && nmin <= c->nmin && nargs <= c->nasmargs_cap) return 0;
+  nmin = std::max({nmin, c->nmin, (size_t)16});
+  nargs = std::max({nargs, c->nasmargs_cap, (size_t)4});
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t off_min = up(kCounterWords * sizeof(u64));
+  const size_t off_progs = up(off_min + nmin * sizeof(u64));
+  const size_t off_args = up(off_progs + nmin * sizeof(ProgDev));
+  const size_t bytes = up(off_args + nargs * sizeof(AsmArgs));
+  if (c->d_blk) HIPCHK(hipFree(c->d_blk));
+  if (c->h_blk) HIPCHK(hipHostFree(c->h_blk));
+  c->d_blk = c->h_blk = nullptr;
+  c->d_counter = c->d_min = nullptr;
+  c->d_progs = nullptr;
   c->d_asmargs = nullptr;
-  c->nasmargs_cap = 0;
-  HIPCHK(hipMalloc(&c->d_asmargs, n * sizeof(AsmArgs)));
-  c->nasmargs_cap = n;
+  c->nmin = c->nasmargs_cap = 0;
+  HIPCHK(hipMalloc(&c->d_blk, bytes));
+  HIPCHK(hipHostMalloc(&c->h_blk, bytes, hipHostMallocDefault));
+  c->off_min = off_min;
+  c->off_progs = off_progs;
+  c->off_args = off_args;
+  c->d_counter = (u64*)c->d_blk;
+  c->d_min = (u64*)(c->d_blk + off_min);
+  c->d_progs = (ProgDev*)(c->d_blk + off_progs);
+  c->d_asmargs = (AsmArgs*)(c->d_blk + off_args);
+  c->nmin = nmin;
+  c->nasmargs_cap = nargs;
   return 0;
+}
+
+// Stage a call's launch records in the pinned mirror and enqueue one upload:
+// zeroed counters, nmin d_min words at MG_NONE, nprogs ProgDev records and
+// nargs AsmArgs records (ensure_launch sized the block).
+hipError_t stage_upload(Ctx* c, size_t nmin, const ProgDev* progs, size_t nprogs, const AsmArgs* args,
+                        size_t nargs) {
+  std::memset(c->h_blk, 0, kCounterWords * sizeof(u64));
+  u64* hm = (u64*)(c->h_blk + c->off_min);
+  for (size_t i = 0; i < nmin; ++i) hm[i] = MG_NONE;
+  size_t end = c->off_min + nmin * sizeof(u64);
+  if (nprogs) {
+    std::memcpy(c->h_blk + c->off_progs, progs, nprogs * sizeof(ProgDev));
+    end = c->off_progs + nprogs * sizeof(ProgDev);
+  }
+  if (nargs) {
+    std::memcpy(c->h_blk + c->off_args, args, nargs * sizeof(AsmArgs));
+    end = c->off_args + nargs * sizeof(AsmArgs);
+  }
+  return hipMemcpyAsync(c->d_blk, c->h_blk, end, hipMemcpyHostToDevice, c->stream);
+}
+
+// Enqueue one readback of the counters and the first nmin d_min words into the
+// pinned mirror (read them there after the stream synchronises).
+hipError_t stage_readback(Ctx* c, size_t nmin) {
+  return hipMemcpyAsync(c->h_blk, c->d_blk, c->off_min + nmin * sizeof(u64), hipMemcpyDeviceToHost, c->stream);
 }
 
 // One launch of a program's assembled kernel: the asm interpreter's grid (x:
@@ -625,18 +681,6 @@ int ensure_spill(Ctx* c, size_t bytes) {
   c->spill_bytes = 0;
   HIPCHK(hipMalloc(&c->d_spill, bytes));
   c->spill_bytes = bytes;
-  return 0;
-}
-
-int ensure_min(Ctx* c, size_t n) {
-  if (n <= c->nmin) return 0;
-  if (c->d_min) HIPCHK(hipFree(c->d_min));
-  if (c->d_progs) HIPCHK(hipFree(c->d_progs));
-  c->d_min = nullptr;
-  c->d_progs = nullptr;
-  HIPCHK(hipMalloc(&c->d_min, n * sizeof(u64)));
-  HIPCHK(hipMalloc(&c->d_progs, n * sizeof(ProgDev)));
-  c->nmin = n;
   return 0;
 }
 
@@ -759,7 +803,7 @@ int mg_init(int device, mg_ctx** out) {
     c->ncu = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
-      hipMalloc(&c->d_counter, kCounterWords * sizeof(u64)) != hipSuccess) {
+      ensure_launch(c.get(), 16, 4) != 0) {
     release_ctx(*c);
     return fail(MG_E_HIP, "context setup failed");
   }
@@ -988,8 +1032,7 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   const double t0 = now_ms();
   HIPCHK(hipSetDevice(c->dev));
   (void)hipGetLastError();  // start from a clean error state: launch errors are read back below
-  int rc = ensure_min(c, nprog);
-  if (rc) return rc;
+  int rc = 0;
   // Programs with a specialised kernel (mg_prog_attach_kernel) get one launch
   // each; the rest share interpreter launches (grid row per program): one of
   // the threaded-dispatch asm interpreter for the programs it handles, one of
@@ -1075,18 +1118,16 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     r.verdict = nullptr;
     spill_need = std::max(spill_need, (size_t)(d.n_spill - r.nlds) * agx * kBlock * sizeof(u32));
   }
+  const bool need_args = groups[0].n || !gasb.empty();
+  rc = ensure_launch(c, nprog, need_args ? ha.size() : 0);
+  if (rc) return rc;
   if (nia) {
     rc = ensure_spill(c, spill_need);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(c->d_progs, hp.data(), nia * sizeof(ProgDev), hipMemcpyHostToDevice, c->stream));
   }
   for (size_t k = 0; k < gasb.size(); ++k) ha[1 + k].spillbuf = c->d_spill;
-  if (groups[0].n || !gasb.empty()) {
-    rc = ensure_asmargs(c, ha.size());
-    if (rc) return rc;
-  }
   AsmArgs& aa = ha[0];
-  if (groups[0].n || !gasb.empty()) {
+  if (need_args) {
     aa.seed = seed;
     aa.begin = begin;
     aa.end = begin + count;
@@ -1097,11 +1138,9 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     aa.gdx = (u32)groups[0].gx;
     aa.spillbuf = c->d_spill;
     aa.verdict = nullptr;
-    HIPCHK(hipMemcpyAsync(c->d_asmargs, ha.data(), ha.size() * sizeof(AsmArgs), hipMemcpyHostToDevice, c->stream));
   }
-  std::vector<u64> init(nprog, MG_NONE);
-  HIPCHK(hipMemcpyAsync(c->d_min, init.data(), nprog * sizeof(u64), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemsetAsync(c->d_counter, 0, kCounterWords * sizeof(u64), c->stream));
+  // one upload: zeroed counters, d_min at MG_NONE, the ProgDev and AsmArgs records
+  HIPCHK(stage_upload(c, nprog, hp.data(), nia, ha.data(), need_args ? ha.size() : 0));
   HIPCHK(hipEventRecord(c->e0, c->stream));
   if (groups[0].n) {
     const Group& G = groups[0];
@@ -1139,12 +1178,10 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     if (rc) return rc;
   }
   HIPCHK(hipEventRecord(c->e1, c->stream));
-  std::vector<u64> stripes(kCounterWords);
-  std::vector<u64> mins(nprog);
-  HIPCHK(hipMemcpyAsync(mins.data(), c->d_min, nprog * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(stripes.data(), c->d_counter, kCounterWords * sizeof(u64), hipMemcpyDeviceToHost,
-                        c->stream));
+  HIPCHK(stage_readback(c, nprog));   // counters and d_min, one copy
   HIPCHK(hipStreamSynchronize(c->stream));
+  const u64* stripes = (const u64*)c->h_blk;
+  const u64* mins = (const u64*)(c->h_blk + c->off_min);
   u64 ctr[kNCounters] = {0, 0, 0, 0, 0};
   for (size_t sidx = 0; sidx <= MW_CTR_STRIPES; ++sidx)
     for (int k = 0; k < kNCounters; ++k) ctr[k] += stripes[sidx * MW_CTR_STRIPE_WORDS + k];
@@ -1222,13 +1259,11 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
   const size_t lds = (size_t)nlds * kBlock * 4 + (size_t)p->dev.npool * 4;
   HIPCHK(hipSetDevice(c->dev));
   (void)hipGetLastError();
-  int rc = ensure_min(c, 1);
+  int rc = ensure_launch(c, 1, 1);
   if (rc) return rc;
   const u64 nchunks = (count + kBlock - 1) / kBlock;
   const u64 gx = std::min<u64>(nchunks, (u64)c->ncu * 8);
   rc = ensure_spill(c, std::max<size_t>(4, (size_t)(p->dev.n_spill - nlds) * gx * kBlock * sizeof(u32)));
-  if (rc) return rc;
-  rc = ensure_asmargs(c, 1);
   if (rc) return rc;
   Scratch s_v(c, count * 4);
   if (!s_v.p) return fail(MG_E_NOMEM, "eval verdict alloc");
@@ -1244,12 +1279,7 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
   aa.gdx = (u32)gx;
   aa.spillbuf = c->d_spill;
   aa.verdict = d_v;
-  const u64 none = MG_NONE;
-  hipError_t e = hipMemcpyAsync(c->d_progs, assembled ? &p->dev : &p->adev, sizeof(ProgDev), hipMemcpyHostToDevice,
-                                c->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->d_min, &none, sizeof(u64), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->d_asmargs, &aa, sizeof(AsmArgs), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, kCounterWords * sizeof(u64), c->stream);
+  hipError_t e = stage_upload(c, 1, assembled ? &p->dev : &p->adev, 1, &aa, 1);
   if (e == hipSuccess && assembled) {
     if (launch_assembled(c, p, (u32)gx, c->d_progs, c->d_asmargs, c->d_min, nlds)) return MG_E_HIP;
   } else if (e == hipSuccess) {
@@ -1283,14 +1313,12 @@ int mg_eval_generated(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t begi
   // verdicts only, on the program's specialised kernel
   if (!verdict || count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad argument");
   HIPCHK(hipSetDevice(c->dev));
-  int rc = ensure_min(c, 1);
+  int rc = ensure_launch(c, 1, 0);
   if (rc) return rc;
   Scratch s_v(c, count * 4);
   if (!s_v.p) return fail(MG_E_NOMEM, "eval verdict alloc");
   u32* d_v = s_v.u();
-  const u64 none = MG_NONE;
-  hipError_t e = hipMemcpyAsync(c->d_min, &none, sizeof(u64), hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(c->d_counter, 0, kCounterWords * sizeof(u64), c->stream);
+  hipError_t e = stage_upload(c, 1, nullptr, 0, nullptr, 0);
   if (e == hipSuccess) {
     rc = launch_jit(c, p, seed, begin, count, 0u, c->d_min, d_v);
     if (rc) return rc;

@@ -14,6 +14,7 @@ argument, traced - compiled on first use.
 from __future__ import annotations
 
 import dataclasses
+import gc
 import logging
 import threading
 import time
@@ -85,8 +86,21 @@ class Query:
 def prepare(conjuncts: Sequence[Node], ctx: Ctx, use_pools: bool = True,
             timings: Optional[Dict[str, float]] = None) -> Query:
     """Lower, harvest candidate pools and compile one constraint set.
-    timings (optional) receives the seconds of each phase (tools/latency_bench.py)."""
-    import time
+    timings (optional) receives the seconds of each phase (tools/latency_bench.py).
+    The cyclic garbage collector is paused for the call: preparation allocates
+    thousands of acyclic terms, and a collection pass over the caller's heap
+    (a LASER process holds a large one) lands on the query's latency.  Reference
+    counting still frees everything; cycles wait for the next pass."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        return _prepare(conjuncts, ctx, use_pools, timings)
+    finally:
+        if was:
+            gc.enable()
+
+
+def _prepare(conjuncts, ctx, use_pools, timings) -> Query:
     t0 = time.perf_counter()
     conj = list(conjuncts)
     low = lower_constraints(conj, ctx)

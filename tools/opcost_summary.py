@@ -32,7 +32,8 @@ def main():
         def per(c):
             return r[c] / w / chunks / ln["repeat"]
         print(f"{ln['engine']:6s} {ln['op']:22s} VALU {per('SQ_INSTS_VALU'):6.1f} SALU {per('SQ_INSTS_SALU'):6.1f} "
-              f"SMEM {per('SQ_INSTS_SMEM'):5.2f} BR {per('SQ_INSTS_BRANCH'):5.1f} cyc {per('SQ_WAVE_CYCLES'):7.1f}")
+              f"SMEM {per('SQ_INSTS_SMEM'):5.2f} BR {per('SQ_INSTS_BRANCH'):5.1f} cyc {per('SQ_WAVE_CYCLES'):7.1f} "
+              f"wait_inst {per('SQ_WAIT_INST_ANY'):6.1f} wait_any {per('SQ_WAIT_ANY'):6.1f}")
 
 
 if __name__ == "__main__":
