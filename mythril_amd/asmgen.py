@@ -303,6 +303,13 @@ class Gen:
     def call_leaf_sub(self):
         self(f"s_call_b64 {sr(LRET, 2)}, Lleaf_%=")
 
+    def consume(self):
+        """take the next instruction into CUR without a dispatch (the next link
+        of a W_CDINS chain, the next handler of a fused sequence) and prefetch
+        the one after it"""
+        self("s_waitcnt lgkmcnt(0)", f"s_mov_b64 {sr(CUR, 2)}, {sr(NXT, 2)}", f"s_mov_b64 {sr(CUR + 2, 2)}, {sr(NXT + 2, 2)}",
+             f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, {s(SOFF)}")
+
     def next(self):
         """dispatch the next instruction (each handler ends in its own copy:
         no jump back to a shared dispatch block).  It was prefetched one ahead;
@@ -794,15 +801,11 @@ def build_handlers():
         last = g.L("cdlast")
         g(f"s_bitcmp1_b32 {s(CUR)}, {CHAIN_BIT}", f"s_cbranch_scc0 {last}")
         g.width(S[2]), g.canon(XR, S[2])
-        consume_next(g)
+        g.consume()
         g(f"s_branch {top}")
         g.label(last)
         g.width(S[2]), g.canon(XR, S[2])
         g.write_w(XR)
-
-    def consume_next(g):
-        g("s_waitcnt lgkmcnt(0)", f"s_mov_b64 {sr(CUR, 2)}, {sr(NXT, 2)}", f"s_mov_b64 {sr(CUR + 2, 2)}, {sr(NXT + 2, 2)}",
-          f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, {s(SOFF)}")
 
     # -------------------------------------------------------- leaves
     def call_leaf(g, li):
@@ -946,6 +949,9 @@ def gen(mode="interp"):
             tgt = f"Lh_{n}_%=" if (n in handlers or n == "END") else "Lunsup_%="
             g(f"v_mov_b32_e32 {v(T)}, (({tgt} - Lpc0_%=) >> 2)", f"v_mov_b32_e32 {v(T + 1)}, {4 * code}",
               f"global_store_dword {v(T + 1)}, {v(T)}, {sr(VERD, 2)}")
+        for k in range(len(isa.ASM_FUSED)):   # the fused handlers' offsets follow (entries NTAB + k)
+            g(f"v_mov_b32_e32 {v(T)}, ((Lf{k}_%= - Lpc0_%=) >> 2)", f"v_mov_b32_e32 {v(T + 1)}, {4 * (NTAB + k)}",
+              f"global_store_dword {v(T + 1)}, {v(T)}, {sr(VERD, 2)}")
         g(f"s_mov_b64 exec, {sr(EXECSV, 2)}", "s_branch Lexit_%=")
         g.label("Lnointro_%=")
         # the program's narrow constants (mw_asm_predecode: after the predecoded
@@ -999,6 +1005,17 @@ def gen(mode="interp"):
                 continue
             g.label(f"Lh_{n}_%=")
             handlers[n](g)
+            g.next()
+            g.flush_tail()
+        # fused sequences (isa.ASM_FUSED): the handlers back to back, each
+        # later one taking its instruction as a W_CDINS chain link does; one
+        # dispatch at the end
+        for k, seq in enumerate(isa.ASM_FUSED):
+            g.label(f"Lf{k}_%=")
+            for j, n in enumerate(seq):
+                if j:
+                    g.consume()
+                handlers[n](g)
             g.next()
             g.flush_tail()
     g.label("Lunsup_%=")
@@ -1219,7 +1236,16 @@ def render_interp() -> str:
            f"#define MW_ASM_NOPS {len(ASM_OPCODES)}",
            f"#define MW_ASM_MAX_DIV {isa.ASM_MAX_DIV}u",
            "#define MW_ASM_OPCODES " + ", ".join(f"MW_{n}" for n in ASM_OPCODES),
-           "#define MW_ASM_LEAF_KINDS " + ", ".join(str(k) for k in ASM_LEAF_KINDS)]
+           "#define MW_ASM_LEAF_KINDS " + ", ".join(str(k) for k in ASM_LEAF_KINDS),
+           # fused handlers (isa.ASM_FUSED, mw_asm_predecode): opcode sequences
+           # padded with 0xff to MW_ASM_FUSED_MAX; their offsets follow the
+           # 128 opcodes' in the introspection table
+           f"#define MW_ASM_NFUSED {len(isa.ASM_FUSED)}",
+           f"#define MW_ASM_FUSED_MAX {isa.ASM_FUSED_MAX}",
+           f"#define MW_ASM_NHANDLERS ({NTAB} + MW_ASM_NFUSED)",
+           "#define MW_ASM_FUSED_SEQS " + ", ".join(
+               "{" + ", ".join([f"MW_{n}" for n in t] + ["0xffu"] * (isa.ASM_FUSED_MAX - len(t))) + "}"
+               for t in isa.ASM_FUSED)]
     out += _inc(gen("interp"), "MW_ASM_BODY")
     out += _inc(gen("template"), "MW_ASMJIT_TEMPLATE_BODY")
     out.append(f"#define MW_ASM_CLOBBERS {CLOBBERS}")

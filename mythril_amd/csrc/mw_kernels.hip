@@ -733,20 +733,20 @@ bool asm_enabled() {
 // asm-eligible (the compiled interpreter runs them: same results).
 std::mutex g_hoff_mu;
 bool g_hoff_ready = false;
-u32 g_hoff[128];
+u32 g_hoff[MW_ASM_NHANDLERS];   // 128 opcodes, then the fused handlers (mw_asm_interp.inc)
 
 int asm_handler_offsets(int dev, hipStream_t stream) {
   std::lock_guard<std::mutex> lk(g_hoff_mu);
   if (g_hoff_ready) return 0;
   HIPCHK(hipSetDevice(dev));
   void* buf = nullptr;
-  const size_t bytes = sizeof(ProgDev) + sizeof(AsmArgs) + 128 * sizeof(u32) + 2 * sizeof(u64);
+  const size_t bytes = sizeof(ProgDev) + sizeof(AsmArgs) + MW_ASM_NHANDLERS * sizeof(u32) + 2 * sizeof(u64);
   HIPCHK(hipMalloc(&buf, bytes));
   char* b = (char*)buf;
   ProgDev* dp = (ProgDev*)b;
   AsmArgs* da = (AsmArgs*)(b + sizeof(ProgDev));
   u32* dout = (u32*)(b + sizeof(ProgDev) + sizeof(AsmArgs));
-  u64* dmin = (u64*)(dout + 128);
+  u64* dmin = (u64*)(dout + MW_ASM_NHANDLERS);
   ProgDev hp{};
   AsmArgs ha{};
   ha.flags = 1u << 7;
@@ -759,12 +759,12 @@ int asm_handler_offsets(int dev, hipStream_t stream) {
                        (const AsmArgs*)da, dmin, dmin + 1, 0u);
     e = hipGetLastError();
   }
-  u32 h[128];
+  u32 h[MW_ASM_NHANDLERS];
   if (e == hipSuccess) e = hipMemcpyAsync(h, dout, sizeof h, hipMemcpyDeviceToHost, stream);
   if (e == hipSuccess) e = hipStreamSynchronize(stream);
   hipFree(buf);
   if (e != hipSuccess) return fail(MG_E_HIP, std::string("asm handler offsets: ") + hipGetErrorString(e));
-  for (int k = 0; k < 128; ++k) {
+  for (int k = 0; k < MW_ASM_NHANDLERS; ++k) {
     if (h[k] == 0 || h[k] > 0x7fffu) return fail(MG_E_HIP, "asm handler offsets out of range");
     g_hoff[k] = h[k];
   }

@@ -9,6 +9,7 @@
 #include <string>
 
 #include "../../include/mythril_witness.h"
+#include "mw_asm_interp.inc"   // MW_ASM_NFUSED / MW_ASM_FUSED_SEQS (macros only here)
 #include "mw_isa.h"
 #include "mw_prog.h"
 
@@ -202,7 +203,7 @@ int mg_validate_desc(const mg_prog_desc* d) {
 // W_CDINS byte index (always a constant) below 0x4000, which becomes
 // 0x4000 | index (the handler then compares it with one 32-bit summary of the
 // size instead of a signed 256-bit subtraction).
-// hoff: the asm interpreter's handler word offsets per opcode (128 entries,
+// hoff: the asm interpreter's handler word offsets per opcode (128 entries, then the fused handlers',
 // reported by the kernel itself, mw_kernels.hip asm_handler_offsets); word 0
 // becomes width [31:16] | FLAG_CHAIN [15] | handler offset [14:0], so the
 // dispatch is one jump (mythril_amd/asmgen.py Gen.next).
@@ -216,6 +217,12 @@ int mg_validate_desc(const mg_prog_desc* d) {
 // interpreter; the corpora have at most 3).
 // Width masks: N_ADD / N_SUB / N_MUL / N_NOT, which have no immediate, get
 // their result mask (width < 32 ? 2^width - 1 : ~0) in word 3.
+// Fused handlers: hoff has MW_ASM_NHANDLERS entries, the fused sequences'
+// (MW_ASM_FUSED_SEQS, mythril_amd/isa.py ASM_FUSED) after the opcodes'.
+// Scanning left to right, the first instruction of every match (longest
+// sequence first, list order among equal lengths) gets its sequence's handler:
+// one dispatch runs the whole sequence, which takes the instructions after
+// the first itself (their own words are left as they are).
 int mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t nconst, const u32* hoff,
                      u32* out, u32* nk) {
   u32 nnk = 0;
@@ -257,6 +264,29 @@ int mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t n
     O[3] = I[3];
     if (op == MW_N_ADD || op == MW_N_SUB || op == MW_N_MUL || op == MW_N_NOT)
       O[3] = w >= 32u ? 0xffffffffu : (1u << w) - 1u;
+  }
+  static const u32 seqs[MW_ASM_NFUSED][MW_ASM_FUSED_MAX] = {MW_ASM_FUSED_SEQS};
+  const size_t n = nwords / 4;
+  for (size_t i = 0; i < n;) {
+    int best = -1;
+    size_t blen = 0;
+    for (int k = 0; k < MW_ASM_NFUSED; ++k) {
+      size_t len = 0;
+      while (len < MW_ASM_FUSED_MAX && seqs[k][len] != 0xffu) ++len;
+      if (len <= blen || i + len > n) continue;
+      bool ok = true;
+      for (size_t j = 0; j < len && ok; ++j) ok = (code[(i + j) * 4] & 0xffu) == seqs[k][j];
+      if (ok) {
+        best = k;
+        blen = len;
+      }
+    }
+    if (best < 0) {
+      ++i;
+      continue;
+    }
+    out[i * 4] = (out[i * 4] & ~0x7fffu) | (hoff[128 + best] & 0x7fffu);
+    i += blen;
   }
   return 0;
 }

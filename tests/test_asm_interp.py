@@ -30,7 +30,9 @@ def test_opcode_lists_agree():
     # reports an offset for all 128 opcodes (handler or Lunsup)
     for o in isa.ASM_OPCODES:
         assert f"Lh_{o}_%=:" in txt, o
-    assert txt.count("- Lpc0_%=) >> 2)") == 128
+    assert txt.count("- Lpc0_%=) >> 2)") == 128 + len(isa.ASM_FUSED)   # and every fused handler's
+    for k in range(len(isa.ASM_FUSED)):
+        assert f"Lf{k}_%=:" in txt
     assert "s_branch Lh_" not in txt          # one jump per dispatch: no table of branches
 
 
@@ -75,8 +77,9 @@ def _predecode(code, consts):
     return (out.reshape(-1, 4), nk) if rc == 0 else (None, None)
 
 
-# stand-in handler word offsets (the kernel reports the real ones at mg_init)
-HOFF = __import__("numpy").arange(1000, 1000 + 128 * 7, 7, dtype="uint32")
+# stand-in handler word offsets (the kernel reports the real ones at mg_init):
+# the 128 opcodes', then the fused handlers'
+HOFF = __import__("numpy").arange(1000, 1000 + (128 + len(isa.ASM_FUSED)) * 7, 7, dtype="uint32")
 
 
 def test_predecode_operand_layout():
@@ -130,3 +133,29 @@ def test_predecode_narrow_constant_bound():
     assert not isa.asm_eligible(code, leaves, consts)
     assert isa.asm_eligible(code[:-8 * 4] + e("END", 0, isa.encode_dst(None)), leaves, consts)
     assert len(isa.asm_narrow_constants(code, consts)) == n
+
+
+def test_predecode_fused_sequences():
+    """The first instruction of every fused-sequence match (left to right,
+    longest first) jumps to that sequence's handler (offset entry 128 + k);
+    the rest of the match keeps its own words, and the match agrees with
+    isa.asm_fused_dispatch."""
+    import numpy as np
+    e = isa.encode
+    N = lambda k: isa.encode_dst("N", k)   # noqa: E731
+    code = (e("N_SLT", 1, N(1), 2, 3) + e("LEAF_N", 8, N(4), imm=0) + e("N_ITE", 8, N(5), 4, 6, 1)
+            + e("N_SHLI", 32, N(6), 5, imm=8)                                  # the 4-op calldata byte
+            + e("N_SLT", 1, N(1), 2, 3) + e("LEAF_N", 8, N(4), imm=1) + e("N_ITE", 8, N(5), 4, 6, 1)
+            + e("N_ADD", 8, N(7), 1, 2)                                        # 3-op prefix, then none
+            + e("N_XOR", 1, N(8), 1, 2) + e("CHECK", 0, isa.encode_dst(None), 8)
+            + e("END", 0, isa.encode_dst(None)))
+    o, _ = _predecode(code, [0])
+    src = np.asarray(code, dtype="uint32").reshape(-1, 4)
+    plain = (src[:, 0] & 0xFFFF0000) | HOFF[src[:, 0] & 0x7F]
+    fused = {i: k for i, k in isa.asm_fused_dispatch(code) if k is not None}
+    seq = lambda *t: isa.ASM_FUSED.index(tuple(t))   # noqa: E731
+    assert fused == {0: seq("N_SLT", "LEAF_N", "N_ITE", "N_SHLI"), 4: seq("N_SLT", "LEAF_N", "N_ITE"),
+                     8: seq("N_XOR", "CHECK")}
+    for i in range(len(src)):
+        want = (plain[i] & 0xFFFF8000) | HOFF[128 + fused[i]] if i in fused else plain[i]
+        assert o[i, 0] == want, i
