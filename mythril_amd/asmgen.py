@@ -93,6 +93,11 @@ ARGP = 36         # s[36:37] AsmArgs (prologue only; then VALID)
 PROGP = 38        # s[38:39] ProgDev (prologue only)
 HIT = 38          # after the prologue: this wave has reported a witness (chunks only grow)
 TID, LO_SREG = 165, 0
+# the pool digit of the last pooled leaf drawn in this chunk (Lleaf) and its
+# digit group (the asm leaf table's word 6, mw_kernels.hip asm_leaf_table;
+# reset to -1 at every chunk)
+DIGV = 166
+DIGKEY = 39
 
 NTAB = 128
 CHAIN_BIT = 15     # predecoded word 0: W_CDINS's FLAG_CHAIN (mw_asm_predecode)
@@ -981,7 +986,8 @@ def gen(mode="interp"):
       f"s_cmp_eq_u32 {s(SX + 1)}, {s(BASE + 1)}", "s_cbranch_scc0 Lnostop_%=",
       f"s_cmp_le_u32 {s(SX)}, {s(BASE)}", "s_cbranch_scc1 Lexit_%=")
     g.label("Lnostop_%=")
-    g(f"v_mov_b32_e32 {v(T + 7)}, {s(BASE + 1)}",
+    g(f"s_mov_b32 {s(DIGKEY)}, -1",
+      f"v_mov_b32_e32 {v(T + 7)}, {s(BASE + 1)}",
       f"v_add_co_u32_e32 {v(CLO)}, vcc, {s(BASE)}, {v(TID)}", "s_nop 1",
       f"v_addc_co_u32_e32 {v(CHI)}, vcc, 0, {v(T + 7)}, vcc",
       f"v_cmp_gt_u64_e32 vcc, {sr(END, 2)}, {vr(CLO, 2)}", "s_nop 1",
@@ -1073,6 +1079,10 @@ def leaf(g):
     g.label("Lleaf_%=")
     g(f"s_lshl_b32 {s(S[7])}, {s(S67)}, 5", f"s_load_dwordx8 {sr(D, 8)}, {sr(LEAVES, 2)}, {s(S[7])}",
       "s_waitcnt lgkmcnt(0)",
+      # the same digit as the last pooled leaf drawn (the bytes of one calldata
+      # word): reuse it (word 6: the digit group; distinct per leaf in the
+      # assembled kernels' table, where it is the input row)
+      f"s_cmp_eq_u32 {s(D + 6)}, {s(DIGKEY)}", "s_cbranch_scc1 Ldig_hit_%=",
       # kind 3 first: the bit-interleaved digits of every pooled leaf that fits the 40 index bits
       f"s_cmp_eq_u32 {s(D + 1)}, 3", "s_cbranch_scc1 Lk3_%=",
       f"s_cmp_eq_u32 {s(D + 1)}, 1", "s_cbranch_scc1 Lk1_%=",
@@ -1118,6 +1128,10 @@ def leaf(g):
     # pool entry in LDS at poolb + 4 * poff: width >= 32: 9 words (flag, 8 limbs)
     # at + 36 * digit; width < 32: one word (bit 31 RANDOM, else the value) at + 4 * digit
     g.label("Lgather_%=")
+    g(f"v_mov_b32_e32 {v(DIGV)}, {v(T + 6)}", f"s_mov_b32 {s(DIGKEY)}, {s(D + 6)}", "s_branch Lgather2_%=")
+    g.label("Ldig_hit_%=")
+    g(f"v_mov_b32_e32 {v(T + 6)}, {v(DIGV)}")
+    g.label("Lgather2_%=")
     g(f"s_lshl_b32 {s(S[6])}, {s(D + 5)}, 2", f"s_add_u32 {s(S[6])}, {s(S[6])}, {s(POOLB)}",
       f"s_cmp_lt_u32 {s(D)}, 32", "s_cbranch_scc1 Lg_narrow_%=",
       f"v_mov_b32_e32 {v(T + 5)}, 36", f"v_mad_u32_u24 {v(T + 5)}, {v(T + 6)}, {v(T + 5)}, {s(S[6])}",

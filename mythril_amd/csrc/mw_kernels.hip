@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -396,7 +397,8 @@ struct Prog {
   u64 ops_per_eval = 0;
   u64 sig = 0;                  // FNV-1a 64 of the program words (mythril_amd/jit.py signature)
   bool asm_ok = false;          // every opcode and leaf kind has a handler in mw_search_asm_kernel
-  ProgDev adev{};               // dev with code = its predecoded copy (mw_asm_predecode), in d_buf
+  ProgDev adev{};               // dev with code = its predecoded copy (mw_asm_predecode) and leaves =
+                                // the asm leaf table (asm_leaf_table), in d_buf
   // specialised kernels (mg_prog_attach_kernel): one per part, launched in order
   struct Part {
     hipModule_t mod = nullptr;
@@ -777,6 +779,29 @@ bool asm_offsets_ready() {
   return g_hoff_ready;
 }
 
+// The asm engines' copy of the leaf table: word 6 (the input row, which only
+// the compiled interpreter's mg_eval reads) becomes the leaf's digit group,
+// the index of the first leaf whose pool digit is the same function of the
+// candidate (kind, shift, bits, stride, and the hash key for hashed digits):
+// the Lleaf subroutine (mythril_amd/asmgen.py leaf) reuses the digit of the
+// last pooled leaf it drew when the group matches, as the bytes of one
+// calldata word do (LeafSpec.tie).  Leaves without a pool digit: 0xfffffffe.
+void asm_leaf_table(const u32* leaves, size_t n, u32* out) {
+  std::map<std::array<u32, 5>, u32> first;
+  for (size_t i = 0; i < n; ++i) {
+    const u32* L = leaves + i * MW_LEAF_WORDS;
+    u32* O = out + i * MW_LEAF_WORDS;
+    std::memcpy(O, L, MW_LEAF_WORDS * sizeof(u32));
+    const u32 kind = L[1];
+    if (kind < 1 || kind > 3) {
+      O[6] = 0xfffffffeu;
+      continue;
+    }
+    const std::array<u32, 5> key = {kind, L[3], L[4], L[7], kind == 2 ? L[2] : 0u};
+    O[6] = first.emplace(key, (u32)i).first->second;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -852,8 +877,8 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
                np = d->npool_words + 8;
   bool asm_ok = asm_offsets_ready() && asm_eligible(d);
   // predecoded copy + the block after END the dispatch prefetches + the narrow
-  // constants the kernel loads into VGPRs (MW_ASM_NK words)
-  const size_t na = asm_ok ? nc + 8 + MW_ASM_NK : 0;
+  // constants the kernel loads into VGPRs (MW_ASM_NK words) + the asm leaf table
+  const size_t na = asm_ok ? nc + 8 + MW_ASM_NK + nl : 0;
   const size_t total = nc + nk + nl + np + na;
   auto p = std::make_shared<Prog>();
   p->ctx = cref;
@@ -871,6 +896,7 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
     u32* pre = hbuf.data() + nc + nk + nl + np;
     // more distinct narrow constants than MW_ASM_NK: the compiled interpreter runs it
     asm_ok = mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, g_hoff, pre, pre + nc + 8) == 0;
+    if (asm_ok) asm_leaf_table(d->leaves, d->nleaves, pre + nc + 8 + MW_ASM_NK);
   }
   if (hipMemcpy(p->d_buf, hbuf.data(), total * 4, hipMemcpyHostToDevice) != hipSuccess) {
     release_prog(*p);
@@ -885,7 +911,10 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   p->dev.n_insn = (u32)(nc / 4);
   p->asm_ok = asm_ok;
   p->adev = p->dev;
-  if (asm_ok) p->adev.code = p->d_buf + nc + nk + nl + np;
+  if (asm_ok) {
+    p->adev.code = p->d_buf + nc + nk + nl + np;
+    p->adev.leaves = p->adev.code + nc + 8 + MW_ASM_NK;
+  }
   // the desc's host pointers are not retained
   p->desc.code = nullptr;
   p->desc.consts = nullptr;
