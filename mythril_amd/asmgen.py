@@ -127,6 +127,8 @@ def sr(a, n):
 
 
 class Gen:
+    inline_leaf = True   # W_CDINS inlines the Lleaf code (leaf_inline) instead of calling it
+
     def __init__(self):
         self.lines = []
         self.tail = []      # out-of-line blocks (constant operands), emitted after the handler
@@ -199,6 +201,29 @@ class Gen:
              f"s_load_dwordx8 {sr(DESC, 8)}, {sr(CPOOL, 2)}, {s(SX)}", "s_waitcnt lgkmcnt(0)"]
         t += [f"v_mov_b32_e32 {v(dst + k)}, {s(DESC + k)}" for k in range(8)]
         self.tail += t + [f"s_branch {lr}"]
+
+    def w_indexed(self, f, mode, emit, scratch=XA):
+        """emit(base): an operation reading the W operand bound to f as VGPRs
+        base..base+7 - a register straight from the W file through the index
+        (gpr_idx(mode): the emitted instructions read it as that operand, and
+        no move copies it out first), a constant from `scratch` after its
+        load (out of line)"""
+        which = self.bound[f]
+        lk, lr = self.L("kx"), self.L("rx")
+        self._is_const(which, lk)
+        self(f"s_set_gpr_idx_on {self._index(which)}, gpr_idx({mode})")
+        emit(W0)
+        self("s_set_gpr_idx_off")
+        self.label(lr)
+        wd, half = self.WORD[which]
+        main, self.lines = self.lines, [f"{lk}:", f"s_bfe_u32 {s(SX)}, {s(wd)}, {(15 << 16) | (16 if half == 'hi' else 0):#x}",
+                                        f"s_lshl_b32 {s(SX)}, {s(SX)}, 2",
+                                        f"s_load_dwordx8 {sr(DESC, 8)}, {sr(CPOOL, 2)}, {s(SX)}", "s_waitcnt lgkmcnt(0)"]
+        self(*[f"v_mov_b32_e32 {v(scratch + k)}, {s(DESC + k)}" for k in range(8)])
+        emit(scratch)
+        self(f"s_branch {lr}")
+        self.tail += self.lines
+        self.lines = main
 
     def width(self, dst):
         self(f"s_lshr_b32 {s(dst)}, {s(CUR)}, 16")
@@ -481,11 +506,16 @@ def build_handlers():
         update_alive(g)
 
     # -------------------------------------------------------- wide -> narrow
+    # N_EQ / N_ULT / N_ULE read operand a (N_ULE: b) as the VALU source
+    # itself (Gen.w_indexed): no eight-move copy out of the W file
     @handler("N_EQ")
     def _(g):
         g.field("a", S[0]), g.field("b", S[1])
-        g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
-        eq8(g, XA, XB, XC)
+        g.fetch_w(S[1], XB)
+        g.w_indexed(S[0], "SRC0", lambda base: g(*[f"v_xor_b32_e32 {v(T + k)}, {v(base + k)}, {v(XB + k)}"
+                                                   for k in range(8)]))
+        g(f"v_or3_b32 {v(T)}, {v(T)}, {v(T + 1)}, {v(T + 2)}", f"v_or3_b32 {v(T + 3)}, {v(T + 3)}, {v(T + 4)}, {v(T + 5)}",
+          f"v_or3_b32 {v(XC)}, {v(T + 6)}, {v(T + 7)}, {v(T)}", f"v_or_b32_e32 {v(XC)}, {v(XC)}, {v(T + 3)}")
         g(f"v_cmp_eq_u32_e32 vcc, 0, {v(XC)}")
         g.bool_from_vcc(XR)
         g.write_n(XR)
@@ -493,16 +523,16 @@ def build_handlers():
     @handler("N_ULT")
     def _(g):
         g.field("a", S[0]), g.field("b", S[1])
-        g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
-        g.sub_chain(XA, XB)
+        g.fetch_w(S[1], XB)
+        g.w_indexed(S[0], "SRC0", lambda base: g.sub_chain(base, XB))
         g.bool_from_vcc(XR)
         g.write_n(XR)
 
     @handler("N_ULE")
     def _(g):
         g.field("a", S[0]), g.field("b", S[1])
-        g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
-        g.sub_chain(XB, XA)                     # b < a  ->  not (a <= b)
+        g.fetch_w(S[0], XA)
+        g.w_indexed(S[1], "SRC0", lambda base: g.sub_chain(base, XA), scratch=XB)   # b < a  ->  not (a <= b)
         g.bool_from_vcc(XR, invert=True)
         g.write_n(XR)
 
@@ -788,7 +818,11 @@ def build_handlers():
         nos = g.L("cdns")
         g("s_nop 1", f"s_cmp_eq_u64 {sr(MSK2, 2)}, 0", f"s_cbranch_scc1 {nos}")
         g(f"s_and_b32 {s(S[3])}, {s(CUR + 3)}, 0xffff")
-        call_leaf(g, S[3])
+        if g.inline_leaf:   # no call / return jumps on the hottest leaf path (C2: 64 of 86 instructions)
+            g(f"s_mov_b32 {s(S67)}, {s(S[3])}")
+            g(*leaf_inline(g.L("il")[1:-3], limb0=True))
+        else:
+            call_leaf(g, S[3])
         # t = in range ? byte : 0, inserted at bit off = imm >> 16 (limb off >> 5)
         g(f"v_cndmask_b32_e64 {v(T)}, 0, {v(XC)}, {sr(MSK2, 2)}",
           f"s_lshr_b32 {s(S[4])}, {s(CUR + 3)}, 16",
@@ -1070,11 +1104,12 @@ def gen(mode="interp"):
     return body
 
 
-def leaf(g):
+def leaf(g, limb0=False):
     """Lleaf: XC = value of leaf S67 for this lane's candidate (mw_leaf.h
     leaf_value with the pool in LDS: kinds 0 random, 1 bit-field digit,
     2 hashed digit, 3 bit-interleaved digit; a pool entry flagged RANDOM draws
-    Philox)."""
+    Philox).  limb0: a narrow leaf leaves XC+1..XC+7 as they are (a caller
+    that reads XC alone: W_CDINS's byte)."""
     D = DESC   # s80 w, s81 kind, s82 id, s83 shift, s84 bits, s85 poff, s86 inrow, s87 stride
     g.label("Lleaf_%=")
     g(f"s_lshl_b32 {s(S[7])}, {s(S67)}, 5", f"s_load_dwordx8 {sr(D, 8)}, {sr(LEAVES, 2)}, {s(S[7])}",
@@ -1092,7 +1127,7 @@ def leaf(g):
       # w < 32: the draw's low word masked to w bits is the canonical value
       f"s_cmp_lt_u32 {s(D)}, 32", "s_cbranch_scc0 Lk0_wide_%=",
       f"s_bfm_b64 {sr(S[6], 2)}, {s(D)}, 0", f"v_and_b32_e32 {v(XC)}, {s(S[6])}, {v(T)}")
-    for k in range(1, 8):
+    for k in range(1, 1 if limb0 else 8):
         g(f"v_mov_b32_e32 {v(XC + k)}, 0")
     g(f"s_setpc_b64 {sr(LRET, 2)}")
     g.label("Lk0_wide_%=")
@@ -1144,7 +1179,7 @@ def leaf(g):
     # masked to w bits (no 8-limb select, no generic canonicalisation)
     g.label("Lg_narrow_%=")
     g(f"v_lshl_add_u32 {v(T + 5)}, {v(T + 6)}, 2, {s(S[6])}", f"ds_read_b32 {v(XC)}, {v(T + 5)}")
-    for k in range(1, 8):
+    for k in range(1, 1 if limb0 else 8):
         g(f"v_mov_b32_e32 {v(XC + k)}, 0")
     g("s_waitcnt lgkmcnt(0)", f"v_lshrrev_b32_e32 {v(T + 4)}, 31, {v(XC)}",
       f"v_cmp_ne_u32_e32 vcc, 0, {v(T + 4)}", "s_nop 1", "s_cmp_eq_u64 vcc, 0", "s_cbranch_scc1 Lleaf_ret_%=",
@@ -1162,6 +1197,22 @@ def leaf(g):
     g.label("Lleaf_canon_%=")
     g.canon(XC, D)
     g(f"s_setpc_b64 {sr(LRET, 2)}")
+
+
+def leaf_inline(tag, limb0=False):
+    """The Lleaf subroutine's code for one call site: its labels prefixed with
+    tag, its returns a branch to the end (the Philox subroutine is still
+    called)"""
+    sub = Gen()
+    leaf(sub, limb0)
+    defined = [ln[:-1] for ln in sub.lines if ln.endswith(":")]
+    done = f"L{tag}ret_%="
+    out = []
+    for ln in sub.lines:
+        for lab in defined:   # "_%=" ends every label: no label is a prefix of another's text
+            ln = ln.replace(lab, f"L{tag}{lab[1:]}")
+        out.append(ln.replace(f"s_setpc_b64 {sr(LRET, 2)}", f"s_branch {done}"))
+    return out + [done + ":"]
 
 
 def fmix64(g, lo, hi, t1, t2):
@@ -1284,6 +1335,7 @@ def _lit(x: int) -> str:
 
 class StaticGen(Gen):
     """Gen for one program whose fields are known at generation time."""
+    inline_leaf = False   # the body calls the template's Lleaf through LEAFADDR
 
     def __init__(self, consts, leaves=None, pool=None):
         super().__init__()
@@ -1325,6 +1377,14 @@ class StaticGen(Gen):
         else:
             for k in range(8):
                 self(f"v_mov_b32_e32 {v(dst + k)}, {v(W0 + 8 * val + k)}")
+
+    def w_indexed(self, f, mode, emit, scratch=XA):
+        val = self._field(f)
+        if val & KBIT:
+            self.fetch_w(f, scratch)
+            emit(scratch)
+        else:
+            emit(W0 + 8 * val)
 
     def _dst(self):
         w, n = isa.decode_dst(self.cur["dst"])
