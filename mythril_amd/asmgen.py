@@ -1258,21 +1258,27 @@ def philox_sub(g):
         base = T + 4 * blk
         if blk == 1:
             g(f"s_cmp_le_u32 {s(D)}, 128", "s_cbranch_scc1 Lphx_done_%=")
-        # counter (c0, c1, c2, c3) = (cand_lo, cand_hi, blk, 0) in base..base+3; temporaries XB..XB+3
+        # counter (c0, c1, c2, c3) = (cand_lo, cand_hi, blk, 0) in base..base+3; temporaries XB..XB+7
         c = [base, base + 1, base + 2, base + 3]
         g(f"v_mov_b32_e32 {v(c[0])}, {v(CLO)}", f"v_mov_b32_e32 {v(c[1])}, {v(CHI)}",
           f"v_mov_b32_e32 {v(c[2])}, {blk}", f"v_mov_b32_e32 {v(c[3])}, 0",
           f"s_xor_b32 {s(PK0)}, {s(SEED)}, {s(D + 2)}", f"s_mov_b32 {s(PK1)}, {s(SEED + 1)}")
+        cur = list(c)   # the registers holding c0..c3 this round
         for r in range(10):
-            # one v_mad_u64_u32 per product (hi:lo in an aligned pair), not a mul_hi + mul_lo
-            lo0, hi0, lo1, hi1 = XB, XB + 1, XB + 2, XB + 3
-            g(f"v_mad_u64_u32 {vr(lo0, 2)}, {sr(SX, 2)}, {v(c[0])}, {s(PM0)}, 0",
-              f"v_mad_u64_u32 {vr(lo1, 2)}, {sr(SX, 2)}, {v(c[2])}, {s(PM1)}, 0",
+            # one v_mad_u64_u32 per product (hi:lo in an aligned pair), not a
+            # mul_hi + mul_lo; the products alternate between XB..XB+3 and
+            # XB+4..XB+7 so the new c1 / c3 (the products' low words) are
+            # renamed instead of moved (two moves per block, not per round)
+            pb = XB + 4 * (r & 1)
+            lo0, hi0, lo1, hi1 = pb, pb + 1, pb + 2, pb + 3
+            g(f"v_mad_u64_u32 {vr(lo0, 2)}, {sr(SX, 2)}, {v(cur[0])}, {s(PM0)}, 0",
+              f"v_mad_u64_u32 {vr(lo1, 2)}, {sr(SX, 2)}, {v(cur[2])}, {s(PM1)}, 0",
               # n0 = hi1 ^ c1 ^ k0 ; n2 = hi0 ^ c3 ^ k1 ; c = (n0, lo1, n2, lo0)
-              f"v_xor_b32_e32 {v(c[0])}, {s(PK0)}, {v(hi1)}", f"v_xor_b32_e32 {v(c[0])}, {v(c[0])}, {v(c[1])}",
-              f"v_xor_b32_e32 {v(c[2])}, {s(PK1)}, {v(hi0)}", f"v_xor_b32_e32 {v(c[2])}, {v(c[2])}, {v(c[3])}",
-              f"v_mov_b32_e32 {v(c[1])}, {v(lo1)}", f"v_mov_b32_e32 {v(c[3])}, {v(lo0)}",
+              f"v_xor_b32_e32 {v(cur[0])}, {s(PK0)}, {v(hi1)}", f"v_xor_b32_e32 {v(cur[0])}, {v(cur[0])}, {v(cur[1])}",
+              f"v_xor_b32_e32 {v(cur[2])}, {s(PK1)}, {v(hi0)}", f"v_xor_b32_e32 {v(cur[2])}, {v(cur[2])}, {v(cur[3])}",
               f"s_add_u32 {s(PK0)}, {s(PK0)}, 0x9E3779B9", f"s_add_u32 {s(PK1)}, {s(PK1)}, 0xBB67AE85")
+            cur[1], cur[3] = lo1, lo0
+        g(f"v_mov_b32_e32 {v(c[1])}, {v(cur[1])}", f"v_mov_b32_e32 {v(c[3])}, {v(cur[3])}")
     g.label("Lphx_done_%=")
     g(f"s_setpc_b64 {sr(PRET, 2)}")
 
