@@ -428,13 +428,45 @@ def cpu_baseline(syn, prog, budget_s, dev, dp):
             if r["verdict_mismatches_vs_gpu"]:
                 print(f"[bench] PARITY FAILURE: {r['verdict_mismatches_vs_gpu']} of {len(v)} CPU verdicts "
                       f"({r['sample'][:40]}...) differ from the GPU's", file=sys.stderr)
+    win = witness_window(syn, prog, dev, dp)
     if rec is None:
+        orc["witness_window"] = win
         return orc
     if vo is not None:
         k = min(len(vo), len(vf))
         orc["verdict_mismatches_vs_host_build"] = int(np.count_nonzero(vo[:k] != vf[:k]))
     rec["checker"] = orc
+    rec["witness_window"] = win
     return rec
+
+
+def witness_window(syn, prog, dev, dp, half=1 << 12):
+    """Mixed-verdict parity at full size (the timed samples above hold no
+    satisfying index): the 2*half candidates around the planted witness, each
+    verdict from the GPU, the host build and the C oracle, compared."""
+    import numpy as np
+    from oracle import cdag
+    from mythril_amd import host_baseline
+    b, n = max(0, syn.witness_index - half), 2 * half
+    vg, _ = dev.eval_generated(dp, syn.seed, b, n, trace=False)
+    vg = vg.astype(np.uint8)
+    out = {"begin": b, "count": n, "satisfied_gpu": int(vg.sum())}
+    legs = []
+    if host_baseline.available():
+        f = host_baseline.specialised(prog)
+        _, vh = (host_baseline.count_specialised(f, prog, syn.seed, b, n) if f is not None
+                 else host_baseline.count(prog, syn.seed, b, n, verdicts=True))
+        legs.append(("host_build", vh))
+    if cdag.available():
+        _, _, vo = cdag.evaluate(syn.conjuncts, syn.seed, b, n, want_verdict=True)
+        legs.append(("oracle", vo))
+    for name, v in legs:
+        out[f"satisfied_{name}"] = int(v.sum())
+        out[f"mismatches_{name}_vs_gpu"] = int(np.count_nonzero(v.astype(np.uint8) != vg))
+        if out[f"mismatches_{name}_vs_gpu"]:
+            print(f"[bench] PARITY FAILURE: {out[f'mismatches_{name}_vs_gpu']} of {n} verdicts around the "
+                  f"planted witness differ ({name} vs GPU)", file=sys.stderr)
+    return out
 
 if __name__ == "__main__":
     main()
