@@ -13,9 +13,11 @@ argument, traced - compiled on first use.
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 import gc
 import logging
+import sys
 import threading
 import time
 from dataclasses import dataclass, field
@@ -154,7 +156,36 @@ def _build_witness_program(q: "Query") -> None:
 PREBUILD_MAX_TERMS = 512
 
 
-def _prebuild_witness_programs(queries) -> None:
+# How soon a search call returning from the device gets the GIL back from the
+# witness-program thread (sys.setswitchinterval, normally 5 ms): the thread
+# holds it through the Python part of a compile, and the caller would wait
+# for its forced switch.  Applied only while a search with queued compiles is
+# in flight (_gil_handoff), then restored.
+SEARCH_SWITCH_INTERVAL = 1e-4
+_HANDOFF = [0, None]              # searches in flight, the interval to restore
+_HANDOFF_LOCK = threading.Lock()
+
+
+@contextlib.contextmanager
+def _gil_handoff(active: bool):
+    if not active:
+        yield
+        return
+    with _HANDOFF_LOCK:
+        if _HANDOFF[0] == 0:
+            _HANDOFF[1] = sys.getswitchinterval()
+            sys.setswitchinterval(min(_HANDOFF[1], SEARCH_SWITCH_INTERVAL))
+        _HANDOFF[0] += 1
+    try:
+        yield
+    finally:
+        with _HANDOFF_LOCK:
+            _HANDOFF[0] -= 1
+            if _HANDOFF[0] == 0:
+                sys.setswitchinterval(_HANDOFF[1])
+
+
+def _prebuild_witness_programs(queries) -> bool:
     """Queue the witness programs a search may need on a host thread, which
     compiles them while the device searches (the search call releases the
     GIL): those of queries whose cells have a non-constant index (the rest
@@ -165,7 +196,7 @@ def _prebuild_witness_programs(queries) -> None:
     todo = [q for q in queries if q._trace is None and q._trace_future is None
             and len(q.arg_terms) <= PREBUILD_MAX_TERMS and not all(t.op == "const" for t in q.arg_terms)]
     if not todo:
-        return
+        return False
     global _PREBUILD
     if _PREBUILD is None:
         with _PREBUILD_LOCK:
@@ -174,6 +205,7 @@ def _prebuild_witness_programs(queries) -> None:
                 _PREBUILD = ThreadPoolExecutor(max_workers=1, thread_name_prefix="mw-witness-program")
     for q in todo:
         q._trace_future = _PREBUILD.submit(_build_witness_program, q)
+    return True
 
 
 def _witness_program(prog: Program, traced: List[Node]) -> Program:
@@ -230,8 +262,8 @@ class WitnessEngine:
             # the witness programs compile on a host thread while the device
             # searches (the search call releases the GIL): a witness then costs
             # one upload and one launch (materialize)
-            _prebuild_witness_programs(queries)
-            found, st = self.dev.search(dps, self.seed, begin, count, flags)
+            with _gil_handoff(_prebuild_witness_programs(queries)):
+                found, st = self.dev.search(dps, self.seed, begin, count, flags)
             self.stats["searches"] += 1
             self.stats["programs"] += len(queries)
             self.stats["evals"] += st["evals"]
