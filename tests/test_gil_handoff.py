@@ -1,22 +1,32 @@
 """engine._gil_handoff: the switch interval is short only while a search with
 queued witness-program compiles is in flight, and restored after the last of
 overlapping searches (threads of MultiDevice) ends."""
+import math
 import sys
 import threading
 
 from mythril_amd import engine
 
 
+def _short(before):
+    """the interval inside a handoff (the interpreter stores it in microseconds)"""
+    return math.isclose(sys.getswitchinterval(), min(before, engine.SEARCH_SWITCH_INTERVAL), rel_tol=1e-6)
+
+
+def _is(x):
+    return math.isclose(sys.getswitchinterval(), x, rel_tol=1e-6)
+
+
 def test_interval_short_inside_and_restored():
     before = sys.getswitchinterval()
     with engine._gil_handoff(False):
-        assert sys.getswitchinterval() == before
+        assert _is(before)
     with engine._gil_handoff(True):
-        assert sys.getswitchinterval() == min(before, engine.SEARCH_SWITCH_INTERVAL)
+        assert _short(before)
         with engine._gil_handoff(True):
-            assert sys.getswitchinterval() == min(before, engine.SEARCH_SWITCH_INTERVAL)
-        assert sys.getswitchinterval() == min(before, engine.SEARCH_SWITCH_INTERVAL)
-    assert sys.getswitchinterval() == before
+            assert _short(before)
+        assert _short(before)
+    assert _is(before)
 
 
 def test_overlapping_threads_restore_once():
@@ -32,9 +42,9 @@ def test_overlapping_threads_restore_once():
     for t in ts:
         t.start()
     inside.wait()
-    assert sys.getswitchinterval() == min(before, engine.SEARCH_SWITCH_INTERVAL)
+    assert _short(before)
     leave.set()
     for t in ts:
         t.join()
-    assert sys.getswitchinterval() == before
+    assert _is(before)
     assert engine._HANDOFF[0] == 0
