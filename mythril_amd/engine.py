@@ -107,13 +107,9 @@ def _prepare(conjuncts, ctx, use_pools, timings) -> Query:
     conj = list(conjuncts)
     low = lower_constraints(conj, ctx)
     t1 = time.perf_counter()
-    leaves = []
-    seen = set()
-    for n in low.nodes:   # topo of the flattened conjuncts, computed once by lower_constraints
-        if n.op == "var" and n.name not in seen:
-            seen.add(n.name)
-            leaves.append(n)
-    specs = harvest(low.conjuncts, leaves, nodes=low.nodes) if use_pools else {}
+    # low.nodes: the topo of the flattened conjuncts, computed once by
+    # lower_constraints; harvest collects the var leaves in the same loop
+    specs = harvest(low.conjuncts, None, nodes=low.nodes) if use_pools else {}
     t2 = time.perf_counter()
     prog = compile_query(low.conjuncts, leaf_specs=specs, reach=(low.flat, low.nodes))
     if timings is not None:

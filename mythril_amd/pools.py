@@ -417,13 +417,19 @@ def _const_props(consts, m: int, split_bytes: bool):
                 yield (c >> (8 * i)) & 0xFF
 
 
-def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
+def harvest(conjuncts: List[Node], leaves: Optional[List[Node]], pool_size: int = 32,
             random_share: float = 0.25, restrict: bool = True,
             nodes: Optional[List[Node]] = None) -> Dict[str, LeafSpec]:
     """nodes: topo(conjuncts) when the caller has it (prepare: Lowered.nodes,
-    the same walk without the top-level `and` nodes, which no rule reads)."""
+    the same walk without the top-level `and` nodes, which no rule reads).
+    leaves None: every var of `nodes`, first occurrence of each name in walk
+    order (collected by the same loop that reads the constants)."""
     if nodes is None:
         nodes = topo(conjuncts)
+    collect = leaves is None
+    if collect:
+        leaves = []
+        seen_leaf = set()
     exact, interval, dom_align = domains(conjuncts) if restrict else ({}, {}, {})
     proposals: Dict[str, List[int]] = {}
     # orderings between two leaves (INVEST_MIN < msg.value < INVEST_MAX with
@@ -453,6 +459,11 @@ def harvest(conjuncts: List[Node], leaves: List[Node], pool_size: int = 32,
         if op == "const":
             if n.width != BOOL:
                 consts.append(n.val)
+            continue
+        if op == "var":
+            if collect and n.name not in seen_leaf:
+                seen_leaf.add(n.name)
+                leaves.append(n)
             continue
         if op == "concat":
             concats.append(n)
