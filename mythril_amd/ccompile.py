@@ -105,11 +105,10 @@ def serialize(conj: Sequence[Node], trace: Sequence[Node], nodes: Optional[List[
     kb = bytearray()
     names: Dict[str, int] = {}
     nk = 0
-    ext = recs.extend
+    ext, put, opc = recs.extend, recs.append, _OPC.get
     for i, n in enumerate(nodes):
         idx[n.id] = i
         op = n.op
-        args = n.args
         if op == "const":
             kb += (n.val & _M256).to_bytes(32, "little")
             ext((_CONST, n.width, 0, nk, 0, 0))
@@ -121,10 +120,19 @@ def serialize(conj: Sequence[Node], trace: Sequence[Node], nodes: Optional[List[
                 nid = names[n.name] = len(names)
             ext((_VAR, n.width, 0 if n.dom is None else 1, nid, 0, 0))
             continue
+        args = n.args
+        na = len(args)
         pr = n.params
-        ext((_OPC.get(op, -1), n.width, 0 if n.dom is None else 1, pr[0] if pr else 0,
-             pr[1] if len(pr) > 1 else 0, len(args)))
-        if args:
+        if pr:
+            ext((opc(op, -1), n.width, 0 if n.dom is None else 1, pr[0], pr[1] if len(pr) > 1 else 0, na))
+        else:
+            ext((opc(op, -1), n.width, 0 if n.dom is None else 1, 0, 0, na))
+        if na == 2:   # the common arities without a comprehension
+            a, b = args
+            ext((idx[a.id], idx[b.id]))
+        elif na == 1:
+            put(idx[args[0].id])
+        elif na:
             ext([idx[a.id] for a in args])
     roots = [idx[c.id] for c in conj] + [idx[t.id] for t in trace]
     return array("i", recs), len(nodes), bytes(kb), nk, array("i", roots), nodes
