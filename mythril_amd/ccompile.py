@@ -185,7 +185,7 @@ def compile_native(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
     stats = {"nodes": int(info.n_nodes), "insns": n_insn, "spills": int(info.n_spills), "fills": int(info.n_fills),
              "div_nominal_ops": int(info.div_nominal_ops), "wide_divisions": int(info.n_div)}
     return Program(code=code, consts=consts if consts.size else np.zeros(1, dtype=np.uint32),
-                   leaves=np.asarray(leaf_words, dtype=np.uint32),
+                   leaves=np.frombuffer(array("I", leaf_words), dtype=np.uint32),
                    pool=pool_words if pool_words.size else np.zeros(1, dtype=np.uint32),
                    n_spill=int(info.n_spill), n_trace_rows=int(info.n_trace_rows), n_input_rows=in_row,
                    ops_per_eval=int(info.ops_per_eval), leaf_specs=specs, leaf_nodes=leaf_nodes,
