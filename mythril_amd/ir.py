@@ -69,7 +69,7 @@ class Node:
         self.name = name
         self.dom = dom
         self.id = nid
-        self._h = hash((op, width, tuple(a.id for a in args), params, val, name, dom)) if h is None else h
+        self._h = h   # computed on first use (__hash__): most terms are never hashed
 
     # -- sort helpers -------------------------------------------------
     @property
@@ -81,7 +81,11 @@ class Node:
         return self.dom is not None
 
     def __hash__(self):
-        return self._h
+        h = self._h
+        if h is None:
+            h = self._h = hash((self.op, self.width, tuple(a.id for a in self.args), self.params, self.val,
+                                self.name, self.dom))
+        return h
 
     def __repr__(self):  # pragma: no cover - debugging aid
         if self.op == "const":
@@ -102,11 +106,21 @@ class Ctx:
         self.nodes: List[Node] = []
 
     def _mk(self, op, width, args=(), params=(), val=None, name=None, dom=None) -> Node:
-        params = tuple(params)
-        key = (op, width, tuple([a.id for a in args]), params, val, name, dom)
+        if params.__class__ is not tuple:
+            params = tuple(params)
+        na = len(args)
+        if na == 2:
+            a, b = args
+            ids = (a.id, b.id)
+        elif na == 1:
+            ids = (args[0].id,)
+        else:
+            ids = tuple([a.id for a in args])
+        key = (op, width, ids, params, val, name, dom)
         n = self._tab.get(key)
         if n is None:
-            n = Node(op, width, tuple(args), params, val, name, dom, len(self.nodes), hash(key))
+            n = Node(op, width, args if args.__class__ is tuple else tuple(args), params, val, name, dom,
+                     len(self.nodes))
             self._tab[key] = n
             self.nodes.append(n)
         return n
