@@ -48,20 +48,36 @@ def tokenize(text: str) -> List[Union[str, tuple]]:
 
 
 def parse_sexps(text: str) -> List[Sexp]:
-    stack: List[list] = [[]]
-    for tok in tokenize(text):
-        if tok == "(":
-            stack.append([])
-        elif tok == ")":
-            if len(stack) == 1:
+    """The s-expressions of text, tokenised on the fly (tokenize's rules: no
+    intermediate token list)."""
+    top: list = []
+    stack: List[list] = []
+    cur = top
+    push, pop = stack.append, stack.pop
+    for t in _TOKEN.findall(text):
+        c = t[0]
+        if c == "(":
+            push(cur)
+            cur = []
+        elif c == ")":
+            if not stack:
                 raise Unsupported("smt2: unbalanced ')'")
-            done = stack.pop()
-            stack[-1].append(done)
+            done = cur
+            cur = pop()
+            cur.append(done)
+        elif c == ";":
+            continue
+        elif c == "|":
+            if len(t) < 2 or t[-1] != "|":
+                raise Unsupported(f"smt2: cannot tokenize at {t!r}")
+            cur.append(("Q", t[1:-1]))
+        elif c == '"' and (len(t) < 2 or t[-1] != '"'):
+            raise Unsupported(f"smt2: cannot tokenize at {t!r}")
         else:
-            stack[-1].append(tok)
-    if len(stack) != 1:
+            cur.append(t)
+    if stack:
         raise Unsupported("smt2: unbalanced '('")
-    return stack[0]
+    return top
 
 
 def _sym(x) -> str:
@@ -108,6 +124,12 @@ def _sort(s) -> Sort:
     raise Unsupported(f"smt2: unsupported sort {s!r}")
 
 
+# applications term() builds straight from their arguments (after ALIASES),
+# and the heads with rules of their own
+_DIRECT_OPS = frozenset({"select", "store", "ite"}) | frozenset(BOOL_OPS) | frozenset(BV_OPS)
+_SPECIAL_HEADS = frozenset({"_", "let", "!", "bvredor", "bvredand"})
+
+
 class _Builder:
     def __init__(self, script: Script):
         self.s = script
@@ -132,6 +154,19 @@ class _Builder:
     def term(self, e: Sexp, env: Dict[str, Node]) -> Node:
         # iterative over let-nesting depth is bounded; recursion depth follows term depth,
         # which z3's let-sharing keeps modest.  Raise the limit for deep ad-hoc inputs.
+        cls = e.__class__
+        if cls is list and e and e[0].__class__ is str:
+            # the common application: a plain function symbol (fast path)
+            head = e[0]
+            if head not in _SPECIAL_HEADS:
+                op = ALIASES.get(head, head)
+                if op in _DIRECT_OPS:
+                    term = self.term
+                    return self.ctx.app(op, *[term(a, env) for a in e[1:]])
+        elif cls is str:
+            v = env.get(e)
+            if v is not None:
+                return v
         if isinstance(e, tuple):
             name = e[1]
             return env[name] if name in env else self.leaf(name)
