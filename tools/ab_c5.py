@@ -44,7 +44,9 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             # LLVM scheduler choices
             "ilp": {"EXTRA_FLAGS": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]},
             "bias0": {"EXTRA_FLAGS": ["-mllvm", "-amdgpu-schedule-metric-bias=0"]},
-            "trackers": {"EXTRA_FLAGS": ["-mllvm", "-amdgpu-use-amdgpu-trackers"]}}
+            "trackers": {"EXTRA_FLAGS": ["-mllvm", "-amdgpu-use-amdgpu-trackers"]},
+            # optimisation levels that trade instructions for code size (instruction-fetch wait)
+            "os": {"EXTRA_FLAGS": ["-Os"]}, "o2": {"EXTRA_FLAGS": ["-O2"]}}
 
 
 def main():
