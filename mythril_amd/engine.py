@@ -181,6 +181,33 @@ def _gil_handoff(active: bool):
                 sys.setswitchinterval(_HANDOFF[1])
 
 
+# A stop-after-hit search first tries the lowest PROBE_CANDIDATES indices in a
+# launch of their own: most satisfiable LASER queries have a witness there
+# (pool-first candidate order), and the full launch runs every block's first
+# chunk (2 048 blocks x 256 candidates) before any can stop.  Programs with no
+# witness in the probe continue from its end; the lowest satisfying index is
+# the same either way.
+PROBE_CANDIDATES = 1 << 16
+
+
+def search_phased(dev, dps, seed: int, begin: int, count: int, flags: int):
+    """dev.search(dps, seed, begin, count, flags) with the probe launch above
+    (stop-after-hit searches longer than twice the probe); the statistics of
+    both launches summed."""
+    if not (flags & isa.FLAG_STOP_AFTER_HIT) or count <= 2 * PROBE_CANDIDATES:
+        return dev.search(dps, seed, begin, count, flags)
+    found, st = dev.search(dps, seed, begin, PROBE_CANDIDATES, flags)
+    rest = [i for i, f in enumerate(found) if f is None]
+    if rest:
+        f2, st2 = dev.search([dps[i] for i in rest], seed, begin + PROBE_CANDIDATES, count - PROBE_CANDIDATES,
+                             flags)
+        found = list(found)
+        for i, f in zip(rest, f2):
+            found[i] = f
+        st = {k: (v + st2[k] if isinstance(v, (int, float)) and k in st2 else v) for k, v in st.items()}
+    return found, st
+
+
 def _prebuild_witness_programs(queries) -> bool:
     """Queue the witness programs a search may need on a host thread, which
     compiles them while the device searches (the search call releases the
@@ -259,7 +286,7 @@ class WitnessEngine:
             # searches (the search call releases the GIL): a witness then costs
             # one upload and one launch (materialize)
             with _gil_handoff(_prebuild_witness_programs(queries)):
-                found, st = self.dev.search(dps, self.seed, begin, count, flags)
+                found, st = search_phased(self.dev, dps, self.seed, begin, count, flags)
             self.stats["searches"] += 1
             self.stats["programs"] += len(queries)
             self.stats["evals"] += st["evals"]

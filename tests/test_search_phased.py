@@ -1,0 +1,54 @@
+"""engine.search_phased: a stop-after-hit search tries the lowest
+PROBE_CANDIDATES indices first and continues from there only for the programs
+with no witness in them; the witness is the same lowest satisfying index as
+one launch over the whole range (the host build standing in for the device)."""
+from mythril_amd import engine, isa
+from mythril_amd.compiler import compile_program
+from mythril_amd.hostemu import term_values
+from mythril_amd.synth import build_c5
+from tests.fakedev import FakeDevice
+
+WITNESS = 0x5EED0005 % (1 << 31)      # synth.build_c5's planted index
+FLAGS = isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT
+
+
+class _Counting(FakeDevice):
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self.ranges = []
+
+    def search(self, dps, seed, begin, count, flags=0):
+        self.ranges.append((len(dps), begin, count))
+        return super().search(dps, seed, begin, count, flags)
+
+
+def _setup():
+    syn = build_c5(term_values, n_nodes=200)
+    dev = _Counting(chunk=1 << 12)
+    return syn, dev, dev.load(compile_program(syn.conjuncts))
+
+
+def test_hit_in_the_probe_is_one_launch():
+    syn, dev, dp = _setup()
+    begin = WITNESS - 1000
+    found, st = engine.search_phased(dev, [dp], syn.seed, begin, 1 << 18, FLAGS)
+    assert found == [WITNESS] and dev.ranges == [(1, begin, engine.PROBE_CANDIDATES)]
+
+
+def test_miss_in_the_probe_continues_and_batches_keep_their_hits():
+    syn, dev, dp = _setup()
+    dp2 = dev.load(compile_program(syn.conjuncts))
+    begin = WITNESS - engine.PROBE_CANDIDATES - 5000      # the witness lies past the probe
+    count = 1 << 18
+    (want,), _ = dev.search([dp], syn.seed, begin, count, FLAGS)
+    dev.ranges.clear()
+    found, st = engine.search_phased(dev, [dp], syn.seed, begin, count, FLAGS)
+    assert found == [want] == [WITNESS]
+    assert dev.ranges == [(1, begin, engine.PROBE_CANDIDATES),
+                          (1, begin + engine.PROBE_CANDIDATES, count - engine.PROBE_CANDIDATES)]
+    assert st["evals"] > 0
+    # exhaustive searches and short ranges are one launch
+    dev.ranges.clear()
+    engine.search_phased(dev, [dp, dp2], syn.seed, begin, count, 0)
+    engine.search_phased(dev, [dp], syn.seed, begin, 2 * engine.PROBE_CANDIDATES, FLAGS)
+    assert [r[2] for r in dev.ranges] == [count, 2 * engine.PROBE_CANDIDATES]
