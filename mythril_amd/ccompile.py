@@ -135,7 +135,7 @@ def serialize(conj: Sequence[Node], trace: Sequence[Node], nodes: Optional[List[
         elif na:
             ext([idx[a.id] for a in args])
     roots = [idx[c.id] for c in conj] + [idx[t.id] for t in trace]
-    return array("i", recs), len(nodes), bytes(kb), nk, array("i", roots), nodes
+    return array("i", recs), len(nodes), bytes(kb), nk, array("i", roots), nodes, idx, names
 
 
 def _addr(buf) -> int:
@@ -151,18 +151,41 @@ def compile_native(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
     fns = _bind()
     if fns is None:
         raise RuntimeError(f"native compiler unavailable: {_why}")
-    lib, c_compile, c_take, c_free = fns
     trace = list(trace)
     if reach is not None and not trace:
         conj, nodes = reach
-        recs, nn, kb, nk, roots, nodes = serialize(conj, trace, nodes)
+        recs, nn, kb, nk, roots, nodes, idx, names = serialize(conj, trace, nodes)
     else:
         conj = _flatten(conjuncts)
-        recs, nn, kb, nk, roots, nodes = serialize(conj, trace)
+        recs, nn, kb, nk, roots, nodes, idx, names = serialize(conj, trace)
+    info, code, consts, leaves, tr = _run(fns, recs, nn, kb, nk, roots, len(conj), len(trace))
+    leaf_nodes = [nodes[i] for i in leaves.tolist()]
+    specs, leaf_words, pool_words, in_row = layout_leaves(leaf_nodes, leaf_specs, pools)
+    t = tr.tolist()
+    trace_map = {nodes[t[k]].id: (t[k + 1], "W" if t[k + 2] else "N") for k in range(0, len(t), 3)}
+    n_insn = int(info.ncode_words) // 4
+    return Program(code=code, consts=consts if consts.size else np.zeros(1, dtype=np.uint32),
+                   leaves=np.frombuffer(array("I", leaf_words), dtype=np.uint32),
+                   pool=pool_words if pool_words.size else np.zeros(1, dtype=np.uint32),
+                   n_spill=int(info.n_spill), n_trace_rows=int(info.n_trace_rows), n_input_rows=in_row,
+                   ops_per_eval=int(info.ops_per_eval), leaf_specs=specs, leaf_nodes=leaf_nodes,
+                   trace_map=trace_map, n_insn=n_insn, n_conjuncts=len(conj), stats=_stats(info, n_insn),
+                   ssa_build=lambda: compile_program(conj, trace=trace).ssa,
+                   native_dag=(recs, nn, kb, nk, nodes, idx, names))
+
+
+def _stats(info, n_insn):
+    return {"nodes": int(info.n_nodes), "insns": n_insn, "spills": int(info.n_spills), "fills": int(info.n_fills),
+            "div_nominal_ops": int(info.div_nominal_ops), "wide_divisions": int(info.n_div)}
+
+
+def _run(fns, recs, nn, kb, nk, roots, nconj, ntrace):
+    """One mw_compile call: (info, code, consts, leaf record indices, trace triples)."""
+    lib, c_compile, c_take, c_free = fns
     kbuf = ctypes.create_string_buffer(kb, len(kb)) if kb else None
     h = _P()
     info = MwCompileInfo()
-    rc = c_compile(_addr(recs), len(recs), nn, kbuf, nk, _addr(roots), len(conj), len(trace),
+    rc = c_compile(_addr(recs), len(recs), nn, kbuf, nk, _addr(roots), nconj, ntrace,
                    ctypes.byref(h), ctypes.byref(info))
     if rc != 0:
         msg = (lib.mg_last_error() or b"").decode()
@@ -173,24 +196,111 @@ def compile_native(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
     consts = np.empty(info.nconst_words, dtype=np.uint32)
     leaves = np.empty(info.nleaves, dtype=np.uint32)
     tr = np.empty(3 * info.ntrace, dtype=np.uint32)
-    ptr = lambda a: a.ctypes.data if a.size else None
+    ptr = lambda a: a.ctypes.data if a.size else None   # noqa: E731
     if c_take(h, ptr(code), ptr(consts), ptr(leaves), ptr(tr)) != 0:
         c_free(h)
         raise RuntimeError("mw_compiled_take failed")
+    return info, code, consts, leaves, tr
+
+
+def _outside(roots: Sequence[Node], idx: Dict[int, int]) -> List[Node]:
+    """The nodes below roots that idx does not hold, operand-first."""
+    out: List[Node] = []
+    seen = set()
+    for r in roots:
+        if r.id in idx or r.id in seen:
+            continue
+        stack = [(r, False)]
+        while stack:
+            n, done = stack.pop()
+            if done:
+                out.append(n)
+                continue
+            if n.id in idx or n.id in seen:
+                continue
+            seen.add(n.id)
+            stack.append((n, True))
+            for a in reversed(n.args):
+                if a.id not in idx and a.id not in seen:
+                    stack.append((a, False))
+    return out
+
+
+def _serialize_more(extra: Sequence[Node], idx: Dict[int, int], names: Dict[str, int], start: int, nk: int):
+    """serialize's records for `extra` (operand-first; operands in idx or
+    earlier in extra), numbered from `start`: (records, constant bytes,
+    constant count, {node id: record index})."""
+    local: Dict[int, int] = {}
+    recs: List[int] = []
+    kb = bytearray()
+    new_names: Dict[str, int] = {}
+    ext = recs.extend
+
+    def at(a):
+        i = local.get(a.id)
+        return idx[a.id] if i is None else i
+    for j, n in enumerate(extra):
+        local[n.id] = start + j
+        op = n.op
+        if op == "const":
+            kb += (n.val & _M256).to_bytes(32, "little")
+            ext((_CONST, n.width, 0, nk, 0, 0))
+            nk += 1
+            continue
+        if op == "var":
+            nid = names.get(n.name)
+            if nid is None:
+                nid = new_names.get(n.name)
+                if nid is None:
+                    nid = new_names[n.name] = len(names) + len(new_names)
+            ext((_VAR, n.width, 0 if n.dom is None else 1, nid, 0, 0))
+            continue
+        pr = n.params
+        ext((_OPC.get(op, -1), n.width, 0 if n.dom is None else 1, pr[0] if pr else 0,
+             pr[1] if len(pr) > 1 else 0, len(n.args)))
+        ext([at(a) for a in n.args])
+    return recs, bytes(kb), nk, local
+
+
+def compile_trace_native(prog: Program, trace: Sequence[Node]) -> Optional[Program]:
+    """The witness program of a natively compiled `prog` (no conjuncts,
+    `trace` traced, its leaves first in prog's order), compiled from prog's
+    own record stream: no second serialisation, and prog's leaf table and
+    pools as they are.  Code generation starts from the roots only, so the
+    program is the one compile_native(trace=trace) makes; its ops_per_eval
+    counts the whole stream (a witness launch is one candidate).  Traced
+    terms outside the stream (cell indices no conjunct reads) get their
+    records appended.  None when the leaves come out in another order: the
+    caller compiles it afresh."""
+    dag = prog.native_dag
+    fns = _bind()
+    if dag is None or fns is None:
+        return None
+    recs, nn, kb, nk, nodes, idx, names = dag
+    extra = _outside(trace, idx)
+    if extra:   # terms no conjunct reads (cell indices): their records appended
+        more, kb2, nk, local = _serialize_more(extra, idx, names, nn, nk)
+        recs = array("i", recs)
+        recs.extend(more)
+        kb += kb2
+        nodes = nodes + extra
+        nn += len(extra)
+        pos = lambda i: local[i] if i in local else idx[i]   # noqa: E731
+    else:
+        pos = idx.__getitem__
+    roots = array("i", [pos(t.id) for t in trace])
+    info, code, consts, leaves, tr = _run(fns, recs, nn, kb, nk, roots, 0, len(roots))
     leaf_nodes = [nodes[i] for i in leaves.tolist()]
-    specs, leaf_words, pool_words, in_row = layout_leaves(leaf_nodes, leaf_specs, pools)
+    if [n.id for n in leaf_nodes] != [n.id for n in prog.leaf_nodes]:
+        return None
     t = tr.tolist()
     trace_map = {nodes[t[k]].id: (t[k + 1], "W" if t[k + 2] else "N") for k in range(0, len(t), 3)}
     n_insn = int(info.ncode_words) // 4
-    stats = {"nodes": int(info.n_nodes), "insns": n_insn, "spills": int(info.n_spills), "fills": int(info.n_fills),
-             "div_nominal_ops": int(info.div_nominal_ops), "wide_divisions": int(info.n_div)}
     return Program(code=code, consts=consts if consts.size else np.zeros(1, dtype=np.uint32),
-                   leaves=np.frombuffer(array("I", leaf_words), dtype=np.uint32),
-                   pool=pool_words if pool_words.size else np.zeros(1, dtype=np.uint32),
-                   n_spill=int(info.n_spill), n_trace_rows=int(info.n_trace_rows), n_input_rows=in_row,
-                   ops_per_eval=int(info.ops_per_eval), leaf_specs=specs, leaf_nodes=leaf_nodes,
-                   trace_map=trace_map, n_insn=n_insn, n_conjuncts=len(conj), stats=stats,
-                   ssa_build=lambda: compile_program(conj, trace=trace).ssa)
+                   leaves=prog.leaves, pool=prog.pool, n_spill=int(info.n_spill),
+                   n_trace_rows=int(info.n_trace_rows), n_input_rows=prog.n_input_rows,
+                   ops_per_eval=int(info.ops_per_eval), leaf_specs=prog.leaf_specs, leaf_nodes=leaf_nodes,
+                   trace_map=trace_map, n_insn=n_insn, n_conjuncts=0, stats=_stats(info, n_insn))
 
 
 USE_PYTHON = os.environ.get("MYTHRIL_AMD_PY_COMPILE", "0") == "1"

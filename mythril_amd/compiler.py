@@ -124,6 +124,9 @@ class Program:
     ssa: List[MInsn] = field(default_factory=list)   # machine IR before slot allocation (jit.py)
     # natively compiled programs (ccompile.py) carry no machine IR; this builds it on first use
     ssa_build: Optional[Callable[[], List[MInsn]]] = None
+    # natively compiled programs: the record stream they were compiled from
+    # (ccompile.compile_trace_native compiles the witness program from it)
+    native_dag: Optional[tuple] = None
 
     def machine_ir(self) -> List[MInsn]:
         """The SSA machine IR the specialised kernels are generated from (jit.py)."""

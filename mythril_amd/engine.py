@@ -234,7 +234,14 @@ def _prebuild_witness_programs(queries) -> bool:
 def _witness_program(prog: Program, traced: List[Node]) -> Program:
     """The witness program of `prog`: its leaf layout (pool fields already
     assigned; copies, layout_leaves updates the specs it is given), no
-    conjuncts, the leaves and cell indices traced."""
+    conjuncts, the leaves and cell indices traced.  A natively compiled prog
+    gives it from its own record stream and leaf table
+    (ccompile.compile_trace_native: the same program, without a second
+    serialisation and layout)."""
+    from .ccompile import compile_trace_native
+    wp = compile_trace_native(prog, traced)
+    if wp is not None:
+        return wp
     fixed = {s.name: dataclasses.replace(s, pool=None if s.pool is None else list(s.pool))
              for s in prog.leaf_specs}
     return compile_query([], leaf_specs=fixed, trace=traced)

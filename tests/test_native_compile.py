@@ -198,3 +198,33 @@ def test_random_dags_deep():
 
 def c_cmp(c, r, a, b):
     return c.app(r.choice(["bvult", "=", "bvsle", "distinct"]), a, b)
+
+
+def test_witness_program_from_the_search_stream_is_the_fresh_compile():
+    """ccompile.compile_trace_native (the witness program compiled from the
+    search program's own record stream, cell-index terms appended, the leaf
+    table reused) gives the program a fresh compile of the trace gives."""
+    import glob
+    import dataclasses
+    import numpy as np
+    from mythril_amd import ccompile, engine
+    from mythril_amd.smt2 import parse_file
+    files = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "laser", "*.smt2*")))[::9] + \
+        sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "solver_log", "*.smt2*")))
+    n = 0
+    for f in files:
+        s = parse_file(f)
+        q = engine.prepare(s.asserts, s.ctx)
+        traced = list(q.program.leaf_nodes) + list(q.arg_terms)
+        b = ccompile.compile_trace_native(q.program, traced)
+        assert b is not None, f
+        fixed = {sp.name: dataclasses.replace(sp, pool=None if sp.pool is None else list(sp.pool))
+                 for sp in q.program.leaf_specs}
+        a = ccompile.compile_native([], leaf_specs=fixed, trace=traced)
+        for k in ("code", "consts", "leaves", "pool"):
+            assert np.array_equal(getattr(a, k), getattr(b, k)), (f, k)
+        assert (a.trace_map, a.n_trace_rows, a.n_spill, a.n_input_rows) == \
+            (b.trace_map, b.n_trace_rows, b.n_spill, b.n_input_rows), f
+        assert [x.id for x in a.leaf_nodes] == [x.id for x in b.leaf_nodes]
+        n += 1
+    assert n >= 60
