@@ -382,7 +382,7 @@ class WitnessEngine:
                 w.functions.setdefault(al.base, {})[args] = val
 
     def _materialize_traced(self, q: Query, index: int, search_dp=None) -> Optional[Witness]:
-        from .runtime import EngineError, unpack_trace
+        from .runtime import EngineError, trace_column, unpack_one
         p = q.trace_program
         if [n.name for n in p.leaf_nodes] != [n.name for n in q.program.leaf_nodes]:
             # an EngineError, so get_model's handler sends the query to z3
@@ -392,7 +392,8 @@ class WitnessEngine:
             _, trace = self.dev.eval_generated(dp, self.seed, index, 1)
         finally:
             dp.free()
-        values = {n.name: unpack_trace(p, trace, n)[0] for n in p.leaf_nodes}
+        col = trace_column(trace)   # the one candidate's rows, read per node below
+        values = {n.name: unpack_one(p, col, n) for n in p.leaf_nodes}
         w = Witness(index, values)
-        self._ack_cells(q, w, values, lambda t: t.val if t.op == "const" else unpack_trace(p, trace, t)[0])
+        self._ack_cells(q, w, values, lambda t: t.val if t.op == "const" else unpack_one(p, col, t))
         return w

@@ -296,6 +296,18 @@ def pack_inputs(p: Program, assignments: Sequence[dict]) -> np.ndarray:
     return rows
 
 
+def trace_column(trace: np.ndarray, j: int = 0) -> bytes:
+    """Candidate j's trace rows as little-endian bytes (one copy; unpack_one
+    reads any node's value from it)."""
+    return np.ascontiguousarray(trace[:, j], dtype="<u4").tobytes()
+
+
+def unpack_one(p: Program, col: bytes, node) -> int:
+    """node's traced value in a trace_column."""
+    row, cls = p.trace_map[node.id]
+    return int.from_bytes(col[4 * row:4 * (row + (8 if cls == "W" else 1))], "little")
+
+
 def unpack_trace(p: Program, trace: np.ndarray, node) -> List[int]:
     """The traced values of node, one per candidate (trace rows are u32 limbs,
     least significant first)."""
