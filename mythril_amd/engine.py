@@ -383,15 +383,21 @@ class WitnessEngine:
 
     def _materialize_traced(self, q: Query, index: int, search_dp=None) -> Optional[Witness]:
         from .runtime import EngineError, trace_column, unpack_one
+        t0 = time.perf_counter()
         p = q.trace_program
         if [n.name for n in p.leaf_nodes] != [n.name for n in q.program.leaf_nodes]:
             # an EngineError, so get_model's handler sends the query to z3
             raise EngineError("witness program's leaf layout differs from the search program's")
+        t1 = time.perf_counter()
         dp = self.dev.load(p)
+        t2 = time.perf_counter()
         try:
             _, trace = self.dev.eval_generated(dp, self.seed, index, 1)
         finally:
             dp.free()
+        t3 = time.perf_counter()
+        # seconds per step of the last traced witness (tools/latency_bench.py)
+        self.last_materialize = {"program": t1 - t0, "load": t2 - t1, "eval": t3 - t2}
         col = trace_column(trace)   # the one candidate's rows, read per node below
         values = {n.name: unpack_one(p, col, n) for n in p.leaf_nodes}
         w = Witness(index, values)

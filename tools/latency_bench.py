@@ -68,8 +68,11 @@ def main():
                         # as WitnessEngine.search does: the search program is still
                         # loaded (mg_witness_leaves when every cell index is constant)
                         t2 = time.perf_counter()
+                        eng.last_materialize = None
                         eng.materialize(q, idx, dp)
                         row["materialise"] = (time.perf_counter() - t2) * 1e3
+                        if getattr(eng, "last_materialize", None):
+                            row["materialise_parts"] = {k: v * 1e3 for k, v in eng.last_materialize.items()}
                         row["leaf_path"] = all(t.op == "const" for t in q.arg_terms)
                 finally:
                     dp.free()
