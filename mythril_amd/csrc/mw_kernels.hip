@@ -379,6 +379,12 @@ struct Ctx {
   size_t nasmargs_cap = 0;
   u32* d_alive = nullptr;     // per-candidate alive bits between the parts of a split program
   size_t alive_cap = 0;
+  // pinned staging of program uploads (mg_prog_load): the copy is queued on
+  // the stream, ahead of every launch that reads the program; the next upload
+  // waits for it before reusing the buffer (up_pending)
+  uint8_t* h_up = nullptr;
+  size_t up_bytes = 0;
+  bool up_pending = false;
   std::mutex mu;                 // serialises the calls on this context (mw_handles.h)
   bool dead = false;             // freed by mg_free (guarded by mu)
   // device buffers returned by freed programs and finished calls, by size
@@ -578,7 +584,9 @@ void release_prog(Prog& p) {
   hipSetDevice(p.ctx->dev);
   p.unload();
   // every call on the context synchronises before it returns (and this runs
-  // under the context's mu): no kernel still reads the buffer
+  // under the context's mu): no kernel still reads the buffer.  Only
+  // mg_prog_load returns with its upload queued; whatever reuses the buffer
+  // next is queued after that copy on the same stream
   if (p.d_buf) pool_put(p.ctx.get(), p.d_buf, p.buf_cls);
   p.d_buf = nullptr;
 }
@@ -590,6 +598,10 @@ void release_ctx(Ctx& c) {
   if (c.d_spill) hipFree(c.d_spill);
   if (c.d_blk) hipFree(c.d_blk);
   if (c.h_blk) hipHostFree(c.h_blk);
+  if (c.h_up) hipHostFree(c.h_up);
+  c.h_up = nullptr;
+  c.up_bytes = 0;
+  c.up_pending = false;
   if (c.d_alive) hipFree(c.d_alive);
   if (c.e0) hipEventDestroy(c.e0);
   if (c.e1) hipEventDestroy(c.e1);
@@ -887,21 +899,42 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   p->sig = prog_signature(d);
   p->d_buf = (u32*)pool_get(c, total * sizeof(u32), &p->buf_cls);
   if (!p->d_buf) return fail(MG_E_NOMEM, "program upload allocation failed");
-  std::vector<u32> hbuf(total, 0u);
-  std::memcpy(hbuf.data(), d->code, nc * 4);
-  if (d->nconst_words) std::memcpy(hbuf.data() + nc, d->consts, d->nconst_words * 4);
-  if (d->nleaves) std::memcpy(hbuf.data() + nc + nk, d->leaves, d->nleaves * MW_LEAF_WORDS * 4);
-  if (d->npool_words) std::memcpy(hbuf.data() + nc + nk + nl, d->pool, d->npool_words * 4);
+  // stage in the context's pinned buffer (after the previous upload from it has landed)
+  if (c->up_pending && hipStreamSynchronize(c->stream) != hipSuccess) {
+    release_prog(*p);
+    return fail(MG_E_HIP, "program upload: stream synchronize failed");
+  }
+  c->up_pending = false;
+  if (total * 4 > c->up_bytes) {
+    if (c->h_up) hipHostFree(c->h_up);
+    c->h_up = nullptr;
+    c->up_bytes = 0;
+    const size_t want = std::max<size_t>(total * 4, (size_t)1 << 18);
+    if (hipHostMalloc(&c->h_up, want, hipHostMallocDefault) != hipSuccess) {
+      release_prog(*p);
+      return fail(MG_E_NOMEM, "program upload staging allocation failed");
+    }
+    c->up_bytes = want;
+  }
+  u32* hbuf = (u32*)c->h_up;
+  std::memset(hbuf, 0, total * 4);
+  std::memcpy(hbuf, d->code, nc * 4);
+  if (d->nconst_words) std::memcpy(hbuf + nc, d->consts, d->nconst_words * 4);
+  if (d->nleaves) std::memcpy(hbuf + nc + nk, d->leaves, d->nleaves * MW_LEAF_WORDS * 4);
+  if (d->npool_words) std::memcpy(hbuf + nc + nk + nl, d->pool, d->npool_words * 4);
   if (asm_ok) {
-    u32* pre = hbuf.data() + nc + nk + nl + np;
+    u32* pre = hbuf + nc + nk + nl + np;
     // more distinct narrow constants than MW_ASM_NK: the compiled interpreter runs it
     asm_ok = mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, g_hoff, pre, pre + nc + 8) == 0;
     if (asm_ok) asm_leaf_table(d->leaves, d->nleaves, pre + nc + 8 + MW_ASM_NK);
   }
-  if (hipMemcpy(p->d_buf, hbuf.data(), total * 4, hipMemcpyHostToDevice) != hipSuccess) {
+  // queued on the context's stream: every launch that reads the program is
+  // queued after it on the same stream
+  if (hipMemcpyAsync(p->d_buf, hbuf, total * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
     release_prog(*p);
     return fail(MG_E_HIP, "program upload copy failed");
   }
+  c->up_pending = true;
   p->dev.code = p->d_buf;
   p->dev.consts = p->d_buf + nc;
   p->dev.leaves = p->d_buf + nc + nk;

@@ -283,16 +283,17 @@ class WitnessEngine:
             return []
         count = count or self.launch_count(queries)
         dps = []
+        # the witness programs compile on a host thread while the programs
+        # upload and the device searches (those calls release the GIL): a
+        # witness then costs one upload and one launch (materialize)
+        queued = _prebuild_witness_programs(queries)
         try:
             for q in queries:   # a failed load frees the programs already loaded
                 dps.append(self.dev.load(q.program))
             if (self.asmjit_min_ops and hasattr(self.dev, "attach_asm")
                     and count * sum(q.ops_per_eval for q in queries) >= self.asmjit_min_ops):
                 self._assemble(dps)
-            # the witness programs compile on a host thread while the device
-            # searches (the search call releases the GIL): a witness then costs
-            # one upload and one launch (materialize)
-            with _gil_handoff(_prebuild_witness_programs(queries)):
+            with _gil_handoff(queued):
                 found, st = search_phased(self.dev, dps, self.seed, begin, count, flags)
             self.stats["searches"] += 1
             self.stats["programs"] += len(queries)

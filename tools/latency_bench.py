@@ -56,11 +56,12 @@ def main():
             row["prepare"] = row["lower"] + row["pools"] + row["compile"]
             if eng is not None:
                 t1 = time.perf_counter()
+                # as WitnessEngine.search: the witness program compiles on the
+                # host thread while the program uploads and the device searches
+                queued = _prebuild_witness_programs([q])
                 dp = eng.dev.load(q.program)
                 try:
-                    # as WitnessEngine.search: the witness program compiles on the
-                    # host thread while the device searches
-                    with _gil_handoff(_prebuild_witness_programs([q])):
+                    with _gil_handoff(queued):
                         (idx,), st = search_phased(eng.dev, [dp], eng.seed, 0, eng.launch_count([q]), 3)
                     row["search"] = (time.perf_counter() - t1) * 1e3
                     row["kernel"] = st["kernel_ms"]
