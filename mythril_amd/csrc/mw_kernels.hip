@@ -385,6 +385,9 @@ struct Ctx {
   uint8_t* h_up = nullptr;
   size_t up_bytes = 0;
   bool up_pending = false;
+  // pinned landing area of small readbacks (eval verdicts and traces)
+  uint8_t* h_rb = nullptr;
+  size_t rb_bytes = 0;
   std::mutex mu;                 // serialises the calls on this context (mw_handles.h)
   bool dead = false;             // freed by mg_free (guarded by mu)
   // device buffers returned by freed programs and finished calls, by size
@@ -599,6 +602,9 @@ void release_ctx(Ctx& c) {
   if (c.d_blk) hipFree(c.d_blk);
   if (c.h_blk) hipHostFree(c.h_blk);
   if (c.h_up) hipHostFree(c.h_up);
+  if (c.h_rb) hipHostFree(c.h_rb);
+  c.h_rb = nullptr;
+  c.rb_bytes = 0;
   c.h_up = nullptr;
   c.up_bytes = 0;
   c.up_pending = false;
@@ -1267,6 +1273,22 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
 }
 
 // The eval paths below run inside a call (the context's mu held, handles live).
+// Readbacks up to this size land in the context's pinned buffer with one copy
+// and are handed over with a host memcpy (a copy straight into pageable
+// memory costs a staged transfer per buffer).
+constexpr size_t kReadbackMax = (size_t)1 << 20;
+
+static bool ensure_readback(Ctx* c, size_t bytes) {
+  if (bytes <= c->rb_bytes) return true;
+  if (c->h_rb) hipHostFree(c->h_rb);
+  c->h_rb = nullptr;
+  c->rb_bytes = 0;
+  const size_t want = std::max<size_t>(bytes, (size_t)1 << 16);
+  if (hipHostMalloc(&c->h_rb, want, hipHostMallocDefault) != hipSuccess) return false;
+  c->rb_bytes = want;
+  return true;
+}
+
 static int eval_common(Ctx* c, const Prog* p, const uint32_t* leaves_soa, size_t ncand, uint64_t seed,
                        uint64_t begin, uint32_t* verdict, uint32_t* trace) {
   if (!verdict || ncand == 0) return fail(MG_E_ARG, "null argument");
@@ -1280,20 +1302,32 @@ static int eval_common(Ctx* c, const Prog* p, const uint32_t* leaves_soa, size_t
   if (rc) return rc;
   const size_t nin = leaves_soa ? (size_t)p->desc.n_input_rows * ncand : 0;
   const size_t ntr = trace ? (size_t)p->desc.n_trace_rows * ncand : 0;
-  Scratch s_in(c, nin * 4), s_v(c, ncand * 4), s_t(c, ntr * 4);
-  if ((nin && !s_in.p) || !s_v.p || (ntr && !s_t.p)) return fail(MG_E_NOMEM, "eval buffers");
-  u32 *d_in = s_in.u(), *d_v = s_v.u(), *d_t = s_t.u();
+  // verdicts and trace rows in one device block: one readback
+  const size_t vb = ncand * 4, tb = ntr * 4;
+  Scratch s_in(c, nin * 4), s_vt(c, vb + tb);
+  if ((nin && !s_in.p) || !s_vt.p) return fail(MG_E_NOMEM, "eval buffers");
+  u32 *d_in = s_in.u(), *d_v = s_vt.u(), *d_t = ntr ? d_v + ncand : nullptr;
   if (nin && hipMemcpyAsync(d_in, leaves_soa, nin * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     return fail(MG_E_HIP, "eval input copy");
-  if (ntr) hipMemsetAsync(d_t, 0, ntr * 4, c->stream);
+  if (ntr) hipMemsetAsync(d_t, 0, tb, c->stream);
   hipLaunchKernelGGL(mw_eval_kernel, dim3((u32)gx), dim3(kBlock), (size_t)nlds * kBlock * 4, c->stream,
                      p->dev, (const u32*)d_in, (u64)ncand, seed, begin, d_v, d_t, c->d_spill, nlds);
   hipError_t e = hipGetLastError();
-  if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, ncand * 4, hipMemcpyDeviceToHost, c->stream);
-  if (e == hipSuccess && ntr) e = hipMemcpyAsync(trace, d_t, ntr * 4, hipMemcpyDeviceToHost, c->stream);
+  const bool pinned = vb + tb <= kReadbackMax && ensure_readback(c, vb + tb);
+  if (e == hipSuccess && pinned) {
+    e = hipMemcpyAsync(c->h_rb, d_v, vb + tb, hipMemcpyDeviceToHost, c->stream);
+  } else {
+    if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, vb, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && ntr) e = hipMemcpyAsync(trace, d_t, tb, hipMemcpyDeviceToHost, c->stream);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  s_in.synced = s_v.synced = s_t.synced = e == hipSuccess;
+  s_in.synced = s_vt.synced = e == hipSuccess;
   if (e != hipSuccess) return fail(MG_E_HIP, std::string("eval: ") + hipGetErrorString(e));
+  c->up_pending = false;   // the stream drained: a queued program upload has landed
+  if (pinned) {
+    std::memcpy(verdict, c->h_rb, vb);
+    if (ntr) std::memcpy(trace, c->h_rb + vb, tb);
+  }
   return 0;
 }
 
