@@ -152,12 +152,12 @@ def _build_witness_program(q: "Query") -> None:
 PREBUILD_MAX_TERMS = 512
 
 
-# How soon a search call returning from the device gets the GIL back from the
-# witness-program thread (sys.setswitchinterval, normally 5 ms): the thread
-# holds it through the Python part of a compile, and the caller would wait
-# for its forced switch.  Applied only while a search with queued compiles is
-# in flight (_gil_handoff), then restored.
-SEARCH_SWITCH_INTERVAL = 1e-4
+# How soon the caller gets the GIL back from the witness-program thread when
+# a program upload or the search returns (sys.setswitchinterval, normally
+# 5 ms): the thread holds it through the Python part of a compile, and the
+# caller would wait for its forced switch.  Applied only while uploads and a
+# search with queued compiles are in flight (_gil_handoff), then restored.
+SEARCH_SWITCH_INTERVAL = 2e-5
 _HANDOFF = [0, None]              # searches in flight, the interval to restore
 _HANDOFF_LOCK = threading.Lock()
 
@@ -288,12 +288,12 @@ class WitnessEngine:
         # witness then costs one upload and one launch (materialize)
         queued = _prebuild_witness_programs(queries)
         try:
-            for q in queries:   # a failed load frees the programs already loaded
-                dps.append(self.dev.load(q.program))
-            if (self.asmjit_min_ops and hasattr(self.dev, "attach_asm")
-                    and count * sum(q.ops_per_eval for q in queries) >= self.asmjit_min_ops):
-                self._assemble(dps)
             with _gil_handoff(queued):
+                for q in queries:   # a failed load frees the programs already loaded
+                    dps.append(self.dev.load(q.program))
+                if (self.asmjit_min_ops and hasattr(self.dev, "attach_asm")
+                        and count * sum(q.ops_per_eval for q in queries) >= self.asmjit_min_ops):
+                    self._assemble(dps)
                 found, st = search_phased(self.dev, dps, self.seed, begin, count, flags)
             self.stats["searches"] += 1
             self.stats["programs"] += len(queries)

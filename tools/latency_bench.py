@@ -59,7 +59,8 @@ def main():
                 # as WitnessEngine.search: the witness program compiles on the
                 # host thread while the program uploads and the device searches
                 queued = _prebuild_witness_programs([q])
-                dp = eng.dev.load(q.program)
+                with _gil_handoff(queued):
+                    dp = eng.dev.load(q.program)
                 try:
                     with _gil_handoff(queued):
                         (idx,), st = search_phased(eng.dev, [dp], eng.seed, 0, eng.launch_count([q]), 3)
