@@ -89,6 +89,11 @@ int mg_device_count(int* n);
 int mg_init(int device, mg_ctx** out);
 int mg_free(mg_ctx* ctx);
 
+/* Upload a program (replaces the per-query z3 model construction the
+ * reference runs, mythril/support/model.py:15-63, with a device-resident
+ * program).  The desc's arrays are copied before the call returns; the device
+ * copy is queued on the context's stream, so every later call on the context
+ * sees it, and a copy failure is reported by the next call that waits. */
 int mg_prog_load(mg_ctx* ctx, const mg_prog_desc* desc, mg_prog** out);
 int mg_prog_free(mg_prog* prog);
 
