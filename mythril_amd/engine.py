@@ -386,7 +386,10 @@ class WitnessEngine:
         from .runtime import EngineError, trace_column, unpack_one
         t0 = time.perf_counter()
         p = q.trace_program
-        if [n.name for n in p.leaf_nodes] != [n.name for n in q.program.leaf_nodes]:
+        # a witness program built from the search program's stream shares its
+        # leaf table (compile_trace_native checked the leaf order)
+        if p.leaves is not q.program.leaves and \
+                [n.name for n in p.leaf_nodes] != [n.name for n in q.program.leaf_nodes]:
             # an EngineError, so get_model's handler sends the query to z3
             raise EngineError("witness program's leaf layout differs from the search program's")
         t1 = time.perf_counter()
