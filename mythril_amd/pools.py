@@ -517,13 +517,27 @@ def harvest(conjuncts: List[Node], leaves: Optional[List[Node]], pool_size: int 
             ra, rb = find(xa.name), find(xb.name)
             if ra != rb:
                 parent[ra] = rb
-    groups: Dict[str, List[int]] = {}
-    for name, props in list(proposals.items()):
-        groups.setdefault(find(name), []).extend(props)
-    for name in list(parent) + list(proposals):
-        merged = groups.get(find(name))
-        if merged:
-            proposals[name] = list(dict.fromkeys(proposals.get(name, []) + merged))
+    if parent:
+        groups: Dict[str, List[int]] = {}
+        for name, props in list(proposals.items()):
+            groups.setdefault(find(name), []).extend(props)
+        members: Dict[str, int] = {}
+        for name in set(parent) | set(proposals):
+            r = find(name)
+            members[r] = members.get(r, 0) + 1
+        uniq: Dict[str, List[int]] = {}   # each group's proposals, first occurrences, once
+        for name in list(parent) + list(proposals):
+            r = find(name)
+            # a group of one keeps its proposals as they are: the pool below
+            # takes first occurrences anyway, and _restrict only their maximum
+            merged = groups.get(r) if members[r] > 1 else None
+            if merged:
+                du = uniq.get(r)
+                if du is None:
+                    du = uniq[r] = list(dict.fromkeys(merged))
+                # = dict.fromkeys(own + merged): own first, then the group's others
+                own = dict.fromkeys(proposals.get(name, ()))
+                proposals[name] = list(own) + [v for v in du if v not in own]
     specs: Dict[str, LeafSpec] = {}
     uniq_consts = list(dict.fromkeys(consts))[:256]
     tails: Dict[int, List[int]] = {}   # width -> the constants' proposals, deduplicated
