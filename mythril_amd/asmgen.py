@@ -30,7 +30,7 @@ Registers (per lane; all clobbered by the block):
   v164 global-spill lane byte offset  v165 thread id  v168..v175 XR (result)
   v176..v183 XC (third operand / Philox output)  v184..v191 temporaries
   v240..v255  the program's narrow constants (interpreter)
-  s16..s95    chunk loop and interpreter state (see the constants below)
+  s16..s98    chunk loop and interpreter state (see the constants below)
 """
 import re
 
@@ -93,6 +93,8 @@ ARGP = 36         # s[36:37] AsmArgs (prologue only; then VALID)
 PROGP = 38        # s[38:39] ProgDev (prologue only)
 HIT = 38          # after the prologue: this wave has reported a witness (chunks only grow)
 TID, LO_SREG = 165, 0
+TRACE = 96        # s[96:97] trace rows (AsmArgs.trace; 0 in searches: STORE is then a no-op)
+NCAND = 98        # candidates per trace row (AsmArgs.ncand)
 # the pool digit of the last pooled leaf drawn in this chunk (Lleaf) and its
 # digit group (the asm leaf table's word 6, mw_kernels.hip asm_leaf_table;
 # reset to -1 at every chunk)
@@ -910,6 +912,35 @@ def build_handlers():
         g("s_waitcnt vmcnt(0) lgkmcnt(0)")
         g.write_n(XR)
 
+    # -------------------------------------------------------- trace rows (mg_eval_generated)
+    def store_rows(g, src, n):
+        """trace[(imm + k) * ncand + (cand - begin)] = v(src + k), k < n, from
+        the chunk's valid lanes only (rows validated against n_trace_rows,
+        mw_validate.cpp; the host sizes the buffer rows x ncand); no trace
+        buffer (searches): nothing"""
+        skip = g.L("ts")
+        g(f"s_cmp_eq_u64 {sr(TRACE, 2)}, 0", f"s_cbranch_scc1 {skip}",
+          f"s_mul_i32 {s(S[1])}, {s(CUR + 3)}, {s(NCAND)}", f"s_lshl_b32 {s(S[2])}, {s(NCAND)}, 2",
+          f"v_subrev_u32_e32 {v(T)}, {s(BEGIN)}, {v(CLO)}", f"v_add_u32_e32 {v(T)}, {s(S[1])}, {v(T)}",
+          f"v_lshlrev_b32_e32 {v(T)}, 2, {v(T)}",
+          f"s_mov_b64 {sr(EXECSV, 2)}, exec", f"s_mov_b64 exec, {sr(VALID, 2)}")
+        for k in range(n):
+            g(f"global_store_dword {v(T)}, {v(src + k)}, {sr(TRACE, 2)}")
+            if k + 1 < n:
+                g(f"v_add_u32_e32 {v(T)}, {s(S[2])}, {v(T)}")
+        g(f"s_mov_b64 exec, {sr(EXECSV, 2)}", "s_waitcnt vmcnt(0)")
+        g.label(skip)
+
+    @handler("STORE_W")
+    def _(g):
+        g.field("a", S[0]), g.fetch_w(S[0], XR)
+        store_rows(g, XR, 8)
+
+    @handler("STORE_N")
+    def _(g):
+        g.field("a", S[0]), g.fetch_n(S[0], XR)
+        store_rows(g, XR, 1)
+
     # -------------------------------------------------------- multiply
     def mul_full(g, hi):
         """XR = low 256 bits of XA * XB; with hi, XC = the high 256 bits.
@@ -962,6 +993,9 @@ def gen(mode="interp"):
       f"s_mov_b64 {sr(END, 2)}, {sr(DESC + 4, 2)}", f"s_mov_b32 {s(FLAGS)}, {s(DESC + 6)}",
       f"s_mov_b32 {s(NLDS)}, {s(DESC + 7)}", f"s_mov_b32 {s(GSTRIDE)}, {s(72)}", f"s_mov_b32 {s(NCH)}, {s(73)}",
       f"s_mov_b32 {s(GDX)}, {s(74)}", f"s_mov_b64 {sr(GSP, 2)}, {sr(76, 2)}", f"s_mov_b64 {sr(VERD, 2)}, {sr(78, 2)}",
+      # AsmArgs (continued): trace(2) ncand pad
+      f"s_load_dwordx4 {sr(72, 4)}, {sr(ARGP, 2)}, 0x40", "s_waitcnt lgkmcnt(0)",
+      f"s_mov_b64 {sr(TRACE, 2)}, {sr(72, 2)}", f"s_mov_b32 {s(NCAND)}, {s(74)}",
       # ProgDev: code(2) consts(2) leaves(2) pool(2) | n_spill npool n_insn pad
       f"s_load_dwordx8 {sr(DESC, 8)}, {sr(PROGP, 2)}, 0x0", f"s_load_dwordx4 {sr(72, 4)}, {sr(PROGP, 2)}, 0x20",
       "s_waitcnt lgkmcnt(0)",
@@ -1284,7 +1318,7 @@ def philox_sub(g):
 
 
 CLOBBERS = (", ".join(f'"v{i}"' for i in list(range(192)) + list(range(NK0, 256))) + ", "
-            + ", ".join(f'"s{i}"' for i in range(16, 96))
+            + ", ".join(f'"s{i}"' for i in range(16, 99))
             + ', "vcc", "scc", "m0", "memory"')
 
 

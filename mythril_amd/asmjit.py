@@ -103,8 +103,14 @@ def available() -> bool:
     return why_unavailable() is None
 
 
+_STORE_OPS = (isa.OPCODES["STORE_W"], isa.OPCODES["STORE_N"])
+
+
 def eligible(p: Program) -> bool:
-    return isa.asm_eligible(p.code, p.leaves, p.consts)
+    """asm-eligible search programs: trace rows (STORE_*) are written by the
+    asm interpreter only (mg_eval_generated), never by an assembled body"""
+    return (isa.asm_eligible(p.code, p.leaves, p.consts)
+            and not any(int(w) & 0xFF in _STORE_OPS for w in list(p.code)[0::4]))
 
 
 def kernel_name(p: Program) -> str:

@@ -24,8 +24,10 @@ struct AsmArgs {
   u32 flags, nlds, gstride, nchunks, gdx, pad;
   u32* spillbuf;
   u32* verdict;   // per-candidate verdicts at cand - begin (mg_eval_generated), or null
+  u32* trace;     // trace rows, row r of candidate cand at r * ncand + cand - begin (STORE_W / STORE_N), or null
+  u32 ncand, pad2;
 };
-static_assert(sizeof(AsmArgs) == 64, "AsmArgs layout (mythril_amd/asmgen.py)");
+static_assert(sizeof(AsmArgs) == 80, "AsmArgs layout (mythril_amd/asmgen.py)");
 static_assert(sizeof(ProgDev) == 48, "ProgDev layout (mythril_amd/asmgen.py)");
 
 }  // namespace mw

@@ -1345,11 +1345,17 @@ int mg_eval(mg_ctx* h, const mg_prog* hp, const uint32_t* leaves_soa, size_t nca
                      verdict, trace);
 }
 
-// Verdicts of generated candidates on the asm interpreter (mw_search_asm_kernel
-// with a verdict array); 1 = not applicable (the caller uses mw_eval_kernel).
-static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t count, uint32_t* verdict) {
+// Verdicts (and trace rows) of generated candidates on the asm interpreter
+// (mw_search_asm_kernel with a verdict array; STORE_W / STORE_N write row r of
+// candidate cand at trace[r * count + cand - begin], mw_eval_kernel's layout);
+// 1 = not applicable (the caller uses mw_eval_kernel).
+static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t count, uint32_t* verdict,
+                    uint32_t* trace) {
   if (!asm_enabled() || !p->asm_ok || begin + count < begin || count >= (1ull << 40)) return 1;
-  const bool assembled = p->afn != nullptr;   // its assembled kernel, else the asm interpreter
+  const size_t ntr = trace ? (size_t)p->desc.n_trace_rows * count : 0;
+  // trace offsets are 32-bit byte offsets in the kernel (asmgen.py store_rows)
+  if (trace && (count >= (1ull << 32) || ntr * 4 >= (1ull << 31))) return 1;
+  const bool assembled = p->afn != nullptr && !trace;   // its assembled kernel, else the asm interpreter
   u32 nlds = 0;
   if (!asm_lds_fit(p->dev.n_spill, p->dev.npool, &nlds)) return 1;
   const size_t lds = (size_t)nlds * kBlock * 4 + (size_t)p->dev.npool * 4;
@@ -1361,9 +1367,11 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
   const u64 gx = std::min<u64>(nchunks, (u64)c->ncu * 8);
   rc = ensure_spill(c, std::max<size_t>(4, (size_t)(p->dev.n_spill - nlds) * gx * kBlock * sizeof(u32)));
   if (rc) return rc;
-  Scratch s_v(c, count * 4);
+  // verdicts and trace rows in one device block: one readback
+  const size_t vb = count * 4, tb = ntr * 4;
+  Scratch s_v(c, vb + tb);
   if (!s_v.p) return fail(MG_E_NOMEM, "eval verdict alloc");
-  u32* d_v = s_v.u();
+  u32 *d_v = s_v.u(), *d_t = ntr ? d_v + count : nullptr;
   AsmArgs aa{};
   aa.seed = seed;
   aa.begin = begin;
@@ -1375,7 +1383,10 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
   aa.gdx = (u32)gx;
   aa.spillbuf = c->d_spill;
   aa.verdict = d_v;
-  hipError_t e = stage_upload(c, 1, assembled ? &p->dev : &p->adev, 1, &aa, 1);
+  aa.trace = d_t;
+  aa.ncand = (u32)count;
+  hipError_t e = ntr ? hipMemsetAsync(d_t, 0, tb, c->stream) : hipSuccess;
+  if (e == hipSuccess) e = stage_upload(c, 1, assembled ? &p->dev : &p->adev, 1, &aa, 1);
   if (e == hipSuccess && assembled) {
     if (launch_assembled(c, p, (u32)gx, c->d_progs, c->d_asmargs, c->d_min, nlds)) return MG_E_HIP;
   } else if (e == hipSuccess) {
@@ -1383,12 +1394,23 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
                        (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, nlds);
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, count * 4, hipMemcpyDeviceToHost, c->stream);
+  const bool pinned = vb + tb <= kReadbackMax && ensure_readback(c, vb + tb);
+  if (e == hipSuccess && pinned) {
+    e = hipMemcpyAsync(c->h_rb, d_v, vb + tb, hipMemcpyDeviceToHost, c->stream);
+  } else {
+    if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, vb, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && ntr) e = hipMemcpyAsync(trace, d_t, tb, hipMemcpyDeviceToHost, c->stream);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   s_v.synced = e == hipSuccess;
   if (e != hipSuccess)
     return fail(MG_E_HIP, std::string(assembled ? "eval (assembled kernel): " : "eval (asm interpreter): ") +
                               hipGetErrorString(e));
+  c->up_pending = false;   // the stream drained: a queued program upload has landed
+  if (pinned) {
+    std::memcpy(verdict, c->h_rb, vb);
+    if (ntr) std::memcpy(trace, c->h_rb + vb, tb);
+  }
   return 0;
 }
 
@@ -1401,8 +1423,8 @@ int mg_eval_generated(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t begi
     return fail(MG_E_ARG, std::string("mg_eval_generated: ") + why);
   Ctx* c = call.c.get();
   const Prog* p = call.ps[0].get();
-  if (!p->jit_ready() && !trace && verdict && count) {
-    const int rc = eval_asm(c, p, seed, begin, count, verdict);
+  if (!p->jit_ready() && verdict && count) {
+    const int rc = eval_asm(c, p, seed, begin, count, verdict, trace);
     if (rc != 1) return rc;
   }
   if (!p->jit_ready() || trace) return eval_common(c, p, nullptr, count, seed, begin, verdict, trace);

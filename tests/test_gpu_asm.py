@@ -218,3 +218,60 @@ def test_asm_search_reports_the_satisfying_lane(dev, k):
                 assert not va.any()              # nothing lower
     finally:
         dp.free()
+
+
+def both_traced(dev, p, seed, begin, n):
+    dp = dev.load(p)
+    try:
+        assert dev.engine_of(dp) == "asm"
+        va, ta = dev.eval_generated(dp, seed, begin, n)
+        with compiled_interpreter():
+            vi, ti = dev.eval_generated(dp, seed, begin, n)
+    finally:
+        dp.free()
+    return va, ta, vi, ti
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_asm_trace_rows(dev, seed):
+    """STORE_W / STORE_N on the asm interpreter (mg_eval_generated with a
+    trace): every trace row of random DAG terms (widths 1..256, wide and
+    narrow rows) equals the compiled interpreter's, at ragged counts (a last
+    chunk with invalid lanes) and offsets past 2^32."""
+    c, conj = _random_supported_dag(9100 + seed)
+    r = random.Random(seed)
+    terms, seen, stack = [], set(), list(conj)
+    while stack:
+        n = stack.pop()
+        if n.id in seen:
+            continue
+        seen.add(n.id)
+        if n.width and n.width > 0 and not n.is_array:
+            terms.append(n)
+        stack.extend(n.args or ())
+    r.shuffle(terms)
+    p = compile_program(conj, trace=terms[:12])
+    if not isa.asm_eligible(p.code, p.leaves, p.consts):
+        pytest.skip("lowered outside the asm opcode set")
+    assert p.n_trace_rows > 0
+    for begin, n in (((1 << 33) + 77, 4096 + 3 * seed + 1), (seed, 255)):
+        va, ta, vi, ti = both_traced(dev, p, DEFAULT_SEED + seed, begin, n)
+        assert np.array_equal(va, vi), (seed, begin)
+        assert np.array_equal(ta, ti), (seed, begin, int(np.count_nonzero(ta != ti)))
+
+
+def test_asm_witness_programs_of_the_corpus(dev, corpus):
+    """The witness program of every corpus query (its leaves traced) on the
+    asm interpreter gives the compiled interpreter's rows."""
+    from mythril_amd.engine import _witness_program
+    checked = 0
+    for name, q in corpus[:16] + corpus[-16:]:
+        p = q.program
+        wp = _witness_program(p, list(p.leaf_nodes))
+        if not isa.asm_eligible(wp.code, wp.leaves, wp.consts) or not wp.n_trace_rows:
+            continue
+        va, ta, vi, ti = both_traced(dev, wp, DEFAULT_SEED, 1 << 20, 1000)
+        assert np.array_equal(va, vi), name
+        assert np.array_equal(ta, ti), name
+        checked += 1
+    assert checked
