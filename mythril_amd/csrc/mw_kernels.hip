@@ -406,6 +406,7 @@ struct Prog {
   u64 ops_per_eval = 0;
   u64 sig = 0;                  // FNV-1a 64 of the program words (mythril_amd/jit.py signature)
   bool asm_ok = false;          // every opcode and leaf kind has a handler in mw_search_asm_kernel
+  bool trace_full = false;      // STOREs cover every trace row: an evaluation needs no zeroed trace block
   ProgDev adev{};               // dev with code = its predecoded copy (mw_asm_predecode) and leaves =
                                 // the asm leaf table (asm_leaf_table), in d_buf
   // specialised kernels (mg_prog_attach_kernel): one per part, launched in order
@@ -878,6 +879,22 @@ int mg_free(mg_ctx* h) {
   return 0;
 }
 
+// Every trace row is written by some STORE of the program (rows validated in
+// range, mw_validate.cpp); evaluations never exit early, so each STORE runs for
+// every candidate and the rows need no zeroing first.
+static bool trace_rows_covered(const mg_prog_desc* d) {
+  if (!d->n_trace_rows) return false;
+  std::vector<char> cov(d->n_trace_rows, 0);
+  size_t left = d->n_trace_rows;
+  for (size_t i = 0; i + 3 < d->ncode_words && left; i += 4) {
+    const u32 op = d->code[i] & 0xffu, r = d->code[i + 3];
+    const u32 n = op == MW_STORE_W ? 8u : op == MW_STORE_N ? 1u : 0u;
+    for (u32 k = 0; k < n; ++k)
+      if ((u64)r + k < d->n_trace_rows && !cov[r + k]) cov[r + k] = 1, --left;
+  }
+  return left == 0;
+}
+
 int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   if (!h || !d || !out) return fail(MG_E_ARG, "null argument");
   *out = nullptr;
@@ -903,6 +920,7 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   p->desc = *d;
   p->ops_per_eval = d->ops_per_eval;
   p->sig = prog_signature(d);
+  p->trace_full = trace_rows_covered(d);
   p->d_buf = (u32*)pool_get(c, total * sizeof(u32), &p->buf_cls);
   if (!p->d_buf) return fail(MG_E_NOMEM, "program upload allocation failed");
   // stage in the context's pinned buffer (after the previous upload from it has landed)
@@ -1309,7 +1327,7 @@ static int eval_common(Ctx* c, const Prog* p, const uint32_t* leaves_soa, size_t
   u32 *d_in = s_in.u(), *d_v = s_vt.u(), *d_t = ntr ? d_v + ncand : nullptr;
   if (nin && hipMemcpyAsync(d_in, leaves_soa, nin * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     return fail(MG_E_HIP, "eval input copy");
-  if (ntr) hipMemsetAsync(d_t, 0, tb, c->stream);
+  if (ntr && !p->trace_full) hipMemsetAsync(d_t, 0, tb, c->stream);
   hipLaunchKernelGGL(mw_eval_kernel, dim3((u32)gx), dim3(kBlock), (size_t)nlds * kBlock * 4, c->stream,
                      p->dev, (const u32*)d_in, (u64)ncand, seed, begin, d_v, d_t, c->d_spill, nlds);
   hipError_t e = hipGetLastError();
@@ -1385,7 +1403,7 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
   aa.verdict = d_v;
   aa.trace = d_t;
   aa.ncand = (u32)count;
-  hipError_t e = ntr ? hipMemsetAsync(d_t, 0, tb, c->stream) : hipSuccess;
+  hipError_t e = ntr && !p->trace_full ? hipMemsetAsync(d_t, 0, tb, c->stream) : hipSuccess;
   if (e == hipSuccess) e = stage_upload(c, 1, assembled ? &p->dev : &p->adev, 1, &aa, 1);
   if (e == hipSuccess && assembled) {
     if (launch_assembled(c, p, (u32)gx, c->d_progs, c->d_asmargs, c->d_min, nlds)) return MG_E_HIP;
