@@ -145,3 +145,21 @@ def test_one_entry_pool_leaves_fold():
     reads = lambda body: sum(1 for ln in body if ln.startswith("ds_read"))   # noqa: E731
     assert reads(folded) < reads(without)
     assert sum(1 for ln in folded if ln.startswith("v_")) < sum(1 for ln in without if ln.startswith("v_"))
+
+
+def test_traced_programs_stay_on_the_interpreter():
+    """STORE_W / STORE_N are asm-interpreter handlers only (trace rows of
+    mg_eval_generated): a traced program is asm-eligible but never assembled."""
+    from mythril_amd import isa
+    from mythril_amd.compiler import compile_program
+    from mythril_amd.ir import Ctx
+    c = Ctx()
+    x = c.var("x", 64)
+    conj = [c.app("bvult", x, c.const(1000, 64))]
+    traced = compile_program(conj, trace=[x])
+    plain = compile_program(conj)
+    assert isa.asm_eligible(traced.code, traced.leaves, traced.consts)
+    assert not asmjit.eligible(traced)
+    assert asmjit.eligible(plain)
+    # and the generated interpreter has both handlers
+    assert "Lh_STORE_W_" in "\n".join(asmgen.gen()) and "Lh_STORE_N_" in "\n".join(asmgen.gen())

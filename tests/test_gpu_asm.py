@@ -275,3 +275,23 @@ def test_asm_witness_programs_of_the_corpus(dev, corpus):
         assert np.array_equal(ta, ti), name
         checked += 1
     assert checked
+
+
+def test_asm_search_of_a_traced_program(dev):
+    """A program with STOREs searched on the asm interpreter (no trace buffer:
+    every STORE is a no-op) finds the compiled interpreter's lowest witness."""
+    c = Ctx()
+    x, y = c.var("x", 256), c.var("y", 8)
+    conj = [c.app("bvult", x, c.const(1 << 250, 256)), c.app("=", y, c.const(77, 8))]
+    p = compile_program(conj, trace=[x, y, c.app("bvadd", x, c.const(5, 256))])
+    assert p.n_trace_rows > 0 and isa.asm_eligible(p.code, p.leaves, p.consts)
+    dp = dev.load(p)
+    try:
+        assert dev.engine_of(dp) == "asm"
+        for flags in (0, isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT):
+            (fa,), sta = dev.search([dp], 11, 0, 1 << 16, flags)
+            with compiled_interpreter():
+                (fi,), sti = dev.search([dp], 11, 0, 1 << 16, flags)
+            assert fa == fi and fa is not None, flags
+    finally:
+        dp.free()
