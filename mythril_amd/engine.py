@@ -365,9 +365,13 @@ class WitnessEngine:
 
     @staticmethod
     def _ack_cells(q: Query, w: Witness, values: Dict[str, int], term_value) -> None:
+        arrays, functions, chunks = w.arrays, w.functions, q.arg_chunks
         for al in q.lowered.ack.values():
             args = []
-            for parts in q.arg_chunks[al.name]:
+            for parts in chunks[al.name]:
+                if len(parts) == 1:
+                    args.append(term_value(parts[0]))
+                    continue
                 v = 0
                 for k, t in enumerate(parts):
                     v |= term_value(t) << (256 * k)
@@ -375,15 +379,22 @@ class WitnessEngine:
             if al.value is not None:
                 val = args.pop()  # defined value (keccak inverse = hashed input)
             else:
-                val = _combine_chunks(values, al.name, al.width)
-            args = tuple(args)
+                val = values.get(al.name)
+                if val is None:
+                    val = _combine_chunks(values, al.name, al.width)
             if al.kind == "select":
-                w.arrays.setdefault(al.base, {})[args[0]] = val
+                cells = arrays.get(al.base)
+                if cells is None:
+                    cells = arrays[al.base] = {}
+                cells[args[0]] = val
             else:
-                w.functions.setdefault(al.base, {})[args] = val
+                cells = functions.get(al.base)
+                if cells is None:
+                    cells = functions[al.base] = {}
+                cells[tuple(args)] = val
 
     def _materialize_traced(self, q: Query, index: int, search_dp=None) -> Optional[Witness]:
-        from .runtime import EngineError, trace_column, unpack_one
+        from .runtime import EngineError, trace_column
         t0 = time.perf_counter()
         p = q.trace_program
         # a witness program built from the search program's stream shares its
@@ -403,7 +414,17 @@ class WitnessEngine:
         # seconds per step of the last traced witness (tools/latency_bench.py)
         self.last_materialize = {"program": t1 - t0, "load": t2 - t1, "eval": t3 - t2}
         col = trace_column(trace)   # the one candidate's rows, read per node below
-        values = {n.name: unpack_one(p, col, n) for n in p.leaf_nodes}
+        tmap, frm = p.trace_map, int.from_bytes
+        values = {}
+        for n in p.leaf_nodes:      # unpack_one, inlined
+            row, cls = tmap[n.id]
+            values[n.name] = frm(col[4 * row:4 * row + (32 if cls == "W" else 4)], "little")
         w = Witness(index, values)
-        self._ack_cells(q, w, values, lambda t: t.val if t.op == "const" else unpack_one(p, col, t))
+
+        def term_value(t):   # unpack_one, inlined: one call per traced term
+            if t.op == "const":
+                return t.val
+            row, cls = tmap[t.id]
+            return frm(col[4 * row:4 * row + (32 if cls == "W" else 4)], "little")
+        self._ack_cells(q, w, values, term_value)
         return w
