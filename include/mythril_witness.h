@@ -110,7 +110,13 @@ int mg_eval(mg_ctx* ctx, const mg_prog* prog, const uint32_t* leaves_soa, size_t
             uint32_t* verdict, uint32_t* trace);
 
 /* Evaluate one program on generated candidates [begin, begin+count): the
- * verdict/trace of exactly what mg_search explores (parity tests). */
+ * verdict/trace of exactly what mg_search explores (parity tests), trace row
+ * r of candidate begin+i at [r*count + i].  Programs the asm interpreter runs
+ * are evaluated there, trace rows included (its STORE_W / STORE_N handlers);
+ * the rest on the compiled interpreter.  The witness program's evaluation
+ * behind WitnessEngine.materialize, in place of z3's model()
+ * (mythril/laser/smt/solver/solver.py:68-77) for array cells and function
+ * arguments. */
 int mg_eval_generated(mg_ctx* ctx, const mg_prog* prog, uint64_t seed, uint64_t begin,
                       size_t count, uint32_t* verdict, uint32_t* trace);
 
