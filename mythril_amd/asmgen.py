@@ -748,6 +748,81 @@ def build_handlers():
         g.width(S[2]), g.canon(XR, S[2])
         g.write_w(XR)
 
+    def var_shift(g, kind):
+        """XR = XA shifted by the per-lane amount XB (W_SHL / W_LSHR / W_ASHR;
+        mw_alu.h wshl / wlshr / washr): amount >= w gives 0 (shl, lshr) or
+        the sign fill (ashr).  A barrel shifter: three limb stages (4, 2, 1
+        limbs, lanes select by bits 7..5 of the amount), then one funnel per
+        limb by bits 4..0."""
+        ge, tmp = SX, MSK2
+        fill = None
+        if kind == "ashr":
+            # sign-extend the w-bit value to 256 bits: (a ^ m) - m, m = 1 << (w - 1)
+            g.width(S[2])
+            g(f"s_sub_u32 {s(S[3])}, {s(S[2])}, 1", f"s_lshr_b32 {s(S[4])}, {s(S[3])}, 5",
+              f"s_and_b32 {s(S[3])}, {s(S[3])}, 31", f"s_lshl_b32 {s(S[3])}, 1, {s(S[3])}")
+            for k in range(8):
+                g(f"v_mov_b32_e32 {v(XC + k)}, 0")
+            g(f"s_set_gpr_idx_on {s(S[4])}, gpr_idx(DST)", f"v_mov_b32_e32 {v(XC)}, {s(S[3])}", "s_set_gpr_idx_off")
+            for k in range(8):
+                g(f"v_xor_b32_e32 {v(XA + k)}, {v(XA + k)}, {v(XC + k)}")
+            g.sub_chain(XA, XC, XA)
+            fill = T + 3
+            g(f"v_ashrrev_i32_e32 {v(fill)}, 31, {v(XA + 7)}")
+        # ge: the amount's limbs 1..7 nonzero, or limb 0 >= w
+        g(f"v_or3_b32 {v(T)}, {v(XB + 1)}, {v(XB + 2)}, {v(XB + 3)}",
+          f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 4)}, {v(XB + 5)}",
+          f"v_or3_b32 {v(T)}, {v(T)}, {v(XB + 6)}, {v(XB + 7)}")
+        g.width(S[2])
+        g(f"v_cmp_ne_u32_e64 {sr(ge, 2)}, 0, {v(T)}", f"v_cmp_ge_u32_e64 {sr(tmp, 2)}, {v(XB)}, {s(S[2])}",
+          "s_nop 1", f"s_or_b64 {sr(ge, 2)}, {sr(ge, 2)}, {sr(tmp, 2)}")
+        if kind == "ashr":   # shift by 255: every bit the sign
+            g(f"v_mov_b32_e32 {v(T + 4)}, 0xff", "s_nop 1",
+              f"v_cndmask_b32_e64 {v(XB)}, {v(XB)}, {v(T + 4)}, {sr(ge, 2)}")
+        for st in range(3):
+            n = 1 << st
+            g(f"v_and_b32_e32 {v(T)}, {1 << (5 + st)}, {v(XB)}", f"v_cmp_ne_u32_e32 vcc, 0, {v(T)}")
+            g.nop_vcc()
+            order = range(7, -1, -1) if kind == "shl" else range(8)
+            for k in order:
+                src = k - n if kind == "shl" else k + n
+                if 0 <= src < 8:
+                    g(f"v_cndmask_b32_e32 {v(XA + k)}, {v(XA + k)}, {v(XA + src)}, vcc")
+                elif fill is not None:
+                    g(f"v_cndmask_b32_e32 {v(XA + k)}, {v(XA + k)}, {v(fill)}, vcc")
+                else:
+                    g(f"v_cndmask_b32_e64 {v(XA + k)}, {v(XA + k)}, 0, vcc")
+        g(f"v_and_b32_e32 {v(T + 1)}, 31, {v(XB)}")
+        if kind == "shl":
+            # fshl(hi, lo, b) = alignbit(hi, lo, 32 - b), and hi itself for b = 0
+            g(f"v_sub_u32_e32 {v(T + 2)}, 32, {v(T + 1)}", f"v_cmp_eq_u32_e32 vcc, 0, {v(T + 1)}")
+            for k in range(7, 0, -1):
+                g(f"v_alignbit_b32 {v(XR + k)}, {v(XA + k)}, {v(XA + k - 1)}, {v(T + 2)}")
+            g(f"v_lshlrev_b32_e32 {v(XR)}, {v(T + 1)}, {v(XA)}")
+            g.nop_vcc()
+            for k in range(1, 8):
+                g(f"v_cndmask_b32_e32 {v(XR + k)}, {v(XR + k)}, {v(XA + k)}, vcc")
+        else:
+            for k in range(7):
+                g(f"v_alignbit_b32 {v(XR + k)}, {v(XA + k + 1)}, {v(XA + k)}, {v(T + 1)}")
+            if fill is None:
+                g(f"v_lshrrev_b32_e32 {v(XR + 7)}, {v(T + 1)}, {v(XA + 7)}")
+            else:
+                g(f"v_alignbit_b32 {v(XR + 7)}, {v(fill)}, {v(XA + 7)}, {v(T + 1)}")
+        if kind != "ashr":
+            for k in range(8):
+                g(f"v_cndmask_b32_e64 {v(XR + k)}, {v(XR + k)}, 0, {sr(ge, 2)}")
+
+    for _name, _kind in (("W_SHL", "shl"), ("W_LSHR", "lshr"), ("W_ASHR", "ashr")):
+        def _h(g, kind=_kind):
+            g.field("a", S[0]), g.field("b", S[1])
+            g.fetch_w(S[0], XA), g.fetch_w(S[1], XB)
+            var_shift(g, kind)
+            if kind != "lshr":
+                g.width(S[2]), g.canon(XR, S[2])
+            g.write_w(XR)
+        handlers[_name] = _h
+
     @handler("W_ZEXTN")
     def _(g):
         g.field("a", S[0]), g.fetch_n(S[0], XR)

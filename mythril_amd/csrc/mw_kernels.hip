@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -521,10 +522,23 @@ inline u64 hid(const void* h) { return (u64)(uintptr_t)h; }
 // per-call scratch come from power-of-two size classes (from 4 KiB) and go
 // back there, instead of a hipMalloc and a hipFree per call (hipFree waits for
 // the whole device; on the get_model path a query loads, searches and frees a
-// program, and a witness loads and frees another).  Up to kPoolCacheBytes stay
-// cached per context; mg_free releases them.  Every call synchronises its
-// stream before it returns a buffer, so a reused buffer has no work pending.
-constexpr size_t kPoolCacheBytes = size_t(512) << 20;
+// program, and a witness loads and frees another).  Idle buffers are capped
+// for the whole process, over all contexts (MYTHRIL_AMD_POOL_CACHE_MB, default
+// 256): another context on the same device (a second Device, the keccak
+// service) never meets an allocation failure behind more than that much
+// cached memory; mg_free releases a context's buffers.  Every call
+// synchronises its stream before it returns a buffer, so a reused buffer has
+// no work pending.
+std::atomic<size_t> g_pool_cached{0};
+
+size_t pool_cache_limit() {
+  static const size_t lim = [] {
+    const char* e = getenv("MYTHRIL_AMD_POOL_CACHE_MB");
+    long mb = e ? atol(e) : 256;
+    return size_t(mb < 0 ? 0 : mb) << 20;
+  }();
+  return lim;
+}
 
 size_t pool_class(size_t bytes) {
   size_t k = 4096;
@@ -536,6 +550,7 @@ void pool_drain(Ctx* c) {
   for (auto& kv : c->pool)
     for (void* q : kv.second) hipFree(q);
   c->pool.clear();
+  g_pool_cached -= c->pool_cached;
   c->pool_cached = 0;
 }
 
@@ -547,6 +562,7 @@ void* pool_get(Ctx* c, size_t bytes, size_t* cls) {
     void* q = it->second.back();
     it->second.pop_back();
     c->pool_cached -= k;
+    g_pool_cached -= k;
     return q;
   }
   void* q = nullptr;
@@ -560,7 +576,8 @@ void* pool_get(Ctx* c, size_t bytes, size_t* cls) {
 
 void pool_put(Ctx* c, void* q, size_t cls) {
   if (!q) return;
-  if (c->pool_cached + cls > kPoolCacheBytes) {
+  if (g_pool_cached.fetch_add(cls) + cls > pool_cache_limit()) {
+    g_pool_cached -= cls;
     hipFree(q);
     return;
   }

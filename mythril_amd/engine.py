@@ -26,7 +26,7 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 from . import isa
 from .ccompile import compile_query
 from .compiler import LeafSpec, Program, Unsupported
-from .ir import BOOL, Ctx, Node
+from .ir import BOOL, Ctx, Node, free_vars
 from .lower import Lowered, lower_constraints, needs_lowering
 from .pools import harvest
 
@@ -109,7 +109,9 @@ def _prepare(conjuncts, ctx, use_pools, timings) -> Query:
     t1 = time.perf_counter()
     # low.nodes: the topo of the flattened conjuncts, computed once by
     # lower_constraints; harvest collects the var leaves in the same loop
-    specs = harvest(low.conjuncts, None, nodes=low.nodes) if use_pools else {}
+    specs = harvest(low.conjuncts, None, nodes=low.nodes,
+                    memo=ctx.__dict__.setdefault("_harvest", {}) if getattr(ctx, "long_lived", False) else None) \
+        if use_pools else {}
     t2 = time.perf_counter()
     prog = compile_query(low.conjuncts, leaf_specs=specs, reach=(low.flat, low.nodes))
     if timings is not None:
@@ -127,9 +129,13 @@ def _prepare(conjuncts, ctx, use_pools, timings) -> Query:
             per.append(parts)
             arg_terms.extend(parts)
         arg_chunks[al.name] = per
-    traced = list(prog.leaf_nodes) + arg_terms
     # the search program's leaves lead the trace list in its order, so the witness
-    # program numbers them identically: same candidate generator, same values
+    # program numbers them identically: same candidate generator, same values;
+    # then the variables only a cell index reads (traced too: the witness
+    # carries their values, so the cell and the formula agree)
+    have = {n.id for n in prog.leaf_nodes}
+    extra = [v for v in free_vars(arg_terms) if v.op == "var" and v.id not in have]
+    traced = list(prog.leaf_nodes) + extra + arg_terms
     q = Query(ctx, conj, low, prog, lambda: _witness_program(prog, traced), arg_terms)
     q.arg_chunks = arg_chunks
     return q
@@ -158,7 +164,7 @@ PREBUILD_MAX_TERMS = 512
 # caller would wait for its forced switch.  Applied only while uploads and a
 # search with queued compiles are in flight (_gil_handoff), then restored.
 SEARCH_SWITCH_INTERVAL = 2e-5
-_HANDOFF = [0, None]              # searches in flight, the interval to restore
+_HANDOFF = [0, None, None]        # searches in flight, the interval to restore, the one set
 _HANDOFF_LOCK = threading.Lock()
 
 
@@ -171,13 +177,15 @@ def _gil_handoff(active: bool):
         if _HANDOFF[0] == 0:
             _HANDOFF[1] = sys.getswitchinterval()
             sys.setswitchinterval(min(_HANDOFF[1], SEARCH_SWITCH_INTERVAL))
+            _HANDOFF[2] = sys.getswitchinterval()    # as stored (microseconds)
         _HANDOFF[0] += 1
     try:
         yield
     finally:
         with _HANDOFF_LOCK:
             _HANDOFF[0] -= 1
-            if _HANDOFF[0] == 0:
+            # restored only if nobody else changed it meanwhile
+            if _HANDOFF[0] == 0 and sys.getswitchinterval() == _HANDOFF[2]:
                 sys.setswitchinterval(_HANDOFF[1])
 
 
@@ -259,10 +267,21 @@ def _combine_chunks(values: Dict[str, int], name: str, width: int) -> int:
 
 
 class WitnessEngine:
-    """Owns one device context; everything goes through the C-ABI."""
+    """Owns one device context; everything goes through the C-ABI.
+
+    The witnesses ``search`` returns are NOT re-evaluated on the device by
+    default: the search launch found their index satisfying, and their
+    values come from the leaf generator (or a witness program) at that
+    index.  The drop-in re-checks every witness with z3 before it is used
+    (model.py, z3bridge.model_from_witness) and the tests with the oracle;
+    other callers that want a device-side check pass ``verify=True`` (one
+    mg_eval_generated of the search program at the index per witness; a
+    witness it does not confirm is dropped and counted in
+    ``stats["verify_rejects"]``)."""
 
     def __init__(self, device: int = 0, seed: int = DEFAULT_SEED, budget: int = DEFAULT_BUDGET, dev=None,
-                 op_budget: Optional[int] = DEFAULT_OP_BUDGET, asmjit_min_ops: Optional[int] = DEFAULT_ASMJIT_MIN_OPS):
+                 op_budget: Optional[int] = DEFAULT_OP_BUDGET, asmjit_min_ops: Optional[int] = DEFAULT_ASMJIT_MIN_OPS,
+                 verify: bool = False):
         if dev is None:
             from .runtime import Device  # raises EngineUnavailable without the HIP library / GPU
             dev = Device(device)
@@ -271,6 +290,7 @@ class WitnessEngine:
         self.budget = budget
         self.op_budget = op_budget
         self.asmjit_min_ops = asmjit_min_ops   # None / 0: never assemble
+        self.verify = verify
         self.stats = {"searches": 0, "programs": 0, "hits": 0, "evals": 0, "kernel_ms": 0.0, "assembled": 0,
                       "assemble_s": 0.0}
 
@@ -283,6 +303,7 @@ class WitnessEngine:
             return []
         count = count or self.launch_count(queries)
         dps = []
+        hits = set()
         # the witness programs compile on a host thread while the programs
         # upload and the device searches (those calls release the GIL): a
         # witness then costs one upload and one launch (materialize)
@@ -302,12 +323,29 @@ class WitnessEngine:
             out: List[Optional[Witness]] = []
             for q, dp, idx in zip(queries, dps, found):
                 w = self.materialize(q, idx, dp) if idx is not None else None
+                if w is not None and self.verify:
+                    v, _ = self.dev.eval_generated(dp, self.seed, idx, 1, trace=False)
+                    if not int(v[0]):
+                        log.warning("witness engine: the search program does not hold at index %d", idx)
+                        self.stats["verify_rejects"] = self.stats.get("verify_rejects", 0) + 1
+                        w = None
                 if w is not None:
                     self.stats["hits"] += 1
+                    hits.add(id(q))
                 out.append(w)
         finally:
             for dp in dps:
                 dp.free()
+            if queued:
+                # the queued compiles of queries without a witness (all of them
+                # when the search raised) are withdrawn: they would hold the GIL
+                # against the caller's next prepare() and keep the queries alive,
+                # and a later search's compiles would queue behind them
+                for q in queries:
+                    f = q._trace_future
+                    if f is not None and id(q) not in hits:
+                        f.cancel()
+                        q._trace_future = None
         return out
 
     def _assemble(self, dps) -> None:
@@ -398,9 +436,13 @@ class WitnessEngine:
         t0 = time.perf_counter()
         p = q.trace_program
         # a witness program built from the search program's stream shares its
-        # leaf table (compile_trace_native checked the leaf order)
+        # leaf table (compile_trace_native checked the leaf order).  Otherwise
+        # the search program's leaves must lead the witness program's in the
+        # same order; it may have more: variables only a cell index reads and
+        # no conjunct (a DependencyPruner tuple `f(x) == 1` reads no x), whose
+        # values no verdict depends on
         if p.leaves is not q.program.leaves and \
-                [n.name for n in p.leaf_nodes] != [n.name for n in q.program.leaf_nodes]:
+                [n.name for n in p.leaf_nodes[:len(q.program.leaf_nodes)]] != [n.name for n in q.program.leaf_nodes]:
             # an EngineError, so get_model's handler sends the query to z3
             raise EngineError("witness program's leaf layout differs from the search program's")
         t1 = time.perf_counter()

@@ -7,7 +7,10 @@
    ``select(ite(c,A,B),j) = ite(c, select(A,j), select(B,j))``.  Every remaining
    base read ``select(A, j)`` becomes a fresh leaf (**Ackermannisation**):
    named ``A@<hex>`` for a concrete index (so the same cell is the same leaf in
-   every program), ``A@s<k>`` otherwise.
+   every program), ``A@s<h>`` otherwise, ``h`` a structural hash of the index
+   term (not its position in the query: a conjunct lowers to the same terms
+   in every set that holds it, which lets ``lower_constraints`` reuse a
+   conjunct's lowering across queries).
 2. **Uninterpreted functions** (``mythril/laser/smt/function.py``; the keccak
    UFs ``keccak256_N`` / ``keccak256_N-1`` of
    ``keccak_function_manager.py:71-84``, ``Power`` of
@@ -40,6 +43,7 @@ for (:class:`AckLeaf`) so a witness can be turned back into a model.
 """
 from __future__ import annotations
 
+import zlib
 from dataclasses import dataclass, field
 from operator import attrgetter
 from typing import Dict, List, Optional, Tuple
@@ -77,7 +81,6 @@ class _Rewriter:
         self.by_base: Dict[str, List[AckLeaf]] = {}
         self.leaf_of_key: Dict[tuple, Node] = {}
         self.inner_apply: Dict[int, tuple] = {}   # leaf id of f(x) -> (f, x)
-        self.nsym = 0
         self.seg_memo: Dict[int, List[Node]] = {}
         self.chunk_memo: Dict[int, List[Node]] = {}
 
@@ -310,8 +313,7 @@ class _Rewriter:
             nm = f"{base}@" + ",".join(f"{a.val:x}" for a in args)
         else:
             key = (base,) + tuple(("t", a.id) for a in args)
-            self.nsym += 1
-            nm = f"{base}@s{self.nsym}"
+            nm = f"{base}@s{_shash_args(self.ctx, args):016x}"
         return key, nm
 
     def read_leaf(self, kind: str, base: str, args: Tuple[Node, ...], width: int) -> Node:
@@ -329,8 +331,7 @@ class _Rewriter:
         """An application whose value is a term (no free leaf); still congruence-checked."""
         key = ("def", base) + tuple(("t", a.id) for a in args)
         if key not in self.leaf_of_key:
-            self.nsym += 1
-            nm = f"{base}@d{self.nsym}"
+            nm = f"{base}@d{_shash_args(self.ctx, args):016x}"
             al = AckLeaf(nm, "apply", base, args, width, value=value)
             self.ack[nm] = al
             self.by_base.setdefault(("apply", base), []).append(al)
@@ -544,21 +545,37 @@ class _Rewriter:
             return c.false()
         return cond if t1 else (cond.args[0] if cond.op == "not" else c.app("not", cond))
 
-    def congruence(self) -> List[Node]:
+    def congruence(self, memo: Optional[dict] = None) -> List[Node]:
+        """memo: the pairs' conjuncts kept with a long-lived context (a pair of
+        reads is the same pair, by leaf name, in every set that holds both)."""
         c = self.ctx
         out = []
         for (kind, base), reads in self.by_base.items():
             for t, u in _pair_order(reads):
-                    if all(a.op == "const" for a in t.args) and all(a.op == "const" for a in u.args):
-                        continue  # distinct concrete cells: nothing to relate
-                    if any(_never_equal(x, y) for x, y in zip(t.args, u.args)):
-                        continue  # e.g. cells base+3 and base+7 of one symbolic offset
-                    same = [self.eq(*_fold_offsets(c, x, y)) for x, y in zip(t.args, u.args)]
-                    prem = c.app("and", *same) if len(same) > 1 else same[0]
-                    vt = t.value if t.value is not None else self.wide_var(t.name, t.width)
-                    vu = u.value if u.value is not None else self.wide_var(u.name, u.width)
-                    out.append(c.app("=>", prem, self.eq(vt, vu)))
+                if memo is not None:
+                    got = memo.get((t.name, u.name), 0)
+                    if got != 0:
+                        if got is not None:
+                            out.append(got)
+                        continue
+                r = self._pair(t, u)
+                if memo is not None:
+                    memo[(t.name, u.name)] = r
+                if r is not None:
+                    out.append(r)
         return out
+
+    def _pair(self, t: AckLeaf, u: AckLeaf) -> Optional[Node]:
+        c = self.ctx
+        if all(a.op == "const" for a in t.args) and all(a.op == "const" for a in u.args):
+            return None   # distinct concrete cells: nothing to relate
+        if any(_never_equal(x, y) for x, y in zip(t.args, u.args)):
+            return None   # e.g. cells base+3 and base+7 of one symbolic offset
+        same = [self.eq(*_fold_offsets(c, x, y)) for x, y in zip(t.args, u.args)]
+        prem = c.app("and", *same) if len(same) > 1 else same[0]
+        vt = t.value if t.value is not None else self.wide_var(t.name, t.width)
+        vu = u.value if u.value is not None else self.wide_var(u.name, u.width)
+        return c.app("=>", prem, self.eq(vt, vu))
 
 
 _POW2_OPS = frozenset({"bvudiv", "bvurem", "bvmul", "bvand", "bvshl", "bvlshr"})
@@ -573,6 +590,62 @@ _width = attrgetter("width")
 _ORDER = {"bvult": ("u", False, True), "bvugt": ("u", True, True), "bvule": ("u", False, False),
           "bvuge": ("u", True, False), "bvslt": ("s", False, True), "bvsgt": ("s", True, True),
           "bvsle": ("s", False, False), "bvsge": ("s", True, False)}
+
+
+_M64 = (1 << 64) - 1
+
+
+def _shash_args(ctx: Ctx, args) -> int:
+    """A 64-bit structural hash of terms (op, width, params, value, name and
+    the operands' hashes; stable across processes and contexts), memoised per
+    node in the context."""
+    memo = ctx.__dict__.setdefault("_shash", {})
+    h = 0xCBF29CE484222325
+    for a in args:
+        h = ((h ^ _shash(a, memo)) * 0x100000001B3) & _M64
+    return h
+
+
+def _shash(root: Node, memo: Dict[int, int]) -> int:
+    got = memo.get(root.id)
+    if got is not None:
+        return got
+    for n in _unhashed(root, memo):
+        h = zlib.crc32(n.op.encode())
+        for x in (n.width, n.dom or 0, *n.params):
+            h = ((h ^ (x & _M64)) * 0x100000001B3) & _M64
+        if n.val is not None:
+            v = n.val
+            while True:
+                h = ((h ^ (v & _M64)) * 0x100000001B3) & _M64
+                v >>= 64
+                if not v:
+                    break
+        if n.name is not None:
+            h = ((h ^ zlib.crc32(n.name.encode())) * 0x100000001B3) & _M64
+        for a in n.args:
+            h = ((h ^ memo[a.id]) * 0x100000001B3 + 1) & _M64
+        memo[n.id] = h
+    return memo[root.id]
+
+
+def _unhashed(root: Node, memo: Dict[int, int]) -> List[Node]:
+    """the nodes under root with no hash yet, operands first"""
+    out, stack = [], [(root, False)]
+    seen = set()
+    while stack:
+        n, done = stack.pop()
+        if done:
+            out.append(n)
+            continue
+        if n.id in memo or n.id in seen:
+            continue
+        seen.add(n.id)
+        stack.append((n, True))
+        for a in reversed(n.args):
+            if a.id not in memo and a.id not in seen:
+                stack.append((a, False))
+    return out
 
 
 def _zeros(c: Ctx, n: int) -> List[Node]:
@@ -632,9 +705,36 @@ def _never_equal(x: Node, y: Node) -> bool:
 
 
 def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
-    rw = _Rewriter(ctx)
-    out = [rw.rw(cj) for cj in conjuncts]
-    cong = rw.congruence()
+    """Rewrite every conjunct, Ackermannise, add the congruence conjuncts.
+
+    In a context marked ``long_lived`` (z3bridge.ConjunctCache's: one per
+    Mythril process, where successor sets share their conjuncts) each
+    conjunct's rewrite and the array / function reads it makes are kept
+    (``ctx._lowered``, by conjunct id) and reused by every later set that
+    holds it; only the congruence over the set's reads is built per query.
+    Leaf names depend on the read alone (``_key_name``), so a rewrite is the
+    same in every set, and the reads are collected in the order one walk of
+    the whole set meets them: the program is the same either way."""
+    lowered = ctx.__dict__.get("_lowered") if getattr(ctx, "long_lived", False) else None
+    if lowered is None:
+        rw = _Rewriter(ctx)
+        out = [rw.rw(cj) for cj in conjuncts]
+    else:
+        out, ack = [], {}
+        for cj in conjuncts:
+            e = lowered.get(cj.id)
+            if e is None:
+                r1 = _Rewriter(ctx)
+                e = lowered[cj.id] = (r1.rw(cj), list(r1.ack.values()))
+            out.append(e[0])
+            for al in e[1]:
+                if al.name not in ack:
+                    ack[al.name] = al
+        rw = _Rewriter(ctx)
+        rw.ack = ack
+        for al in ack.values():
+            rw.by_base.setdefault((al.kind, al.base), []).append(al)
+    cong = rw.congruence(ctx.__dict__.setdefault("_pairs", {}) if lowered is not None else None)
     flat = _flatten(out + cong)
     nodes = topo(flat)
     if nodes and max(map(_width, nodes)) > MAXW:   # every consumer chunks its wide operands; none may remain

@@ -198,18 +198,30 @@ def _gpu_model(constraints, timeout):
         return None
     STATS["gpu_witnesses"] += 1
     try:
-        zm = z3bridge.model_from_witness(raws, script, witness, timeout)
+        zm, slow = z3bridge.recheck(raws, script, witness, timeout, PINNED_CHECK_MS)
     except Exception as e:   # fail closed: the reference answers
         STATS["recheck_errors"] = STATS.get("recheck_errors", 0) + 1
         log.warning("witness engine: z3 re-check failed (%s); z3 answers", e)
         return None
     if zm is None:
         return None
+    if slow:
+        # visible divergence risk (SURVEY §7 hard part 5): z3 needed more than
+        # the pinned budget even with every symbol pinned, so the reference's
+        # check of the unpinned formula may well have timed out (unknown ->
+        # UnsatError, a pruned state) where this path answers sat
+        STATS["slow_rechecks"] = STATS.get("slow_rechecks", 0) + 1
+        log.warning("witness engine: z3 confirmed a GPU witness only after the pinned re-check budget "
+                    "(%d ms); the reference solver may have answered unknown on this query", PINNED_CHECK_MS)
     STATS["z3_confirmed"] += 1
     from mythril.laser.smt.model import Model
     return Model([zm])
 
 
+# z3's budget for the re-check of a witness with every symbol pinned; a
+# re-check that needs more is retried with the query's timeout and counted
+# (STATS["slow_rechecks"], logged)
+PINNED_CHECK_MS = int(os.environ.get("MYTHRIL_AMD_PINNED_CHECK_MS", "250"))
 MINIMIZE_HINTS = os.environ.get("MYTHRIL_AMD_MINIMIZE_HINTS", "0") == "1"
 MINIMIZE_ROUNDS = int(os.environ.get("MYTHRIL_AMD_MINIMIZE_ROUNDS", "8"))   # device descent searches
 

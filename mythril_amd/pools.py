@@ -417,13 +417,38 @@ def _const_props(consts, m: int, split_bytes: bool):
                 yield (c >> (8 * i)) & 0xFF
 
 
+def _cmp_effect(n: Node):
+    """What one comparison node contributes to harvest: the proposals its
+    constant side projects onto leaves (per leaf, in order), the whole-word
+    proposals of the concats on the way, and (for =) the partial bit fixes."""
+    op = n.op
+    props: Dict[str, List[int]] = {}
+    words: Dict[int, List[int]] = {}
+    part: List[Dict[str, List[int]]] = []
+    a, b = n.args
+    for x, k in ((a, b), (b, a)):
+        if k.op == "const" and x.op != "const":
+            deltas = (0,) if op in ("=", "distinct") else (0, 1, -1)
+            for d in deltas:
+                _project(x, k.val + d, props, words=words)
+            if op == "=" and x.width != BOOL:
+                f: Dict[str, List[int]] = {}
+                _assign(x, k.val, 0, x.width - 1, f)
+                if any(m != (1 << w) - 1 for m, _, w in f.values()):
+                    part.append(f)
+    return props, words, part
+
+
 def harvest(conjuncts: List[Node], leaves: Optional[List[Node]], pool_size: int = 32,
             random_share: float = 0.25, restrict: bool = True,
-            nodes: Optional[List[Node]] = None) -> Dict[str, LeafSpec]:
+            nodes: Optional[List[Node]] = None, memo: Optional[dict] = None) -> Dict[str, LeafSpec]:
     """nodes: topo(conjuncts) when the caller has it (prepare: Lowered.nodes,
     the same walk without the top-level `and` nodes, which no rule reads).
     leaves None: every var of `nodes`, first occurrence of each name in walk
-    order (collected by the same loop that reads the constants)."""
+    order (collected by the same loop that reads the constants).
+    memo: a dict kept with a long-lived context (engine.prepare passes the
+    context's), holding each comparison node's contribution (_cmp_effect):
+    the same proposals in the same order, computed once per node."""
     if nodes is None:
         nodes = topo(conjuncts)
     collect = leaves is None
@@ -471,17 +496,25 @@ def harvest(conjuncts: List[Node], leaves: Optional[List[Node]], pool_size: int 
         if op in _CMP and len(n.args) == 2:
             if op == "=":
                 eq2.append(n)
-            a, b = n.args
-            for x, k in ((a, b), (b, a)):
-                if k.op == "const" and x.op != "const":
-                    deltas = (0,) if op in ("=", "distinct") else (0, 1, -1)
-                    for d in deltas:
-                        _project(x, k.val + d, proposals, words=word_props)
-                    if op == "=" and x.width != BOOL:
-                        f: Dict[str, List[int]] = {}
-                        _assign(x, k.val, 0, x.width - 1, f)
-                        if any(m != (1 << w) - 1 for m, _, w in f.values()):
-                            dm.append(f)      # fixes only part of some leaf's bits
+            eff = memo.get(n.id) if memo is not None else None
+            if eff is None:
+                eff = _cmp_effect(n)
+                if memo is not None:
+                    memo[n.id] = eff
+            props, words, part = eff
+            for name, vs in props.items():
+                got = proposals.get(name)
+                if got is None:
+                    proposals[name] = list(vs)
+                else:
+                    got.extend(vs)
+            for wid, vs in words.items():
+                got = word_props.get(wid)
+                if got is None:
+                    word_props[wid] = list(vs)
+                else:
+                    got.extend(vs)
+            dm.extend(part)                    # facts fixing only part of some leaf's bits
     # packed-array indexing: t / K == c and t % K == r -> t = c*K + r, tried first
     combos = _combine_partial(dm)
     # alignment facts: (= (bvurem x K) 0)  ->  x should be a multiple of K

@@ -101,7 +101,8 @@ class Query:
     constraints: List[Node]        # world-state constraints + keccak conditions
     sat: Optional[bool]            # True for the followed successor; None = unknown
     keccak_cond: Optional[Node] = None   # the manager's conditions: the last element of constraints
-    kind: str = "jumpi"            # "jumpi", or the detection module whose get_model asks it
+    kind: str = "jumpi"            # "jumpi", or the detection module / plugin whose get_model asks it
+    tuple_form: bool = False       # get_model((...,)): a tuple, so no keccak conditions (model.py:35-36)
 
 
 @dataclass
@@ -139,13 +140,30 @@ class ConcolicLaser:
         self.annotations: List[Tuple[str, int, int, List[Node], Node]] = []
         self.tx_anns: set = set()
         self.tx = 0
+        # PredictableVars (dependence_on_predictable_vars.py): node id -> the
+        # PredictableValueAnnotation operations it carries
+        self.pred: Dict[int, frozenset] = {}
+        self.deps = DependencyPruner()
+        self.mutated = False                        # MutationPruner's MutationAnnotation (this tx)
+        self.creation_txs: set = set()
+        self.deleted = False                        # SELFDESTRUCT ran: later message calls are skipped
+        self.sequence: List[int] = []               # world_state.transaction_sequence: the txs that ended without revert
 
     # ---------------------------------------------------------------- terms
     @staticmethod
-    def _jumpdests(code: bytes):
+    def _jumpdests(code):
+        """JUMPDEST offsets.  ``code`` is bytes, or a list of ints and 8-bit
+        terms: runtime code returned by a constructor that patched symbolic
+        immutables into it (transaction_models.py:252-262 assign_bytecode of
+        the RETURN data; disassembler/asm.py:120-140 keeps symbolic PUSH
+        arguments).  A symbolic byte is never an opcode here (it sits inside
+        PUSH data)."""
         out, i = set(), 0
         while i < len(code):
             op = code[i]
+            if not isinstance(op, int):
+                i += 1
+                continue
             if op == 0x5B:
                 out.add(i)
             i += (op - 0x5F + 1) if 0x60 <= op <= 0x7F else 1
@@ -176,10 +194,11 @@ class ConcolicLaser:
         annotations from the operands to the result as smt/bitvec.py does
         (not through array reads: BaseArray.__getitem__ starts a fresh BitVec)."""
         r = self._app(op, *args, params=params)
-        if self.ann and op not in ("select", "store", "apply"):
-            u = frozenset().union(*[self.ann.get(a.id, frozenset()) for a in args])
-            if u:
-                self.ann[r.id] = self.ann.get(r.id, frozenset()) | u
+        for tags in (self.ann, self.pred):
+            if tags and op not in ("select", "store", "apply"):
+                u = frozenset().union(*[tags.get(a.id, frozenset()) for a in args])
+                if u:
+                    tags[r.id] = tags.get(r.id, frozenset()) | u
         return r
 
     def _app(self, op: str, *args: Node, params=()) -> Node:
@@ -312,22 +331,42 @@ class ConcolicLaser:
         body = [x for x in list(self.constraints) + list(extra) if not (x.op == "const" and x.val)]
         return body + tail
 
-    def module_query(self, kind: str, extra, base: Optional[List[Node]] = None) -> None:
-        """A detection module's get_model(constraints + extra): recorded with
-        status sat when the concrete model satisfies it, else unknown."""
+    def module_query(self, kind: str, extra, base: Optional[List[Node]] = None, first: bool = False) -> Optional[bool]:
+        """A detection module's get_model(constraints + extra) (``first``:
+        ``Constraints(extra) + constraints``, the extra conjuncts leading):
+        recorded with status sat when the concrete model satisfies it, else
+        unknown.  Returns that status (None: folded to False, not asked)."""
         saved = self.constraints
         if base is not None:
             self.constraints = base
         try:
             extra = [self.bv(x) if x.width != BOOL else x for x in extra]
-            qset = self.query_set(extra)
+            if first:
+                cond = self.km.create_conditions()
+                qset = [x for x in list(extra) + list(self.constraints) if not (x.op == "const" and x.val)] + \
+                    ([] if (cond.op == "const" and cond.val) else [cond])
+            else:
+                qset = self.query_set(extra)
         finally:
             self.constraints = saved
         if any(x.op == "const" and not x.val for x in qset):
-            return                    # folded to False: nothing to ask
+            return None               # folded to False: nothing to ask
         kc = qset[-1] if self.km.create_conditions().op != "const" else None
         ok = check_model(qset, self.model)
         self.run_log.queries.append(Query(self.tx, self.pc, True, qset, True if ok else None, kc, kind))
+        return bool(ok)
+
+    def tuple_query(self, kind: str, conds: List[Node]) -> Optional[bool]:
+        """get_model((c, ...)) with a tuple (dependency_pruner.py:164,180,190):
+        no keccak conditions are added (model.py:35-36).  Constant answers are
+        not asked of the engine (z3 folds them); returns True/False for them,
+        else the recorded status (True: the model satisfies it; None: unknown)."""
+        if all(x.op == "const" for x in conds):
+            return all(x.val for x in conds)
+        ok = check_model(conds, self.model)
+        self.run_log.queries.append(Query(self.tx, self.pc, True, list(conds), True if ok else None, None, kind,
+                                          tuple_form=True))
+        return True if ok else None
 
     def annotate(self, kind: str, op0: Node, res: Node, cond: Node) -> None:
         """integer.py:_handle_add/_mul/_sub: the overflow condition annotates
@@ -380,8 +419,13 @@ class ConcolicLaser:
 
     def message_call(self, tx: int, inp: TxInput, max_steps: int = 20000) -> str:
         sender = self.leaf(f"sender_{tx}", inp.sender)
+        self.deps.iteration += 1        # start_sym_trans (svm.py:239-240; dependency_pruner.py:204-206)
         self._setup_tx(tx, inp, sender, self.k(CONTRACT))
-        return self._exec(max_steps)
+        self.mutated = False
+        res = self._exec(max_steps)
+        if res in ("STOP", "RETURN", "SELFDESTRUCT"):
+            self.end_world_state(False)
+        return res
 
     def contract_creation(self, tx: int, inp: TxInput, max_steps: int = 20000) -> str:
         """ContractCreationTransaction (transaction_models.py:195-245): CREATOR
@@ -391,11 +435,15 @@ class ConcolicLaser:
             self.accounts.insert(0, ACTORS["CREATOR"])
         self.storage = self.c.const_array(256, self.k(0))
         self.balance = self.app("store", self.balance, self.k(CONTRACT), self.k(0))
+        self.creation_txs.add(tx)
         self._setup_tx(tx, inp, self.k(inp.sender), self.k(CONTRACT))
+        self.mutated = False
         res = self._exec(max_steps)
         if res == "RETURN":
             self.code = self.returned
             self.jumpdests = self._jumpdests(self.code)
+            if len(self.code):        # transaction_models.py:252-262 / svm.py:416-425
+                self.end_world_state(True)
         return res
 
     def _calldata_byte(self, i: Node) -> Node:
@@ -414,6 +462,71 @@ class ConcolicLaser:
         self.balance = self.app("store", self.balance, sender,
                                 self.app("bvsub", self.app("select", self.balance, sender), value))
         self.vals.clear()
+
+    def _predictable(self, op: str, x: Node) -> Node:
+        """PredictableVars post hook of COINBASE / TIMESTAMP / NUMBER
+        (dependence_on_predictable_vars.py:176-184): the pushed value carries a
+        PredictableValueAnnotation (GASLIMIT is a constant here; not tagged)."""
+        self.pred[x.id] = self.pred.get(x.id, frozenset()) | {op}
+        return x
+
+    def _blockhash(self, param: Node) -> Node:
+        """PredictableVars BLOCKHASH pre hook (dependence_on_predictable_vars.py:
+        142-159): get_model(world constraints + [ULT(param, block_number),
+        ULT(block_number, 2^255)]); if SAT the state gets an
+        OldBlockNumberUsedAnnotation and the post hook tags the hash.  The hash
+        is the fresh symbol '{tx}_blockhash_block_{param}' (instructions.py:
+        1369-1380)."""
+        param = self.bv(param)
+        bn = self.leaf("block_number", 10_000_000)
+        ok = self.module_query("PredictableVars/blockhash",
+                               [self.c.app("bvult", param, bn), self.c.app("bvult", bn, self.k(1 << 255))])
+        h = self._env_leaf(f"blockhash_block_{_z3_str(param)}", 0x1234)
+        if ok:
+            self.pred[h.id] = self.pred.get(h.id, frozenset()) | {"blockhash"}
+        return h
+
+    @staticmethod
+    def _assertion_failure(off: Node, ln: Node, mbyte) -> bool:
+        """exceptions.py is_assertion_failure: concrete offset and length, the
+        data starts with Panic(uint256)'s selector 4e487b71 and ends in 0x01."""
+        if off.width == BOOL or ln.width == BOOL or off.op != "const" or ln.op != "const" or ln.val < 5:
+            return False
+        data = [mbyte(off.val + i) for i in range(ln.val)]
+        if not all(x.op == "const" for x in data[:4] + data[-1:]):
+            return False
+        return [x.val for x in data[:4]] == [78, 72, 123, 113] and data[-1].val == 1
+
+    def _selfdestruct(self, to: Node) -> None:
+        """AccidentallyKillable SELFDESTRUCT pre hook (suicide.py:50-96): for every
+        message call of the sequence And(caller == ATTACKER, caller == origin)
+        (caller and origin are the one 'sender_N' symbol); get_transaction_
+        sequence(world + [to == ATTACKER] + those), and without a model of that,
+        world + those alone."""
+        c = self.c
+        att = self.k(ACTORS["ATTACKER"])
+        ac = []
+        for t in self.sequence + [self.tx]:
+            if t in self.creation_txs:
+                continue
+            s = c.var(f"sender_{t}", 256)
+            ac.append(c.app("and", c.app("=", s, att), c.app("=", s, s)))
+        ok = self.module_query("AccidentallyKillable/attacker_beneficiary", [self.app("=", to, att)] + ac)
+        if not ok:
+            self.module_query("AccidentallyKillable/any_sender", ac)
+        self.deleted = True
+
+    def end_world_state(self, creation: bool) -> None:
+        """svm.py:416-425: a transaction that ends without revert adds its
+        world state; the add_world_state hooks run.  MutationPruner
+        (mutation_pruner.py:60-86): for a message call, get_model(world
+        constraints + [UGT(callvalue, 0)]) (a Constraints: keccak conditions
+        included); UNSAT with no mutation on the path drops the world state
+        (the scenarios put non-mutating calls last).  DependencyPruner resets
+        the path's annotation (dependency_pruner.py:320-340)."""
+        if not creation:
+            self.module_query("MutationPruner", [self.c.app("bvugt", self.value, self.k(0))])
+        self.deps.world_state_added(creation)
 
     def _exec(self, max_steps: int) -> str:
         code, stack, mem = self.code, [], {}
@@ -456,10 +569,13 @@ class ConcolicLaser:
                 self.tx_end_queries()
                 return "STOP"
             op = code[pc]
+            if not isinstance(op, int):
+                raise Unsupported(f"symbolic opcode byte at {pc}")
             self.pc = pc
             pc += 1
             a = self.app
             if op == 0x00:
+                self.deps.tx_end()
                 self.tx_end_queries()
                 return "STOP"
             elif op == 0x01:   # integer.py:140-145 Not(BVAddNoOverflow(op0, op1, False))
@@ -534,15 +650,35 @@ class ConcolicLaser:
             elif op == 0x36:
                 stack.append(self.cdsize)
             elif op == 0x37:   # CALLDATACOPY (concrete destination and size)
+                if self.inp.creation:   # a no-op in a creation (instructions.py:885-887)
+                    pop(), pop(), pop()
+                    continue
                 dst, src, ln = conc(pop()), popbv(), conc(pop())
                 for i in range(ln):
                     mem[dst + i] = self._calldata_byte(a("bvadd", src, self.k(i)) if i else src)
             elif op == 0x38:
-                stack.append(self.k(len(code)))
+                if self.inp.creation:
+                    # instructions.py:980-993: the code plus 0x200 bytes of symbolic
+                    # constructor arguments, calldatasize pinned to that
+                    n = len(code) + 0x200
+                    self.constraints.append(a("=", self.cdsize, self.k(n)))
+                    # the concrete choice follows the pin (the argument bytes lead the calldata)
+                    self.model[f"{self.tx}_calldatasize"] = n
+                    self.vals.clear()
+                    stack.append(self.k(n))
+                else:
+                    stack.append(self.k(len(code)))
             elif op == 0x39:   # CODECOPY (instructions.py:1065-1130; concrete operands)
                 dst, src, ln = conc(pop()), conc(pop()), conc(pop())
-                for i in range(ln):
-                    mem[dst + i] = self.k(code[src + i] if src + i < len(code) else 0, 8)
+                if self.inp.creation and src >= len(code):
+                    # creation code past its end is the symbolic calldata (:1078-1092)
+                    off = self.k(src - len(code))
+                    for i in range(ln):
+                        mem[dst + i] = self._calldata_byte(a("bvadd", off, self.k(i)) if i else off)
+                else:
+                    for i in range(ln):
+                        b = code[src + i] if src + i < len(code) else 0
+                        mem[dst + i] = self.k(b, 8) if isinstance(b, int) else b
             elif op == 0x3A:
                 stack.append(self.c.var(f"gas_price{self.tx}", 256))
             elif op == 0x3D:   # RETURNDATASIZE, no call returned data (instructions.py:1350-1365)
@@ -552,12 +688,14 @@ class ConcolicLaser:
                 dst, src, ln = pop(), pop(), pop()
                 if self.returndata is not None:
                     raise Unsupported("RETURNDATACOPY of real return data")
+            elif op == 0x40:   # BLOCKHASH (instructions.py:1369-1380) + PredictableVars' hooks
+                stack.append(self._blockhash(pop()))
             elif op == 0x41:
-                stack.append(self._env_leaf("coinbase", 0))
+                stack.append(self._predictable("coinbase", self._env_leaf("coinbase", 0)))
             elif op == 0x42:   # TIMESTAMP (instructions.py:1393-1400)
-                stack.append(self._env_leaf("timestamp", 1_600_000_000))
+                stack.append(self._predictable("timestamp", self._env_leaf("timestamp", 1_600_000_000)))
             elif op == 0x43:   # NUMBER: environment.block_number (environment.py:47)
-                stack.append(self.leaf("block_number", 10_000_000))
+                stack.append(self._predictable("number", self.leaf("block_number", 10_000_000)))
             elif op == 0x44:
                 stack.append(self._env_leaf("block_difficulty", 0))
             elif op == 0x45:   # GASLIMIT: the transaction's concrete gas limit
@@ -577,9 +715,13 @@ class ConcolicLaser:
                 off, v = conc(pop()), popbv()
                 mem[off] = a("extract", v, params=(7, 0))
             elif op == 0x54:
-                stack.append(a("select", self.storage, popbv()))
+                key = popbv()
+                self.deps.sload(key)          # DependencyPruner SLOAD pre hook
+                stack.append(a("select", self.storage, key))
             elif op == 0x55:
                 key, v = popbv(), popbv()
+                self.deps.sstore(key)         # DependencyPruner SSTORE pre hook
+                self.mutated = True           # MutationPruner SSTORE pre hook (mutation_pruner.py:45-47)
                 self.collect(v)
                 self.storage = a("store", self.storage, key, v)
             elif op == 0x56:
@@ -587,8 +729,14 @@ class ConcolicLaser:
                 if dest not in self.jumpdests:
                     raise Halt("bad jump")
                 pc = dest
+                if not self.deps.block(self, dest):   # DependencyPruner JUMP post hook
+                    return "PRUNED"
             elif op == 0x57:
                 dest, cond = conc(pop()), pop()
+                if self.pred.get(cond.id):
+                    # PredictableVars JUMPI pre hook (dependence_on_predictable_vars.py:68-82):
+                    # get_transaction_sequence(state, world constraints)
+                    self.module_query("PredictableVars/jumpi", [])
                 self.collect(cond)
                 if cond.width == BOOL:
                     pos, neg = cond, a("not", cond)
@@ -611,6 +759,8 @@ class ConcolicLaser:
                     if dest not in self.jumpdests:
                         raise Halt("bad jump")
                     pc = dest
+                if not self.deps.block(self, pc):    # DependencyPruner JUMPI post hook (the followed successor)
+                    return "PRUNED"
             elif op == 0x58:
                 stack.append(self.k(pc - 1))
             elif op == 0x59:
@@ -623,7 +773,12 @@ class ConcolicLaser:
                 stack.append(self.k(0))
             elif 0x60 <= op <= 0x7F:
                 n = op - 0x5F
-                stack.append(self.k(int.from_bytes(code[pc:pc + n].ljust(n, b"\0"), "big")))
+                bs = [code[pc + i] if pc + i < len(code) else 0 for i in range(n)]
+                if all(isinstance(b, int) for b in bs):
+                    stack.append(self.k(int.from_bytes(bytes(bs), "big")))
+                else:   # a patched immutable (instructions.py:277-310 push_ of a symbolic argument)
+                    v = a("concat", *[self.k(b, 8) if isinstance(b, int) else b for b in bs])
+                    stack.append(v if v.width == 256 else a("concat", self.k(0, 256 - v.width), v))
                 pc += n
             elif 0x80 <= op <= 0x8F:
                 d = op - 0x7F
@@ -646,18 +801,24 @@ class ConcolicLaser:
                 data = [mbyte(off + i) for i in range(ln)]
                 for x in data:
                     self.collect(x)
+                self.deps.tx_end()
                 self.tx_end_queries()
                 if all(x.op == "const" for x in data):
                     self.returned = bytes(x.val for x in data)
-                elif self.inp.creation:
-                    raise Unsupported("symbolic runtime code")
+                else:   # symbolic bytes: immutables patched into the runtime code
+                    self.returned = [x.val if x.op == "const" else x for x in data]
                 return "RETURN"
             elif op == 0xFD:
+                off, ln = pop(), pop()
+                if self._assertion_failure(off, ln, mbyte):
+                    # Exceptions REVERT pre hook (exceptions.py:58-84): a Panic(0x01) revert
+                    self.module_query("Exceptions", [])
                 return "REVERT"
             elif op == 0xFE:
+                self.module_query("Exceptions", [])   # Exceptions INVALID pre hook (exceptions.py:62-84)
                 return "INVALID"
             elif op == 0xFF:
-                pop()
+                self._selfdestruct(popbv())
                 return "SELFDESTRUCT"
             else:
                 raise Unsupported(f"opcode 0x{op:02x} at {pc - 1}")
@@ -671,6 +832,21 @@ class ConcolicLaser:
             raise Halt("stack underflow")
         a = self.app
         gas, to = self.bv(stack[-1]), self.bv(stack[-2])
+        if op in (0xF1, 0xFA):
+            self.deps.call()           # DependencyPruner CALL / STATICCALL pre hooks (dependency_pruner.py:258-270)
+            self.mutated = True        # MutationPruner CALL / STATICCALL pre hooks (mutation_pruner.py:52-58)
+        if op == 0xF1:
+            # ExternalCalls (CALL pre hook): _analyze_state's constraint set,
+            # Constraints([UGT(gas, 2300), to == ATTACKER]) + world constraints,
+            # handed to get_transaction_sequence (external_calls.py:75-82); and
+            # the shape of _is_precompile_call (:29-43), world constraints +
+            # Or(to <s 1, to >s PRECOMPILE_COUNT = 9) (natives.py:253-265)
+            # (defined in v0.23.0 but not called by the module)
+            if to.op != "const":
+                self.module_query("ExternalCalls/user_supplied",
+                                  [a("bvugt", gas, self.k(2300)), a("=", to, self.k(ACTORS["ATTACKER"]))], first=True)
+                self.module_query("ExternalCalls/precompile",
+                                  [a("or", a("bvslt", to, self.k(1)), a("bvsgt", to, self.k(9)))])
         if op in (0xF1, 0xF4, 0xF2):
             # StateChangeAfterCall pre hook (state_change_external_calls.py:183-197, 119-140)
             v3 = self.bv(stack[-3])
@@ -695,6 +871,155 @@ class ConcolicLaser:
             self.module_query("EtherThief", [
                 a("bvugt", a("select", self.balance, att), a("select", self.balance0, att)),
                 a("=", self.sender, att), self.c.true()])
+
+
+class DependencyPruner:
+    """``laser/plugin/plugins/dependency_pruner.py`` restated on the one path a
+    concolic run follows (a default-loaded plugin; A10 feasibility caller).
+
+    Plugin state (``:92-103``): ``iteration`` (+1 at every symbolic message
+    call, ``start_sym_trans :204-206``; 0 after a creation's world state,
+    ``:325-328``), ``sloads_on_path`` / ``sstores_on_path`` / ``calls_on_path``
+    keyed by block address.  The path's ``DependencyAnnotation``
+    (``plugin_annotations.py:26-72``): ``storage_loaded``, ``storage_written``
+    (per iteration), ``has_call``, ``path``, ``blocks_seen``; it is carried to
+    the next transaction through the world state (``:22-50``) with ``path``
+    and ``storage_loaded`` reset (``:330-340``).
+
+    At every JUMP / JUMPI post hook (``:208-228``) from iteration 2 on, a
+    block already seen asks ``wanna_execute`` (``:146-200``): for each storage
+    location written in the previous transaction, ``get_model((location ==
+    dependency,))`` over the locations read on paths through the block, then
+    over this path's loads; the first SAT keeps the state, none prunes it
+    (``PluginSkipState``).  The queries are TUPLES: no keccak conditions
+    (``model.py:35-36``), so keccak UF terms reach the engine unconstrained.
+
+    Not restated: the branch at ``:170-177`` (``address in
+    self.storage_accessed_global``), a membership test of an int block
+    address in a set of z3 BitVec keys, which holds only on a hash collision
+    (and then compares two ints as a Python bool)."""
+
+    def __init__(self):
+        self.iteration = 0
+        self.sloads_on_path: Dict[int, List[Node]] = {}
+        self.sstore_blocks: set = set()          # sstores_on_path's keys (update_calls reads only those)
+        self.calls_on_path: set = set()
+        self.asked: Dict[int, Optional[bool]] = {}   # eq node id -> answer (get_model's lru_cache)
+        self.reset_annotation()
+
+    def reset_annotation(self):
+        self.storage_loaded: List[Node] = []
+        self.storage_written: Dict[int, List[Node]] = {}
+        self.has_call = False
+        self.path: List[int] = [0]
+        self.blocks_seen: set = set()
+
+    def snapshot(self):
+        return (list(self.storage_loaded), {k: list(v) for k, v in self.storage_written.items()}, self.has_call,
+                list(self.path), set(self.blocks_seen))
+
+    def restore(self, snap):
+        (self.storage_loaded, self.storage_written, self.has_call, self.path, self.blocks_seen) = snap
+
+    def _sloads(self, loc: Node) -> None:
+        for a in self.path:
+            lst = self.sloads_on_path.setdefault(a, [])
+            if not any(x is loc for x in lst):
+                lst.append(loc)
+
+    def sload(self, loc: Node) -> None:         # :244-256
+        if not any(x is loc for x in self.storage_loaded):
+            self.storage_loaded.append(loc)
+        self._sloads(loc)
+
+    def sstore(self, loc: Node) -> None:        # :236-242
+        self.sstore_blocks.update(self.path)
+        lst = self.storage_written.setdefault(self.iteration, [])
+        if not any(x is loc for x in lst):
+            lst.append(loc)
+
+    def _calls(self) -> None:                   # update_calls :131-140
+        self.calls_on_path.update(a for a in self.path if a in self.sstore_blocks)
+
+    def call(self) -> None:                     # :258-270
+        self._calls()
+        self.has_call = True
+
+    def tx_end(self) -> None:                   # STOP / RETURN pre hooks, _transaction_end :280-297
+        for loc in self.storage_loaded:
+            self._sloads(loc)
+        # `for index in annotation.storage_written`: the dict's keys (iterations)
+        self.sstore_blocks.update(self.path)
+        if self.has_call:
+            self._calls()
+
+    def world_state_added(self, creation: bool) -> None:   # :320-340
+        if creation:
+            self.iteration = 0
+            return
+        self.path = [0]
+        self.storage_loaded = []
+
+    def block(self, m: "ConcolicLaser", address: int) -> bool:
+        """JUMP / JUMPI post hook on the followed successor: False = pruned."""
+        self.path.append(address)
+        if self.iteration < 2:
+            return True
+        if address not in self.blocks_seen:
+            self.blocks_seen.add(address)
+            return True
+        if address in self.calls_on_path:
+            return True
+        if address not in self.sloads_on_path:
+            return False
+        deps = self.sloads_on_path[address]
+        for loc in self.storage_written.get(self.iteration - 1, []):
+            for dep in list(deps) + list(self.storage_loaded):
+                if self._ask(m, loc, dep):
+                    return True
+        return False
+
+    def _ask(self, m: "ConcolicLaser", loc: Node, dep: Node) -> bool:
+        """get_model((location == dependency,)): identical or constant pairs
+        are decided here (z3 answers them at once, nothing for the engine);
+        a recorded pair keeps the state unless it is `t + j == t + k` (j != k).
+        z3's answer on the others is unknown here (SAT whenever a keccak UF is
+        involved: the tuple carries no keccak conditions)."""
+        if loc is dep:
+            return True
+        eq = m.c.app("=", loc, dep)
+        if eq.id in self.asked:
+            return self.asked[eq.id] is not False
+        ans = m.tuple_query("DependencyPruner", [eq]) if not (loc.op == "const" and dep.op == "const") \
+            else loc.val == dep.val
+        if ans is None:
+            (b1, k1), (b2, k2) = _base_offset(loc), _base_offset(dep)
+            ans = False if (b1 is b2 and k1 != k2) else None
+        self.asked[eq.id] = ans
+        return ans is not False
+
+
+def _z3_str(n: Node) -> str:
+    """str() of a BitVec as z3 prints the few shapes a BLOCKHASH argument takes
+    (a numeral, a symbol, symbol +/- numeral); anything else gets a stable tag."""
+    if n.op == "const":
+        return str(n.val)
+    if n.op == "var":
+        return n.name
+    if n.op in ("bvadd", "bvsub") and len(n.args) == 2 and all(x.op in ("var", "const") for x in n.args):
+        return f"{_z3_str(n.args[0])} {'+' if n.op == 'bvadd' else '-'} {_z3_str(n.args[1])}"
+    return f"term{n.id}"
+
+
+def _base_offset(n: Node) -> Tuple[Node, int]:
+    """t + k (k a constant) -> (t, k); anything else -> (n, 0)."""
+    if n.op == "bvadd" and len(n.args) == 2:
+        a, b = n.args
+        if b.op == "const":
+            return a, b.val
+        if a.op == "const":
+            return b, a.val
+    return n, 0
 
 
 def _postorder(root: Node, done: Dict[int, object]) -> List[Node]:
@@ -733,6 +1058,32 @@ def _merge_slices(c: Ctx, parts: List[Node]) -> List[Node]:
     return out
 
 
+
+
+
+def asm(items):
+    """A tiny assembler for the SYNTHETIC contracts (tests/test_concolic_env.py,
+    tools/make_laser_corpus.py): ints are opcodes, ("push", n, v) pushes, ("label", x)
+    marks a JUMPDEST, ("ref", x) pushes the label's offset (PUSH1)."""
+    out, fix, labels = bytearray(), [], {}
+    for it in items:
+        if isinstance(it, int):
+            out.append(it)
+        elif it[0] == "push":
+            out.append(0x5F + it[1])
+            out += it[2].to_bytes(it[1], "big")
+        elif it[0] == "label":
+            labels[it[1]] = len(out)
+            out.append(0x5B)
+        else:
+            out.append(0x60)
+            fix.append((len(out), it[1]))
+            out.append(0)
+    for pos, lab in fix:
+        out[pos] = labels[lab]
+    return bytes(out)
+
+
 def check_model(constraints: List[Node], model: Dict) -> bool:
     vals = eval_nodes(constraints, model)
     return all(vals[x.id] for x in constraints)
@@ -745,15 +1096,23 @@ def abi_call(selector: int, *words: int) -> bytes:
 def run_sequence(code: bytes, txs: List[TxInput], storage=None, balances=None) -> Tuple[ConcolicLaser, Run]:
     m = ConcolicLaser(code, storage, balances)
     for t, inp in enumerate(txs, start=1):
-        # a reverted transaction leaves no open state (svm.py _execute_transactions):
-        # the next one starts from the world state before it
-        snap = (list(m.constraints), m.storage, m.balance, m.code, m.jumpdests)
+        if m.deleted and not inp.creation:
+            # execute_message_call skips a self-destructed contract (transaction/symbolic.py:112-114)
+            m.run_log.halts.append("skipped: contract deleted")
+            continue
+        # a reverted (or pruned) transaction leaves no open state (svm.py
+        # _execute_transactions): the next one starts from the world state
+        # before it, with that state's dependency annotation
+        snap = (list(m.constraints), m.storage, m.balance, m.code, m.jumpdests, m.deps.snapshot())
         try:
             res = m.contract_creation(t, inp) if inp.creation else m.message_call(t, inp)
         except Halt as e:
             res = f"halt: {e}"
         if res not in ("STOP", "RETURN", "SELFDESTRUCT"):
-            m.constraints, m.storage, m.balance, m.code, m.jumpdests = snap
+            m.constraints, m.storage, m.balance, m.code, m.jumpdests, dsnap = snap
+            m.deps.restore(dsnap)
+        else:
+            m.sequence.append(t)
         m.run_log.halts.append(res)
     m.run_log.model = m.model
     return m, m.run_log

@@ -99,7 +99,8 @@ class ReplayVM:
         self.laser_hooks: Dict[str, list] = {}
         self.post_hooks: Dict[str, list] = {}
         self.open_states: list = []
-        self.counts = {"is_possible": 0, "tx_prunes": 0, "jumpi_prunes": 0, "keccaks": 0, "module_queries": 0}
+        self.counts = {"is_possible": 0, "tx_prunes": 0, "jumpi_prunes": 0, "keccaks": 0, "module_queries": 0,
+                       "tuple_queries": 0}
 
     def register_laser_hooks(self, kind, hook):
         self.laser_hooks.setdefault(kind, []).append(hook)
@@ -151,7 +152,14 @@ class ReplayVM:
                         while kk and kk[0][0] == tx and kk[0][1] <= qs[j][0]:
                             self._keccak(keccak, kk.pop(0))
                         self.counts["module_queries"] += 1
-                        answers.append(self._module(_state(qs[j][1]).world_state.constraints))
+                        q = qs[j][1]
+                        if q.tuple_form:
+                            # DependencyPruner's get_model((location == dependency,)): a
+                            # tuple, so the drop-in adds no keccak conditions (model.py:35-36)
+                            self.counts["tuple_queries"] += 1
+                            answers.append(self._module(tuple(FakeBool(n) for n in q.constraints)))
+                        else:
+                            answers.append(self._module(_state(q).world_state.constraints))
                         j += 1
                         continue
                     # one JUMPI: its successor sets are recorded consecutively
@@ -270,7 +278,7 @@ def concolic_runs(contracts=None):
     """[(ConcolicLaser, Run, n_tx)] for the corpus scenarios (tools/make_laser_corpus.py)."""
     import os
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
-    from make_laser_corpus import SCENARIOS, load_code
+    from make_laser_corpus import SCENARIOS, load_code, scenario_balances
     out = []
     for contract, scenarios in SCENARIOS.items():
         if contracts and contract not in contracts:
@@ -278,7 +286,6 @@ def concolic_runs(contracts=None):
         code = load_code(contract)
         for name, txs, *opt in scenarios:
             opts = opt[0] if opt else {}
-            bal = opts.get("balances", 10 ** 18)
-            m, run = run_sequence(code, txs, storage=opts.get("storage"), balances={x: bal for x in ACTORS.values()})
+            m, run = run_sequence(code, txs, storage=opts.get("storage"), balances=scenario_balances(opts))
             out.append((f"{contract}/{name}", m, run, len(txs)))
     return out

@@ -21,7 +21,7 @@ def test_template_is_built_and_marked():
 
 
 @pytest.mark.parametrize("which", ["c2_token_transfer_underflow.smt2", "c4_wallet_onlyowner.smt2",
-                                   "underflow_t3_send_send_balance_q38_sat.smt2.gz",
+                                   "underflow_t3_send_send_balance_q41_sat.smt2.gz",
                                    "flag_array_t2_extract_money_q15_sat.smt2.gz"])   # W_UDIV: the loop
 def test_corpus_programs_assemble(which, tmp_path):
     from mythril_amd.engine import prepare

@@ -10,30 +10,8 @@ environment.py:47) and that the engine witnesses every followed successor."""
 from mythril_amd.engine import WitnessEngine, prepare
 from mythril_amd.ir import Ctx
 from tests.fakedev import FakeDevice
-from tests.laser_concolic import ACTORS, TxInput, check_model, run_sequence
+from tests.laser_concolic import ACTORS, TxInput, asm as _asm, check_model, run_sequence
 from tests.test_engine_cpu import holds
-
-
-def _asm(items):
-    """A tiny assembler: ints are opcodes, ("push", n, v) pushes, ("label", x)
-    marks a JUMPDEST, ("ref", x) pushes the label's offset (PUSH1)."""
-    out, fix, labels = bytearray(), [], {}
-    for it in items:
-        if isinstance(it, int):
-            out.append(it)
-        elif it[0] == "push":
-            out.append(0x5F + it[1])
-            out += it[2].to_bytes(it[1], "big")
-        elif it[0] == "label":
-            labels[it[1]] = len(out)
-            out.append(0x5B)
-        else:
-            out.append(0x60)
-            fix.append((len(out), it[1]))
-            out.append(0)
-    for pos, lab in fix:
-        out[pos] = labels[lab]
-    return bytes(out)
 
 
 TIMESTAMP, GASPRICE, COINBASE, DIFFICULTY, NUMBER = 0x42, 0x3A, 0x41, 0x44, 0x43
@@ -65,7 +43,10 @@ def test_environment_leaf_names_follow_laser():
             from mythril_amd.ir import topo
             names |= {x.name for x in topo([n]) if x.op == "var"}
     assert {"1_timestamp", "gas_price1", "1_coinbase", "1_block_difficulty", "block_number"} <= names
-    assert sum(q.sat is True for q in run.queries) == 5
+    assert sum(q.sat is True for q in run.queries if q.kind == "jumpi") == 5
+    # PredictableVars' JUMPI pre hook (dependence_on_predictable_vars.py:68-82) on the
+    # TIMESTAMP, COINBASE and NUMBER branches (GASPRICE and DIFFICULTY are not predictable_ops)
+    assert sum(q.kind == "PredictableVars/jumpi" for q in run.queries) == 3
 
 
 def test_environment_queries_witnessed():

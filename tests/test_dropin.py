@@ -455,3 +455,40 @@ def test_constant_cells_materialise_from_leaves(mythril):
     res = dropin.get_model(SAT)
     assert res.raw[0][0] == "z3"
     assert getattr(dev, "witness_leaf_calls", 0) == n0 + 1
+
+
+def test_slow_recheck_is_counted_and_logged(mythril, monkeypatch, caplog):
+    """VERDICT r4 item 8 (SURVEY §7 hard part 5): the z3 re-check runs under
+    the pinned budget first; a witness z3 confirms only with more time (it
+    answered unknown under the pinned budget) is still returned, and counted
+    and logged, because the reference's check of the unpinned formula may
+    have timed out there."""
+    calls = []
+
+    def slow_confirm(raws, script, w, timeout_ms=2000):
+        calls.append(timeout_ms)
+        if timeout_ms <= dropin.PINNED_CHECK_MS:
+            z3bridge._last.info = {"result": "unknown", "ms": timeout_ms}
+            return None
+        z3bridge._last.info = {"result": "sat", "ms": 1.0}
+        return ("z3", dict(w.values))
+    monkeypatch.setattr(z3bridge, "model_from_witness", slow_confirm)
+    n0 = dropin.STATS.get("slow_rechecks", 0)
+    with caplog.at_level("WARNING"):
+        res = dropin.get_model(SAT)
+    assert res.raw[0][0] == "z3"
+    assert calls == [dropin.PINNED_CHECK_MS, mythril.args.solver_timeout]
+    assert dropin.STATS["slow_rechecks"] == n0 + 1
+    assert "pinned re-check budget" in caplog.text
+    # an unsat answer under the pinned budget is final: no second check
+    dropin.get_model.cache_clear()
+    dropin._memo.clear()
+    calls.clear()
+
+    def refuted(raws, script, w, timeout_ms=2000):
+        calls.append(timeout_ms)
+        z3bridge._last.info = {"result": "unsat", "ms": 1.0}
+        return None
+    monkeypatch.setattr(z3bridge, "model_from_witness", refuted)
+    assert dropin.get_model(SAT).raw[0] == "ref"
+    assert calls == [dropin.PINNED_CHECK_MS]

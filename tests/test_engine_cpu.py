@@ -156,3 +156,28 @@ def test_batched_search_equals_individual():
     single = [e.search([q])[0] for q in qs]
     assert [w and w.index for w in batched] == [w and w.index for w in single]
     assert all(w is not None for w in batched)
+
+
+def test_verify_confirms_witnesses_on_the_device():
+    """WitnessEngine(verify=True) evaluates the search program at
+    each witness index once more; a confirmed witness is returned unchanged,
+    and one the device does not confirm is dropped."""
+    from mythril_amd.engine import WitnessEngine, prepare
+    from mythril_amd.ir import Ctx
+    from tests.fakedev import FakeDevice
+    c = Ctx()
+    x = c.var("x", 256)
+    conj = [c.app("bvugt", x, c.const(1 << 200, 256)), c.app("bvult", x, c.const(1 << 201, 256))]
+    plain = WitnessEngine(dev=FakeDevice(chunk=256), budget=1 << 12).search([prepare(conj, c)])[0]
+    eng = WitnessEngine(dev=FakeDevice(chunk=256), budget=1 << 12, verify=True)
+    (w,) = eng.search([prepare(conj, c)])
+    assert w is not None and plain is not None and w.values == plain.values
+    assert holds(conj, w) and eng.stats.get("verify_rejects", 0) == 0
+
+    class Denies(FakeDevice):
+        def eval_generated(self, dp, seed, begin, count, trace=True):
+            v, t = super().eval_generated(dp, seed, begin, count, trace)
+            return v * 0, t
+    eng = WitnessEngine(dev=Denies(chunk=256), budget=1 << 12, verify=True)
+    assert eng.search([prepare(conj, c)]) == [None]
+    assert eng.stats["verify_rejects"] == 1

@@ -48,3 +48,44 @@ def test_overlapping_threads_restore_once():
         t.join()
     assert _is(before)
     assert engine._HANDOFF[0] == 0
+
+
+def test_a_change_made_meanwhile_is_kept():
+    """the saved interval is put back only if the interval is still
+    the one the hand-off set; another component's change stays."""
+    before = sys.getswitchinterval()
+    try:
+        with engine._gil_handoff(True):
+            sys.setswitchinterval(0.002)
+        assert _is(0.002)
+    finally:
+        sys.setswitchinterval(before)
+
+
+def test_search_withdraws_queued_compiles_of_misses():
+    """a search that finds nothing leaves no witness-program
+    compile queued on the host thread (nor when the device raises)."""
+    from mythril_amd.engine import WitnessEngine, prepare
+    from mythril_amd.ir import Ctx
+    from tests.fakedev import FakeDevice
+    c = Ctx()
+    arr = c.array("cd", 256, 8)
+    x = c.var("x", 256)
+    # a cell with a variable index: the witness program is queued for compile
+    miss = [c.app("=", c.app("select", arr, x), c.const(7, 8)), c.app("=", x, c.const(3, 256)),
+            c.app("=", x, c.const(4, 256))]
+    eng = WitnessEngine(dev=FakeDevice(chunk=256), budget=1 << 10)
+    q = prepare(miss, c)
+    assert eng.search([q]) == [None]
+    assert q._trace_future is None
+
+    class Boom(FakeDevice):
+        def search(self, *a, **k):
+            raise RuntimeError("device")
+    q2 = prepare(miss, c)
+    eng2 = WitnessEngine(dev=Boom(chunk=256), budget=1 << 10)
+    try:
+        eng2.search([q2])
+    except RuntimeError:
+        pass
+    assert q2._trace_future is None

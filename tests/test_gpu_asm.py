@@ -295,3 +295,47 @@ def test_asm_search_of_a_traced_program(dev):
             assert fa == fi and fa is not None, flags
     finally:
         dp.free()
+
+
+def _shift_dag(seed):
+    """Shifts by per-lane amounts (W_SHL / W_LSHR / W_ASHR, round 5): amounts
+    drawn below the width (masked leaves), at and just past it, and whole
+    random 256-bit values (>= w: zero, or the sign fill for ashr)."""
+    r = random.Random(seed)
+    c = Ctx()
+    terms, conj = [], []
+    for i in range(10):
+        w = r.choice([33, 64, 100, 160, 255, 256])
+        a = c.var(f"a{i}_{w}", w)
+        amt = c.var(f"s{i}_{w}", w)
+        k = r.random()
+        if k < 0.5:      # below the width: mask to 8 bits, then reduce mod w
+            amt = c.app("bvurem", c.app("bvand", amt, c.const(0x1FF, w)), c.const(w, w)) if r.random() < 0.3 \
+                else c.app("bvand", amt, c.const((1 << max(1, (w - 1).bit_length() - 1)) - 1, w))
+        elif k < 0.7:    # at or past the width by a little
+            amt = c.app("bvadd", c.app("bvand", amt, c.const(3, w)), c.const(w - 2, w))
+        op = r.choice(["bvshl", "bvlshr", "bvashr"])
+        t = c.app(op, a, amt)
+        terms.append(t)
+        conj.append(c.app(r.choice(["bvult", "bvule", "bvslt"]), t, c.var(f"b{i}_{w}", w))
+                    if r.random() < 0.5 else c.app("not", c.app("=", t, c.const(0, w))))
+    return c, conj, terms
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_asm_variable_shifts(dev, seed):
+    c, conj, terms = _shift_dag(9300 + seed)
+    p = compile_program(conj, trace=terms)
+    ops = {int(x) & 0xFF for x in list(p.code)[0::4]}
+    assert ops & {isa.OPCODES[n] for n in ("W_SHL", "W_LSHR", "W_ASHR")}
+    if not isa.asm_eligible(p.code, p.leaves, p.consts):
+        pytest.skip("lowered outside the asm opcode set")
+    for begin, n in ((seed, 4096 + 7), ((1 << 33) + 5, 300)):
+        va, ta, vi, ti = both_traced(dev, p, DEFAULT_SEED + seed, begin, n)
+        assert np.array_equal(va, vi), (seed, begin)
+        assert np.array_equal(ta, ti), (seed, begin, int(np.count_nonzero(ta != ti)))
+    pair = conj[2 * (seed % 5):2 * (seed % 5) + 2]
+    va, vi = both(dev, compile_program(pair), DEFAULT_SEED + seed, 0, 1 << 12)
+    _, _, vo = cdag.evaluate(pair, DEFAULT_SEED + seed, 0, 1 << 12, want_verdict=True)
+    assert np.array_equal(va, vo) and np.array_equal(vi, vo)
+    assert int(vo.sum()) > 0

@@ -188,3 +188,25 @@ def test_check_runs_with_true_premises(dev):
                              specs=cdag.program_specs(p))
     assert np.array_equal(vi.astype(np.uint8), vo)
     assert np.array_equal(va.astype(np.uint8), vo), int(np.count_nonzero(va.astype(np.uint8) != vo))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_asmjit_variable_shifts(dev, seed):
+    """W_SHL / W_LSHR / W_ASHR by per-lane amounts (round 5) instantiated in
+    an assembled body: verdicts equal the asm interpreter's and the oracle's."""
+    from tests.test_gpu_asm import _shift_dag
+    c, conj, _ = _shift_dag(9300 + seed)
+    for k in range(0, len(conj), 2):
+        sub = conj[k:k + 2]
+        p = compile_program(sub)
+        assert asmjit.eligible(p)
+        di, da = pair(dev, p)
+        try:
+            va, _ = dev.eval_generated(da, DEFAULT_SEED + seed, 1 << 20, 1 << 12, trace=False)
+            vi, _ = dev.eval_generated(di, DEFAULT_SEED + seed, 1 << 20, 1 << 12, trace=False)
+        finally:
+            di.free()
+            da.free()
+        _, _, vo = cdag.evaluate(sub, DEFAULT_SEED + seed, 1 << 20, 1 << 12, want_verdict=True)
+        assert np.array_equal(va, vi), (seed, k)
+        assert np.array_equal(va.astype(np.uint8), vo), (seed, k)

@@ -30,15 +30,27 @@ def test_manifest_matches_files():
     assert files == {m["file"] for m in MANIFEST}
     assert len(MANIFEST) >= 100
     contracts = {m["contract"] for m in MANIFEST}
+    # all 17 reference .sol.o fixtures (tests/testdata/inputs), two VMTests, one synthetic
     assert contracts == {"underflow", "overflow", "metacoin", "suicide", "flag_array", "origin", "calls",
                          "kinds_of_calls", "returnvalue", "ether_send", "exceptions_0.8.0", "environments",
+                         "exceptions", "multi_contracts", "nonascii", "safe_funcs", "symbolic_exec_bytecode",
                          "vm:vmIOandFlowOperations/DynamicJumpJD_DependsOnJumps0",
-                         "vm:vmIOandFlowOperations/DynamicJumpJD_DependsOnJumps1"}
-    assert sum(m["status"] == "sat" for m in MANIFEST) >= 250
+                         "vm:vmIOandFlowOperations/DynamicJumpJD_DependsOnJumps1", "synthetic:predictable"}
+    assert sum(m["status"] == "sat" for m in MANIFEST) >= 390
     kinds = {m["kind"] for m in MANIFEST}
+    # every feasibility caller of SURVEY §8a A10 and the modules whose
+    # get_transaction_sequence sets the reference's issue tests pin
     assert {"jumpi", "EtherThief", "StateChangeAfterCall/external_call", "StateChangeAfterCall/attacker_callee",
             "StateChangeAfterCall/balance_change", "IntegerArithmetics/addition",
-            "IntegerArithmetics/subtraction", "IntegerArithmetics/multiplication"} <= kinds
+            "IntegerArithmetics/subtraction", "IntegerArithmetics/multiplication",
+            "MutationPruner", "DependencyPruner", "ExternalCalls/precompile", "ExternalCalls/user_supplied",
+            "PredictableVars/blockhash", "PredictableVars/jumpi", "Exceptions",
+            "AccidentallyKillable/attacker_beneficiary", "AccidentallyKillable/any_sender"} <= kinds
+    # DependencyPruner's queries are tuples: no keccak conditions (model.py:35-36)
+    for m in MANIFEST:
+        assert m["tuple"] == (m["kind"] == "DependencyPruner"), m["file"]
+        if m["tuple"]:
+            assert "keccak256_512-1" not in gzip.open(os.path.join(CORPUS, m["file"]), "rt").read()
     # multi-transaction sets carry one sender-among-actors constraint per transaction
     last = max(MANIFEST, key=lambda m: (m["tx"], m["conjuncts"]))
     text = gzip.open(os.path.join(CORPUS, last["file"]), "rt").read()
@@ -132,3 +144,73 @@ def test_ether_thief_query_pinned_by_reference_calldata():
     assert w is not None and holds(s.asserts, w)
     idx = sum(w.arrays["2_calldata"].get(i, 0) << (8 * (35 - i)) for i in range(4, 36))
     assert idx == 1234           # the only flagged index: the witness's calldata is the reference's
+
+
+def _run(contract, scenario):
+    from tests.laser_concolic import run_sequence
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tools"))
+    from make_laser_corpus import SCENARIOS, load_code, scenario_balances
+    for name, txs, *opt in SCENARIOS[contract]:
+        if name == scenario:
+            opts = opt[0] if opt else {}
+            return txs, run_sequence(load_code(contract), txs, storage=opts.get("storage"),
+                                     balances=scenario_balances(opts))[1]
+    raise KeyError(scenario)
+
+
+def test_exceptions_issues_pinned_by_reference():
+    """tests/integration_tests/analysis_tests.py:21-31: myth analyze of
+    exceptions_0.8.0.sol.o -t 1 -m Exceptions reports TWO issues.  With one
+    message call after the creation, the paths that reach an assertion
+    failure (a Panic(0x01) REVERT, exceptions.py:58-84) are assert1() and
+    fail() (val is still 0); change_val() reaches none.  The constraint set
+    the module hands to get_transaction_sequence at each is satisfied by the
+    concrete model (and witnessed on the device, test_gpu_laser.py)."""
+    issues = {}
+    for scen in ("t2_assert_fails", "t2_fail", "t2_change_val"):
+        txs, run = _run("exceptions_0.8.0", scen)
+        assert len(txs) == 2 and txs[0].creation        # -t 1: the creation, then one message call
+        exc = [q for q in run.queries if q.kind == "Exceptions"]
+        issues[scen] = len(exc)
+        assert all(q.sat and q.tx == 2 for q in exc), scen
+    assert issues == {"t2_assert_fails": 1, "t2_fail": 1, "t2_change_val": 0}
+    mf = [m for m in MANIFEST if m["contract"] == "exceptions_0.8.0" and m["kind"] == "Exceptions"
+          and m["scenario"] in ("t2_assert_fails", "t2_fail")]
+    assert len(mf) == 2 and all(m["status"] == "sat" for m in mf)
+
+
+def test_accidentally_killable_issue_pinned_by_reference():
+    """analysis_tests.py:32-41: myth analyze of symbolic_exec_bytecode.sol.o -t 1
+    -m AccidentallyKillable reports ONE issue.  The creation takes a symbolic
+    constructor argument (the creation calldata behind CODESIZE / CODECOPY,
+    instructions.py:977-993,1065-1130) that becomes an immutable of the
+    runtime code; commencekilling() then self-destructs to msg.sender.  The
+    module's first constraint set (suicide.py:70-80: world + [to == ATTACKER]
+    + the sender conditions) is satisfiable, so the issue is the
+    'attacker_beneficiary' one, and it is the only SELFDESTRUCT query."""
+    txs, run = _run("symbolic_exec_bytecode", "t2_commence_killing")
+    assert len(txs) == 2 and txs[0].creation
+    kill = [q for q in run.queries if q.kind.startswith("AccidentallyKillable")]
+    assert [(q.kind, q.sat) for q in kill] == [("AccidentallyKillable/attacker_beneficiary", True)]
+    mf = [m for m in MANIFEST if m["contract"] == "symbolic_exec_bytecode"
+          and m["scenario"] == "t2_commence_killing" and m["kind"].startswith("AccidentallyKillable")]
+    assert len(mf) == 1 and mf[0]["status"] == "sat"
+    # the immutable is symbolic in the runtime code: getBytes compares against it
+    txs, run = _run("symbolic_exec_bytecode", "t2_get_bytes")
+    from mythril_amd.ir import topo
+    assert any(n.op == "bvshl" for q in run.queries if q.tx == 2 for n in topo(q.constraints))
+
+
+def test_pruners_follow_the_reference():
+    """MutationPruner asks world + [callvalue >u 0] at every message call's end
+    (mutation_pruner.py:60-86); DependencyPruner's tuples compare a location
+    written in the previous transaction with one read on a path through the
+    revisited block (dependency_pruner.py:146-200), and a path whose previous
+    transaction wrote nothing is pruned (metacoin's third call)."""
+    txs, run = _run("underflow", "t3_send_send_balance")
+    assert sum(q.kind == "MutationPruner" for q in run.queries) == 3
+    dep = [q for q in run.queries if q.kind == "DependencyPruner"]
+    assert dep and all(q.tuple_form and len(q.constraints) == 1 and q.constraints[0].op == "=" for q in dep)
+    assert all(q.tx == 3 for q in dep)
+    _, run = _run("metacoin", "t3_sendtoken")
+    assert run.halts[2] == "PRUNED"

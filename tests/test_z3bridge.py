@@ -81,7 +81,8 @@ def fake_z3(monkeypatch):
 
 
 def test_to_ir_parses_the_solver_text(fake_z3):
-    s = z3bridge.to_ir(["raw-assertion"])
+    from mythril_amd.ir import Ctx
+    s = z3bridge.to_ir(["raw-assertion"], Ctx())     # the text route (a context of the caller's)
     assert [d for d in s.decls] == ["x", "cd", "f", "b"] and len(s.asserts) == 1
 
 

@@ -12,6 +12,7 @@
 #   prof           rocprofv3 --kernel-trace --stats on a short bench run
 #   pmc            PMC passes on one bench launch (SQ, instruction mix, FETCH_SIZE, WRITE_SIZE)
 #   config         tools/config_bench.py (C2-C4 queries) -> config_bench.json
+#   gt[=LOG2]      tools/ground_truth.py: the corpus's unknown queries searched up to 2^LOG2 (32)
 #   latency        tools/latency_bench.py (drop-in prepare/search/materialise per query)
 #   replay         python -m mythril_amd.replay tests/golden/solver_log
 #   opbench        tools/opbench.py jit
@@ -81,6 +82,11 @@ for step in "$@"; do
     config)
       run 600 "$OUT/config_bench.log" python3 tools/config_bench.py --out "$OUT/config_bench.json"
       tail -12 "$OUT/config_bench.log" ;;
+    gt|gt=*)
+      G=()
+      [ "$step" != gt ] && G=(--max-log2 "${step#gt=}")
+      run 1100 "$OUT/ground_truth.log" python3 -u tools/ground_truth.py --out "$OUT/ground_truth.json" "${G[@]}"
+      tail -8 "$OUT/ground_truth.log" ;;
     latency)
       run 600 "$OUT/latency.log" python3 tools/latency_bench.py --out "$OUT/latency.json"
       tail -20 "$OUT/latency.log" ;;

@@ -46,7 +46,7 @@ sys.path.insert(0, ROOT)
 
 from mythril_amd.smt2 import to_smt2  # noqa: E402
 from oracle.keccak import keccak256  # noqa: E402
-from tests.laser_concolic import ACTORS, TxInput, abi_call, check_model, run_sequence  # noqa: E402
+from tests.laser_concolic import ACTORS, CONTRACT, TxInput, abi_call, asm, check_model, run_sequence  # noqa: E402
 
 OUT = os.path.join(ROOT, "tests", "golden", "laser")
 
@@ -137,10 +137,18 @@ SCENARIOS = {
             TxInput(abi_call(sel("withdrawfunds()")), sender=A)],
          {"balances": 10 ** 20, "storage": {2: 10 ** 18, 3: 10 * 10 ** 18}}),   # INVEST_MIN, INVEST_MAX
     ],
+    # analysis_tests.py:21-31: -t 1 -m Exceptions reports two issues, assert1() and
+    # fail() (val is 0 after the creation); change_val() reaches none
     "exceptions_0.8.0": [
         ("t2_assert_fails", [
             TxInput(b"", sender=C, creation=True),
             TxInput(abi_call(sel("assert1()")), sender=A)]),
+        ("t2_fail", [
+            TxInput(b"", sender=C, creation=True),
+            TxInput(abi_call(sel("fail()")), sender=S)]),
+        ("t2_change_val", [
+            TxInput(b"", sender=C, creation=True),
+            TxInput(abi_call(sel("change_val()")), sender=A)]),
         ("t3_change_then_fail", [
             TxInput(b"", sender=C, creation=True),
             TxInput(abi_call(sel("change_val()")), sender=A),
@@ -153,6 +161,63 @@ SCENARIOS = {
             TxInput(abi_call(sel("batchTransfer(address[],uint256)"), 0x40, 5, 2, A, S), sender=A)]),
         ("t1_batch_transfer_overflow", [
             TxInput(abi_call(sel("batchTransfer(address[],uint256)"), 0x40, 1 << 255, 2, A, S), sender=S)]),
+    ],
+    # Solidity 0.5 asserts end in INVALID: the Exceptions module's INVALID pre hook
+    # (exceptions.py:62-84); requireisfine / thisisfine / thisisalsofind reach none
+    "exceptions": [
+        ("t1_assert1", [TxInput(abi_call(sel("assert1()")), sender=A)]),
+        ("t1_assert3_23", [TxInput(abi_call(sel("assert3(uint256)"), 23), sender=S)]),
+        ("t1_division_by_zero", [TxInput(abi_call(sel("divisionby0(uint256)"), 0), sender=A)]),
+        ("t1_array_out_of_bounds", [TxInput(abi_call(sel("arrayaccess(uint256)"), 8), sender=C)]),
+        ("t3_fine_paths", [
+            TxInput(abi_call(sel("thisisfine(uint256)"), 5), sender=A),
+            TxInput(abi_call(sel("thisisalsofind(uint256)"), 3), sender=S),
+            TxInput(abi_call(sel("requireisfine(uint256)"), 22), sender=A)]),
+    ],
+    # msg.sender.transfer(1 ether): a CALL with value to the (symbolic) caller,
+    # the contract's own balance symbolic in the starting world state
+    "multi_contracts": [
+        ("t2_transfer_twice", [
+            TxInput(abi_call(sel("transfer()")), sender=A),
+            TxInput(abi_call(sel("transfer()")), sender=S)], {"contract_balance": 5 * 10 ** 18}),
+    ],
+    "nonascii": [
+        ("t2_render", [
+            TxInput(abi_call(sel("renderNonAscii()")), sender=A),
+            TxInput(abi_call(0x12345678), sender=S)]),
+    ],
+    # the runtime code of tests/testdata/input_contracts/safe_funcs.sol (0.8:
+    # assert -> Panic(0x01) REVERT, the Exceptions REVERT pre hook), symbolic storage
+    "safe_funcs": [
+        ("t2_change_then_fail", [
+            TxInput(abi_call(sel("change_val()")), sender=A),
+            TxInput(abi_call(sel("fail()")), sender=S)]),
+        ("t1_fail_holds", [TxInput(abi_call(sel("fail()")), sender=A)], {"storage": {0: 2}}),
+        ("t1_assert1", [TxInput(abi_call(sel("assert1()")), sender=C)]),
+    ],
+    # creation code with a constructor argument (CODESIZE / CODECOPY past the
+    # code read the creation's symbolic calldata, instructions.py:977-993,
+    # 1065-1130) that becomes an immutable patched into the runtime code;
+    # analysis_tests.py:32-41: -t 1 -m AccidentallyKillable reports one issue
+    "symbolic_exec_bytecode": [
+        ("t2_commence_killing", [
+            TxInput((5).to_bytes(32, "big").ljust(0x200, b"\0"), sender=C, creation=True),
+            TxInput(abi_call(sel("commencekilling()")), sender=A)]),
+        ("t2_get_bytes", [
+            TxInput((5).to_bytes(32, "big").ljust(0x200, b"\0"), sender=C, creation=True),
+            TxInput(abi_call(sel("getBytes(bytes)"), 0x20, 3, 0xABCDEF << 232), sender=S)]),
+        ("t2_get_bytes_too_long", [
+            TxInput((1).to_bytes(32, "big").ljust(0x200, b"\0"), sender=C, creation=True),
+            TxInput(abi_call(sel("getBytes(bytes)"), 0x20, 3, 0xABCDEF << 232), sender=A)]),
+    ],
+    # SYNTHETIC (builder-written; no reference fixture reaches BLOCKHASH): the
+    # lottery shape `blockhash(block.number - 1) % 2 == 0` plus a timestamp
+    # check, for PredictableVars' BLOCKHASH and JUMPI queries
+    # (dependence_on_predictable_vars.py:68-82,142-159)
+    "synthetic:predictable": [
+        ("t1_blockhash_lottery", [TxInput(b"", sender=A, env={"blockhash_block_block_number - 1": 0x1234,
+                                                               "timestamp": 0x60000001})]),
+        ("t1_blockhash_odd", [TxInput(b"", sender=S, env={"blockhash_block_block_number - 1": 0x1235})]),
     ],
     "vm:vmIOandFlowOperations/DynamicJumpJD_DependsOnJumps0": [
         ("t1_number_branch", [TxInput(b"", sender=A, env={"block_number": 1})]),
@@ -178,9 +243,25 @@ def main():
     write(a.out, a.ref, a.only)
 
 
+def synthetic_code(name: str) -> bytes:
+    """SYNTHETIC contracts (builder-written, tests/laser_concolic.py asm)."""
+    assert name == "predictable"
+    NUMBER, BLOCKHASH, TIMESTAMP, SUB, MOD, ISZERO, GT, JUMPI, STOP = 0x43, 0x40, 0x42, 0x03, 0x06, 0x15, 0x11, 0x57, 0x00
+    CALLVALUE, SSTORE, SWAP1 = 0x34, 0x55, 0x90
+    return asm([
+        ("push", 1, 1), NUMBER, SUB, BLOCKHASH,                  # blockhash(block.number - 1)
+        ("push", 1, 2), SWAP1, MOD, ISZERO, ("ref", "win"), JUMPI, STOP,   # ... % 2 == 0
+        ("label", "win"), ("push", 4, 0x60000000), TIMESTAMP, GT, ("ref", "late"), JUMPI, STOP,
+        ("label", "late"), CALLVALUE, ("push", 1, 0), SSTORE, STOP,
+    ])
+
+
 def load_code(contract: str, ref=None) -> bytes:
     """The bytecode of a fixture: ``name`` is tests/testdata/inputs/name.sol.o,
-    ``vm:category/test`` the ``exec.code`` of a VMTests json."""
+    ``vm:category/test`` the ``exec.code`` of a VMTests json, ``synthetic:x``
+    a builder-written contract (synthetic_code)."""
+    if contract.startswith("synthetic:"):
+        return synthetic_code(contract.split(":", 1)[1])
     if ref:
         if contract.startswith("vm:"):
             path = os.path.join(ref, "tests", "laser", "evm_testsuite", "VMTests", contract[3:] + ".json")
@@ -198,10 +279,21 @@ def import_bytecode(ref: str) -> None:
     path = os.path.join(ROOT, "tests", "golden", "laser_bytecode.json")
     d = json.load(open(path))
     for contract in SCENARIOS:
-        d["bytecode"][contract] = load_code(contract, ref).hex()
+        if not contract.startswith("synthetic:"):
+            d["bytecode"][contract] = load_code(contract, ref).hex()
     d["source"] = ("runtime / creation bytecode of /root/reference/tests/testdata/inputs/*.sol.o and exec.code "
                    "of tests/laser/evm_testsuite/VMTests/*/*.json (reference test data)")
     json.dump(d, open(path, "w"), indent=1)
+
+
+def scenario_balances(opts) -> dict:
+    """The starting balances of the model: every actor's, and the contract's own
+    when the scenario names one (its balance is symbolic in LASER's world state)."""
+    bal = opts.get("balances", 10 ** 18)
+    out = {x: bal for x in ACTORS.values()}
+    if "contract_balance" in opts:
+        out[CONTRACT] = opts["contract_balance"]
+    return out
 
 
 def write(out_dir: str, ref=None, only=None):
@@ -216,17 +308,17 @@ def write(out_dir: str, ref=None, only=None):
             if only is not None and only != f"{contract}/{name}":
                 continue
             opts = opt[0] if opt else {}
-            bal = opts.get("balances", 10 ** 18)
-            m, run = run_sequence(code, txs, storage=opts.get("storage"), balances={x: bal for x in ACTORS.values()})
+            m, run = run_sequence(code, txs, storage=opts.get("storage"), balances=scenario_balances(opts))
             for qi, q in enumerate(run.queries):
                 if q.sat:
                     assert check_model(q.constraints, run.model), (contract, name, qi)
-                tag = contract.replace("vm:", "vm_").replace("/", "_")
+                tag = contract.replace("vm:", "vm_").replace("synthetic:", "synthetic_").replace("/", "_")
                 kt = "" if q.kind == "jumpi" else q.kind.replace("/", "-") + "_"
                 fn = f"{tag}_{name}_q{qi:02d}_{kt}{'sat' if q.sat else 'unknown'}.smt2.gz"
                 with io.TextIOWrapper(gzip.GzipFile(os.path.join(out_dir, fn), "wb", 9, mtime=0)) as fh:
                     fh.write(f"; expect: {'sat' if q.sat else 'unknown'}\n")
                     src = (f"tests/laser/evm_testsuite/VMTests/{contract[3:]}.json" if contract.startswith("vm:")
+                           else "SYNTHETIC (builder-written) " + contract if contract.startswith("synthetic:")
                            else f"tests/testdata/inputs/{contract}.sol.o")
                     where = (f"JUMPI at pc {q.pc}, {'followed' if q.taken else 'other'} successor" if q.kind == "jumpi"
                              else f"{q.kind} get_model at pc {q.pc}")
@@ -235,6 +327,7 @@ def write(out_dir: str, ref=None, only=None):
                 scalars = {k: hex(v) for k, v in run.model.items() if isinstance(v, int)}
                 manifest.append({"file": fn, "contract": contract, "scenario": name, "tx": q.tx, "pc": q.pc,
                                  "kind": q.kind, "status": "sat" if q.sat else "unknown",
+                                 "tuple": q.tuple_form,
                                  "conjuncts": len(q.constraints),
                                  "model_scalars": scalars if q.sat else None})
             kinds = {}
