@@ -33,6 +33,7 @@ Registers (per lane; all clobbered by the block):
   s16..s98    chunk loop and interpreter state (see the constants below)
 """
 import re
+import sys
 
 from mythril_amd import isa
 
@@ -41,9 +42,20 @@ ASM_OPCODES = isa.ASM_OPCODES
 ASM_LEAF_KINDS = isa.ASM_LEAF_KINDS
 
 # ---------------------------------------------------------------- registers
+# Two register layouts (round 5).  "wide": the files above, 256 VGPRs, two
+# waves per SIMD.  "narrow" (the asm interpreter's second kernel,
+# mw_search_asm_kernel_n): the same structure with a 24-slot N file and the
+# narrow constants right after the temporaries - 168 VGPRs, three waves per
+# SIMD - for programs whose N slots all lie below NFILE (95 % of the LASER
+# corpus).  A dispatch is a chain of dependent instructions (profiles/r4m):
+# a third wave per SIMD hides more of it.  variant("narrow") builds this
+# module again with that layout (render_interp emits both bodies).
+_LAYOUT_NAME = globals().get("_LAYOUT_OVERRIDE", "wide")
 W0, N0 = 0, 64
-XA, XB, XR, XC, T = 136, 152, 168, 176, 184
-CLO, CHI, ALIVE, LDSOFF, GOFF = 160, 161, 162, 163, 164
+NFILE = 64 if _LAYOUT_NAME == "wide" else 24     # N slots the layout holds
+_OPB = N0 + NFILE                                # first register after the files: the shift padding
+XA, XB, XR, XC, T = _OPB + 8, _OPB + 24, _OPB + 40, _OPB + 48, _OPB + 56
+CLO, CHI, ALIVE, LDSOFF, GOFF = _OPB + 32, _OPB + 33, _OPB + 34, _OPB + 35, _OPB + 36
 # scalar state
 CUR = 40          # s40..s43 current instruction words w0..w3
 NXT = 44          # s44..s47 next instruction (prefetched)
@@ -92,13 +104,13 @@ VALID = 36        # s[36:37] valid lanes of the chunk
 ARGP = 36         # s[36:37] AsmArgs (prologue only; then VALID)
 PROGP = 38        # s[38:39] ProgDev (prologue only)
 HIT = 38          # after the prologue: this wave has reported a witness (chunks only grow)
-TID, LO_SREG = 165, 0
+TID, LO_SREG = _OPB + 37, 0
 TRACE = 96        # s[96:97] trace rows (AsmArgs.trace; 0 in searches: STORE is then a no-op)
 NCAND = 98        # candidates per trace row (AsmArgs.ncand)
 # the pool digit of the last pooled leaf drawn in this chunk (Lleaf) and its
 # digit group (the asm leaf table's word 6, mw_kernels.hip asm_leaf_table;
 # reset to -1 at every chunk)
-DIGV = 166
+DIGV = _OPB + 38
 DIGKEY = 39
 
 NTAB = 128
@@ -106,9 +118,13 @@ CHAIN_BIT = 15     # predecoded word 0: W_CDINS's FLAG_CHAIN (mw_asm_predecode)
 # narrow constants: v240..v255, filled once per block from the table after the
 # predecoded code; a constant N operand is predecoded as index NK0 - N0 + k
 # (mw_isa.h MW_ASM_NK / MW_ASM_NK_INDEX)
-NK0 = 240
+NK0 = 240 if _LAYOUT_NAME == "wide" else T + 8
 NK_INDEX = NK0 - N0
-assert NK_INDEX == 176 and NK0 + isa.ASM_NK == 256
+# the narrow layout holds two constants fewer: the kernel's own two inputs
+# (thread id, spill offset) need VGPRs outside the asm block's 168
+NKN = isa.ASM_NK if _LAYOUT_NAME == "wide" else isa.ASM_NK - 2
+NVGPR = NK0 + NKN                                # registers the interpreter's asm block uses
+assert (NK_INDEX, NVGPR) == ((176, 256) if _LAYOUT_NAME == "wide" else (88, 166))
 INTROSPECT_FLAG = 7   # AsmArgs.flags bit: report the handler offsets and exit
 
 
@@ -1106,15 +1122,15 @@ def gen(mode="interp"):
         # code and the 8 words the dispatch prefetches past END) -> v240..v255
         g(f"s_lshl_b32 {s(74)}, {s(74)}, 4", f"s_add_u32 {s(74)}, {s(74)}, 32",
           f"s_load_dwordx16 {sr(DESC, 16)}, {sr(CODE0, 2)}, {s(74)}", "s_waitcnt lgkmcnt(0)")
-        for k in range(isa.ASM_NK):
+        for k in range(NKN):
             g(f"v_mov_b32_e32 {v(NK0 + k)}, {s(DESC + k)}")
     else:
         for reg, lab in ((LEAFADDR, "Lleaf_%="), (STOPADDR, "Lstop_%="), (ENDADDR, "Lh_END_%="),
                          (PHILOXADDR, "Lphilox_%=")):
             g.long_addr(reg, lab)
-    for k in range(128, 136, 2):
+    for k in range(XA - 8, XA, 2):       # the shift padding below and above XA
         g(f"v_mov_b64 {vr(k, 2)}, 0")
-    for k in range(144, 152, 2):
+    for k in range(XA + 8, XA + 16, 2):
         g(f"v_mov_b64 {vr(k, 2)}, 0")
     # ---- chunk loop: chunk ch covers [begin + 256 ch, +256)
     g.label("Lchunk_%=")
@@ -1138,7 +1154,7 @@ def gen(mode="interp"):
     if mode == "interp":
         # the register files start at zero (an assembled body zeroes the
         # registers it reads before writing them: static_body / dead_code)
-        for k in range(0, 128, 2):
+        for k in range(0, N0 + NFILE, 2):
             g(f"v_mov_b64 {vr(k, 2)}, 0")
     if mode == "template":
         g.long_addr(SX, "Lbody_%=")
@@ -1392,7 +1408,7 @@ def philox_sub(g):
     g(f"s_setpc_b64 {sr(PRET, 2)}")
 
 
-CLOBBERS = (", ".join(f'"v{i}"' for i in list(range(192)) + list(range(NK0, 256))) + ", "
+CLOBBERS = (", ".join(f'"v{i}"' for i in list(range(T + 8)) + list(range(NK0, NVGPR))) + ", "
             + ", ".join(f'"s{i}"' for i in range(16, 99))
             + ', "vcc", "scc", "m0", "memory"')
 
@@ -1429,7 +1445,34 @@ def render_interp() -> str:
     out += _inc(gen("interp"), "MW_ASM_BODY")
     out += _inc(gen("template"), "MW_ASMJIT_TEMPLATE_BODY")
     out.append(f"#define MW_ASM_CLOBBERS {CLOBBERS}")
+    # the narrow layout's interpreter (mw_search_asm_kernel_n): programs whose N
+    # slots all lie below its NFILE; its narrow constants sit at NK_INDEX
+    nv = variant("narrow")
+    out.append(f"#define MW_ASM_NFILE_N {nv.NFILE}u")
+    out.append(f"#define MW_ASM_NK_INDEX_N {nv.NK_INDEX}u")
+    out.append(f"#define MW_ASM_NK_N {nv.NKN}u")
+    out += _inc(nv.gen("interp"), "MW_ASM_BODY_N")
+    out.append(f"#define MW_ASM_CLOBBERS_N {nv.CLOBBERS}")
     return "\n".join(out) + "\n"
+
+
+_VARIANTS = {}
+
+
+def variant(name: str):
+    """This module built again with register layout `name` ("wide": this one)."""
+    if name == _LAYOUT_NAME:
+        return sys.modules[__name__]
+    mod = _VARIANTS.get(name)
+    if mod is None:
+        import types
+        mod = types.ModuleType(f"{__name__}_{name}")
+        mod.__dict__["_LAYOUT_OVERRIDE"] = name
+        mod.__dict__["__file__"] = __file__
+        with open(__file__) as f:
+            exec(compile(f.read(), __file__, "exec"), mod.__dict__)
+        _VARIANTS[name] = mod
+    return mod
 
 
 # ======================================================== assembled kernels

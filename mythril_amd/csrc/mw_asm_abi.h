@@ -35,7 +35,9 @@ static_assert(sizeof(ProgDev) == 48, "ProgDev layout (mythril_amd/asmgen.py)");
 // Kernel body: stage the program's pool in LDS after the spill words (LDS: the
 // dynamic shared array), run ASMTEXT over this block's chunks (grid x: chunk
 // stride, grid y: program), add the evals to the launch counter (stripe 0).
-#define MW_ASM_KERNEL_BODY(ASMTEXT, LDS)                                                             \
+#define MW_ASM_KERNEL_BODY(ASMTEXT, LDS) MW_ASM_KERNEL_BODY_C(ASMTEXT, LDS, MW_ASM_CLOBBERS)
+// CLOB: the asm block's clobbers (the interpreter's wide or narrow register layout)
+#define MW_ASM_KERNEL_BODY_C(ASMTEXT, LDS, CLOB)                                                     \
   const mw::ProgDev* P = progs + blockIdx.y;                                                         \
   {                                                                                                  \
     mw::u32* dst = LDS + nlds * 256u;                                                                \
@@ -54,5 +56,5 @@ static_assert(sizeof(ProgDev) == 48, "ProgDev layout (mythril_amd/asmgen.py)");
                : [evals] "=s"(evals)                                                                 \
                : [args] "s"(args), [prog] "s"(P), [outmin] "s"(om), [ch0] "s"(ch0), [tid] "v"(tid), \
                  [goff] "v"(goff)                                                                    \
-               : MW_ASM_CLOBBERS);                                                                   \
+               : CLOB);                                                                              \
   if ((threadIdx.x & 63u) == 0 && evals) atomicAdd((unsigned long long*)counter, (unsigned long long)evals);

@@ -35,6 +35,9 @@ extern "C" int mw_fail(int code, const char* msg);
 extern "C" int mg_validate_desc(const mg_prog_desc* d);
 extern "C" int mw_asm_predecode(const uint32_t* code, size_t nwords, const uint32_t* consts, size_t nconst,
                                 const uint32_t* hoff, uint32_t* out, uint32_t* nk);
+extern "C" int mw_asm_predecode_layout(const uint32_t* code, size_t nwords, const uint32_t* consts, size_t nconst,
+                                       const uint32_t* hoff, uint32_t* out, uint32_t* nk, uint32_t nk_index,
+                                       uint32_t nk_max, uint32_t nfile);
 
 using namespace mw;
 
@@ -254,7 +257,20 @@ __global__ __launch_bounds__(kBlock, 2) void mw_search_asm_kernel(const ProgDev*
                                                                 const AsmArgs* __restrict__ args,
                                                                 u64* __restrict__ out_min,
                                                                 u64* __restrict__ counter, u32 nlds) {
-  MW_ASM_KERNEL_BODY(MW_ASM_BODY, lds_spill)
+  MW_ASM_KERNEL_BODY_C(MW_ASM_BODY, lds_spill, MW_ASM_CLOBBERS)
+}
+
+// The same interpreter in the narrow register layout (round 5, asmgen.py
+// variant("narrow")): a 24-slot N file, 166 VGPRs in the asm block, three
+// waves per SIMD where the wide kernel's 256 allow two.  Programs whose N
+// registers all lie below MW_ASM_NFILE_N are predecoded for it at load
+// (Prog::asm_narrow); its launches keep the block's LDS within
+// kLdsSpillWordsN KiB so that three blocks share a CU.
+__global__ __launch_bounds__(kBlock, 3) void mw_search_asm_kernel_n(const ProgDev* __restrict__ progs,
+                                                                  const AsmArgs* __restrict__ args,
+                                                                  u64* __restrict__ out_min,
+                                                                  u64* __restrict__ counter, u32 nlds) {
+  MW_ASM_KERNEL_BODY_C(MW_ASM_BODY_N, lds_spill, MW_ASM_CLOBBERS_N)
 }
 
 __global__ __launch_bounds__(kBlock, 2) void mw_eval_kernel(ProgDev P, const u32* __restrict__ in,
@@ -407,6 +423,7 @@ struct Prog {
   u64 ops_per_eval = 0;
   u64 sig = 0;                  // FNV-1a 64 of the program words (mythril_amd/jit.py signature)
   bool asm_ok = false;          // every opcode and leaf kind has a handler in mw_search_asm_kernel
+  bool asm_narrow = false;      // adev is predecoded for mw_search_asm_kernel_n (the narrow layout)
   bool trace_full = false;      // STOREs cover every trace row: an evaluation needs no zeroed trace block
   ProgDev adev{};               // dev with code = its predecoded copy (mw_asm_predecode) and leaves =
                                 // the asm leaf table (asm_leaf_table), in d_buf
@@ -749,17 +766,32 @@ bool asm_eligible(const mg_prog_desc* d) {
 // words: the pool is staged whole in LDS, the hottest spill words take what is
 // left of the block's 80 KiB and the rest spill to the global buffer.  False if
 // the pool alone does not fit (the programs then run on the compiled interpreter).
-bool asm_lds_fit(u32 max_spill, u32 max_pool, u32* nlds) {
-  const size_t budget = (size_t)kLdsSpillWords * kBlock * 4, pool_bytes = (size_t)max_pool * 4;
+// The narrow-layout kernel's budget: 52 KiB per block, so three blocks (three
+// waves per SIMD) fit a CU's 160 KiB.
+constexpr u32 kLdsSpillWordsN = 52;
+
+bool asm_lds_fit(u32 max_spill, u32 max_pool, u32* nlds, bool narrow = false) {
+  const u32 words = narrow ? kLdsSpillWordsN : kLdsSpillWords;
+  const size_t budget = (size_t)words * kBlock * 4, pool_bytes = (size_t)max_pool * 4;
   if (pool_bytes > budget) return false;
   const u32 pool_words_lds = (u32)((pool_bytes + kBlock * 4 - 1) / (kBlock * 4));  // in spill-word rows
-  *nlds = std::min(max_spill, kLdsSpillWords - pool_words_lds);
+  *nlds = std::min(max_spill, words - pool_words_lds);
   return true;
+}
+
+bool asm_lds_fit(const Prog* p, u32* nlds) {
+  return asm_lds_fit(p->dev.n_spill, p->dev.npool, nlds, p->asm_narrow);
 }
 
 // MYTHRIL_AMD_ASM=0 keeps every program on the compiled interpreter (A/B runs, tests)
 bool asm_enabled() {
   const char* e = std::getenv("MYTHRIL_AMD_ASM");
+  return !(e && e[0] == '0');
+}
+
+// MYTHRIL_AMD_ASM_NARROW=0 predecodes every asm program for the wide kernel (A/B runs)
+bool asm_narrow_enabled() {
+  const char* e = std::getenv("MYTHRIL_AMD_ASM_NARROW");
   return !(e && e[0] == '0');
 }
 
@@ -771,12 +803,11 @@ bool asm_enabled() {
 // asm-eligible (the compiled interpreter runs them: same results).
 std::mutex g_hoff_mu;
 bool g_hoff_ready = false;
-u32 g_hoff[MW_ASM_NHANDLERS];   // 128 opcodes, then the fused handlers (mw_asm_interp.inc)
+u32 g_hoff[MW_ASM_NHANDLERS];     // 128 opcodes, then the fused handlers (mw_asm_interp.inc)
+u32 g_hoff_n[MW_ASM_NHANDLERS];   // the same for mw_search_asm_kernel_n
 
-int asm_handler_offsets(int dev, hipStream_t stream) {
-  std::lock_guard<std::mutex> lk(g_hoff_mu);
-  if (g_hoff_ready) return 0;
-  HIPCHK(hipSetDevice(dev));
+template <typename K>
+int introspect(K kernel, hipStream_t stream, u32* hout) {
   void* buf = nullptr;
   const size_t bytes = sizeof(ProgDev) + sizeof(AsmArgs) + MW_ASM_NHANDLERS * sizeof(u32) + 2 * sizeof(u64);
   HIPCHK(hipMalloc(&buf, bytes));
@@ -793,7 +824,7 @@ int asm_handler_offsets(int dev, hipStream_t stream) {
   if (e == hipSuccess) e = hipMemcpyAsync(dp, &hp, sizeof hp, hipMemcpyHostToDevice, stream);
   if (e == hipSuccess) e = hipMemcpyAsync(da, &ha, sizeof ha, hipMemcpyHostToDevice, stream);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(mw_search_asm_kernel, dim3(1u, 1u), dim3(kBlock), 0, stream, (const ProgDev*)dp,
+    hipLaunchKernelGGL(kernel, dim3(1u, 1u), dim3(kBlock), 0, stream, (const ProgDev*)dp,
                        (const AsmArgs*)da, dmin, dmin + 1, 0u);
     e = hipGetLastError();
   }
@@ -804,10 +835,19 @@ int asm_handler_offsets(int dev, hipStream_t stream) {
   if (e != hipSuccess) return fail(MG_E_HIP, std::string("asm handler offsets: ") + hipGetErrorString(e));
   for (int k = 0; k < MW_ASM_NHANDLERS; ++k) {
     if (h[k] == 0 || h[k] > 0x7fffu) return fail(MG_E_HIP, "asm handler offsets out of range");
-    g_hoff[k] = h[k];
+    hout[k] = h[k];
   }
-  g_hoff_ready = true;
   return 0;
+}
+
+int asm_handler_offsets(int dev, hipStream_t stream) {
+  std::lock_guard<std::mutex> lk(g_hoff_mu);
+  if (g_hoff_ready) return 0;
+  HIPCHK(hipSetDevice(dev));
+  int rc = introspect(mw_search_asm_kernel, stream, g_hoff);
+  if (rc == 0) rc = introspect(mw_search_asm_kernel_n, stream, g_hoff_n);
+  if (rc == 0) g_hoff_ready = true;
+  return rc;
 }
 
 bool asm_offsets_ready() {
@@ -877,6 +917,8 @@ int mg_init(int device, mg_ctx** out) {
       hipFuncSetAttribute((const void*)mw_eval_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
           hipSuccess ||
       hipFuncSetAttribute((const void*)mw_search_asm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
+          hipSuccess ||
+      hipFuncSetAttribute((const void*)mw_search_asm_kernel_n, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
           hipSuccess) {
     (void)hipGetLastError();  // older runtimes: the default limit already covers it
   }
@@ -963,10 +1005,20 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   if (d->nconst_words) std::memcpy(hbuf + nc, d->consts, d->nconst_words * 4);
   if (d->nleaves) std::memcpy(hbuf + nc + nk, d->leaves, d->nleaves * MW_LEAF_WORDS * 4);
   if (d->npool_words) std::memcpy(hbuf + nc + nk + nl, d->pool, d->npool_words * 4);
+  bool narrow = false;
   if (asm_ok) {
     u32* pre = hbuf + nc + nk + nl + np;
-    // more distinct narrow constants than MW_ASM_NK: the compiled interpreter runs it
-    asm_ok = mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, g_hoff, pre, pre + nc + 8) == 0;
+    // the narrow-layout kernel when every N register fits its file, the pool
+    // its LDS budget and the narrow constants its registers; else the wide one.
+    // More distinct narrow constants than MW_ASM_NK: the compiled interpreter runs it
+    u32 nl0 = 0;
+    narrow = asm_narrow_enabled() && asm_lds_fit(d->n_spill, (u32)d->npool_words, &nl0, true) &&
+             mw_asm_predecode_layout(d->code, nc, d->consts, d->nconst_words, g_hoff_n, pre, pre + nc + 8,
+                                     MW_ASM_NK_INDEX_N, MW_ASM_NK_N, MW_ASM_NFILE_N) == 0;
+    if (!narrow) {
+      std::memset(pre, 0, (nc + 8 + MW_ASM_NK) * 4);
+      asm_ok = mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, g_hoff, pre, pre + nc + 8) == 0;
+    }
     if (asm_ok) asm_leaf_table(d->leaves, d->nleaves, pre + nc + 8 + MW_ASM_NK);
   }
   // queued on the context's stream: every launch that reads the program is
@@ -984,6 +1036,7 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   p->dev.npool = (u32)d->npool_words;
   p->dev.n_insn = (u32)(nc / 4);
   p->asm_ok = asm_ok;
+  p->asm_narrow = asm_ok && narrow;
   p->adev = p->dev;
   if (asm_ok) {
     p->adev.code = p->d_buf + nc + nk + nl + np;
@@ -1079,7 +1132,7 @@ int mg_prog_engine(const mg_prog* h) {
   const Prog* p = call.ps[0].get();
   if (p->jit_ready()) return 2;
   u32 nlds = 0;   // the engine mg_search gives this program alone (a pool too big for LDS: compiled)
-  if (!p->asm_ok || !asm_enabled() || !asm_lds_fit(p->dev.n_spill, p->dev.npool, &nlds)) return 0;
+  if (!p->asm_ok || !asm_enabled() || !asm_lds_fit(p, &nlds)) return 0;
   return p->afn ? 3 : 1;
 }
 
@@ -1143,7 +1196,7 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   // the compiled group, then the specialised programs.
   // Programs with an assembled kernel (mg_prog_attach_asm) get one launch each
   // on the asm interpreter's records, after the interpreter groups.
-  std::vector<size_t> gasm, gcpp, gasb, special;
+  std::vector<size_t> gasm, gasn, gcpp, gasb, special;
   u64 ops = 0;
   const bool use_asm = asm_enabled();
   for (size_t i = 0; i < nprog; ++i) {
@@ -1155,40 +1208,46 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     else (use_asm && progs[i]->asm_ok ? gasm : gcpp).push_back(i);
     ops += progs[i]->ops_per_eval;
   }
-  // the asm group needs its pools staged in LDS (programs whose pool does not
-  // fit run on the compiled interpreter)
-  u32 asm_nlds = 0;
+  // the asm groups need their pools staged in LDS (programs whose pool does not
+  // fit run on the compiled interpreter); the narrow-layout programs form a
+  // group of their own (mw_search_asm_kernel_n)
+  u32 asm_nlds = 0, asn_nlds = 0;
   if (!gasm.empty()) {
-    std::vector<size_t> fit;
-    u32 ms = 0;
+    std::vector<size_t> fit, fitn;
+    u32 ms = 0, msn = 0;
     for (size_t i : gasm) {
       u32 n1 = 0;
-      if (count < (1ull << 40) && asm_lds_fit(progs[i]->dev.n_spill, progs[i]->dev.npool, &n1)) {
-        fit.push_back(i);
-        ms = std::max(ms, progs[i]->dev.n_spill);
+      if (count < (1ull << 40) && asm_lds_fit(progs[i], &n1)) {
+        (progs[i]->asm_narrow ? fitn : fit).push_back(i);
+        (progs[i]->asm_narrow ? msn : ms) = std::max(progs[i]->asm_narrow ? msn : ms, progs[i]->dev.n_spill);
       } else {
         gcpp.push_back(i);
       }
     }
     gasm.swap(fit);
-    u32 mp = 0;
+    gasn.swap(fitn);
+    u32 mp = 0, mpn = 0;
     for (size_t i : gasm) mp = std::max(mp, progs[i]->dev.npool);
+    for (size_t i : gasn) mpn = std::max(mpn, progs[i]->dev.npool);
     if (!gasm.empty()) (void)asm_lds_fit(ms, mp, &asm_nlds);
+    if (!gasn.empty()) (void)asm_lds_fit(msn, mpn, &asn_nlds, true);
   }
   std::vector<size_t> interp(gasm);
+  interp.insert(interp.end(), gasn.begin(), gasn.end());
   interp.insert(interp.end(), gcpp.begin(), gcpp.end());
   const size_t ni = interp.size();
   interp.insert(interp.end(), gasb.begin(), gasb.end());   // d_progs / d_min: then the assembled ones
   const size_t nia = interp.size();
   std::vector<ProgDev> hp;
-  for (size_t j = 0; j < nia; ++j)   // the asm group reads the predecoded code
-    hp.push_back(j < gasm.size() ? progs[interp[j]]->adev : progs[interp[j]]->dev);
+  const size_t nasm = gasm.size() + gasn.size();
+  for (size_t j = 0; j < nia; ++j)   // the asm groups read the predecoded code
+    hp.push_back(j < nasm ? progs[interp[j]]->adev : progs[interp[j]]->dev);
   const u64 nchunks = (count + kBlock - 1) / kBlock;
   struct Group {
     size_t first, n;
     u64 gx;
     u32 nlds, max_pool;
-  } groups[2] = {{0, gasm.size(), 1, 0, 0}, {gasm.size(), gcpp.size(), 1, 0, 0}};
+  } groups[3] = {{0, gasm.size(), 1, 0, 0}, {gasm.size(), gasn.size(), 1, 0, 0}, {nasm, gcpp.size(), 1, 0, 0}};
   size_t spill_need = 4;
   for (Group& G : groups) {
     if (!G.n) continue;
@@ -1201,15 +1260,15 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     G.gx = std::max<u64>(1, (u64)c->ncu * 8 / G.n);
     G.gx = std::min<u64>(G.gx, nchunks);
     const u64 nthreads = G.gx * G.n * kBlock;
-    G.nlds = &G == &groups[0] ? asm_nlds : std::min(max_spill, kLdsSpillWords);
+    G.nlds = &G == &groups[0] ? asm_nlds : &G == &groups[1] ? asn_nlds : std::min(max_spill, kLdsSpillWords);
     spill_need = std::max(spill_need, (size_t)(max_spill - G.nlds) * nthreads * sizeof(u32));
   }
   // assembled kernels: records 1.. (one program, the whole chip each)
   const u64 agx = std::min<u64>((u64)c->ncu * 8, nchunks);
-  std::vector<AsmArgs> ha(1 + gasb.size());
+  std::vector<AsmArgs> ha(2 + gasb.size());   // the wide and narrow groups, then the assembled kernels
   for (size_t k = 0; k < gasb.size(); ++k) {
     const ProgDev& d = hp[ni + k];
-    AsmArgs& r = ha[1 + k];
+    AsmArgs& r = ha[2 + k];
     (void)asm_lds_fit(d.n_spill, d.npool, &r.nlds);
     r.seed = seed;
     r.begin = begin;
@@ -1221,25 +1280,25 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     r.verdict = nullptr;
     spill_need = std::max(spill_need, (size_t)(d.n_spill - r.nlds) * agx * kBlock * sizeof(u32));
   }
-  const bool need_args = groups[0].n || !gasb.empty();
+  const bool need_args = groups[0].n || groups[1].n || !gasb.empty();
   rc = ensure_launch(c, nprog, need_args ? ha.size() : 0);
   if (rc) return rc;
   if (nia) {
     rc = ensure_spill(c, spill_need);
     if (rc) return rc;
   }
-  for (size_t k = 0; k < gasb.size(); ++k) ha[1 + k].spillbuf = c->d_spill;
-  AsmArgs& aa = ha[0];
-  if (need_args) {
+  for (size_t k = 0; k < gasb.size(); ++k) ha[2 + k].spillbuf = c->d_spill;
+  for (int gi = 0; gi < 2 && need_args; ++gi) {
+    AsmArgs& aa = ha[gi];
     aa.seed = seed;
     aa.begin = begin;
     aa.end = begin + count;
     aa.flags = flags;
-    aa.nlds = groups[0].nlds;
-    aa.gstride = (u32)(groups[0].gx * groups[0].n * kBlock * 4);
+    aa.nlds = groups[gi].nlds;
+    aa.gstride = (u32)(groups[gi].gx * groups[gi].n * kBlock * 4);
     aa.nchunks = (u32)nchunks;
-    aa.gdx = (u32)groups[0].gx;
-    aa.spillbuf = c->d_spill;
+    aa.gdx = (u32)groups[gi].gx;
+    aa.spillbuf = c->d_spill;   // the launches run one after the other on the stream
     aa.verdict = nullptr;
   }
   // one upload: zeroed counters, d_min at MG_NONE, the ProgDev and AsmArgs records
@@ -1254,6 +1313,14 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   }
   if (groups[1].n) {
     const Group& G = groups[1];
+    const size_t lds = (size_t)G.nlds * kBlock * 4 + (size_t)G.max_pool * 4;
+    hipLaunchKernelGGL(mw_search_asm_kernel_n, dim3((u32)G.gx, (u32)G.n), dim3(kBlock), lds, c->stream,
+                       c->d_progs + G.first, (const AsmArgs*)c->d_asmargs + 1, c->d_min + G.first, c->d_counter,
+                       G.nlds);
+    HIPCHK(hipGetLastError());
+  }
+  if (groups[2].n) {
+    const Group& G = groups[2];
     // stage the pools in LDS when they fit beside the spill words (80 KiB per
     // block keeps two blocks per CU)
     const size_t spill_bytes = (size_t)G.nlds * kBlock * 4, pool_bytes = (size_t)G.max_pool * 4;
@@ -1272,8 +1339,8 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     HIPCHK(hipGetLastError());
   }
   for (size_t k = 0; k < gasb.size(); ++k) {
-    rc = launch_assembled(c, progs[gasb[k]], (u32)agx, c->d_progs + ni + k, c->d_asmargs + 1 + k,
-                          c->d_min + ni + k, ha[1 + k].nlds);
+    rc = launch_assembled(c, progs[gasb[k]], (u32)agx, c->d_progs + ni + k, c->d_asmargs + 2 + k,
+                          c->d_min + ni + k, ha[2 + k].nlds);
     if (rc) return rc;
   }
   for (size_t j = 0; j < special.size(); ++j) {
@@ -1392,7 +1459,7 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
   if (trace && (count >= (1ull << 32) || ntr * 4 >= (1ull << 31))) return 1;
   const bool assembled = p->afn != nullptr && !trace;   // its assembled kernel, else the asm interpreter
   u32 nlds = 0;
-  if (!asm_lds_fit(p->dev.n_spill, p->dev.npool, &nlds)) return 1;
+  if (!(assembled ? asm_lds_fit(p->dev.n_spill, p->dev.npool, &nlds) : asm_lds_fit(p, &nlds))) return 1;
   const size_t lds = (size_t)nlds * kBlock * 4 + (size_t)p->dev.npool * 4;
   HIPCHK(hipSetDevice(c->dev));
   (void)hipGetLastError();
@@ -1425,8 +1492,12 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
   if (e == hipSuccess && assembled) {
     if (launch_assembled(c, p, (u32)gx, c->d_progs, c->d_asmargs, c->d_min, nlds)) return MG_E_HIP;
   } else if (e == hipSuccess) {
-    hipLaunchKernelGGL(mw_search_asm_kernel, dim3((u32)gx, 1u), dim3(kBlock), lds, c->stream, c->d_progs,
-                       (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, nlds);
+    if (p->asm_narrow)
+      hipLaunchKernelGGL(mw_search_asm_kernel_n, dim3((u32)gx, 1u), dim3(kBlock), lds, c->stream, c->d_progs,
+                         (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, nlds);
+    else
+      hipLaunchKernelGGL(mw_search_asm_kernel, dim3((u32)gx, 1u), dim3(kBlock), lds, c->stream, c->d_progs,
+                         (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, nlds);
     e = hipGetLastError();
   }
   const bool pinned = vb + tb <= kReadbackMax && ensure_readback(c, vb + tb);

@@ -223,22 +223,29 @@ int mg_validate_desc(const mg_prog_desc* d) {
 // sequence first, list order among equal lengths) gets its sequence's handler:
 // one dispatch runs the whole sequence, which takes the instructions after
 // the first itself (their own words are left as they are).
-int mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t nconst, const u32* hoff,
-                     u32* out, u32* nk) {
+// Layouts (mythril_amd/asmgen.py, round 5): nk_index / nk_max place the narrow
+// constants of the interpreter kernel the copy is for (the wide kernel:
+// MW_ASM_NK_INDEX / MW_ASM_NK; the narrow-layout kernel: MW_ASM_NK_INDEX_N /
+// MW_ASM_NK_N); nfile > 0 also requires every N register operand and N result
+// to lie below nfile slots (-2 otherwise: the program needs the wide kernel).
+int mw_asm_predecode_layout(const u32* code, size_t nwords, const u32* consts, size_t nconst, const u32* hoff,
+                            u32* out, u32* nk, u32 nk_index, u32 nk_max, u32 nfile) {
   u32 nnk = 0;
   for (u32 k = 0; k < MW_ASM_NK; ++k) nk[k] = 0;
+  if (nk_max > MW_ASM_NK) return -1;
   auto narrow = [&](int kind, u32 f, u32* dst) -> bool {   // dst: the predecoded field
     if (kind != 2 || !(f & MW_KBIT)) return true;
     const u32 val = consts[f & 0x7fffu];
     u32 k = 0;
     while (k < nnk && nk[k] != val) ++k;
     if (k == nnk) {
-      if (nnk == MW_ASM_NK) return false;
+      if (nnk == nk_max) return false;
       nk[nnk++] = val;
     }
-    *dst = MW_ASM_NK_INDEX + k;
+    *dst = nk_index + k;
     return true;
   };
+  auto in_file = [&](int kind, u32 f) { return kind != 2 || (f & MW_KBIT) || !nfile || f < nfile; };
   for (size_t i = 0; i + 3 < nwords; i += 4) {
     const u32* I = code + i;
     u32* O = out + i;
@@ -257,6 +264,8 @@ int mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t n
       for (int k = 1; k < 8 && small; ++k) small = consts[o + k] == 0u;
       if (small) c2 = 0x4000u | consts[o];
     }
+    if (nfile && (!in_file(sh.a, a) || !in_file(sh.b, b) || !in_file(sh.c, c) || (sh.dst == 4 && d2 >= nfile)))
+      return -2;
     if (!narrow(sh.a, a, &a2) || !narrow(sh.b, b, &b2) || !narrow(sh.c, c, &c2)) return -1;
     O[0] = (I[0] & 0xffff0000u) | ((I[0] >> 8) & MW_FLAG_CHAIN ? 0x8000u : 0u) | (hoff[op & 0x7fu] & 0x7fffu);
     O[1] = a2 | (d2 << 16);   // s_set_gpr_idx_on reads bits [7:0]: a indexes from the word as it is
@@ -289,6 +298,11 @@ int mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t n
     i += blen;
   }
   return 0;
+}
+
+int mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t nconst, const u32* hoff,
+                     u32* out, u32* nk) {
+  return mw_asm_predecode_layout(code, nwords, consts, nconst, hoff, out, nk, MW_ASM_NK_INDEX, MW_ASM_NK, 0);
 }
 
 }  // extern "C"

@@ -30,7 +30,8 @@ def test_opcode_lists_agree():
     # reports an offset for all 128 opcodes (handler or Lunsup)
     for o in isa.ASM_OPCODES:
         assert f"Lh_{o}_%=:" in txt, o
-    assert txt.count("- Lpc0_%=) >> 2)") == 128 + len(isa.ASM_FUSED)   # and every fused handler's
+    # (twice: the wide and the narrow layout's interpreter)
+    assert txt.count("- Lpc0_%=) >> 2)") == 2 * (128 + len(isa.ASM_FUSED))   # and every fused handler's
     for k in range(len(isa.ASM_FUSED)):
         assert f"Lf{k}_%=:" in txt
     assert "s_branch Lh_" not in txt          # one jump per dispatch: no table of branches
@@ -159,3 +160,56 @@ def test_predecode_fused_sequences():
     for i in range(len(src)):
         want = (plain[i] & 0xFFFF8000) | HOFF[128 + fused[i]] if i in fused else plain[i]
         assert o[i, 0] == want, i
+
+
+def _predecode_layout(code, consts, nk_index, nk_max, nfile):
+    import ctypes
+
+    import numpy as np
+
+    from mythril_amd.runtime import LIB_PATH
+    f = ctypes.CDLL(LIB_PATH).mw_asm_predecode_layout
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+    code = np.ascontiguousarray(code, dtype=np.uint32)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32)
+    out = np.zeros_like(code)
+    nk = np.full(isa.ASM_NK, 0xDEAD, dtype=np.uint32)
+    rc = f(code.ctypes.data, code.size, consts.ctypes.data, consts.size, HOFF.ctypes.data, out.ctypes.data,
+           nk.ctypes.data, nk_index, nk_max, nfile)
+    return rc, out.reshape(-1, 4), nk
+
+
+def test_narrow_layout_predecode():
+    """Round 5: the asm interpreter's second kernel holds a 24-slot N file and
+    14 narrow constants at v64 + 88 (asmgen.variant("narrow")).  A program is
+    predecoded for it only when every N register lies below 24 (else -2: the
+    wide kernel runs it); its narrow constants then name VGPR 88 + k, and the
+    rest of the copy is the wide predecode's."""
+    from mythril_amd import asmgen
+    nv = asmgen.variant("narrow")
+    assert (nv.NFILE, nv.NK_INDEX, nv.NKN, nv.NVGPR) == (24, 88, 14, 166)
+    assert nv.XA == 96 and nv.T + 8 == nv.NK0 and asmgen.XA == 136
+    e = isa.encode
+    consts = [0] * 9
+    consts[8] = 0x77
+    code = (e("N_ADD", 8, isa.encode_dst("N", 7), 3, isa.KBIT | 8) + e("N_ULT", 8, isa.encode_dst("N", 23), 7, 3)
+            + e("END", 0, isa.encode_dst(None)))
+    rc, o, nk = _predecode_layout(code, consts, 88, 14, 24)
+    assert rc == 0 and o[0, 2] == 88 and nk[0] == 0x77
+    wide, _ = _predecode(code, consts)
+    assert (o[:, 0] == wide[:, 0]).all() and (o[1:, 1:] == wide[1:, 1:]).all()
+    high = code[:-4] + e("N_NOT", 8, isa.encode_dst("N", 24), 23) + e("END", 0, isa.encode_dst(None))
+    assert _predecode_layout(high, consts, 88, 14, 24)[0] == -2
+    assert _predecode_layout(high, consts, 176, 16, 0)[0] == 0      # no file bound: the wide layout
+    many = [0] * 15 + list(range(100, 115))
+    wide_k = sum((e("N_ADD", 8, isa.encode_dst("N", 1), 0, isa.KBIT | (15 + i)) for i in range(15)), [])
+    assert _predecode_layout(wide_k + e("END", 0, isa.encode_dst(None)), many, 88, 14, 24)[0] == -1
+
+
+def test_corpus_mostly_fits_the_narrow_layout():
+    """The LASER corpus: most programs keep their N registers below 24 slots."""
+    progs = [p for f, p in _corpus_programs() if ".gz" in f]
+    fit = sum(_predecode_layout(p.code, p.consts, 88, 14, 24)[0] == 0 for p in progs)
+    assert fit >= 0.9 * len(progs), (fit, len(progs))
