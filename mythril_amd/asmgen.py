@@ -32,6 +32,7 @@ Registers (per lane; all clobbered by the block):
   v240..v255  the program's narrow constants (interpreter)
   s16..s98    chunk loop and interpreter state (see the constants below)
 """
+import os
 import re
 import sys
 
@@ -50,16 +51,31 @@ ASM_LEAF_KINDS = isa.ASM_LEAF_KINDS
 # corpus).  A dispatch is a chain of dependent instructions (profiles/r4m):
 # a third wave per SIMD hides more of it.  variant("narrow") builds this
 # module again with that layout (render_interp emits both bodies).
+# "quarter" (mw_search_asm_kernel_q): 4 W slots and 16 N slots, 126 VGPRs in
+# the asm block, four waves per SIMD, for programs whose registers all lie
+# in those files (about half of the LASER corpus as compiled).
 _LAYOUT_NAME = globals().get("_LAYOUT_OVERRIDE", "wide")
-W0, N0 = 0, 64
-NFILE = 64 if _LAYOUT_NAME == "wide" else 24     # N slots the layout holds
+WFILE = 4 if _LAYOUT_NAME == "quarter" else 8     # W slots the layout holds
+W0, N0 = 0, 8 * WFILE
+NFILE = {"wide": 64, "narrow": 24, "quarter": 16}[_LAYOUT_NAME]   # N slots the layout holds
 _OPB = N0 + NFILE                                # first register after the files: the shift padding
 XA, XB, XR, XC, T = _OPB + 8, _OPB + 24, _OPB + 40, _OPB + 48, _OPB + 56
 CLO, CHI, ALIVE, LDSOFF, GOFF = _OPB + 32, _OPB + 33, _OPB + 34, _OPB + 35, _OPB + 36
 # scalar state
-CUR = 40          # s40..s43 current instruction words w0..w3
-NXT = 44          # s44..s47 next instruction (prefetched)
-SOFF = 48         # byte offset of the next instruction from CODE0
+# The interpreter keeps two instructions in SGPRs, in two banks: instruction
+# i of the predecoded stream always lives in bank i & 1 (s40..s43 for even i,
+# s44..s47 for odd).  While the handler of i runs, i + 1 is already in (or on
+# its way to) the other bank; dispatching to it loads i + 2 into the bank i
+# vacates and jumps through the other bank's word 0 - the handler's absolute
+# address, low word (mw_asm_predecode) - with no register moves.  Every
+# handler is generated once per bank (Gen.CUR names the bank it reads).
+# DISPATCH "single" (MYTHRIL_AMD_ASM_DISPATCH at generation time) keeps one
+# current bank and copies the prefetched words into it instead: the handlers
+# are emitted once and both banks' entries of the offset table name them.
+CUR = 40          # s40..s43 bank A: the current instruction of even index (or of every index, "single")
+NXT = 44          # s44..s47 bank B: the odd instructions (the prefetched one, "single")
+DISPATCH = os.environ.get("MYTHRIL_AMD_ASM_DISPATCH", "pingpong")
+SOFF = 48         # byte offset of the instruction last loaded, from CODE0
 TABLO = 49        # address of the handlers' base (Lpc0), low / high word
 TABHI = 58
 SIDX = 19         # register-file index of an operand / write-back
@@ -87,8 +103,9 @@ S = list(range(72, 80))   # scratch s72..s79
 DESC = 80         # s[80:87] leaf descriptor / wide constant
 MSK = 88          # s[88:89] saved lane mask
 MSK2 = 90         # s[90:91]
-JMP = 92          # s[92:93]
+JMP = 92          # s[92:93] the dispatch target: s92 the handler's low word, s93 the code's high word
 SX = 94           # s[94:95] scratch pair
+AM = 100          # s[100:101] the chunk's live lanes (valid, every check so far held)
 
 # chunk loop state (s16..s39)
 CH, NCH, GDX = 16, 17, 18
@@ -114,7 +131,7 @@ DIGV = _OPB + 38
 DIGKEY = 39
 
 NTAB = 128
-CHAIN_BIT = 15     # predecoded word 0: W_CDINS's FLAG_CHAIN (mw_asm_predecode)
+CHAIN_BIT = 31     # predecoded word 3 (the immediate): W_CDINS's FLAG_CHAIN (mw_asm_predecode)
 # narrow constants: v240..v255, filled once per block from the table after the
 # predecoded code; a constant N operand is predecoded as index NK0 - N0 + k
 # (mw_isa.h MW_ASM_NK / MW_ASM_NK_INDEX)
@@ -124,7 +141,7 @@ NK_INDEX = NK0 - N0
 # (thread id, spill offset) need VGPRs outside the asm block's 168
 NKN = isa.ASM_NK if _LAYOUT_NAME == "wide" else isa.ASM_NK - 2
 NVGPR = NK0 + NKN                                # registers the interpreter's asm block uses
-assert (NK_INDEX, NVGPR) == ((176, 256) if _LAYOUT_NAME == "wide" else (88, 166))
+assert (NK_INDEX, NVGPR) == {"wide": (176, 256), "narrow": (88, 166), "quarter": (80, 126)}[_LAYOUT_NAME]
 INTROSPECT_FLAG = 7   # AsmArgs.flags bit: report the handler offsets and exit
 
 
@@ -152,6 +169,7 @@ class Gen:
         self.tail = []      # out-of-line blocks (constant operands), emitted after the handler
         self.n = 0
         self.bound = {}     # name -> operand field (field())
+        self.CUR = CUR      # the bank holding the current instruction (s40 or s44; consume() flips it)
 
     def L(self, base):
         self.n += 1
@@ -177,7 +195,9 @@ class Gen:
     # SGPR (tools/exp/gpridx_probe.hip), so a and b index straight from their
     # word; c and dst take one shift.
     # field() only binds an operand to a name; fetch_n / fetch_w read it.
-    WORD = {"a": (CUR + 1, "lo"), "b": (CUR + 2, "lo"), "c": (CUR + 2, "hi")}
+    def word(self, which):
+        """(SGPR, half) holding operand field `which` of the current instruction"""
+        return {"a": (self.CUR + 1, "lo"), "b": (self.CUR + 2, "lo"), "c": (self.CUR + 2, "hi")}[which]
 
     def field(self, which, dst):
         """bind operand field a/b/c to the name dst (no code)"""
@@ -185,14 +205,14 @@ class Gen:
 
     def _index(self, which):
         """the SGPR to hand s_set_gpr_idx_on for operand field `which`"""
-        wd, half = self.WORD[which]
+        wd, half = self.word(which)
         if half == "hi":
             self(f"s_lshr_b32 {s(SIDX)}, {s(wd)}, 16")
             return s(SIDX)
         return s(wd)
 
     def _is_const(self, which, label):
-        wd, half = self.WORD[which]
+        wd, half = self.word(which)
         self(f"s_bitcmp1_b32 {s(wd)}, {31 if half == 'hi' else 15}", f"s_cbranch_scc1 {label}")
 
     def fetch_n(self, f, dst):
@@ -201,6 +221,14 @@ class Gen:
         file, NK0)"""
         idx = self._index(self.bound[f])
         self(f"s_set_gpr_idx_on {idx}, gpr_idx(SRC0)", f"v_mov_b32_e32 {v(dst)}, {v(N0)}", "s_set_gpr_idx_off")
+
+    def op_n(self, f, fmt, scratch, mode="SRC0"):
+        """emit fmt with {a} = the N operand bound to f, read in place through
+        the index register (gpr_idx(mode): fmt's instruction reads {a} as that
+        source and no other file register); scratch: the VGPR an assembled
+        body may stage it in"""
+        idx = self._index(self.bound[f])
+        self(f"s_set_gpr_idx_on {idx}, gpr_idx({mode})", fmt.format(a=v(N0)), "s_set_gpr_idx_off")
 
     def fetch_w(self, f, dst):
         """W/K operand bound to f -> VGPRs dst..dst+7"""
@@ -213,7 +241,7 @@ class Gen:
             self(f"v_mov_b32_e32 {v(dst + k)}, {v(W0 + k)}")
         self("s_set_gpr_idx_off")
         self.label(lr)
-        wd, half = self.WORD[which]
+        wd, half = self.word(which)
         off = f"s_bfe_u32 {s(SX)}, {s(wd)}, {(15 << 16) | (16 if half == 'hi' else 0):#x}"   # the word offset
         t = [f"{lk}:", off, f"s_lshl_b32 {s(SX)}, {s(SX)}, 2",
              f"s_load_dwordx8 {sr(DESC, 8)}, {sr(CPOOL, 2)}, {s(SX)}", "s_waitcnt lgkmcnt(0)"]
@@ -233,7 +261,7 @@ class Gen:
         emit(W0)
         self("s_set_gpr_idx_off")
         self.label(lr)
-        wd, half = self.WORD[which]
+        wd, half = self.word(which)
         main, self.lines = self.lines, [f"{lk}:", f"s_bfe_u32 {s(SX)}, {s(wd)}, {(15 << 16) | (16 if half == 'hi' else 0):#x}",
                                         f"s_lshl_b32 {s(SX)}, {s(SX)}, 2",
                                         f"s_load_dwordx8 {sr(DESC, 8)}, {sr(CPOOL, 2)}, {s(SX)}", "s_waitcnt lgkmcnt(0)"]
@@ -244,7 +272,8 @@ class Gen:
         self.lines = main
 
     def width(self, dst):
-        self(f"s_lshr_b32 {s(dst)}, {s(CUR)}, 16")
+        # predecoded word 1 [31:24]: the width - 1
+        self(f"s_lshr_b32 {s(dst)}, {s(self.CUR + 1)}, 24", f"s_add_u32 {s(dst)}, {s(dst)}, 1")
 
     def nmask(self, w, dst):
         """dst = w >= 32 ? ~0 : (1 << w) - 1 (w in SGPR, <= 32): the low word of
@@ -255,16 +284,16 @@ class Gen:
     def insn_mask(self, dst):
         """the SGPR holding this instruction's result mask: word 3, where
         mw_asm_predecode puts it for N_ADD / N_SUB / N_MUL / N_NOT (no code)"""
-        return s(CUR + 3)
+        return s(self.CUR + 3)
 
     def write_n(self, src):
         """N result in VGPR src -> the N slot in the predecoded dst field (word 1 [31:16])"""
-        self(f"s_lshr_b32 {s(SIDX)}, {s(CUR + 1)}, 16", f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(DST)",
+        self(f"s_lshr_b32 {s(SIDX)}, {s(self.CUR + 1)}, 16", f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(DST)",
              f"v_mov_b32_e32 {v(N0)}, {v(src)}", "s_set_gpr_idx_off")
 
     def write_w(self, src):
         """W result in VGPRs src.. -> the W slot x 8 in the predecoded dst field (word 1 [31:16])"""
-        self(f"s_lshr_b32 {s(SIDX)}, {s(CUR + 1)}, 16", f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(DST)")
+        self(f"s_lshr_b32 {s(SIDX)}, {s(self.CUR + 1)}, 16", f"s_set_gpr_idx_on {s(SIDX)}, gpr_idx(DST)")
         for k in range(8):
             self(f"v_mov_b32_e32 {v(W0 + k)}, {v(src + k)}")
         self("s_set_gpr_idx_off")
@@ -286,7 +315,13 @@ class Gen:
         self.label(done)
 
     def nop_vcc(self):
-        self("s_nop 1")
+        """a VALU reading the vcc the previous VALU wrote needs no wait states
+        (carry chains measured exact without them)"""
+
+    def all_dead_exit(self):
+        """SCC = AM != 0 (just ANDed): no live lane -> the dead stub of this
+        bank (the chunk ends, or with early exit off, the next instruction)"""
+        self(f"s_cbranch_scc0 Ldead{'AB'[self.CUR == NXT and DISPATCH != 'single']}_%=")
 
     def bit_at(self, base, w, dst):
         """v(dst) = bit w (SGPR) of the limbs at VGPR base (limb w >> 5 read
@@ -311,7 +346,7 @@ class Gen:
     def extract_limb(self, q, r):
         """XR = bits imm..imm+31 of XA (imm: the instruction's immediate word;
         limb 8 reads v144, zeroed once per block); q, r: scratch SGPRs"""
-        self(f"s_lshr_b32 {s(q)}, {s(CUR + 3)}, 5", f"s_and_b32 {s(r)}, {s(CUR + 3)}, 31",
+        self(f"s_lshr_b32 {s(q)}, {s(self.CUR + 3)}, 5", f"s_and_b32 {s(r)}, {s(self.CUR + 3)}, 31",
              f"s_set_gpr_idx_on {s(q)}, gpr_idx(SRC0,SRC1)",
              f"v_alignbit_b32 {v(XR)}, {v(XA + 1)}, {v(XA)}, {s(r)}", "s_set_gpr_idx_off")
 
@@ -351,12 +386,43 @@ class Gen:
     def call_leaf_sub(self):
         self(f"s_call_b64 {sr(LRET, 2)}, Lleaf_%=")
 
+    def other(self):
+        """the bank that is not CUR"""
+        return CUR + NXT - self.CUR
+
+    _WRITE_MOV = re.compile(r"v_mov_b32_e32 v(\d+), v(\d+)")
+
+    def fuse_write(self):
+        """Before a dispatch: `v_op vR, ...` then write_n's `s_lshr; on(DST);
+        v_mov vN0, vR; off` becomes `s_lshr; on(DST); v_op vN0, ...; off` -
+        the producer writes the N slot through the index register itself (vR
+        is dead once the handler ends; the op's sources are not indexed in
+        DST mode)."""
+        L = self.lines
+        if len(L) < 5:
+            return
+        op, sh, on, mv, off = L[-5:]
+        m = self._WRITE_MOV.fullmatch(mv)
+        if not (m and int(m.group(1)) == N0 and on.endswith("gpr_idx(DST)") and off == "s_set_gpr_idx_off"
+                and sh.startswith(f"s_lshr_b32 {s(SIDX)}, ")):
+            return
+        mo = re.fullmatch(rf"(v_\w+) v{m.group(2)}, (.*)", op)
+        if not mo or "gpr_idx" in op:
+            return
+        L[-5:] = [sh, on, f"{mo.group(1)} {v(N0)}, {mo.group(2)}", off]
+
     def consume(self):
-        """take the next instruction into CUR without a dispatch (the next link
+        """make the next instruction current without a dispatch (the next link
         of a W_CDINS chain, the next handler of a fused sequence) and prefetch
-        the one after it"""
-        self("s_waitcnt lgkmcnt(0)", f"s_mov_b64 {sr(CUR, 2)}, {sr(NXT, 2)}", f"s_mov_b64 {sr(CUR + 2, 2)}, {sr(NXT + 2, 2)}",
-             f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, {s(SOFF)}")
+        the one after it into the bank this one vacates"""
+        self.fuse_write()
+        if DISPATCH == "single":
+            self("s_waitcnt lgkmcnt(0)", f"s_mov_b64 {sr(CUR, 2)}, {sr(NXT, 2)}", f"s_mov_b64 {sr(CUR + 2, 2)}, {sr(NXT + 2, 2)}",
+                 f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, {s(SOFF)}")
+            return
+        self("s_waitcnt lgkmcnt(0)", f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16",
+             f"s_load_dwordx4 {sr(self.CUR, 4)}, {sr(CODE0, 2)}, {s(SOFF)}")
+        self.CUR = self.other()
 
     def next(self):
         """dispatch the next instruction (each handler ends in its own copy:
@@ -366,11 +432,16 @@ class Gen:
         word offset from Lpc0 in bits [14:0] (mw_asm_predecode, from the
         offsets the kernel reports in its introspection mode): one jump, no
         table."""
-        self("s_waitcnt lgkmcnt(0)", f"s_mov_b64 {sr(CUR, 2)}, {sr(NXT, 2)}",
-             f"s_mov_b64 {sr(CUR + 2, 2)}, {sr(NXT + 2, 2)}",
-             f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, {s(SOFF)}",
-             f"s_and_b32 {s(JMP)}, {s(CUR)}, 0x7fff", f"s_lshl2_add_u32 {s(SX)}, {s(JMP)}, {s(TABLO)}",
-             f"s_addc_u32 {s(SX + 1)}, {s(TABHI)}, 0", f"s_setpc_b64 {sr(SX, 2)}")
+        self.fuse_write()
+        if DISPATCH == "single":
+            self("s_waitcnt lgkmcnt(0)", f"s_mov_b32 {s(JMP)}, {s(NXT)}", f"s_mov_b64 {sr(CUR, 2)}, {sr(NXT, 2)}",
+                 f"s_mov_b64 {sr(CUR + 2, 2)}, {sr(NXT + 2, 2)}",
+                 f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, {s(SOFF)}",
+                 f"s_setpc_b64 {sr(JMP, 2)}")
+            return
+        self("s_waitcnt lgkmcnt(0)", f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16",
+             f"s_load_dwordx4 {sr(self.CUR, 4)}, {sr(CODE0, 2)}, {s(SOFF)}",
+             f"s_mov_b32 {s(JMP)}, {s(self.other())}", f"s_setpc_b64 {sr(JMP, 2)}")
 
 
 def build_handlers():
@@ -392,8 +463,8 @@ def build_handlers():
                                ("N_XOR", "v_xor_b32_e32 {d}, {a}, {b}", False)):
         def h(g, expr=expr, masked=masked):
             g.field("a", S[0]), g.field("b", S[1])
-            g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
-            g(expr.format(d=v(XR), a=v(T), b=v(T + 1)))
+            g.fetch_n(S[1], T + 1)
+            g.op_n(S[0], expr.format(d=v(XR), a="{a}", b=v(T + 1)), T)
             if masked:
                 g(f"v_and_b32_e32 {v(XR)}, {g.insn_mask(S[4])}, {v(XR)}")
             g.write_n(XR)
@@ -402,8 +473,8 @@ def build_handlers():
     @handler("N_MUL")
     def _(g):
         g.field("a", S[0]), g.field("b", S[1])
-        g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
-        g(f"v_mul_lo_u32 {v(XR)}, {v(T)}, {v(T + 1)}")
+        g.fetch_n(S[1], T + 1)
+        g.op_n(S[0], f"v_mul_lo_u32 {v(XR)}, {{a}}, {v(T + 1)}", T)
         g(f"v_and_b32_e32 {v(XR)}, {g.insn_mask(S[4])}, {v(XR)}")
         g.write_n(XR)
 
@@ -434,15 +505,15 @@ def build_handlers():
 
     @handler("N_NOT")
     def _(g):
-        g.field("a", S[0]), g.fetch_n(S[0], T)
-        g(f"v_xor_b32_e32 {v(XR)}, {g.insn_mask(S[4])}, {v(T)}")      # ~a & m == a ^ m (a canonical)
+        g.field("a", S[0])
+        g.op_n(S[0], f"v_xor_b32_e32 {v(XR)}, {g.insn_mask(S[4])}, {{a}}", T, "SRC1")   # ~a & m == a ^ m (a canonical)
         g.write_n(XR)
 
     for name, cmp in (("N_EQN", "v_cmp_eq_u32_e32"), ("N_ULTN", "v_cmp_lt_u32_e32"), ("N_ULEN", "v_cmp_le_u32_e32")):
         def h(g, cmp=cmp):
             g.field("a", S[0]), g.field("b", S[1])
-            g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
-            g(f"{cmp} vcc, {v(T)}, {v(T + 1)}")
+            g.fetch_n(S[1], T + 1)
+            g.op_n(S[0], f"{cmp} vcc, {{a}}, {v(T + 1)}", T)
             g.bool_from_vcc(XR)
             g.write_n(XR)
         handlers[name] = h
@@ -450,18 +521,18 @@ def build_handlers():
     @handler("N_ITE")
     def _(g):
         g.field("a", S[0]), g.field("b", S[1]), g.field("c", S[2])
-        g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1), g.fetch_n(S[2], T + 2)
-        g(f"v_cmp_ne_u32_e32 vcc, 0, {v(T + 2)}")
+        g.fetch_n(S[0], T)
+        g.op_n(S[2], "v_cmp_ne_u32_e32 vcc, 0, {a}", T + 2, "SRC1")
         g.nop_vcc()
-        g(f"v_cndmask_b32_e32 {v(XR)}, {v(T + 1)}, {v(T)}, vcc")
+        g.op_n(S[1], f"v_cndmask_b32_e32 {v(XR)}, {{a}}, {v(T)}, vcc", T + 1)
         g.write_n(XR)
 
     for name, op in (("N_SHLI", "v_lshlrev_b32_e32"), ("N_LSHRI", "v_lshrrev_b32_e32")):
         def h(g, op=op):
-            g.field("a", S[0]), g.fetch_n(S[0], T)
+            g.field("a", S[0])
             big, j = g.L("sb"), g.L("sj")
-            g(f"s_cmp_ge_u32 {s(CUR + 3)}, 32", f"s_cbranch_scc1 {big}",
-              f"{op} {v(XR)}, {s(CUR + 3)}, {v(T)}")
+            g(f"s_cmp_ge_u32 {s(g.CUR + 3)}, 32", f"s_cbranch_scc1 {big}")
+            g.op_n(S[0], f"{op} {v(XR)}, {s(g.CUR + 3)}, {{a}}", T, "SRC1")
             g.width(S[2]), g.nmask(S[2], S[4])
             g(f"v_and_b32_e32 {v(XR)}, {s(S[4])}, {v(XR)}", f"s_branch {j}")
             g.label(big)
@@ -477,34 +548,30 @@ def build_handlers():
     # -------------------------------------------------------- checks
     def update_alive(g):
         """alive &= vcc, then the early-exit test"""
-        g.nop_vcc()
-        g(f"v_cndmask_b32_e32 {v(ALIVE)}, 0, {v(ALIVE)}, vcc")
-        skip = g.L("ee")
-        g(f"s_bitcmp1_b32 {s(FLAGS)}, 0", f"s_cbranch_scc0 {skip}",
-          f"v_cmp_ne_u32_e32 vcc, 0, {v(ALIVE)}", "s_nop 1", "s_cmp_eq_u64 vcc, 0")
-        g.stop_if_scc1()
-        g.label(skip)
+        g(f"s_and_b64 {sr(AM, 2)}, {sr(AM, 2)}, vcc")
+        g.all_dead_exit()
 
     @handler("CHECK")
     def _(g):
-        g.field("a", S[0]), g.fetch_n(S[0], T)
-        g(f"v_cmp_ne_u32_e32 vcc, 0, {v(T)}")
+        g.field("a", S[0])
+        g.op_n(S[0], "v_cmp_ne_u32_e32 vcc, 0, {a}", T, "SRC1")
         update_alive(g)
 
     @handler("CHECK_IMP")
     def _(g):
         g.field("a", S[0]), g.field("b", S[1])
-        g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1)
-        g(f"v_cmp_eq_u32_e64 {sr(MSK, 2)}, 0, {v(T)}", f"v_cmp_ne_u32_e32 vcc, 0, {v(T + 1)}",
-          "s_nop 1", f"s_or_b64 vcc, vcc, {sr(MSK, 2)}")
+        g.op_n(S[0], f"v_cmp_eq_u32_e64 {sr(MSK, 2)}, 0, {{a}}", T, "SRC1")
+        g.op_n(S[1], "v_cmp_ne_u32_e32 vcc, 0, {a}", T + 1, "SRC1")
+        g(f"s_or_b64 vcc, vcc, {sr(MSK, 2)}")
         update_alive(g)
 
     @handler("CHECK_IMPEQ")
     def _(g):
         g.field("a", S[0]), g.field("b", S[1]), g.field("c", S[2])
-        g.fetch_n(S[0], T), g.fetch_n(S[1], T + 1), g.fetch_n(S[2], T + 2)
-        g(f"v_cmp_eq_u32_e64 {sr(MSK, 2)}, 0, {v(T)}", f"v_cmp_eq_u32_e32 vcc, {v(T + 1)}, {v(T + 2)}",
-          "s_nop 1", f"s_or_b64 vcc, vcc, {sr(MSK, 2)}")
+        g.op_n(S[0], f"v_cmp_eq_u32_e64 {sr(MSK, 2)}, 0, {{a}}", T, "SRC1")
+        g.fetch_n(S[2], T + 2)
+        g.op_n(S[1], f"v_cmp_eq_u32_e32 vcc, {{a}}, {v(T + 2)}", T + 1)
+        g(f"s_or_b64 vcc, vcc, {sr(MSK, 2)}")
         update_alive(g)
 
     def eq8(g, a, b, dst_v):
@@ -707,7 +774,7 @@ def build_handlers():
         """dst..dst+7 = XA << amount (SGPR, < 256): written through a positive
         destination index (limbs past dst+7 land in the next 8 temporaries
         and are dropped); XA has zeros below it"""
-        if amount == CUR + 3 and g.static_imm() is not None:   # an assembled body: literal limbs
+        if amount == g.CUR + 3 and g.static_imm() is not None:   # an assembled body: literal limbs
             n = g.static_imm() & 255
             q, b = n >> 5, n & 31
             src = lambda i: v(XA + i) if i >= 0 else "0"   # noqa: E731
@@ -740,7 +807,7 @@ def build_handlers():
     @handler("W_SHLI")
     def _(g):
         g.field("a", S[0]), g.fetch_w(S[0], XA)
-        shl_into(g, CUR + 3, XR)
+        shl_into(g, g.CUR + 3, XR)
         g.width(S[2]), g.canon(XR, S[2])
         g.write_w(XR)
 
@@ -756,7 +823,7 @@ def build_handlers():
                   else f"v_mov_b32_e32 {v(XR + k)}, 0")
         else:
             q, b = S[4], S[5]
-            g(f"s_lshr_b32 {s(q)}, {s(CUR + 3)}, 5", f"s_and_b32 {s(b)}, {s(CUR + 3)}, 31",
+            g(f"s_lshr_b32 {s(q)}, {s(g.CUR + 3)}, 5", f"s_and_b32 {s(b)}, {s(g.CUR + 3)}, 31",
               f"s_set_gpr_idx_on {s(q)}, gpr_idx(SRC0,SRC1)")
             for k in range(8):
                 g(f"v_alignbit_b32 {v(XR + k)}, {v(XA + k + 1)}, {v(XA + k)}, {s(b)}")
@@ -861,7 +928,7 @@ def build_handlers():
         else:
             for k in range(1, 8):
                 g(f"v_mov_b32_e32 {v(XA + k)}, 0")
-            shl_imm_into_or(g, CUR + 3)
+            shl_imm_into_or(g, g.CUR + 3)
         g.width(S[2]), g.canon(XR, S[2])
         g.write_w(XR)
 
@@ -871,18 +938,13 @@ def build_handlers():
         for k in range(8):
             g(f"v_or_b32_e32 {v(XR + k)}, {v(XR + k)}, {v(XC + k)}")
 
-    @handler("W_CDINS")
-    def _(g):
-        # acc | ((K[c] <s size) ? leaf(imm & 0xffff) : 0) << (imm >> 16), chained
-        # links keep the word in XR (mw_interp.h MW_W_CDINS, MW_FLAG_CHAIN)
-        g.field("a", S[0]), g.fetch_w(S[0], XR)
-        g(f"s_mov_b32 {s(S[0])}, -1")                 # b operand of the cached size summary: none
-        top, slow, rng, ins = g.L("cdtop"), g.L("cdslow"), g.L("cdrng"), g.L("cdins")
-        g.label(top)
+    def cdins_link(g):
+        """one W_CDINS link on the current bank's instruction: XR |= the byte"""
+        slow, rng, ins = g.L("cdslow"), g.L("cdrng"), g.L("cdins")
         # predecoded small index (mw_asm_predecode): c = 0x4000 | i, i < 0x4000
-        g(f"s_bitcmp1_b32 {s(CUR + 2)}, 30", f"s_cbranch_scc0 {slow}",
-          f"s_bfe_u32 {s(S[1])}, {s(CUR + 2)}, 0xe0010",        # i = bits [29:16]
-          f"s_and_b32 {s(S[2])}, {s(CUR + 2)}, 0xffff",
+        g(f"s_bitcmp1_b32 {s(g.CUR + 2)}, 30", f"s_cbranch_scc0 {slow}",
+          f"s_bfe_u32 {s(S[1])}, {s(g.CUR + 2)}, 0xe0010",        # i = bits [29:16]
+          f"s_and_b32 {s(S[2])}, {s(g.CUR + 2)}, 0xffff",
           f"s_cmp_eq_u32 {s(S[2])}, {s(S[0])}", f"s_cbranch_scc1 {rng}",
           f"s_mov_b32 {s(S[0])}, {s(S[2])}")
         # size summary in XA: i <s size  <=>  i <u XA, XA = size < 0 ? 0 :
@@ -910,7 +972,7 @@ def build_handlers():
         # no lane in range: the inserted byte is 0 in every lane (no leaf draw)
         nos = g.L("cdns")
         g("s_nop 1", f"s_cmp_eq_u64 {sr(MSK2, 2)}, 0", f"s_cbranch_scc1 {nos}")
-        g(f"s_and_b32 {s(S[3])}, {s(CUR + 3)}, 0xffff")
+        g(f"s_and_b32 {s(S[3])}, {s(g.CUR + 3)}, 0xffff")
         if g.inline_leaf:   # no call / return jumps on the hottest leaf path (C2: 64 of 86 instructions)
             g(f"s_mov_b32 {s(S67)}, {s(S[3])}")
             g(*leaf_inline(g.L("il")[1:-3], limb0=True))
@@ -918,7 +980,7 @@ def build_handlers():
             call_leaf(g, S[3])
         # t = in range ? byte : 0, inserted at bit off = imm >> 16 (limb off >> 5)
         g(f"v_cndmask_b32_e64 {v(T)}, 0, {v(XC)}, {sr(MSK2, 2)}",
-          f"s_lshr_b32 {s(S[4])}, {s(CUR + 3)}, 16",
+          f"s_bfe_u32 {s(S[4])}, {s(g.CUR + 3)}, 0x80010",      # off: imm [23:16] (bit 31: the chain flag)
           f"s_lshr_b32 {s(S[5])}, {s(S[4])}, 5", f"s_and_b32 {s(S[4])}, {s(S[4])}, 31",
           f"s_set_gpr_idx_on {s(S[5])}, gpr_idx(SRC2,DST)",
           f"v_lshl_or_b32 {v(XR)}, {v(T)}, {s(S[4])}, {v(XR)}", "s_set_gpr_idx_off")
@@ -929,14 +991,34 @@ def build_handlers():
           f"s_set_gpr_idx_on {s(S[5])}, gpr_idx(SRC1,DST)",
           f"v_or_b32_e32 {v(XR)}, {v(T)}, {v(XR)}", "s_set_gpr_idx_off")
         g.label(nos)
-        # chained: consume the next instruction (a W_CDINS whose acc is this word)
-        last = g.L("cdlast")
-        g(f"s_bitcmp1_b32 {s(CUR)}, {CHAIN_BIT}", f"s_cbranch_scc0 {last}")
-        g.width(S[2]), g.canon(XR, S[2])
-        g.consume()
-        g(f"s_branch {top}")
-        g.label(last)
-        g.width(S[2]), g.canon(XR, S[2])
+
+    @handler("W_CDINS")
+    def _(g):
+        # acc | ((K[c] <s size) ? leaf(imm & 0xffff) : 0) << (imm >> 16), chained
+        # links keep the word in XR (mw_interp.h MW_W_CDINS, MW_FLAG_CHAIN).
+        # Two links per loop trip, one per bank, each with its own exit: the
+        # first exit falls through to this handler's dispatch, the second
+        # dispatches from the other bank
+        g.field("a", S[0]), g.fetch_w(S[0], XR)
+        g(f"s_mov_b32 {s(S[0])}, -1")                 # b operand of the cached size summary: none
+        nlinks = 1 if DISPATCH == "single" else 2
+        tops, exits = [g.L("cdtop") for _ in range(nlinks)], []
+        for j in range(nlinks):
+            g.label(tops[j])
+            cdins_link(g)
+            g.width(S[2]), g.canon(XR, S[2])
+            # chained (imm bit 31): consume the next instruction (a W_CDINS whose acc is this word)
+            exits.append((g.L("cdlast"), g.CUR))
+            g(f"s_bitcmp1_b32 {s(g.CUR + 3)}, {CHAIN_BIT}", f"s_cbranch_scc0 {exits[-1][0]}")
+            g.consume()
+        g(f"s_branch {tops[0]}")
+        for lab, bank in exits[1:]:
+            g.label(lab)
+            g.CUR = bank
+            g.write_w(XR)
+            g.next()
+        g.label(exits[0][0])
+        g.CUR = exits[0][1]
         g.write_w(XR)
 
     # -------------------------------------------------------- leaves
@@ -947,13 +1029,13 @@ def build_handlers():
 
     @handler("LEAF_W")
     def _(g):
-        g(f"s_mov_b32 {s(S[0])}, {s(CUR + 3)}")
+        g(f"s_mov_b32 {s(S[0])}, {s(g.CUR + 3)}")
         call_leaf(g, S[0])
         g.write_w(XC)
 
     @handler("LEAF_N")
     def _(g):
-        g(f"s_mov_b32 {s(S[0])}, {s(CUR + 3)}")
+        g(f"s_mov_b32 {s(S[0])}, {s(g.CUR + 3)}")
         call_leaf(g, S[0])
         g.write_n(XC)
 
@@ -977,28 +1059,28 @@ def build_handlers():
     def _(g):
         g.field("a", S[0]), g.fetch_w(S[0], XA)
         for k in range(8):
-            g(f"s_add_u32 {s(S[1])}, {s(CUR + 3)}, {k}")
+            g(f"s_add_u32 {s(S[1])}, {s(g.CUR + 3)}, {k}")
             spill_word(g, S[1], XA + k)
         g("s_waitcnt vmcnt(0) lgkmcnt(0)")
 
     @handler("SPILL_N")
     def _(g):
         g.field("a", S[0]), g.fetch_n(S[0], XA)
-        g(f"s_mov_b32 {s(S[1])}, {s(CUR + 3)}")
+        g(f"s_mov_b32 {s(S[1])}, {s(g.CUR + 3)}")
         spill_word(g, S[1], XA)
         g("s_waitcnt vmcnt(0) lgkmcnt(0)")
 
     @handler("FILL_W")
     def _(g):
         for k in range(8):
-            g(f"s_add_u32 {s(S[1])}, {s(CUR + 3)}, {k}")
+            g(f"s_add_u32 {s(S[1])}, {s(g.CUR + 3)}, {k}")
             spill_word(g, S[1], XR + k, store=False)
         g("s_waitcnt vmcnt(0) lgkmcnt(0)")
         g.write_w(XR)
 
     @handler("FILL_N")
     def _(g):
-        g(f"s_mov_b32 {s(S[1])}, {s(CUR + 3)}")
+        g(f"s_mov_b32 {s(S[1])}, {s(g.CUR + 3)}")
         spill_word(g, S[1], XR, store=False)
         g("s_waitcnt vmcnt(0) lgkmcnt(0)")
         g.write_n(XR)
@@ -1011,7 +1093,7 @@ def build_handlers():
         buffer (searches): nothing"""
         skip = g.L("ts")
         g(f"s_cmp_eq_u64 {sr(TRACE, 2)}, 0", f"s_cbranch_scc1 {skip}",
-          f"s_mul_i32 {s(S[1])}, {s(CUR + 3)}, {s(NCAND)}", f"s_lshl_b32 {s(S[2])}, {s(NCAND)}, 2",
+          f"s_mul_i32 {s(S[1])}, {s(g.CUR + 3)}, {s(NCAND)}", f"s_lshl_b32 {s(S[2])}, {s(NCAND)}, 2",
           f"v_subrev_u32_e32 {v(T)}, {s(BEGIN)}, {v(CLO)}", f"v_add_u32_e32 {v(T)}, {s(S[1])}, {v(T)}",
           f"v_lshlrev_b32_e32 {v(T)}, 2, {v(T)}",
           f"s_mov_b64 {sr(EXECSV, 2)}, exec", f"s_mov_b64 exec, {sr(VALID, 2)}")
@@ -1062,6 +1144,36 @@ HANDLERS = build_handlers()
 MARKER = "; MWJIT_BODY"
 
 
+_NOT_SALU = ("s_cbranch", "s_branch", "s_setpc", "s_set_gpr_idx", "s_call", "s_swappc", "s_endpgm", "s_movrel")
+
+
+def drop_idx_offs(lines):
+    """`s_set_gpr_idx_off` then only scalar instructions (no VALU, no label,
+    no branch) then `s_set_gpr_idx_on`: the off is dropped - the on replaces
+    the index and the mode, and nothing between reads a VGPR."""
+    out = []
+    n = len(lines)
+    for i, ln in enumerate(lines):
+        if ln == "s_set_gpr_idx_off":
+            j = i + 1
+            while j < n and lines[j].startswith("s_") and not lines[j].startswith(_NOT_SALU) \
+                    and not lines[j].endswith(":"):
+                j += 1
+            if j < n and lines[j].startswith("s_set_gpr_idx_on "):
+                continue
+        out.append(ln)
+    return out
+
+
+def _hlabel(n, bank):
+    """an opcode's handler label in bank 0 (A) or 1 (B); "single" has bank A only"""
+    return f"Lh_{n}_%=" if bank == 0 or DISPATCH == "single" else f"Lh_{n}_B_%="
+
+
+def _flabel(k, bank):
+    return f"Lf{k}_%=" if bank == 0 or DISPATCH == "single" else f"Lf{k}_B_%="
+
+
 def gen(mode="interp"):
     """The inline-asm body, as a list of lines.  mode "interp": the
     threaded-dispatch interpreter; "template": the same kernel with the
@@ -1102,19 +1214,28 @@ def gen(mode="interp"):
         g.label("Lpc0_%=")
         if TABHI != TABLO + 1:
             g(f"s_mov_b32 {s(TABLO)}, {s(SX)}", f"s_mov_b32 {s(TABHI)}, {s(SX + 1)}")
+        g(f"s_mov_b32 {s(JMP + 1)}, {s(TABHI)}")   # the dispatch target's high word, for good
         # introspection (AsmArgs.flags bit 7): lane 0 writes the word offset of
-        # every opcode's handler from Lpc0 to the verdict pointer and the kernel
-        # exits; mg_init reads them once for mw_asm_predecode
+        # every opcode's handler from Lpc0 to the verdict pointer, bank A's
+        # table (opcodes, then the fused sequences) then bank B's, then Lpc0's
+        # address (low, high word), and the kernel exits; mg_init reads them
+        # once for mw_asm_predecode
         names = {c: n for n, c in isa.OPCODES.items()}
         g(f"s_bitcmp1_b32 {s(FLAGS)}, {INTROSPECT_FLAG}", "s_cbranch_scc0 Lnointro_%=",
           f"s_mov_b64 {sr(EXECSV, 2)}, exec", "s_mov_b64 exec, 1")
-        for code in range(NTAB):
-            n = names.get(code)
-            tgt = f"Lh_{n}_%=" if (n in handlers or n == "END") else "Lunsup_%="
-            g(f"v_mov_b32_e32 {v(T)}, (({tgt} - Lpc0_%=) >> 2)", f"v_mov_b32_e32 {v(T + 1)}, {4 * code}",
-              f"global_store_dword {v(T + 1)}, {v(T)}, {sr(VERD, 2)}")
-        for k in range(len(isa.ASM_FUSED)):   # the fused handlers' offsets follow (entries NTAB + k)
-            g(f"v_mov_b32_e32 {v(T)}, ((Lf{k}_%= - Lpc0_%=) >> 2)", f"v_mov_b32_e32 {v(T + 1)}, {4 * (NTAB + k)}",
+        nh = NTAB + len(isa.ASM_FUSED)
+        for bank in range(2):
+            for code in range(NTAB):
+                n = names.get(code)
+                tgt = f"{_hlabel(n, bank)}" if n in handlers else "Lh_END_%=" if n == "END" else "Lunsup_%="
+                g(f"v_mov_b32_e32 {v(T)}, (({tgt} - Lpc0_%=) >> 2)", f"v_mov_b32_e32 {v(T + 1)}, {4 * (bank * nh + code)}",
+                  f"global_store_dword {v(T + 1)}, {v(T)}, {sr(VERD, 2)}")
+            for k in range(len(isa.ASM_FUSED)):   # the fused handlers' offsets follow (entries NTAB + k)
+                g(f"v_mov_b32_e32 {v(T)}, (({_flabel(k, bank)} - Lpc0_%=) >> 2)",
+                  f"v_mov_b32_e32 {v(T + 1)}, {4 * (bank * nh + NTAB + k)}",
+                  f"global_store_dword {v(T + 1)}, {v(T)}, {sr(VERD, 2)}")
+        for j, reg in enumerate((TABLO, TABHI)):
+            g(f"v_mov_b32_e32 {v(T)}, {s(reg)}", f"v_mov_b32_e32 {v(T + 1)}, {4 * (2 * nh + j)}",
               f"global_store_dword {v(T + 1)}, {v(T)}, {sr(VERD, 2)}")
         g(f"s_mov_b64 exec, {sr(EXECSV, 2)}", "s_branch Lexit_%=")
         g.label("Lnointro_%=")
@@ -1150,7 +1271,7 @@ def gen(mode="interp"):
       f"v_add_co_u32_e32 {v(CLO)}, vcc, {s(BASE)}, {v(TID)}", "s_nop 1",
       f"v_addc_co_u32_e32 {v(CHI)}, vcc, 0, {v(T + 7)}, vcc",
       f"v_cmp_gt_u64_e32 vcc, {sr(END, 2)}, {vr(CLO, 2)}", "s_nop 1",
-      f"s_mov_b64 {sr(VALID, 2)}, vcc", f"v_cndmask_b32_e64 {v(ALIVE)}, 0, 1, vcc")
+      f"s_mov_b64 {sr(VALID, 2)}, vcc", f"s_mov_b64 {sr(AM, 2)}, vcc")
     if mode == "interp":
         # the register files start at zero (an assembled body zeroes the
         # registers it reads before writing them: static_body / dead_code)
@@ -1160,37 +1281,52 @@ def gen(mode="interp"):
         g.long_addr(SX, "Lbody_%=")
         g(f"s_setpc_b64 {sr(SX, 2)}")
     else:
-        g(f"s_mov_b32 {s(SOFF)}, 0", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, 0x0")
-        # ---- dispatch
-        g.label("Ldisp_%=")
-        g.next()
-        # handlers
-        for n in ASM_OPCODES:
-            if n == "END":
-                continue
-            g.label(f"Lh_{n}_%=")
-            handlers[n](g)
+        # ---- the first dispatch: instruction 0 into bank A, 1 into bank B
+        if DISPATCH == "single":
+            g(f"s_mov_b32 {s(SOFF)}, 0", f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, 0x0")
             g.next()
-            g.flush_tail()
-        # fused sequences (isa.ASM_FUSED): the handlers back to back, each
-        # later one taking its instruction as a W_CDINS chain link does; one
-        # dispatch at the end
-        for k, seq in enumerate(isa.ASM_FUSED):
-            g.label(f"Lf{k}_%=")
-            for j, n in enumerate(seq):
-                if j:
-                    g.consume()
+        else:
+            g(f"s_mov_b32 {s(SOFF)}, 16", f"s_load_dwordx4 {sr(CUR, 4)}, {sr(CODE0, 2)}, 0x0",
+              f"s_load_dwordx4 {sr(NXT, 4)}, {sr(CODE0, 2)}, 0x10", "s_waitcnt lgkmcnt(0)",
+              f"s_mov_b32 {s(JMP)}, {s(CUR)}", f"s_setpc_b64 {sr(JMP, 2)}")
+        # handlers, once per bank
+        for bank in range(1 if DISPATCH == "single" else 2):
+            for n in ASM_OPCODES:
+                if n == "END":
+                    continue
+                g.CUR = (CUR, NXT)[bank]
+                g.label(_hlabel(n, bank))
                 handlers[n](g)
+                g.next()
+                g.flush_tail()
+            # fused sequences (isa.ASM_FUSED): the handlers back to back, each
+            # later one taking its instruction as a W_CDINS chain link does;
+            # one dispatch at the end
+            for k, seq in enumerate(isa.ASM_FUSED):
+                g.CUR = (CUR, NXT)[bank]
+                g.label(_flabel(k, bank))
+                for j, n in enumerate(seq):
+                    if j:
+                        g.consume()
+                    handlers[n](g)
+                g.next()
+                g.flush_tail()
+            # every lane dead (a check's all_dead_exit): the chunk ends, or
+            # without early exit (traces, verdicts) the next instruction runs
+            g.CUR = (CUR, NXT)[bank]
+            g.label(f"Ldead{'AB'[bank]}_%=")
+            g(f"s_bitcmp1_b32 {s(FLAGS)}, 0", "s_cbranch_scc1 Lstop_%=")
             g.next()
-            g.flush_tail()
+        g.CUR = CUR
+    if mode == "interp":
+        body[:] = drop_idx_offs(body)
     g.label("Lunsup_%=")
     g.label("Lstop_%=")
-    g(f"v_mov_b32_e32 {v(ALIVE)}, 0")
+    g(f"s_mov_b64 {sr(AM, 2)}, 0")
     g.label("Lh_END_%=")
     # ---- this chunk's result: verdicts, evals, lowest satisfying lane -> atomic min
     g("s_waitcnt vmcnt(0) lgkmcnt(0)",
-      f"v_cmp_ne_u32_e32 vcc, 0, {v(ALIVE)}", "s_nop 1",
-      f"s_and_b64 {sr(MSK, 2)}, vcc, {sr(VALID, 2)}",
+      f"s_and_b64 {sr(MSK, 2)}, {sr(AM, 2)}, {sr(VALID, 2)}",
       f"s_bcnt1_i32_b64 {s(SX)}, {sr(VALID, 2)}",
       f"s_add_u32 {s(EVALS)}, {s(EVALS)}, {s(SX)}", f"s_addc_u32 {s(EVALS + 1)}, {s(EVALS + 1)}, 0",
       f"s_cmp_eq_u64 {sr(VERD, 2)}, 0", "s_cbranch_scc1 Lnoverd_%=",
@@ -1207,8 +1343,8 @@ def gen(mode="interp"):
       # one per satisfied chunk: dense programs queued them on one address)
       f"s_cmp_lg_u32 {s(HIT)}, 0", "s_cbranch_scc1 Lnohit_%=",
       # the wave's lowest satisfying lane issues the atomic with its own candidate index
-      f"s_ff1_i32_b64 {s(SX)}, {sr(MSK, 2)}", f"s_lshl_b64 {sr(JMP, 2)}, 1, {s(SX)}",
-      f"s_mov_b64 {sr(EXECSV, 2)}, exec", f"s_mov_b64 exec, {sr(JMP, 2)}",
+      f"s_ff1_i32_b64 {s(SX)}, {sr(MSK, 2)}", f"s_lshl_b64 {sr(MSK2, 2)}, 1, {s(SX)}",
+      f"s_mov_b64 {sr(EXECSV, 2)}, exec", f"s_mov_b64 exec, {sr(MSK2, 2)}",
       f"v_mov_b32_e32 {v(T + 2)}, 0",
       f"global_atomic_umin_x2 {v(T + 2)}, {vr(CLO, 2)}, {sr(OUTMIN, 2)}",
       f"s_mov_b64 exec, {sr(EXECSV, 2)}", f"s_mov_b32 {s(HIT)}, 1")
@@ -1409,7 +1545,7 @@ def philox_sub(g):
 
 
 CLOBBERS = (", ".join(f'"v{i}"' for i in list(range(T + 8)) + list(range(NK0, NVGPR))) + ", "
-            + ", ".join(f'"s{i}"' for i in range(16, 99))
+            + ", ".join(f'"s{i}"' for i in list(range(16, 99)) + [AM, AM + 1])
             + ', "vcc", "scc", "m0", "memory"')
 
 
@@ -1439,6 +1575,9 @@ def render_interp() -> str:
            f"#define MW_ASM_NFUSED {len(isa.ASM_FUSED)}",
            f"#define MW_ASM_FUSED_MAX {isa.ASM_FUSED_MAX}",
            f"#define MW_ASM_NHANDLERS ({NTAB} + MW_ASM_NFUSED)",
+           # the introspection table: bank A's handlers, bank B's, Lpc0 (lo, hi)
+           "#define MW_ASM_NHTAB (2 * MW_ASM_NHANDLERS + 2)",
+           f"// dispatch: {DISPATCH}",
            "#define MW_ASM_FUSED_SEQS " + ", ".join(
                "{" + ", ".join([f"MW_{n}" for n in t] + ["0xffu"] * (isa.ASM_FUSED_MAX - len(t))) + "}"
                for t in isa.ASM_FUSED)]
@@ -1453,6 +1592,14 @@ def render_interp() -> str:
     out.append(f"#define MW_ASM_NK_N {nv.NKN}u")
     out += _inc(nv.gen("interp"), "MW_ASM_BODY_N")
     out.append(f"#define MW_ASM_CLOBBERS_N {nv.CLOBBERS}")
+    # the quarter layout's (mw_search_asm_kernel_q): W slots below WFILE too
+    qv = variant("quarter")
+    out.append(f"#define MW_ASM_WFILE_Q {qv.WFILE}u")
+    out.append(f"#define MW_ASM_NFILE_Q {qv.NFILE}u")
+    out.append(f"#define MW_ASM_NK_INDEX_Q {qv.NK_INDEX}u")
+    out.append(f"#define MW_ASM_NK_Q {qv.NKN}u")
+    out += _inc(qv.gen("interp"), "MW_ASM_BODY_Q")
+    out.append(f"#define MW_ASM_CLOBBERS_Q {qv.CLOBBERS}")
     return "\n".join(out) + "\n"
 
 
@@ -1525,6 +1672,14 @@ class StaticGen(Gen):
             self(f"v_mov_b32_e32 {v(dst)}, {_lit(self.consts[val & 0x7FFF])}")
         else:
             self(f"v_mov_b32_e32 {v(dst)}, {v(N0 + val)}")
+
+    def op_n(self, f, fmt, scratch, mode="SRC0"):
+        val = self._field(f)
+        if val & KBIT:
+            self.fetch_n(f, scratch)
+            self(fmt.format(a=v(scratch)))
+        else:
+            self(fmt.format(a=v(N0 + val)))
 
     def fetch_w(self, f, dst):
         val = self._field(f)
@@ -1616,6 +1771,14 @@ class StaticGen(Gen):
         lab = self.L("go")
         self(f"s_cbranch_scc0 {lab}", f"s_setpc_b64 {sr(STOPADDR, 2)}")
         self.label(lab)
+
+    def all_dead_exit(self):
+        """straight-line body: no live lane -> Lstop when early exit is on,
+        else on with the next instruction"""
+        live = self.L("lv")
+        self(f"s_cbranch_scc1 {live}", f"s_bitcmp1_b32 {s(FLAGS)}, 0")
+        self.stop_if_scc1()
+        self.label(live)
 
     def call_leaf_sub(self):
         self(f"s_swappc_b64 {sr(LRET, 2)}, {sr(LEAFADDR, 2)}")
@@ -1958,12 +2121,8 @@ def _check_run_static(g, run):
         pending, pending_lines = m, combine
     g("s_nop 1")
     g(*pending_lines)
-    g(f"v_cndmask_b32_e64 {v(ALIVE)}, 0, {v(ALIVE)}, {sr(ACC, 2)}")
-    skip = g.L("ee")
-    g(f"s_bitcmp1_b32 {s(FLAGS)}, 0", f"s_cbranch_scc0 {skip}",
-      f"v_cmp_ne_u32_e32 vcc, 0, {v(ALIVE)}", "s_nop 1", "s_cmp_eq_u64 vcc, 0")
-    g.stop_if_scc1()
-    g.label(skip)
+    g(f"s_and_b64 {sr(AM, 2)}, {sr(AM, 2)}, {sr(ACC, 2)}")
+    g.all_dead_exit()
 
 
 LDS_SPILL_WORDS = 80   # mw_kernels.hip kLdsSpillWords

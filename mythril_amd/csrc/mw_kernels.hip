@@ -37,7 +37,7 @@ extern "C" int mw_asm_predecode(const uint32_t* code, size_t nwords, const uint3
                                 const uint32_t* hoff, uint32_t* out, uint32_t* nk);
 extern "C" int mw_asm_predecode_layout(const uint32_t* code, size_t nwords, const uint32_t* consts, size_t nconst,
                                        const uint32_t* hoff, uint32_t* out, uint32_t* nk, uint32_t nk_index,
-                                       uint32_t nk_max, uint32_t nfile);
+                                       uint32_t nk_max, uint32_t nfile, uint32_t wfile);
 
 using namespace mw;
 
@@ -273,6 +273,23 @@ __global__ __launch_bounds__(kBlock, 3) void mw_search_asm_kernel_n(const ProgDe
   MW_ASM_KERNEL_BODY_C(MW_ASM_BODY_N, lds_spill, MW_ASM_CLOBBERS_N)
 }
 
+// The quarter layout (asmgen.py variant("quarter")): 4 W slots and 16 N
+// slots, 126 VGPRs in the asm block, four waves per SIMD, for programs whose
+// W and N registers all lie in those files; LDS within kLdsSpillWordsQ KiB
+// per block so that four blocks share a CU.
+__global__ __launch_bounds__(kBlock, 4) void mw_search_asm_kernel_q(const ProgDev* __restrict__ progs,
+                                                                  const AsmArgs* __restrict__ args,
+                                                                  u64* __restrict__ out_min,
+                                                                  u64* __restrict__ counter, u32 nlds) {
+  MW_ASM_KERNEL_BODY_C(MW_ASM_BODY_Q, lds_spill, MW_ASM_CLOBBERS_Q)
+}
+
+// the asm interpreter's kernels by register layout (Prog::asm_layout)
+typedef uint8_t u8;
+enum AsmLayout : u8 { kWide = 0, kNarrow = 1, kQuarter = 2, kAsmLayouts = 3 };
+typedef void (*AsmKernel)(const ProgDev*, const AsmArgs*, u64*, u64*, u32);
+const AsmKernel kAsmKernel[kAsmLayouts] = {mw_search_asm_kernel, mw_search_asm_kernel_n, mw_search_asm_kernel_q};
+
 __global__ __launch_bounds__(kBlock, 2) void mw_eval_kernel(ProgDev P, const u32* __restrict__ in,
                                                          u64 ncand, u64 seed, u64 begin,
                                                          u32* __restrict__ verdict,
@@ -423,7 +440,7 @@ struct Prog {
   u64 ops_per_eval = 0;
   u64 sig = 0;                  // FNV-1a 64 of the program words (mythril_amd/jit.py signature)
   bool asm_ok = false;          // every opcode and leaf kind has a handler in mw_search_asm_kernel
-  bool asm_narrow = false;      // adev is predecoded for mw_search_asm_kernel_n (the narrow layout)
+  u8 asm_layout = kWide;        // the asm kernel adev is predecoded for (kAsmKernel)
   bool trace_full = false;      // STOREs cover every trace row: an evaluation needs no zeroed trace block
   ProgDev adev{};               // dev with code = its predecoded copy (mw_asm_predecode) and leaves =
                                 // the asm leaf table (asm_leaf_table), in d_buf
@@ -767,11 +784,11 @@ bool asm_eligible(const mg_prog_desc* d) {
 // left of the block's 80 KiB and the rest spill to the global buffer.  False if
 // the pool alone does not fit (the programs then run on the compiled interpreter).
 // The narrow-layout kernel's budget: 52 KiB per block, so three blocks (three
-// waves per SIMD) fit a CU's 160 KiB.
-constexpr u32 kLdsSpillWordsN = 52;
+// waves per SIMD) fit a CU's 160 KiB; the quarter layout's 40 KiB (four).
+constexpr u32 kLdsSpillWordsByLayout[kAsmLayouts] = {kLdsSpillWords, 52, 40};
 
-bool asm_lds_fit(u32 max_spill, u32 max_pool, u32* nlds, bool narrow = false) {
-  const u32 words = narrow ? kLdsSpillWordsN : kLdsSpillWords;
+bool asm_lds_fit(u32 max_spill, u32 max_pool, u32* nlds, u8 layout = kWide) {
+  const u32 words = kLdsSpillWordsByLayout[layout];
   const size_t budget = (size_t)words * kBlock * 4, pool_bytes = (size_t)max_pool * 4;
   if (pool_bytes > budget) return false;
   const u32 pool_words_lds = (u32)((pool_bytes + kBlock * 4 - 1) / (kBlock * 4));  // in spill-word rows
@@ -780,7 +797,7 @@ bool asm_lds_fit(u32 max_spill, u32 max_pool, u32* nlds, bool narrow = false) {
 }
 
 bool asm_lds_fit(const Prog* p, u32* nlds) {
-  return asm_lds_fit(p->dev.n_spill, p->dev.npool, nlds, p->asm_narrow);
+  return asm_lds_fit(p->dev.n_spill, p->dev.npool, nlds, p->asm_layout);
 }
 
 // MYTHRIL_AMD_ASM=0 keeps every program on the compiled interpreter (A/B runs, tests)
@@ -789,33 +806,43 @@ bool asm_enabled() {
   return !(e && e[0] == '0');
 }
 
-// MYTHRIL_AMD_ASM_NARROW=0 predecodes every asm program for the wide kernel (A/B runs)
+// MYTHRIL_AMD_ASM_NARROW=0 predecodes every asm program for the wide kernel,
+// MYTHRIL_AMD_ASM_QUARTER=0 keeps programs off the quarter layout (A/B runs)
 bool asm_narrow_enabled() {
   const char* e = std::getenv("MYTHRIL_AMD_ASM_NARROW");
   return !(e && e[0] == '0');
 }
 
-// The asm interpreter's handler word offsets per opcode, as the kernel itself
-// reports them (AsmArgs.flags bit 7, mythril_amd/asmgen.py gen "introspection"):
-// mw_asm_predecode writes them into the instructions so the dispatch is one
-// jump.  Read once per process on the first context's device (every device
-// runs the same code object); until then, or if it fails, no program is
-// asm-eligible (the compiled interpreter runs them: same results).
+bool asm_quarter_enabled() {
+  const char* e = std::getenv("MYTHRIL_AMD_ASM_QUARTER");
+  return asm_narrow_enabled() && !(e && e[0] == '0');
+}
+
+// The asm interpreter's introspection table, as the kernel itself reports it
+// (AsmArgs.flags bit 7, mythril_amd/asmgen.py gen "introspection"): handler
+// word offsets per opcode and fused sequence for each of its two instruction
+// banks, then its base address.  mw_asm_predecode turns them into absolute
+// handler addresses in the instructions, so the dispatch is one move and one
+// jump.  Read once per device (each device loads the code object at its own
+// address); until then, or if it fails, no program is asm-eligible there (the
+// compiled interpreter runs them: same results).
+constexpr int kMaxDevices = 64;
 std::mutex g_hoff_mu;
-bool g_hoff_ready = false;
-u32 g_hoff[MW_ASM_NHANDLERS];     // 128 opcodes, then the fused handlers (mw_asm_interp.inc)
-u32 g_hoff_n[MW_ASM_NHANDLERS];   // the same for mw_search_asm_kernel_n
+bool g_hoff_ready[kMaxDevices];
+u32 g_hoff[kMaxDevices][MW_ASM_NHTAB];     // mw_search_asm_kernel (mw_asm_interp.inc)
+u32 g_hoff_n[kMaxDevices][MW_ASM_NHTAB];   // the same for mw_search_asm_kernel_n
+u32 g_hoff_q[kMaxDevices][MW_ASM_NHTAB];   // and mw_search_asm_kernel_q
 
 template <typename K>
 int introspect(K kernel, hipStream_t stream, u32* hout) {
   void* buf = nullptr;
-  const size_t bytes = sizeof(ProgDev) + sizeof(AsmArgs) + MW_ASM_NHANDLERS * sizeof(u32) + 2 * sizeof(u64);
+  const size_t bytes = sizeof(ProgDev) + sizeof(AsmArgs) + MW_ASM_NHTAB * sizeof(u32) + 2 * sizeof(u64);
   HIPCHK(hipMalloc(&buf, bytes));
   char* b = (char*)buf;
   ProgDev* dp = (ProgDev*)b;
   AsmArgs* da = (AsmArgs*)(b + sizeof(ProgDev));
   u32* dout = (u32*)(b + sizeof(ProgDev) + sizeof(AsmArgs));
-  u64* dmin = (u64*)(dout + MW_ASM_NHANDLERS);
+  u64* dmin = (u64*)(dout + MW_ASM_NHTAB + (MW_ASM_NHTAB & 1));
   ProgDev hp{};
   AsmArgs ha{};
   ha.flags = 1u << 7;
@@ -828,31 +855,37 @@ int introspect(K kernel, hipStream_t stream, u32* hout) {
                        (const AsmArgs*)da, dmin, dmin + 1, 0u);
     e = hipGetLastError();
   }
-  u32 h[MW_ASM_NHANDLERS];
+  u32 h[MW_ASM_NHTAB];
   if (e == hipSuccess) e = hipMemcpyAsync(h, dout, sizeof h, hipMemcpyDeviceToHost, stream);
   if (e == hipSuccess) e = hipStreamSynchronize(stream);
   hipFree(buf);
   if (e != hipSuccess) return fail(MG_E_HIP, std::string("asm handler offsets: ") + hipGetErrorString(e));
-  for (int k = 0; k < MW_ASM_NHANDLERS; ++k) {
-    if (h[k] == 0 || h[k] > 0x7fffu) return fail(MG_E_HIP, "asm handler offsets out of range");
+  for (int k = 0; k < 2 * MW_ASM_NHANDLERS; ++k) {
+    if (h[k] == 0 || h[k] > 0xfffffu) return fail(MG_E_HIP, "asm handler offsets out of range");
     hout[k] = h[k];
   }
+  if (h[2 * MW_ASM_NHANDLERS] == 0 && h[2 * MW_ASM_NHANDLERS + 1] == 0)
+    return fail(MG_E_HIP, "asm interpreter base address missing");
+  hout[2 * MW_ASM_NHANDLERS] = h[2 * MW_ASM_NHANDLERS];
+  hout[2 * MW_ASM_NHANDLERS + 1] = h[2 * MW_ASM_NHANDLERS + 1];
   return 0;
 }
 
 int asm_handler_offsets(int dev, hipStream_t stream) {
   std::lock_guard<std::mutex> lk(g_hoff_mu);
-  if (g_hoff_ready) return 0;
+  if (dev < 0 || dev >= kMaxDevices) return 0;   // no asm engine on that device
+  if (g_hoff_ready[dev]) return 0;
   HIPCHK(hipSetDevice(dev));
-  int rc = introspect(mw_search_asm_kernel, stream, g_hoff);
-  if (rc == 0) rc = introspect(mw_search_asm_kernel_n, stream, g_hoff_n);
-  if (rc == 0) g_hoff_ready = true;
+  int rc = introspect(mw_search_asm_kernel, stream, g_hoff[dev]);
+  if (rc == 0) rc = introspect(mw_search_asm_kernel_n, stream, g_hoff_n[dev]);
+  if (rc == 0) rc = introspect(mw_search_asm_kernel_q, stream, g_hoff_q[dev]);
+  if (rc == 0) g_hoff_ready[dev] = true;
   return rc;
 }
 
-bool asm_offsets_ready() {
+bool asm_offsets_ready(int dev) {
   std::lock_guard<std::mutex> lk(g_hoff_mu);
-  return g_hoff_ready;
+  return dev >= 0 && dev < kMaxDevices && g_hoff_ready[dev];
 }
 
 // The asm engines' copy of the leaf table: word 6 (the input row, which only
@@ -919,6 +952,8 @@ int mg_init(int device, mg_ctx** out) {
       hipFuncSetAttribute((const void*)mw_search_asm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
           hipSuccess ||
       hipFuncSetAttribute((const void*)mw_search_asm_kernel_n, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
+          hipSuccess ||
+      hipFuncSetAttribute((const void*)mw_search_asm_kernel_q, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
           hipSuccess) {
     (void)hipGetLastError();  // older runtimes: the default limit already covers it
   }
@@ -969,7 +1004,7 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   // operand fetch reads cpool[slot] (slot < 64) before selecting the register
   const size_t nc = d->ncode_words, nk = (d->nconst_words + 8 > MW_KPAD ? d->nconst_words + 8 : MW_KPAD), nl = d->nleaves * MW_LEAF_WORDS + 8,
                np = d->npool_words + 8;
-  bool asm_ok = asm_offsets_ready() && asm_eligible(d);
+  bool asm_ok = asm_offsets_ready(c->dev) && asm_eligible(d);
   // predecoded copy + the block after END the dispatch prefetches + the narrow
   // constants the kernel loads into VGPRs (MW_ASM_NK words) + the asm leaf table
   const size_t na = asm_ok ? nc + 8 + MW_ASM_NK + nl : 0;
@@ -1005,19 +1040,28 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   if (d->nconst_words) std::memcpy(hbuf + nc, d->consts, d->nconst_words * 4);
   if (d->nleaves) std::memcpy(hbuf + nc + nk, d->leaves, d->nleaves * MW_LEAF_WORDS * 4);
   if (d->npool_words) std::memcpy(hbuf + nc + nk + nl, d->pool, d->npool_words * 4);
-  bool narrow = false;
+  u8 layout = kWide;
   if (asm_ok) {
     u32* pre = hbuf + nc + nk + nl + np;
-    // the narrow-layout kernel when every N register fits its file, the pool
-    // its LDS budget and the narrow constants its registers; else the wide one.
+    // the smallest register layout whose files hold every register of the
+    // program, whose LDS budget holds its pool (the quarter layout: its spill
+    // words too) and whose registers its narrow constants: the quarter kernel
+    // (four waves per SIMD), else the narrow one (three), else the wide one.
     // More distinct narrow constants than MW_ASM_NK: the compiled interpreter runs it
     u32 nl0 = 0;
-    narrow = asm_narrow_enabled() && asm_lds_fit(d->n_spill, (u32)d->npool_words, &nl0, true) &&
-             mw_asm_predecode_layout(d->code, nc, d->consts, d->nconst_words, g_hoff_n, pre, pre + nc + 8,
-                                     MW_ASM_NK_INDEX_N, MW_ASM_NK_N, MW_ASM_NFILE_N) == 0;
-    if (!narrow) {
+    if (asm_quarter_enabled() && asm_lds_fit(d->n_spill, (u32)d->npool_words, &nl0, kQuarter) &&
+        nl0 == d->n_spill &&
+        mw_asm_predecode_layout(d->code, nc, d->consts, d->nconst_words, g_hoff_q[c->dev], pre, pre + nc + 8,
+                                MW_ASM_NK_INDEX_Q, MW_ASM_NK_Q, MW_ASM_NFILE_Q, MW_ASM_WFILE_Q) == 0) {
+      layout = kQuarter;
+    } else if (asm_narrow_enabled() && asm_lds_fit(d->n_spill, (u32)d->npool_words, &nl0, kNarrow) &&
+               (std::memset(pre, 0, (nc + 8 + MW_ASM_NK) * 4),
+                mw_asm_predecode_layout(d->code, nc, d->consts, d->nconst_words, g_hoff_n[c->dev], pre,
+                                        pre + nc + 8, MW_ASM_NK_INDEX_N, MW_ASM_NK_N, MW_ASM_NFILE_N, 0) == 0)) {
+      layout = kNarrow;
+    } else {
       std::memset(pre, 0, (nc + 8 + MW_ASM_NK) * 4);
-      asm_ok = mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, g_hoff, pre, pre + nc + 8) == 0;
+      asm_ok = mw_asm_predecode(d->code, nc, d->consts, d->nconst_words, g_hoff[c->dev], pre, pre + nc + 8) == 0;
     }
     if (asm_ok) asm_leaf_table(d->leaves, d->nleaves, pre + nc + 8 + MW_ASM_NK);
   }
@@ -1036,7 +1080,7 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   p->dev.npool = (u32)d->npool_words;
   p->dev.n_insn = (u32)(nc / 4);
   p->asm_ok = asm_ok;
-  p->asm_narrow = asm_ok && narrow;
+  p->asm_layout = asm_ok ? layout : (u8)kWide;
   p->adev = p->dev;
   if (asm_ok) {
     p->adev.code = p->d_buf + nc + nk + nl + np;
@@ -1196,7 +1240,7 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   // the compiled group, then the specialised programs.
   // Programs with an assembled kernel (mg_prog_attach_asm) get one launch each
   // on the asm interpreter's records, after the interpreter groups.
-  std::vector<size_t> gasm, gasn, gcpp, gasb, special;
+  std::vector<size_t> gasm, gcpp, gasb, special;
   u64 ops = 0;
   const bool use_asm = asm_enabled();
   for (size_t i = 0; i < nprog; ++i) {
@@ -1209,37 +1253,34 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     ops += progs[i]->ops_per_eval;
   }
   // the asm groups need their pools staged in LDS (programs whose pool does not
-  // fit run on the compiled interpreter); the narrow-layout programs form a
-  // group of their own (mw_search_asm_kernel_n)
-  u32 asm_nlds = 0, asn_nlds = 0;
-  if (!gasm.empty()) {
-    std::vector<size_t> fit, fitn;
-    u32 ms = 0, msn = 0;
+  // fit run on the compiled interpreter); one group per register layout
+  // (kAsmKernel: the wide, narrow and quarter kernels)
+  std::vector<size_t> glay[kAsmLayouts];
+  u32 lay_nlds[kAsmLayouts] = {0, 0, 0};
+  {
+    u32 ms[kAsmLayouts] = {0, 0, 0}, mp[kAsmLayouts] = {0, 0, 0};
     for (size_t i : gasm) {
       u32 n1 = 0;
+      const u8 L = progs[i]->asm_layout;
       if (count < (1ull << 40) && asm_lds_fit(progs[i], &n1)) {
-        (progs[i]->asm_narrow ? fitn : fit).push_back(i);
-        (progs[i]->asm_narrow ? msn : ms) = std::max(progs[i]->asm_narrow ? msn : ms, progs[i]->dev.n_spill);
+        glay[L].push_back(i);
+        ms[L] = std::max(ms[L], progs[i]->dev.n_spill);
+        mp[L] = std::max(mp[L], progs[i]->dev.npool);
       } else {
         gcpp.push_back(i);
       }
     }
-    gasm.swap(fit);
-    gasn.swap(fitn);
-    u32 mp = 0, mpn = 0;
-    for (size_t i : gasm) mp = std::max(mp, progs[i]->dev.npool);
-    for (size_t i : gasn) mpn = std::max(mpn, progs[i]->dev.npool);
-    if (!gasm.empty()) (void)asm_lds_fit(ms, mp, &asm_nlds);
-    if (!gasn.empty()) (void)asm_lds_fit(msn, mpn, &asn_nlds, true);
+    for (int L = 0; L < kAsmLayouts; ++L)
+      if (!glay[L].empty()) (void)asm_lds_fit(ms[L], mp[L], &lay_nlds[L], (u8)L);
   }
-  std::vector<size_t> interp(gasm);
-  interp.insert(interp.end(), gasn.begin(), gasn.end());
+  std::vector<size_t> interp;
+  for (int L = 0; L < kAsmLayouts; ++L) interp.insert(interp.end(), glay[L].begin(), glay[L].end());
+  const size_t nasm = interp.size();
   interp.insert(interp.end(), gcpp.begin(), gcpp.end());
   const size_t ni = interp.size();
   interp.insert(interp.end(), gasb.begin(), gasb.end());   // d_progs / d_min: then the assembled ones
   const size_t nia = interp.size();
   std::vector<ProgDev> hp;
-  const size_t nasm = gasm.size() + gasn.size();
   for (size_t j = 0; j < nia; ++j)   // the asm groups read the predecoded code
     hp.push_back(j < nasm ? progs[interp[j]]->adev : progs[interp[j]]->dev);
   const u64 nchunks = (count + kBlock - 1) / kBlock;
@@ -1247,9 +1288,18 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     size_t first, n;
     u64 gx;
     u32 nlds, max_pool;
-  } groups[3] = {{0, gasm.size(), 1, 0, 0}, {gasm.size(), gasn.size(), 1, 0, 0}, {nasm, gcpp.size(), 1, 0, 0}};
+  } groups[kAsmLayouts + 1];   // the asm layouts' groups, then the compiled interpreter's
+  {
+    size_t first = 0;
+    for (int L = 0; L < kAsmLayouts; ++L) {
+      groups[L] = {first, glay[L].size(), 1, 0, 0};
+      first += glay[L].size();
+    }
+    groups[kAsmLayouts] = {nasm, gcpp.size(), 1, 0, 0};
+  }
   size_t spill_need = 4;
-  for (Group& G : groups) {
+  for (int gi = 0; gi <= kAsmLayouts; ++gi) {
+    Group& G = groups[gi];
     if (!G.n) continue;
     u32 max_spill = 0;
     for (size_t j = G.first; j < G.first + G.n; ++j) {
@@ -1260,15 +1310,15 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     G.gx = std::max<u64>(1, (u64)c->ncu * 8 / G.n);
     G.gx = std::min<u64>(G.gx, nchunks);
     const u64 nthreads = G.gx * G.n * kBlock;
-    G.nlds = &G == &groups[0] ? asm_nlds : &G == &groups[1] ? asn_nlds : std::min(max_spill, kLdsSpillWords);
+    G.nlds = gi < kAsmLayouts ? lay_nlds[gi] : std::min(max_spill, kLdsSpillWords);
     spill_need = std::max(spill_need, (size_t)(max_spill - G.nlds) * nthreads * sizeof(u32));
   }
-  // assembled kernels: records 1.. (one program, the whole chip each)
+  // assembled kernels: records kAsmLayouts.. (one program, the whole chip each)
   const u64 agx = std::min<u64>((u64)c->ncu * 8, nchunks);
-  std::vector<AsmArgs> ha(2 + gasb.size());   // the wide and narrow groups, then the assembled kernels
+  std::vector<AsmArgs> ha(kAsmLayouts + gasb.size());   // the layouts' groups, then the assembled kernels
   for (size_t k = 0; k < gasb.size(); ++k) {
     const ProgDev& d = hp[ni + k];
-    AsmArgs& r = ha[2 + k];
+    AsmArgs& r = ha[kAsmLayouts + k];
     (void)asm_lds_fit(d.n_spill, d.npool, &r.nlds);
     r.seed = seed;
     r.begin = begin;
@@ -1280,15 +1330,15 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     r.verdict = nullptr;
     spill_need = std::max(spill_need, (size_t)(d.n_spill - r.nlds) * agx * kBlock * sizeof(u32));
   }
-  const bool need_args = groups[0].n || groups[1].n || !gasb.empty();
+  const bool need_args = nasm || !gasb.empty();
   rc = ensure_launch(c, nprog, need_args ? ha.size() : 0);
   if (rc) return rc;
   if (nia) {
     rc = ensure_spill(c, spill_need);
     if (rc) return rc;
   }
-  for (size_t k = 0; k < gasb.size(); ++k) ha[2 + k].spillbuf = c->d_spill;
-  for (int gi = 0; gi < 2 && need_args; ++gi) {
+  for (size_t k = 0; k < gasb.size(); ++k) ha[kAsmLayouts + k].spillbuf = c->d_spill;
+  for (int gi = 0; gi < kAsmLayouts && need_args; ++gi) {
     AsmArgs& aa = ha[gi];
     aa.seed = seed;
     aa.begin = begin;
@@ -1304,23 +1354,17 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   // one upload: zeroed counters, d_min at MG_NONE, the ProgDev and AsmArgs records
   HIPCHK(stage_upload(c, nprog, hp.data(), nia, ha.data(), need_args ? ha.size() : 0));
   HIPCHK(hipEventRecord(c->e0, c->stream));
-  if (groups[0].n) {
-    const Group& G = groups[0];
+  for (int gi = 0; gi < kAsmLayouts; ++gi) {
+    const Group& G = groups[gi];
+    if (!G.n) continue;
     const size_t lds = (size_t)G.nlds * kBlock * 4 + (size_t)G.max_pool * 4;
-    hipLaunchKernelGGL(mw_search_asm_kernel, dim3((u32)G.gx, (u32)G.n), dim3(kBlock), lds, c->stream,
-                       c->d_progs, (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, G.nlds);
-    HIPCHK(hipGetLastError());
-  }
-  if (groups[1].n) {
-    const Group& G = groups[1];
-    const size_t lds = (size_t)G.nlds * kBlock * 4 + (size_t)G.max_pool * 4;
-    hipLaunchKernelGGL(mw_search_asm_kernel_n, dim3((u32)G.gx, (u32)G.n), dim3(kBlock), lds, c->stream,
-                       c->d_progs + G.first, (const AsmArgs*)c->d_asmargs + 1, c->d_min + G.first, c->d_counter,
+    hipLaunchKernelGGL(kAsmKernel[gi], dim3((u32)G.gx, (u32)G.n), dim3(kBlock), lds, c->stream,
+                       c->d_progs + G.first, (const AsmArgs*)c->d_asmargs + gi, c->d_min + G.first, c->d_counter,
                        G.nlds);
     HIPCHK(hipGetLastError());
   }
-  if (groups[2].n) {
-    const Group& G = groups[2];
+  if (groups[kAsmLayouts].n) {
+    const Group& G = groups[kAsmLayouts];
     // stage the pools in LDS when they fit beside the spill words (80 KiB per
     // block keeps two blocks per CU)
     const size_t spill_bytes = (size_t)G.nlds * kBlock * 4, pool_bytes = (size_t)G.max_pool * 4;
@@ -1339,8 +1383,8 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     HIPCHK(hipGetLastError());
   }
   for (size_t k = 0; k < gasb.size(); ++k) {
-    rc = launch_assembled(c, progs[gasb[k]], (u32)agx, c->d_progs + ni + k, c->d_asmargs + 2 + k,
-                          c->d_min + ni + k, ha[2 + k].nlds);
+    rc = launch_assembled(c, progs[gasb[k]], (u32)agx, c->d_progs + ni + k, c->d_asmargs + kAsmLayouts + k,
+                          c->d_min + ni + k, ha[kAsmLayouts + k].nlds);
     if (rc) return rc;
   }
   for (size_t j = 0; j < special.size(); ++j) {
@@ -1364,7 +1408,8 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     st->kernel_ms = ms;
     st->wall_ms = now_ms() - t0;
     st->evals = evals;  // summed over every program's blocks
-    st->launches = (groups[0].n ? 1 : 0) + (groups[1].n ? 1 : 0) + gasb.size() + special.size();
+    st->launches = gasb.size() + special.size();
+    for (const Group& G : groups) st->launches += G.n ? 1 : 0;
     st->ops = (double)evals / (double)nprog * (double)ops;
     st->lane_div_steps = ctr[1];
     st->lane_div_full = ctr[2];
@@ -1492,12 +1537,8 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
   if (e == hipSuccess && assembled) {
     if (launch_assembled(c, p, (u32)gx, c->d_progs, c->d_asmargs, c->d_min, nlds)) return MG_E_HIP;
   } else if (e == hipSuccess) {
-    if (p->asm_narrow)
-      hipLaunchKernelGGL(mw_search_asm_kernel_n, dim3((u32)gx, 1u), dim3(kBlock), lds, c->stream, c->d_progs,
-                         (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, nlds);
-    else
-      hipLaunchKernelGGL(mw_search_asm_kernel, dim3((u32)gx, 1u), dim3(kBlock), lds, c->stream, c->d_progs,
-                         (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, nlds);
+    hipLaunchKernelGGL(kAsmKernel[p->asm_layout], dim3((u32)gx, 1u), dim3(kBlock), lds, c->stream, c->d_progs,
+                       (const AsmArgs*)c->d_asmargs, c->d_min, c->d_counter, nlds);
     e = hipGetLastError();
   }
   const bool pinned = vb + tb <= kReadbackMax && ensure_readback(c, vb + tb);

@@ -203,10 +203,16 @@ int mg_validate_desc(const mg_prog_desc* d) {
 // W_CDINS byte index (always a constant) below 0x4000, which becomes
 // 0x4000 | index (the handler then compares it with one 32-bit summary of the
 // size instead of a signed 256-bit subtraction).
-// hoff: the asm interpreter's handler word offsets per opcode (128 entries, then the fused handlers',
-// reported by the kernel itself, mw_kernels.hip asm_handler_offsets); word 0
-// becomes width [31:16] | FLAG_CHAIN [15] | handler offset [14:0], so the
-// dispatch is one jump (mythril_amd/asmgen.py Gen.next).
+// hoff: the asm interpreter's introspection table (MW_ASM_NHTAB words,
+// reported by the kernel itself, mw_kernels.hip asm_handler_offsets): the
+// handler word offsets from Lpc0 per opcode (128 entries, then the fused
+// handlers') of bank A, the same for bank B, then Lpc0's address (low, high).
+// Instruction i runs in bank i & 1 (mythril_amd/asmgen.py: the interpreter
+// alternates two SGPR banks), so word 0 becomes the low word of its handler's
+// absolute address in that bank: the dispatch moves it into the jump target
+// and jumps (Gen.next).  The width moves to word 1 [31:24] (as width - 1) and
+// W_CDINS's FLAG_CHAIN to bit 31 of its immediate.  Returns -3 when a handler
+// address would carry into the high word (the kernel keeps one high word).
 // Narrow constants: every N-class constant operand becomes a register operand
 // naming one of MW_ASM_NK VGPRs above the N file (index MW_ASM_NK_INDEX + k
 // from its base), which the kernel fills once per block from nk[0..MW_ASM_NK)
@@ -227,12 +233,17 @@ int mg_validate_desc(const mg_prog_desc* d) {
 // constants of the interpreter kernel the copy is for (the wide kernel:
 // MW_ASM_NK_INDEX / MW_ASM_NK; the narrow-layout kernel: MW_ASM_NK_INDEX_N /
 // MW_ASM_NK_N); nfile > 0 also requires every N register operand and N result
-// to lie below nfile slots (-2 otherwise: the program needs the wide kernel).
+// to lie below nfile slots, wfile > 0 every W register operand and W result
+// below wfile slots (-2 otherwise: the program needs a wider kernel).
 int mw_asm_predecode_layout(const u32* code, size_t nwords, const u32* consts, size_t nconst, const u32* hoff,
-                            u32* out, u32* nk, u32 nk_index, u32 nk_max, u32 nfile) {
+                            u32* out, u32* nk, u32 nk_index, u32 nk_max, u32 nfile, u32 wfile) {
   u32 nnk = 0;
   for (u32 k = 0; k < MW_ASM_NK; ++k) nk[k] = 0;
   if (nk_max > MW_ASM_NK) return -1;
+  const u32 nh = MW_ASM_NHANDLERS, lpc0 = hoff[2 * nh];
+  for (u32 k = 0; k < 2 * nh; ++k)
+    if (uint64_t(lpc0) + 4ull * hoff[k] > 0xffffffffull) return -3;
+  auto target = [&](size_t insn, u32 h) { return lpc0 + 4u * hoff[(insn & 1u) * nh + h]; };
   auto narrow = [&](int kind, u32 f, u32* dst) -> bool {   // dst: the predecoded field
     if (kind != 2 || !(f & MW_KBIT)) return true;
     const u32 val = consts[f & 0x7fffu];
@@ -245,7 +256,12 @@ int mw_asm_predecode_layout(const u32* code, size_t nwords, const u32* consts, s
     *dst = nk_index + k;
     return true;
   };
-  auto in_file = [&](int kind, u32 f) { return kind != 2 || (f & MW_KBIT) || !nfile || f < nfile; };
+  auto in_file = [&](int kind, u32 f) {
+    if (f & MW_KBIT) return true;
+    if (kind == 2) return !nfile || f < nfile;
+    if (kind == 1) return !wfile || f < wfile;
+    return true;
+  };
   for (size_t i = 0; i + 3 < nwords; i += 4) {
     const u32* I = code + i;
     u32* O = out + i;
@@ -264,13 +280,18 @@ int mw_asm_predecode_layout(const u32* code, size_t nwords, const u32* consts, s
       for (int k = 1; k < 8 && small; ++k) small = consts[o + k] == 0u;
       if (small) c2 = 0x4000u | consts[o];
     }
-    if (nfile && (!in_file(sh.a, a) || !in_file(sh.b, b) || !in_file(sh.c, c) || (sh.dst == 4 && d2 >= nfile)))
+    if (!in_file(sh.a, a) || !in_file(sh.b, b) || !in_file(sh.c, c) || (nfile && sh.dst == 4 && d2 >= nfile) ||
+        (wfile && sh.dst == 3 && MW_DST_W(dst) >= wfile))
       return -2;
     if (!narrow(sh.a, a, &a2) || !narrow(sh.b, b, &b2) || !narrow(sh.c, c, &c2)) return -1;
-    O[0] = (I[0] & 0xffff0000u) | ((I[0] >> 8) & MW_FLAG_CHAIN ? 0x8000u : 0u) | (hoff[op & 0x7fu] & 0x7fffu);
-    O[1] = a2 | (d2 << 16);   // s_set_gpr_idx_on reads bits [7:0]: a indexes from the word as it is
+    const bool chain = op == MW_W_CDINS && ((I[0] >> 8) & MW_FLAG_CHAIN);
+    if (chain && (I[3] & 0x80000000u)) return -1;   // validated: leaf index | offset < 256 << 16
+    O[0] = target(i / 4, op & 0x7fu);
+    // s_set_gpr_idx_on reads bits [7:0]: a indexes from the word as it is, dst
+    // (< 64) from word 1 >> 16 with the width above it
+    O[1] = a2 | (d2 << 16) | (((w - 1u) & 0xffu) << 24);
     O[2] = b2 | (c2 << 16);
-    O[3] = I[3];
+    O[3] = I[3] | (chain ? 0x80000000u : 0u);
     if (op == MW_N_ADD || op == MW_N_SUB || op == MW_N_MUL || op == MW_N_NOT)
       O[3] = w >= 32u ? 0xffffffffu : (1u << w) - 1u;
   }
@@ -294,7 +315,7 @@ int mw_asm_predecode_layout(const u32* code, size_t nwords, const u32* consts, s
       ++i;
       continue;
     }
-    out[i * 4] = (out[i * 4] & ~0x7fffu) | (hoff[128 + best] & 0x7fffu);
+    out[i * 4] = target(i, 128u + u32(best));
     i += blen;
   }
   return 0;
@@ -302,7 +323,7 @@ int mw_asm_predecode_layout(const u32* code, size_t nwords, const u32* consts, s
 
 int mw_asm_predecode(const u32* code, size_t nwords, const u32* consts, size_t nconst, const u32* hoff,
                      u32* out, u32* nk) {
-  return mw_asm_predecode_layout(code, nwords, consts, nconst, hoff, out, nk, MW_ASM_NK_INDEX, MW_ASM_NK, 0);
+  return mw_asm_predecode_layout(code, nwords, consts, nconst, hoff, out, nk, MW_ASM_NK_INDEX, MW_ASM_NK, 0, 0);
 }
 
 }  // extern "C"

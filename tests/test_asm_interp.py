@@ -30,8 +30,9 @@ def test_opcode_lists_agree():
     # reports an offset for all 128 opcodes (handler or Lunsup)
     for o in isa.ASM_OPCODES:
         assert f"Lh_{o}_%=:" in txt, o
-    # (twice: the wide and the narrow layout's interpreter)
-    assert txt.count("- Lpc0_%=) >> 2)") == 2 * (128 + len(isa.ASM_FUSED))   # and every fused handler's
+    # every fused handler's too, per bank, in each of the three layouts'
+    # interpreters (wide, narrow, quarter)
+    assert txt.count("- Lpc0_%=) >> 2)") == 3 * 2 * (128 + len(isa.ASM_FUSED))
     for k in range(len(isa.ASM_FUSED)):
         assert f"Lf{k}_%=:" in txt
     assert "s_branch Lh_" not in txt          # one jump per dispatch: no table of branches
@@ -78,19 +79,32 @@ def _predecode(code, consts):
     return (out.reshape(-1, 4), nk) if rc == 0 else (None, None)
 
 
-# stand-in handler word offsets (the kernel reports the real ones at mg_init):
-# the 128 opcodes', then the fused handlers'
-HOFF = __import__("numpy").arange(1000, 1000 + (128 + len(isa.ASM_FUSED)) * 7, 7, dtype="uint32")
+# a stand-in introspection table (the kernel reports the real one at mg_init):
+# bank A's handler word offsets (the 128 opcodes', then the fused handlers'),
+# bank B's, then the interpreter's base address (low, high word)
+NH = 128 + len(isa.ASM_FUSED)
+LPC0 = 0x7F001000
+HOFF = __import__("numpy").concatenate([__import__("numpy").arange(1000, 1000 + NH * 7, 7),
+                                        __import__("numpy").arange(9000, 9000 + NH * 5, 5),
+                                        [LPC0, 0x7FFF]]).astype("uint32")
+
+
+def _target(i, h):
+    """word 0 of instruction i dispatching to handler entry h: the handler's
+    absolute address (low word) in bank i & 1"""
+    return LPC0 + 4 * int(HOFF[(i & 1) * NH + h])
 
 
 def test_predecode_operand_layout():
-    """The asm engine's copy of the code: word 0 -> width | FLAG_CHAIN at bit 15
-    | the opcode's handler word offset (one-jump dispatch), word 1 -> a [15:0]
-    | dst [31:16] with dst the written register's index (N slot, W slot x 8),
+    """The asm engine's copy of the code: word 0 -> the low word of the
+    opcode's handler address in the instruction's bank (i & 1: a move and a
+    jump dispatch it), word 1 -> a [15:0] | dst [23:16] | width - 1 [31:24]
+    with dst the written register's index (N slot, W slot x 8),
     W register operands -> slot x 8, N register operands and W constants
     unchanged, N constants -> the index of their VGPR above the N file
     (176 + k, the value in table slot k), a W_CDINS index constant below
-    0x4000 -> 0x4000 | index, and N_ADD's word 3 -> its width mask."""
+    0x4000 -> 0x4000 | index, a chained W_CDINS's FLAG_CHAIN -> bit 31 of its
+    immediate, and N_ADD's word 3 -> its width mask."""
     e = isa.encode
     consts = [0] * 17
     consts[0], consts[8], consts[16] = 0x24, 0x5000, 0x77   # two 256-bit constants, one narrow
@@ -98,21 +112,22 @@ def test_predecode_operand_layout():
             + e("W_ADD", 256, isa.encode_dst("W", 5), 2, isa.KBIT | 0)
             + e("N_ULT", 256, isa.encode_dst("N", 4), 6, 1)
             + e("W_ITE", 256, isa.encode_dst("W", 1), 3, 4, 9)
-            + e("W_CDINS", 256, isa.encode_dst("W", 2), 2, 1, isa.KBIT | 0, imm=7 | (8 << 16))
+            + e("W_CDINS", 256, isa.encode_dst("W", 2), 2, 1, isa.KBIT | 0, imm=7 | (8 << 16), flags=isa.FLAG_CHAIN)
             + e("W_CDINS", 256, isa.encode_dst("W", 2), 2, 1, isa.KBIT | 8, imm=7)
             + e("N_EQN", 8, isa.encode_dst("N", 5), isa.KBIT | 0, isa.KBIT | 16)
             + e("END", 0, isa.encode_dst(None)))
     o, nk = _predecode(code, consts)
     src = __import__("numpy").asarray(code, dtype="uint32").reshape(-1, 4)
-    want0 = (src[:, 0] & 0xFFFF0000) | HOFF[src[:, 0] & 0x7F] | (((src[:, 0] >> 8) & isa.FLAG_CHAIN) << 15)
-    assert (o[:, 0] == want0).all()
-    assert o[0, 3] == 0xFF and (o[1:, 3] == src[1:, 3]).all()       # N_ADD: the 8-bit mask
-    assert o[0, 1] == 3 | (37 << 16) and o[0, 2] == 176 + 0          # narrow constant 0x77 -> NK slot 0
+    assert [int(x) for x in o[:, 0]] == [_target(i, int(op) & 0x7F) for i, op in enumerate(src[:, 0])]
+    assert o[0, 3] == 0xFF and (o[[1, 2, 3, 5, 6, 7], 3] == src[[1, 2, 3, 5, 6, 7], 3]).all()   # N_ADD: the mask
+    assert o[4, 3] == src[4, 3] | 0x80000000                         # the chain flag
+    w1 = lambda lo, d, w: lo | (d << 16) | ((w - 1) << 24)           # noqa: E731
+    assert o[0, 1] == w1(3, 37, 8) and o[0, 2] == 176 + 0            # narrow constant 0x77 -> NK slot 0
     assert list(nk[:2]) == [0x77, 0x24] and not nk[2:].any()
-    assert o[6, 1] == (176 + 1) | (5 << 16) and o[6, 2] == 176 + 0  # 0x24 (narrow use) -> slot 1, 0x77 reused
-    assert o[1, 1] == 16 | (40 << 16) and o[1, 2] == isa.KBIT | 0
-    assert o[2, 1] == 48 | (4 << 16) and o[2, 2] == 8
-    assert o[3, 1] == 24 | (8 << 16) and o[3, 2] == 32 | (9 << 16)   # c is the N condition
+    assert o[6, 1] == w1(176 + 1, 5, 8) and o[6, 2] == 176 + 0       # 0x24 (narrow use) -> slot 1, 0x77 reused
+    assert o[1, 1] == w1(16, 40, 256) and o[1, 2] == isa.KBIT | 0
+    assert o[2, 1] == w1(48, 4, 256) and o[2, 2] == 8
+    assert o[3, 1] == w1(24, 8, 256) and o[3, 2] == 32 | (9 << 16)   # c is the N condition
     assert o[4, 2] == 8 | ((0x4000 | 0x24) << 16)
     assert o[5, 2] == 8 | ((isa.KBIT | 8) << 16)                          # 0x5000: stays a constant
 
@@ -138,7 +153,7 @@ def test_predecode_narrow_constant_bound():
 
 def test_predecode_fused_sequences():
     """The first instruction of every fused-sequence match (left to right,
-    longest first) jumps to that sequence's handler (offset entry 128 + k);
+    longest first) jumps to that sequence's handler (entry 128 + k of its bank);
     the rest of the match keeps its own words, and the match agrees with
     isa.asm_fused_dispatch."""
     import numpy as np
@@ -152,17 +167,35 @@ def test_predecode_fused_sequences():
             + e("END", 0, isa.encode_dst(None)))
     o, _ = _predecode(code, [0])
     src = np.asarray(code, dtype="uint32").reshape(-1, 4)
-    plain = (src[:, 0] & 0xFFFF0000) | HOFF[src[:, 0] & 0x7F]
+    plain = [_target(i, int(op) & 0x7F) for i, op in enumerate(src[:, 0])]
     fused = {i: k for i, k in isa.asm_fused_dispatch(code) if k is not None}
     seq = lambda *t: isa.ASM_FUSED.index(tuple(t))   # noqa: E731
     assert fused == {0: seq("N_SLT", "LEAF_N", "N_ITE", "N_SHLI"), 4: seq("N_SLT", "LEAF_N", "N_ITE"),
                      8: seq("N_XOR", "CHECK")}
     for i in range(len(src)):
-        want = (plain[i] & 0xFFFF8000) | HOFF[128 + fused[i]] if i in fused else plain[i]
+        want = _target(i, 128 + fused[i]) if i in fused else plain[i]
         assert o[i, 0] == want, i
 
 
-def _predecode_layout(code, consts, nk_index, nk_max, nfile):
+def test_predecode_refuses_a_carry_into_the_high_word():
+    """The kernel keeps one high word for every handler address (s93): code
+    whose handlers straddle a 4 GiB boundary is not predecoded (-3; the
+    compiled interpreter runs it)."""
+    import numpy as np
+    global HOFF
+    code = isa.encode("N_ADD", 8, isa.encode_dst("N", 1), 2, 3) + isa.encode("END", 0, isa.encode_dst(None))
+    saved = HOFF
+    try:
+        HOFF = saved.copy()
+        HOFF[2 * NH] = np.uint32(0xFFFFFFFF - 4 * 1000)
+        rc, _, _ = _predecode_layout(code, [0], 176, 16, 0)
+        assert rc == -3
+    finally:
+        HOFF = saved
+    assert _predecode_layout(code, [0], 176, 16, 0)[0] == 0
+
+
+def _predecode_layout(code, consts, nk_index, nk_max, nfile, wfile=0):
     import ctypes
 
     import numpy as np
@@ -171,13 +204,14 @@ def _predecode_layout(code, consts, nk_index, nk_max, nfile):
     f = ctypes.CDLL(LIB_PATH).mw_asm_predecode_layout
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
-                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                  ctypes.c_uint32]
     code = np.ascontiguousarray(code, dtype=np.uint32)
     consts = np.ascontiguousarray(consts, dtype=np.uint32)
     out = np.zeros_like(code)
     nk = np.full(isa.ASM_NK, 0xDEAD, dtype=np.uint32)
     rc = f(code.ctypes.data, code.size, consts.ctypes.data, consts.size, HOFF.ctypes.data, out.ctypes.data,
-           nk.ctypes.data, nk_index, nk_max, nfile)
+           nk.ctypes.data, nk_index, nk_max, nfile, wfile)
     return rc, out.reshape(-1, 4), nk
 
 
@@ -213,3 +247,34 @@ def test_corpus_mostly_fits_the_narrow_layout():
     progs = [p for f, p in _corpus_programs() if ".gz" in f]
     fit = sum(_predecode_layout(p.code, p.consts, 88, 14, 24)[0] == 0 for p in progs)
     assert fit >= 0.9 * len(progs), (fit, len(progs))
+
+
+def test_quarter_layout_predecode():
+    """Round 5: the third asm kernel (asmgen.variant("quarter")) holds 4 W
+    slots and 16 N slots in 126 VGPRs (four waves per SIMD).  A program is
+    predecoded for it only when every W register (operand or result) lies
+    below 4 and every N register below 16 (else -2)."""
+    from mythril_amd import asmgen
+    qv = asmgen.variant("quarter")
+    assert (qv.WFILE, qv.NFILE, qv.N0, qv.NK_INDEX, qv.NKN, qv.NVGPR) == (4, 16, 32, 80, 14, 126)
+    e = isa.encode
+    consts = [0] * 9
+    consts[8] = 0x77
+    ok = (e("LEAF_W", 256, isa.encode_dst("W", 3), imm=0) + e("W_ADD", 256, isa.encode_dst("W", 1), 3, 3)
+          + e("N_EQ", 256, isa.encode_dst("N", 15), 1, isa.KBIT | 0) + e("END", 0, isa.encode_dst(None)))
+    rc, o, _ = _predecode_layout(ok, consts, 80, 14, 16, 4)
+    assert rc == 0 and o[1, 1] & 0xFF == 24 and (o[1, 1] >> 16) & 0xFF == 8      # a = W3 x 8, dst = W1 x 8
+    wdst = ok[:-4] + e("MOV_W", 256, isa.encode_dst("W", 4), 1) + e("END", 0, isa.encode_dst(None))
+    wsrc = ok[:-4] + e("W_NOT", 256, isa.encode_dst("W", 0), 5) + e("END", 0, isa.encode_dst(None))
+    nsrc = ok[:-4] + e("N_NOT", 8, isa.encode_dst("N", 2), 16) + e("END", 0, isa.encode_dst(None))
+    for bad in (wdst, wsrc, nsrc):
+        assert _predecode_layout(bad, consts, 80, 14, 16, 4)[0] == -2
+        assert _predecode_layout(bad, consts, 88, 14, 24, 0)[0] == 0      # the narrow layout holds them
+
+
+def test_corpus_fits_the_quarter_layout_in_part():
+    """About half of the LASER corpus (as compiled) keeps its registers in the
+    quarter layout's files."""
+    progs = [p for f, p in _corpus_programs() if ".gz" in f]
+    fit = sum(_predecode_layout(p.code, p.consts, 80, 14, 16, 4)[0] == 0 for p in progs)
+    assert fit >= 0.35 * len(progs), (fit, len(progs))

@@ -177,6 +177,39 @@ def test_asm_corpus_verdicts(dev, corpus):
         assert np.array_equal(va, vo), name
 
 
+class layout_env:
+    """MYTHRIL_AMD_ASM_QUARTER / _NARROW for the programs loaded meanwhile
+    (read by the library at each load: which register layout's kernel a
+    program is predecoded for)."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("env", [{"MYTHRIL_AMD_ASM_QUARTER": "0"}, {"MYTHRIL_AMD_ASM_NARROW": "0"}])
+def test_asm_corpus_verdicts_on_the_wider_layouts(dev, corpus, env):
+    """Round 5: a program runs on the smallest register layout that holds it
+    (quarter: 4 waves per SIMD, narrow: 3, wide: 2).  With the smaller
+    layouts switched off the same programs run on the wider kernels: the
+    same verdicts as the compiled interpreter there too."""
+    n = 1 << 13
+    for name, q in corpus[::3]:
+        with layout_env(**env):
+            va, vi = both(dev, q.program, DEFAULT_SEED, 0, n)
+        assert np.array_equal(va, vi), (name, env, int(np.count_nonzero(va != vi)))
+
+
 def test_asm_corpus_search_modes(dev, corpus):
     """64 programs per launch, exhaustive / early exit / stop after hit: the
     same lowest witness index per program as the compiled interpreter."""

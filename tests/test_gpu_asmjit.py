@@ -210,3 +210,67 @@ def test_asmjit_variable_shifts(dev, seed):
         _, _, vo = cdag.evaluate(sub, DEFAULT_SEED + seed, 1 << 20, 1 << 12, want_verdict=True)
         assert np.array_equal(va, vi), (seed, k)
         assert np.array_equal(va.astype(np.uint8), vo), (seed, k)
+
+
+def _check_run_dag(seed):
+    """Long runs of CHECK / CHECK_IMP / CHECK_IMPEQ (the r4b
+    miscompile class): 24-40 top-level conjuncts that mostly hold - bounds,
+    disequalities, implications between equalities - plus calldata-like byte
+    reads at symbolic offsets, whose Ackermann congruence pairs become runs of
+    CHECK_IMPEQ with premises that hold in some lanes (pooled candidates make
+    the offsets collide)."""
+    import random
+    r = random.Random(seed)
+    c = Ctx()
+    xs = [c.var(f"x{i}", w) for i, w in enumerate((8, 16, 32, 64, 160, 256))]
+    cd = c.array("cd", 256, 8)
+    off = c.app("bvand", c.var("off", 256), c.const(7, 256))
+    reads = [c.app("select", cd, c.app("bvadd", off, c.const(k, 256)) if k else off) for k in range(4)]
+    reads += [c.app("select", cd, c.const(k, 256)) for k in range(4)]
+    conj = []
+    for _ in range(r.randrange(24, 41)):
+        k = r.random()
+        x = r.choice(xs)
+        if k < 0.3:
+            conj.append(c.app("bvule", x, c.const((1 << x.width) - 1 - r.randrange(1 << max(1, x.width - 4)), x.width)))
+        elif k < 0.5:
+            conj.append(c.app("not", c.app("=", x, c.const(r.getrandbits(x.width), x.width))))
+        elif k < 0.75:
+            y = r.choice(xs)
+            conj.append(c.app("=>", c.app("=", x, c.const(r.randrange(4), x.width)),
+                              c.app("=", y, c.const(r.randrange(4), y.width))))
+        else:
+            a, b = r.sample(reads, 2)
+            conj.append(c.app("=>", c.app("=", a, c.const(r.randrange(4), 8)), c.app("bvule", b, c.const(250, 8))))
+    return c, conj
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_asmjit_long_check_runs(dev, seed):
+    c, conj = _check_run_dag(9500 + seed)
+    for pools in (False, True):
+        q = prepare(conj, c, use_pools=pools)
+        p = q.program
+        ops = [int(w) & 0xFF for w in p.code[0::4]]
+        checks = {isa.OPCODES[n] for n in ("CHECK", "CHECK_IMP", "CHECK_IMPEQ")}
+        run = best = 0
+        for o in ops:
+            run = run + 1 if o in checks else 0
+            best = max(best, run)
+        assert best >= 6, best
+        if not asmjit.eligible(p):      # e.g. more distinct narrow constants than the asm engines hold
+            continue
+        n = 1 << 14
+        di, da = pair(dev, p)
+        try:
+            va, _ = dev.eval_generated(da, DEFAULT_SEED + seed, 0, n, trace=False)
+            vi, _ = dev.eval_generated(di, DEFAULT_SEED + seed, 0, n, trace=False)
+        finally:
+            di.free()
+            da.free()
+        _, _, vo = cdag.evaluate(q.lowered.conjuncts, DEFAULT_SEED + seed, 0, n, want_verdict=True,
+                                 specs=cdag.program_specs(p) if pools else None)
+        assert np.array_equal(vi.astype(np.uint8), vo), (seed, pools)
+        assert np.array_equal(va.astype(np.uint8), vo), (seed, pools, int(np.count_nonzero(va.astype(np.uint8) != vo)))
+        if not pools:   # pooled candidates lead with the values that break the facts: often none holds
+            assert 0 < int(vo.sum()) < n, (seed, int(vo.sum()))
