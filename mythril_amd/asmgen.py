@@ -195,8 +195,12 @@ class Gen:
     # SGPR (tools/exp/gpridx_probe.hip), so a and b index straight from their
     # word; c and dst take one shift.
     # field() only binds an operand to a name; fetch_n / fetch_w read it.
+    c_in_imm = False   # the current opcode's c operand is in word 3 (C_IN_IMM, mw_asm_predecode)
+
     def word(self, which):
         """(SGPR, half) holding operand field `which` of the current instruction"""
+        if which == "c" and self.c_in_imm:
+            return self.CUR + 3, "lo"
         return {"a": (self.CUR + 1, "lo"), "b": (self.CUR + 2, "lo"), "c": (self.CUR + 2, "hi")}[which]
 
     def field(self, which, dst):
@@ -442,6 +446,11 @@ class Gen:
         self("s_waitcnt lgkmcnt(0)", f"s_add_u32 {s(SOFF)}, {s(SOFF)}, 16",
              f"s_load_dwordx4 {sr(self.CUR, 4)}, {sr(CODE0, 2)}, {s(SOFF)}",
              f"s_mov_b32 {s(JMP)}, {s(self.other())}", f"s_setpc_b64 {sr(JMP, 2)}")
+
+
+# opcodes with a c operand and no immediate: mw_asm_predecode copies the c
+# field into word 3, where s_set_gpr_idx_on takes it with no shift
+C_IN_IMM = ("N_ITE", "W_ITE", "CHECK_IMPEQ", "CHECK_IMPEQW")
 
 
 def build_handlers():
@@ -1296,6 +1305,7 @@ def gen(mode="interp"):
                     continue
                 g.CUR = (CUR, NXT)[bank]
                 g.label(_hlabel(n, bank))
+                g.c_in_imm = n in C_IN_IMM
                 handlers[n](g)
                 g.next()
                 g.flush_tail()
@@ -1308,6 +1318,7 @@ def gen(mode="interp"):
                 for j, n in enumerate(seq):
                     if j:
                         g.consume()
+                    g.c_in_imm = n in C_IN_IMM
                     handlers[n](g)
                 g.next()
                 g.flush_tail()

@@ -292,6 +292,9 @@ int mw_asm_predecode_layout(const u32* code, size_t nwords, const u32* consts, s
     O[1] = a2 | (d2 << 16) | (((w - 1u) & 0xffu) << 24);
     O[2] = b2 | (c2 << 16);
     O[3] = I[3] | (chain ? 0x80000000u : 0u);
+    // no immediate: the c operand goes to word 3 too (mythril_amd/asmgen.py
+    // C_IN_IMM: the handler indexes with it as it is, no shift)
+    if (op == MW_N_ITE || op == MW_W_ITE || op == MW_CHECK_IMPEQ || op == MW_CHECK_IMPEQW) O[3] = c2;
     if (op == MW_N_ADD || op == MW_N_SUB || op == MW_N_MUL || op == MW_N_NOT)
       O[3] = w >= 32u ? 0xffffffffu : (1u << w) - 1u;
   }

@@ -119,7 +119,8 @@ def test_predecode_operand_layout():
     o, nk = _predecode(code, consts)
     src = __import__("numpy").asarray(code, dtype="uint32").reshape(-1, 4)
     assert [int(x) for x in o[:, 0]] == [_target(i, int(op) & 0x7F) for i, op in enumerate(src[:, 0])]
-    assert o[0, 3] == 0xFF and (o[[1, 2, 3, 5, 6, 7], 3] == src[[1, 2, 3, 5, 6, 7], 3]).all()   # N_ADD: the mask
+    assert o[0, 3] == 0xFF and (o[[1, 2, 5, 6, 7], 3] == src[[1, 2, 5, 6, 7], 3]).all()   # N_ADD: the mask
+    assert o[3, 3] == 9                                              # W_ITE: c (no immediate) in word 3 too
     assert o[4, 3] == src[4, 3] | 0x80000000                         # the chain flag
     w1 = lambda lo, d, w: lo | (d << 16) | ((w - 1) << 24)           # noqa: E731
     assert o[0, 1] == w1(3, 37, 8) and o[0, 2] == 176 + 0            # narrow constant 0x77 -> NK slot 0
