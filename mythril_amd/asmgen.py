@@ -1223,7 +1223,6 @@ def gen(mode="interp"):
         g.label("Lpc0_%=")
         if TABHI != TABLO + 1:
             g(f"s_mov_b32 {s(TABLO)}, {s(SX)}", f"s_mov_b32 {s(TABHI)}, {s(SX + 1)}")
-        g(f"s_mov_b32 {s(JMP + 1)}, {s(TABHI)}")   # the dispatch target's high word, for good
         # introspection (AsmArgs.flags bit 7): lane 0 writes the word offset of
         # every opcode's handler from Lpc0 to the verdict pointer, bank A's
         # table (opcodes, then the fused sequences) then bank B's, then Lpc0's
@@ -1254,6 +1253,8 @@ def gen(mode="interp"):
           f"s_load_dwordx16 {sr(DESC, 16)}, {sr(CODE0, 2)}, {s(74)}", "s_waitcnt lgkmcnt(0)")
         for k in range(NKN):
             g(f"v_mov_b32_e32 {v(NK0 + k)}, {s(DESC + k)}")
+        # the dispatch target's high word, for good (after that load: s80..s95)
+        g(f"s_mov_b32 {s(JMP + 1)}, {s(TABHI)}")
     else:
         for reg, lab in ((LEAFADDR, "Lleaf_%="), (STOPADDR, "Lstop_%="), (ENDADDR, "Lh_END_%="),
                          (PHILOXADDR, "Lphilox_%=")):
