@@ -55,6 +55,14 @@ typedef struct mw_compile_info {
 int mw_compile(const int32_t* recs, size_t nrecs_words, size_t nnodes, const uint8_t* kvals, size_t nkvals,
                const int32_t* roots, size_t nconj, size_t ntrace, mw_compiled** out, mw_compile_info* info);
 
+/* mw_compile with the register allocator limited to the W slots below
+ * w_slots (4..8) and the N slots below n_slots (8..64): the programs of the
+ * asm interpreter's smaller register layouts (mythril_amd/asmgen.py
+ * variant("quarter"): 4 and 16).  MG_E_ARG for limits out of range. */
+int mw_compile_slots(const int32_t* recs, size_t nrecs_words, size_t nnodes, const uint8_t* kvals, size_t nkvals,
+                     const int32_t* roots, size_t nconj, size_t ntrace, uint32_t w_slots, uint32_t n_slots,
+                     mw_compiled** out, mw_compile_info* info);
+
 /* Copy the result out (buffers sized from mw_compile_info) and release it.
  * leaves: record index of each leaf's var node; trace: 3 words per entry. */
 int mw_compiled_take(mw_compiled* r, uint32_t* code, uint32_t* consts, uint32_t* leaves, uint32_t* trace);

@@ -23,7 +23,7 @@ import ctypes
 import os
 import threading
 from array import array
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -71,12 +71,13 @@ def _bind():
                 from .runtime import EngineUnavailable, load_library
                 try:
                     lib = load_library()
-                    c, t, f = lib.mw_compile, lib.mw_compiled_take, lib.mw_compiled_free
+                    c, t, f = lib.mw_compile_slots, lib.mw_compiled_take, lib.mw_compiled_free
                 except (EngineUnavailable, AttributeError) as e:
                     _why = str(e)
                     return None
                 c.restype, c.argtypes = ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_size_t, _P, ctypes.c_size_t,
-                                                       _P, ctypes.c_size_t, ctypes.c_size_t, ctypes.POINTER(_P),
+                                                       _P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint32,
+                                                       ctypes.c_uint32, ctypes.POINTER(_P),
                                                        ctypes.POINTER(MwCompileInfo)]
                 t.restype, t.argtypes = ctypes.c_int, [_P, _P, _P, _P, _P]
                 f.restype, f.argtypes = None, [_P]
@@ -144,8 +145,8 @@ def _addr(buf) -> int:
 
 def compile_native(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, LeafSpec]] = None,
                    trace: Sequence[Node] = (), pools: Optional[Dict[str, List[Optional[int]]]] = None,
-                   reach=None) -> Program:
-    """compile_program(conjuncts, leaf_specs, trace, pools), natively.
+                   reach=None, slots: Optional[Tuple[int, int]] = None) -> Program:
+    """compile_program(conjuncts, leaf_specs, trace, pools, slots), natively.
     reach: (flattened conjuncts, their topo) when the caller has them and
     nothing is traced (prepare: Lowered.flat, Lowered.nodes)."""
     fns = _bind()
@@ -158,7 +159,7 @@ def compile_native(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
     else:
         conj = _flatten(conjuncts)
         recs, nn, kb, nk, roots, nodes, idx, names = serialize(conj, trace)
-    info, code, consts, leaves, tr = _run(fns, recs, nn, kb, nk, roots, len(conj), len(trace))
+    info, code, consts, leaves, tr = _run(fns, recs, nn, kb, nk, roots, len(conj), len(trace), slots)
     leaf_nodes = [nodes[i] for i in leaves.tolist()]
     specs, leaf_words, pool_words, in_row = layout_leaves(leaf_nodes, leaf_specs, pools)
     t = tr.tolist()
@@ -170,7 +171,7 @@ def compile_native(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
                    n_spill=int(info.n_spill), n_trace_rows=int(info.n_trace_rows), n_input_rows=in_row,
                    ops_per_eval=int(info.ops_per_eval), leaf_specs=specs, leaf_nodes=leaf_nodes,
                    trace_map=trace_map, n_insn=n_insn, n_conjuncts=len(conj), stats=_stats(info, n_insn),
-                   ssa_build=lambda: compile_program(conj, trace=trace).ssa,
+                   ssa_build=lambda: compile_program(conj, trace=trace, slots=slots).ssa,
                    native_dag=(recs, nn, kb, nk, nodes, idx, names))
 
 
@@ -179,13 +180,14 @@ def _stats(info, n_insn):
             "div_nominal_ops": int(info.div_nominal_ops), "wide_divisions": int(info.n_div)}
 
 
-def _run(fns, recs, nn, kb, nk, roots, nconj, ntrace):
-    """One mw_compile call: (info, code, consts, leaf record indices, trace triples)."""
+def _run(fns, recs, nn, kb, nk, roots, nconj, ntrace, slots=None):
+    """One mw_compile_slots call: (info, code, consts, leaf record indices, trace triples)."""
     lib, c_compile, c_take, c_free = fns
     kbuf = ctypes.create_string_buffer(kb, len(kb)) if kb else None
     h = _P()
     info = MwCompileInfo()
-    rc = c_compile(_addr(recs), len(recs), nn, kbuf, nk, _addr(roots), nconj, ntrace,
+    nw, nsl = slots or (isa.NW, isa.NN)
+    rc = c_compile(_addr(recs), len(recs), nn, kbuf, nk, _addr(roots), nconj, ntrace, nw, nsl,
                    ctypes.byref(h), ctypes.byref(info))
     if rc != 0:
         msg = (lib.mg_last_error() or b"").decode()
@@ -307,9 +309,9 @@ USE_PYTHON = os.environ.get("MYTHRIL_AMD_PY_COMPILE", "0") == "1"
 
 
 def compile_query(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, LeafSpec]] = None,
-                  trace: Sequence[Node] = (), pools=None, reach=None) -> Program:
+                  trace: Sequence[Node] = (), pools=None, reach=None, slots=None) -> Program:
     """The product's compiler: native when the library is built (always, on
     a GPU box: the device path needs the same library), else compiler.py."""
     if not USE_PYTHON and available():
-        return compile_native(conjuncts, leaf_specs, trace, pools, reach)
-    return compile_program(conjuncts, leaf_specs=leaf_specs, trace=trace, pools=pools)
+        return compile_native(conjuncts, leaf_specs, trace, pools, reach, slots)
+    return compile_program(conjuncts, leaf_specs=leaf_specs, trace=trace, pools=pools, slots=slots)

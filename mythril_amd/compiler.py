@@ -724,8 +724,9 @@ def _schedule_narrow_early(insns: List[MInsn]) -> List[MInsn]:
 
 
 # --------------------------------------------------------------------------- register allocation
-def _allocate(insns: List[MInsn]):
-    """Belady allocation of W/N vregs to MW_NW/MW_NN slots; returns (insns, n_spill)."""
+def _allocate(insns: List[MInsn], slots: Optional[Tuple[int, int]] = None):
+    """Belady allocation of W/N vregs to MW_NW/MW_NN slots (slots: fewer,
+    (W, N) - mw_compile.cpp mw_compile_slots); returns (insns, n_spill)."""
     uses: Dict[int, List[int]] = {}
     for i, ins in enumerate(insns):
         for s in ins.srcs:
@@ -743,10 +744,10 @@ def _allocate(insns: List[MInsn]):
         ptr[vid] = p
         return lst[p] if p < len(lst) else 1 << 60
 
-    cap = {"W": isa.NW, "N": isa.NN}
+    nw, nn = slots or (isa.NW, isa.NN)
     # the interpreter's write-back scratch slots are never allocated (mw_isa.h)
-    free = {"W": [k for k in range(isa.NW - 1, -1, -1) if k != isa.W_RESERVED],
-            "N": [k for k in range(isa.NN - 1, -1, -1) if k & 31 != isa.N_RESERVED]}
+    free = {"W": [k for k in range(nw - 1, -1, -1) if k != isa.W_RESERVED],
+            "N": [k for k in range(nn - 1, -1, -1) if k & 31 != isa.N_RESERVED]}
     reg_of: Dict[int, int] = {}
     resident: Dict[str, Dict[int, VReg]] = {"W": {}, "N": {}}
     # spill slots: per class (a W slot is 8 words of the per-lane spill area,
@@ -950,9 +951,10 @@ def layout_leaves(leaf_nodes: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
 
 
 def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, LeafSpec]] = None,
-                    trace: Sequence[Node] = (), pools: Optional[Dict[str, List[Optional[int]]]] = None
-                    ) -> Program:
-    """Compile the conjunction of `conjuncts` (IR Bool terms)."""
+                    trace: Sequence[Node] = (), pools: Optional[Dict[str, List[Optional[int]]]] = None,
+                    slots: Optional[Tuple[int, int]] = None) -> Program:
+    """Compile the conjunction of `conjuncts` (IR Bool terms).  slots: the
+    (W, N) register slots the allocator may use, when fewer than MW_NW / MW_NN."""
     conj = _flatten(conjuncts)
     lw = _Lowerer()
     for t in trace:
@@ -972,7 +974,7 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
     lw.emit_void("END", 0, [])
 
     lw.insns = _schedule_narrow_early(lw.insns)
-    insns, n_spill = _allocate(_fuse_checks(lw.insns))
+    insns, n_spill = _allocate(_fuse_checks(lw.insns), slots)
 
     # constant pool
     consts: List[int] = []

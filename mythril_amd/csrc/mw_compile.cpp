@@ -145,6 +145,9 @@ struct Node {
 };
 
 struct Compiler {
+  // register slots the allocator may use (mw_compile_slots: fewer, for the
+  // asm interpreter's smaller register layouts; W7 / N31 / N63 never)
+  int w_slots = MW_NW, n_slots = MW_NN;
   std::vector<Node> nodes;
   const uint8_t* kvals = nullptr;
   size_t nkvals = 0;
@@ -762,9 +765,9 @@ struct Compiler {
       return p < end ? ulist[p] : NEVER;
     };
     std::vector<int> freeW, freeN;
-    for (int s = MW_NW - 1; s >= 0; --s)
+    for (int s = w_slots - 1; s >= 0; --s)
       if (s != MW_W_RESERVED) freeW.push_back(s);
-    for (int s = MW_NN - 1; s >= 0; --s)
+    for (int s = n_slots - 1; s >= 0; --s)
       if ((s & 31) != MW_N_RESERVED) freeN.push_back(s);
     std::vector<int> reg_of(nv, -1), spill_of(nv, -1);
     std::vector<int> resW, resN;   // insertion-ordered resident vregs (compiler.py dict order)
@@ -1010,13 +1013,18 @@ struct mw_compiled {
 
 extern "C" {
 
-int mw_compile(const int32_t* recs, size_t nrecs_words, size_t nnodes, const uint8_t* kvals, size_t nkvals,
-               const int32_t* roots, size_t nconj, size_t ntrace, mw_compiled** out, mw_compile_info* info) {
+int mw_compile_slots(const int32_t* recs, size_t nrecs_words, size_t nnodes, const uint8_t* kvals, size_t nkvals,
+                     const int32_t* roots, size_t nconj, size_t ntrace, uint32_t w_slots, uint32_t n_slots,
+                     mw_compiled** out, mw_compile_info* info) {
   if (!out || !info || (nnodes && !recs) || ((nconj + ntrace) && !roots))
     return mw_fail(MG_E_ARG, "mw_compile: null argument");
   *out = nullptr;
+  if (w_slots < 4 || w_slots > MW_NW || n_slots < 8 || n_slots > MW_NN)
+    return mw_fail(MG_E_ARG, "mw_compile: register slots out of range");
   try {
     Compiler c;
+    c.w_slots = (int)w_slots;
+    c.n_slots = (int)n_slots;
     c.kvals = kvals;
     c.nkvals = nkvals;
     c.nodes.reserve(nnodes);
@@ -1072,6 +1080,11 @@ int mw_compile(const int32_t* recs, size_t nrecs_words, size_t nnodes, const uin
   } catch (const std::bad_alloc&) {
     return mw_fail(MG_E_NOMEM, "mw_compile: out of host memory");
   }
+}
+
+int mw_compile(const int32_t* recs, size_t nrecs_words, size_t nnodes, const uint8_t* kvals, size_t nkvals,
+               const int32_t* roots, size_t nconj, size_t ntrace, mw_compiled** out, mw_compile_info* info) {
+  return mw_compile_slots(recs, nrecs_words, nnodes, kvals, nkvals, roots, nconj, ntrace, MW_NW, MW_NN, out, info);
 }
 
 int mw_compiled_take(mw_compiled* r, uint32_t* code, uint32_t* consts, uint32_t* leaves, uint32_t* trace) {

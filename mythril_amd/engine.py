@@ -23,6 +23,8 @@ import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
+import numpy as np
+
 from . import isa
 from .ccompile import compile_query
 from .compiler import LeafSpec, Program, Unsupported
@@ -65,6 +67,18 @@ class Query:
     arg_chunks: Dict[str, List[List[Node]]] = field(default_factory=dict)
     _trace: Optional[Program] = None
     _trace_future: Optional[object] = None   # a queued compile (_prebuild_witness_programs)
+    _long: Optional[Program] = None
+
+    @property
+    def long_program(self) -> Program:
+        """The program a long search runs (search_phased's launch after the
+        probe): ``program`` itself, or the same constraints compiled for the
+        asm interpreter's quarter register layout (four waves per SIMD, more
+        spills) when that is worth it (_quarter_program).  Same leaf table
+        and pools: the same candidates, the same lowest satisfying index."""
+        if self._long is None:
+            self._long = _quarter_program(self)
+        return self._long
 
     @property
     def trace_program(self) -> Program:
@@ -198,17 +212,30 @@ def _gil_handoff(active: bool):
 PROBE_CANDIDATES = 1 << 16
 
 
-def search_phased(dev, dps, seed: int, begin: int, count: int, flags: int):
+def search_phased(dev, dps, seed: int, begin: int, count: int, flags: int, long_programs=None):
     """dev.search(dps, seed, begin, count, flags) with the probe launch above
     (stop-after-hit searches longer than twice the probe); the statistics of
-    both launches summed."""
+    both launches summed.  long_programs: per program, a callable giving the
+    program the launch after the probe runs instead (Query.long_program: the
+    same candidates; loaded here and freed after that launch)."""
     if not (flags & isa.FLAG_STOP_AFTER_HIT) or count <= 2 * PROBE_CANDIDATES:
         return dev.search(dps, seed, begin, count, flags)
     found, st = dev.search(dps, seed, begin, PROBE_CANDIDATES, flags)
     rest = [i for i, f in enumerate(found) if f is None]
     if rest:
-        f2, st2 = dev.search([dps[i] for i in rest], seed, begin + PROBE_CANDIDATES, count - PROBE_CANDIDATES,
-                             flags)
+        rdps, extra = [], []
+        try:
+            for i in rest:
+                lp = long_programs[i]() if long_programs is not None else None
+                if lp is not None and lp is not dps[i].prog:
+                    extra.append(dev.load(lp))
+                    rdps.append(extra[-1])
+                else:
+                    rdps.append(dps[i])
+            f2, st2 = dev.search(rdps, seed, begin + PROBE_CANDIDATES, count - PROBE_CANDIDATES, flags)
+        finally:
+            for d in extra:
+                d.free()
         found = list(found)
         for i, f in zip(rest, f2):
             found[i] = f
@@ -237,6 +264,54 @@ def _prebuild_witness_programs(queries) -> bool:
     for q in todo:
         q._trace_future = _PREBUILD.submit(_build_witness_program, q)
     return True
+
+
+# The asm interpreter's quarter register layout (mw_kernels.hip
+# mw_search_asm_kernel_q, asmgen.py variant("quarter")): 4 W and 16 N slots,
+# four waves per SIMD where the other layouts run three or two; its LDS
+# budget per thread (spill words and pool rows) is QUARTER_LDS_WORDS.  A
+# program the compiler allocated over more slots is compiled again within
+# those for long searches, when it spills within that budget and grows by at
+# most QUARTER_MAX_GROWTH in instructions (profiles/r5c: the quarter kernel
+# runs the LASER group 1.28x as fast as the narrow and wide ones).
+QUARTER_SLOTS = (4, 16)
+QUARTER_LDS_WORDS = 40
+QUARTER_MAX_GROWTH = 1.3
+
+
+def _slots_used(p: Program) -> Tuple[int, int]:
+    """(W slots, N slots) the program's results occupy (highest + 1)."""
+    mw = mn = -1
+    code = p.code
+    for i in range(1, len(code), 4):
+        w, n = isa.decode_dst(int(code[i]) & 0xFFFF)
+        if w is not None and w > mw:
+            mw = w
+        if n is not None and n > mn:
+            mn = n
+    return mw + 1, mn + 1
+
+
+def _pool_rows(p: Program) -> int:
+    """LDS words per thread the program's pool takes (256 threads a block)"""
+    return (int(p.pool.size) + 255) // 256 if p.pool is not None else 0
+
+
+def _quarter_program(q: "Query") -> Program:
+    p = q.program
+    w, n = _slots_used(p)
+    if (w <= QUARTER_SLOTS[0] and n <= QUARTER_SLOTS[1]) or _pool_rows(p) >= QUARTER_LDS_WORDS:
+        return p       # fits already (the loader picks the quarter kernel), or its pool alone fills the budget
+    fixed = {s.name: dataclasses.replace(s, pool=None if s.pool is None else list(s.pool)) for s in p.leaf_specs}
+    try:
+        qp = compile_query(q.lowered.conjuncts, leaf_specs=fixed, reach=(q.lowered.flat, q.lowered.nodes),
+                           slots=QUARTER_SLOTS)
+    except Exception:   # noqa: BLE001 - the program as it is
+        return p
+    if (qp.n_insn > QUARTER_MAX_GROWTH * p.n_insn or qp.n_spill + _pool_rows(qp) > QUARTER_LDS_WORDS
+            or not np.array_equal(qp.leaves, p.leaves) or not np.array_equal(qp.pool, p.pool)):
+        return p
+    return qp
 
 
 def _witness_program(prog: Program, traced: List[Node]) -> Program:
@@ -315,7 +390,8 @@ class WitnessEngine:
                 if (self.asmjit_min_ops and hasattr(self.dev, "attach_asm")
                         and count * sum(q.ops_per_eval for q in queries) >= self.asmjit_min_ops):
                     self._assemble(dps)
-                found, st = search_phased(self.dev, dps, self.seed, begin, count, flags)
+                found, st = search_phased(self.dev, dps, self.seed, begin, count, flags,
+                                          [lambda q=q: q.long_program for q in queries])
             self.stats["searches"] += 1
             self.stats["programs"] += len(queries)
             self.stats["evals"] += st["evals"]

@@ -210,6 +210,33 @@ def test_asm_corpus_verdicts_on_the_wider_layouts(dev, corpus, env):
         assert np.array_equal(va, vi), (name, env, int(np.count_nonzero(va != vi)))
 
 
+def test_asm_quarter_long_programs(dev, corpus):
+    """Round 5: a long search runs Query.long_program, the constraints compiled
+    again within the quarter layout's 4 W / 16 N slots (more spills, four
+    waves per SIMD): per candidate the same verdicts as the search program,
+    and the same lowest witness in a stop-after-hit search."""
+    n = 1 << 13
+    done = 0
+    for name, q in corpus:
+        lp = q.long_program
+        if lp is q.program:
+            continue
+        dp, dl = dev.load(q.program), dev.load(lp)
+        try:
+            assert dev.engine_of(dl) == "asm"
+            va, _ = dev.eval_generated(dp, DEFAULT_SEED, 0, n, trace=False)
+            vl, _ = dev.eval_generated(dl, DEFAULT_SEED, 0, n, trace=False)
+            assert np.array_equal(va, vl), (name, int(np.count_nonzero(va != vl)))
+            fa, _ = dev.search([dp], DEFAULT_SEED, 0, 1 << 16, isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT)
+            fl, _ = dev.search([dl], DEFAULT_SEED, 0, 1 << 16, isa.FLAG_EARLY_EXIT | isa.FLAG_STOP_AFTER_HIT)
+            assert fa == fl, name
+        finally:
+            dp.free()
+            dl.free()
+        done += 1
+    assert done >= 20
+
+
 def test_asm_corpus_search_modes(dev, corpus):
     """64 programs per launch, exhaustive / early exit / stop after hit: the
     same lowest witness index per program as the compiled interpreter."""

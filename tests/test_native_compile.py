@@ -172,7 +172,7 @@ def test_malformed_records_rejected():
                             (array("i", [1, 8, 0]), 1, array("i", [0])),                 # truncated
                             (array("i", [1, 8, 0, 0, 0, 0]), 1, array("i", [3]))):       # root out of range
         rc = comp(ccompile._addr(recs), len(recs), nn, None, 0, ccompile._addr(roots), len(roots), 0,
-                  ctypes.byref(h), ctypes.byref(info))
+                  isa.NW, isa.NN, ctypes.byref(h), ctypes.byref(info))
         assert rc == -3 and not h.value, lib.mg_last_error()
 
 
@@ -228,3 +228,41 @@ def test_witness_program_from_the_search_stream_is_the_fresh_compile():
         assert [x.id for x in a.leaf_nodes] == [x.id for x in b.leaf_nodes]
         n += 1
     assert n >= 60
+
+
+def _max_slots(p):
+    mw = mn = -1
+    for i in range(0, len(p.code), 4):
+        w, n = isa.decode_dst(int(p.code[i + 1]) & 0xFFFF)
+        mw = max(mw, -1 if w is None else w)
+        mn = max(mn, -1 if n is None else n)
+    return mw + 1, mn + 1
+
+
+def test_slot_limited_programs_identical():
+    """Round 5: compiled for the asm interpreter's quarter layout (4 W and 16
+    N slots, mw_compile_slots), a program keeps its registers within those
+    slots (spilling more) on both compilers, byte-identically; a program that
+    fit already comes out unchanged."""
+    files = _corpus("laser")[::9]
+    grew = 0
+    for f in files:
+        s = parse_file(f)
+        q = prepare(s.asserts, s.ctx)
+        specs = {x.name: x for x in q.program.leaf_specs}
+        cp = lambda: {k: dataclasses.replace(v) for k, v in specs.items()}  # noqa: E731
+        a = compile_program(q.lowered.conjuncts, leaf_specs=cp(), slots=(4, 16))
+        b = ccompile.compile_native(q.lowered.conjuncts, leaf_specs=cp(), slots=(4, 16))
+        _same(a, b)
+        w, n = _max_slots(b)
+        assert w <= 4 and n <= 16, f
+        w0, n0 = _max_slots(q.program)
+        if w0 <= 4 and n0 <= 16:
+            assert np.array_equal(b.code, q.program.code)
+        else:
+            grew += b.n_insn >= q.program.n_insn
+    assert grew > 0
+    c = Ctx()
+    x = c.var("x", 8)
+    with pytest.raises(RuntimeError):
+        ccompile.compile_native([c.app("=", x, c.const(1, 8))], slots=(3, 16))

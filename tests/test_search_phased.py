@@ -52,3 +52,31 @@ def test_miss_in_the_probe_continues_and_batches_keep_their_hits():
     engine.search_phased(dev, [dp, dp2], syn.seed, begin, count, 0)
     engine.search_phased(dev, [dp], syn.seed, begin, 2 * engine.PROBE_CANDIDATES, FLAGS)
     assert [r[2] for r in dev.ranges] == [count, 2 * engine.PROBE_CANDIDATES]
+
+
+def test_the_launch_after_the_probe_runs_the_long_program():
+    """Round 5: the launch after the probe may run another compile of the same
+    constraints (Query.long_program: the quarter register layout's); it is
+    loaded for that launch alone and freed after it, and the witness is the
+    same lowest satisfying index."""
+    syn, dev, dp = _setup()
+    begin = WITNESS - engine.PROBE_CANDIDATES - 5000
+    count = 1 << 18
+    (want,), _ = dev.search([dp], syn.seed, begin, count, FLAGS)
+    long_prog = compile_program(syn.conjuncts, slots=(4, 16))
+    loaded = []
+    real_load = dev.load
+
+    def load(p):
+        loaded.append(real_load(p))
+        return loaded[-1]
+    dev.load = load
+    dev.ranges.clear()
+    found, _ = engine.search_phased(dev, [dp], syn.seed, begin, count, FLAGS, [lambda: long_prog])
+    assert found == [want] == [WITNESS]
+    assert len(loaded) == 1 and loaded[0].prog is long_prog
+    assert len(dev.ranges) == 2
+    # a program that is its own long program is not loaded again
+    loaded.clear()
+    engine.search_phased(dev, [dp], syn.seed, begin, count, FLAGS, [lambda: dp.prog])
+    assert loaded == []

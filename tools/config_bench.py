@@ -92,7 +92,9 @@ def main():
         if a.only and name not in a.only.split(","):
             continue
         for gfiles, g in _groups(files, together):
-            dps = [dev.load(q.program) for q in g]
+            # the program a long search runs (engine.search_phased after the
+            # probe: Query.long_program, the quarter layout's compile when it pays)
+            dps = [dev.load(q.long_program) for q in g]
             ops = sum(q.ops_per_eval for q in g)
             count = 1 << log2
             # time to first witness (interpreter, early exit)

@@ -21,7 +21,8 @@ def main():
     for row in csv.DictReader(open(path)):
         if "mw_search" in row["Kernel_Name"]:
             rows[int(row["Dispatch_Id"])][row["Counter_Name"]] = float(row["Counter_Value"])
-    ids = sorted(rows)
+    # the context's introspection launches (one block per asm kernel) come first
+    ids = [i for i in sorted(rows) if rows[i].get("SQ_WAVES", 0) > 16]
     for k, ln in enumerate(lines):
         if 2 * k + 1 >= len(ids):
             break
