@@ -106,6 +106,8 @@ MSK2 = 90         # s[90:91]
 JMP = 92          # s[92:93] the dispatch target: s92 the handler's low word, s93 the code's high word
 SX = 94           # s[94:95] scratch pair
 AM = 100          # s[100:101] the chunk's live lanes (valid, every check so far held)
+POLL = 99         # chunks this wave has started (stop-after-hit polls every POLL_EVERY-th)
+POLL_EVERY = 16
 
 # chunk loop state (s16..s39)
 CH, NCH, GDX = 16, 17, 18
@@ -1215,7 +1217,7 @@ def gen(mode="interp"):
       f"s_mov_b64 {sr(LEAVES, 2)}, {sr(DESC + 4, 2)}",
       f"s_lshl_b32 {s(POOLB)}, {s(NLDS)}, 10",
       f"s_mov_b32 {s(PM0)}, 0xD2511F53", f"s_mov_b32 {s(PM1)}, 0xCD9E8D57",
-      f"s_mov_b64 {sr(EVALS, 2)}, 0", f"s_mov_b32 {s(HIT)}, 0",
+      f"s_mov_b64 {sr(EVALS, 2)}, 0", f"s_mov_b32 {s(HIT)}, 0", f"s_mov_b32 {s(POLL)}, 0",
       f"v_lshlrev_b32_e32 {v(LDSOFF)}, 2, {v(T)}", f"v_mov_b32_e32 {v(TID)}, {v(T)}")
     if mode == "interp":
         # the handlers' base address (s_getpc_b64 gives the next instruction's)
@@ -1268,8 +1270,15 @@ def gen(mode="interp"):
     g(f"s_cmp_lt_u32 {s(CH)}, {s(NCH)}", "s_cbranch_scc0 Lexit_%=",
       f"s_lshl_b32 {s(BASE)}, {s(CH)}, 8", f"s_lshr_b32 {s(BASE + 1)}, {s(CH)}, 24",
       f"s_add_u32 {s(BASE)}, {s(BASE)}, {s(BEGIN)}", f"s_addc_u32 {s(BASE + 1)}, {s(BASE + 1)}, {s(BEGIN + 1)}",
-      # stop after hit: a witness below this chunk is known (a stale read only delays the stop)
+      # stop after hit: a witness below this chunk is known (a stale read only
+      # delays the stop).  Polled every POLL_EVERY-th chunk of the wave, not
+      # its first: every wave reading the one witness word past the caches
+      # queues at one memory channel (a 2^22-candidate miss spent most of its
+      # 1.8 ms there, profiles/r5d), and a probe launch covers the lowest
+      # indices (engine.search_phased)
       f"s_bitcmp1_b32 {s(FLAGS)}, 1", "s_cbranch_scc0 Lnostop_%=",
+      f"s_add_u32 {s(POLL)}, {s(POLL)}, 1", f"s_and_b32 {s(SX)}, {s(POLL)}, {POLL_EVERY - 1}",
+      f"s_cmp_lg_u32 {s(SX)}, 0", "s_cbranch_scc1 Lnostop_%=",
       f"s_load_dwordx2 {sr(SX, 2)}, {sr(OUTMIN, 2)}, 0x0 glc", "s_waitcnt lgkmcnt(0)",
       # m <= base  <=>  !(base < m): compare (hi, lo) lexicographically
       f"s_cmp_lt_u32 {s(SX + 1)}, {s(BASE + 1)}", "s_cbranch_scc1 Lexit_%=",
@@ -1557,7 +1566,7 @@ def philox_sub(g):
 
 
 CLOBBERS = (", ".join(f'"v{i}"' for i in list(range(T + 8)) + list(range(NK0, NVGPR))) + ", "
-            + ", ".join(f'"s{i}"' for i in list(range(16, 99)) + [AM, AM + 1])
+            + ", ".join(f'"s{i}"' for i in list(range(16, 99)) + [POLL, AM, AM + 1])
             + ', "vcc", "scc", "m0", "memory"')
 
 

@@ -15,6 +15,7 @@
 #   gt[=LOG2]      tools/ground_truth.py: the corpus's unknown queries searched up to 2^LOG2 (32)
 #   latency        tools/latency_bench.py (drop-in prepare/search/materialise per query)
 #   replay         python -m mythril_amd.replay tests/golden/solver_log
+#   replaylat      tools/replay_latency.py (LASER-order translation + preparation, host only)
 #   opbench        tools/opbench.py jit
 #   keccak         tools/keccak_bench.py
 #   ipmc=FILE      PMC passes on one exhaustive interpreter launch of FILE (tools/interp_once.py)
@@ -93,6 +94,9 @@ for step in "$@"; do
     replay)
       run 300 "$OUT/replay.txt" python3 -m mythril_amd.replay tests/golden/solver_log
       tail -12 "$OUT/replay.txt" ;;
+    replaylat)
+      run 400 "$OUT/replay_latency.log" python3 -u tools/replay_latency.py --out "$OUT/replay_latency.json"
+      tail -3 "$OUT/replay_latency.log" ;;
     opbench)
       run 400 "$OUT/opbench.log" python3 tools/opbench.py jit
       tail -20 "$OUT/opbench.log" ;;
