@@ -1206,7 +1206,9 @@ def gen(mode="interp"):
       f"s_mov_b64 {sr(SEED, 2)}, {sr(DESC, 2)}", f"s_mov_b64 {sr(BEGIN, 2)}, {sr(DESC + 2, 2)}",
       f"s_mov_b64 {sr(END, 2)}, {sr(DESC + 4, 2)}", f"s_mov_b32 {s(FLAGS)}, {s(DESC + 6)}",
       f"s_mov_b32 {s(NLDS)}, {s(DESC + 7)}", f"s_mov_b32 {s(GSTRIDE)}, {s(72)}", f"s_mov_b32 {s(NCH)}, {s(73)}",
-      f"s_mov_b32 {s(GDX)}, {s(74)}", f"s_mov_b64 {sr(GSP, 2)}, {sr(76, 2)}", f"s_mov_b64 {sr(VERD, 2)}, {sr(78, 2)}",
+      # the chunk stride: the kernel body's (AsmArgs.gdx, or this program's
+      # share of a 1D grid over several, mw_asm_abi.h)
+      f"s_mov_b32 {s(GDX)}, %[gdx]", f"s_mov_b64 {sr(GSP, 2)}, {sr(76, 2)}", f"s_mov_b64 {sr(VERD, 2)}, {sr(78, 2)}",
       # AsmArgs (continued): trace(2) ncand pad
       f"s_load_dwordx4 {sr(72, 4)}, {sr(ARGP, 2)}, 0x40", "s_waitcnt lgkmcnt(0)",
       f"s_mov_b64 {sr(TRACE, 2)}, {sr(72, 2)}", f"s_mov_b32 {s(NCAND)}, {s(74)}",

@@ -1309,7 +1309,22 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     // enough blocks to fill the chip several times over, split across programs
     G.gx = std::max<u64>(1, (u64)c->ncu * 8 / G.n);
     G.gx = std::min<u64>(G.gx, nchunks);
-    const u64 nthreads = G.gx * G.n * kBlock;
+    u64 nthreads = G.gx * G.n * kBlock;
+    if (gi < kAsmLayouts) {
+      // the asm groups: one 1D grid, blocks in proportion to each program's
+      // instructions (its cost per candidate), at least one, at most its chunks
+      double wsum = 0;
+      for (size_t j = G.first; j < G.first + G.n; ++j) wsum += std::max<u32>(1, hp[j].n_insn);
+      const double B = (double)std::max<u64>(G.n, (u64)c->ncu * 8);
+      u64 at = 0;
+      for (size_t j = G.first; j < G.first + G.n; ++j) {
+        const u64 b = std::min<u64>(nchunks, std::max<u64>(1, (u64)(B * std::max<u32>(1, hp[j].n_insn) / wsum)));
+        hp[j].first_block = (u32)at;
+        at += b;
+      }
+      G.gx = at;   // the whole grid
+      nthreads = G.gx * kBlock;
+    }
     G.nlds = gi < kAsmLayouts ? lay_nlds[gi] : std::min(max_spill, kLdsSpillWords);
     spill_need = std::max(spill_need, (size_t)(max_spill - G.nlds) * nthreads * sizeof(u32));
   }
@@ -1345,9 +1360,10 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     aa.end = begin + count;
     aa.flags = flags;
     aa.nlds = groups[gi].nlds;
-    aa.gstride = (u32)(groups[gi].gx * groups[gi].n * kBlock * 4);
+    aa.gstride = (u32)(groups[gi].gx * kBlock * 4);   // a 1D grid of gx blocks (above)
     aa.nchunks = (u32)nchunks;
     aa.gdx = (u32)groups[gi].gx;
+    aa.nprog = (u32)groups[gi].n;
     aa.spillbuf = c->d_spill;   // the launches run one after the other on the stream
     aa.verdict = nullptr;
   }
@@ -1358,7 +1374,7 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     const Group& G = groups[gi];
     if (!G.n) continue;
     const size_t lds = (size_t)G.nlds * kBlock * 4 + (size_t)G.max_pool * 4;
-    hipLaunchKernelGGL(kAsmKernel[gi], dim3((u32)G.gx, (u32)G.n), dim3(kBlock), lds, c->stream,
+    hipLaunchKernelGGL(kAsmKernel[gi], dim3((u32)G.gx, 1u), dim3(kBlock), lds, c->stream,
                        c->d_progs + G.first, (const AsmArgs*)c->d_asmargs + gi, c->d_min + G.first, c->d_counter,
                        G.nlds);
     HIPCHK(hipGetLastError());
