@@ -165,6 +165,7 @@ def sr(a, n):
 
 class Gen:
     inline_leaf = True   # W_CDINS inlines the Lleaf code (leaf_inline) instead of calling it
+    chains = True        # CHECK_IMPEQ runs chain (the interpreter; an assembled body has no dispatch)
 
     def __init__(self):
         self.lines = []
@@ -576,14 +577,41 @@ def build_handlers():
         g(f"s_or_b64 vcc, vcc, {sr(MSK, 2)}")
         update_alive(g)
 
-    @handler("CHECK_IMPEQ")
-    def _(g):
+    def impeq(g):
+        """alive &= (a == 0) | (b == c) for the current bank's instruction"""
         g.field("a", S[0]), g.field("b", S[1]), g.field("c", S[2])
         g.op_n(S[0], f"v_cmp_eq_u32_e64 {sr(MSK, 2)}, 0, {{a}}", T, "SRC1")
         g.fetch_n(S[2], T + 2)
         g.op_n(S[1], f"v_cmp_eq_u32_e32 vcc, {{a}}, {v(T + 2)}", T + 1)
         g(f"s_or_b64 vcc, vcc, {sr(MSK, 2)}")
         update_alive(g)
+
+    @handler("CHECK_IMPEQ")
+    def _(g):
+        # congruence checks come in runs (a C3 program: 2 176 of its 3 218
+        # instructions): mw_asm_predecode flags a CHECK_IMPEQ followed by
+        # another with bit 31 of word 3 (its c field sits in the low bits),
+        # and the handler takes the next one itself - a branch not taken per
+        # link instead of a jump per instruction, two links per loop trip,
+        # one per bank, each with its own exit (as W_CDINS chains)
+        if not g.chains:
+            impeq(g)
+            return
+        nlinks = 1 if DISPATCH == "single" else 2
+        tops, exits = [g.L("iqtop") for _ in range(nlinks)], []
+        for j in range(nlinks):
+            g.label(tops[j])
+            impeq(g)
+            exits.append((g.L("iqlast"), g.CUR))
+            g(f"s_bitcmp1_b32 {s(g.CUR + 3)}, 31", f"s_cbranch_scc0 {exits[-1][0]}")
+            g.consume()
+        g(f"s_branch {tops[0]}")
+        for lab, bank in exits[1:]:
+            g.label(lab)
+            g.CUR = bank
+            g.next()
+        g.label(exits[0][0])
+        g.CUR = exits[0][1]
 
     def eq8(g, a, b, dst_v):
         """dst_v = OR of the limb XORs (0 iff equal)"""
@@ -1664,6 +1692,7 @@ def _lit(x: int) -> str:
 class StaticGen(Gen):
     """Gen for one program whose fields are known at generation time."""
     inline_leaf = False   # the body calls the template's Lleaf through LEAFADDR
+    chains = False
 
     def __init__(self, consts, leaves=None, pool=None):
         super().__init__()

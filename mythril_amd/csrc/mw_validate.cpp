@@ -295,6 +295,9 @@ int mw_asm_predecode_layout(const u32* code, size_t nwords, const u32* consts, s
     // no immediate: the c operand goes to word 3 too (mythril_amd/asmgen.py
     // C_IN_IMM: the handler indexes with it as it is, no shift)
     if (op == MW_N_ITE || op == MW_W_ITE || op == MW_CHECK_IMPEQ || op == MW_CHECK_IMPEQW) O[3] = c2;
+    // a CHECK_IMPEQ followed by another: the handler takes that one itself
+    // (a chain, mythril_amd/asmgen.py), bit 31 above its c field
+    if (op == MW_CHECK_IMPEQ && i + 7 < nwords && (code[i + 4] & 0xffu) == MW_CHECK_IMPEQ) O[3] |= 0x80000000u;
     if (op == MW_N_ADD || op == MW_N_SUB || op == MW_N_MUL || op == MW_N_NOT)
       O[3] = w >= 32u ? 0xffffffffu : (1u << w) - 1u;
   }

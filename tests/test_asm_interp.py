@@ -279,3 +279,17 @@ def test_corpus_fits_the_quarter_layout_in_part():
     progs = [p for f, p in _corpus_programs() if ".gz" in f]
     fit = sum(_predecode_layout(p.code, p.consts, 80, 14, 16, 4)[0] == 0 for p in progs)
     assert fit >= 0.35 * len(progs), (fit, len(progs))
+
+
+def test_predecode_chains_check_impeq_runs():
+    """Round 5: a CHECK_IMPEQ followed by another gets bit 31 of word 3 (its c
+    field in the low bits): the handler takes the next one itself."""
+    e = isa.encode
+    N = lambda k: isa.encode_dst("N", k)   # noqa: E731
+    none = isa.encode_dst(None)
+    code = (e("N_EQN", 8, N(1), 2, 3) + e("CHECK_IMPEQ", 0, none, 1, 4, 5) + e("CHECK_IMPEQ", 0, none, 1, 6, 7)
+            + e("CHECK_IMPEQ", 0, none, 1, 8, 9) + e("CHECK", 0, none, 1) + e("CHECK_IMPEQ", 0, none, 1, 2, 3)
+            + e("END", 0, none))
+    o, _ = _predecode(code, [0])
+    assert [int(x) >> 31 for x in o[:, 3]] == [0, 1, 1, 0, 0, 0, 0]
+    assert [int(x) & 0xFFFF for x in o[1:4, 3]] == [5, 7, 9]      # c in the low bits, as before
