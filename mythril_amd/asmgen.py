@@ -51,11 +51,12 @@ ASM_LEAF_KINDS = isa.ASM_LEAF_KINDS
 # corpus).  A dispatch is a chain of dependent instructions (profiles/r4m):
 # a third wave per SIMD hides more of it.  variant("narrow") builds this
 # module again with that layout (render_interp emits both bodies).
-# "quarter" (mw_search_asm_kernel_q): 4 W slots and 16 N slots, 126 VGPRs in
+# "quarter" (mw_search_asm_kernel_q): 5 W slots, 16 N slots and 4 narrow
+# constants (no corpus program has more than 3), 124 VGPRs in
 # the asm block, four waves per SIMD, for programs whose registers all lie
 # in those files (about half of the LASER corpus as compiled).
 _LAYOUT_NAME = globals().get("_LAYOUT_OVERRIDE", "wide")
-WFILE = 4 if _LAYOUT_NAME == "quarter" else 8     # W slots the layout holds
+WFILE = 5 if _LAYOUT_NAME == "quarter" else 8     # W slots the layout holds
 W0, N0 = 0, 8 * WFILE
 NFILE = {"wide": 64, "narrow": 24, "quarter": 16}[_LAYOUT_NAME]   # N slots the layout holds
 _OPB = N0 + NFILE                                # first register after the files: the shift padding
@@ -141,9 +142,9 @@ NK0 = 240 if _LAYOUT_NAME == "wide" else T + 8
 NK_INDEX = NK0 - N0
 # the narrow layout holds two constants fewer: the kernel's own two inputs
 # (thread id, spill offset) need VGPRs outside the asm block's 168
-NKN = isa.ASM_NK if _LAYOUT_NAME == "wide" else isa.ASM_NK - 2
+NKN = {"wide": isa.ASM_NK, "narrow": isa.ASM_NK - 2, "quarter": 4}[_LAYOUT_NAME]
 NVGPR = NK0 + NKN                                # registers the interpreter's asm block uses
-assert (NK_INDEX, NVGPR) == {"wide": (176, 256), "narrow": (88, 166), "quarter": (80, 126)}[_LAYOUT_NAME]
+assert (NK_INDEX, NVGPR) == {"wide": (176, 256), "narrow": (88, 166), "quarter": (80, 124)}[_LAYOUT_NAME]
 INTROSPECT_FLAG = 7   # AsmArgs.flags bit: report the handler offsets and exit
 
 

@@ -267,14 +267,14 @@ def _prebuild_witness_programs(queries) -> bool:
 
 
 # The asm interpreter's quarter register layout (mw_kernels.hip
-# mw_search_asm_kernel_q, asmgen.py variant("quarter")): 4 W and 16 N slots,
+# mw_search_asm_kernel_q, asmgen.py variant("quarter")): 5 W and 16 N slots,
 # four waves per SIMD where the other layouts run three or two; its LDS
 # budget per thread (spill words and pool rows) is QUARTER_LDS_WORDS.  A
 # program the compiler allocated over more slots is compiled again within
 # those for long searches, when it spills within that budget and grows by at
 # most QUARTER_MAX_GROWTH in instructions (profiles/r5c: the quarter kernel
 # runs the LASER group 1.28x as fast as the narrow and wide ones).
-QUARTER_SLOTS = (4, 16)
+QUARTER_SLOTS = (5, 16)
 QUARTER_LDS_WORDS = 40
 QUARTER_MAX_GROWTH = 1.3
 

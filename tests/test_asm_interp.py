@@ -251,25 +251,25 @@ def test_corpus_mostly_fits_the_narrow_layout():
 
 
 def test_quarter_layout_predecode():
-    """Round 5: the third asm kernel (asmgen.variant("quarter")) holds 4 W
-    slots and 16 N slots in 126 VGPRs (four waves per SIMD).  A program is
-    predecoded for it only when every W register (operand or result) lies
-    below 4 and every N register below 16 (else -2)."""
+    """Round 5: the third asm kernel (asmgen.variant("quarter")) holds 5 W
+    slots, 16 N slots and 4 narrow constants in 124 VGPRs (four waves per
+    SIMD).  A program is predecoded for it only when every W register
+    (operand or result) lies below 5 and every N register below 16 (else -2)."""
     from mythril_amd import asmgen
     qv = asmgen.variant("quarter")
-    assert (qv.WFILE, qv.NFILE, qv.N0, qv.NK_INDEX, qv.NKN, qv.NVGPR) == (4, 16, 32, 80, 14, 126)
+    assert (qv.WFILE, qv.NFILE, qv.N0, qv.NK_INDEX, qv.NKN, qv.NVGPR) == (5, 16, 40, 80, 4, 124)
     e = isa.encode
     consts = [0] * 9
     consts[8] = 0x77
     ok = (e("LEAF_W", 256, isa.encode_dst("W", 3), imm=0) + e("W_ADD", 256, isa.encode_dst("W", 1), 3, 3)
           + e("N_EQ", 256, isa.encode_dst("N", 15), 1, isa.KBIT | 0) + e("END", 0, isa.encode_dst(None)))
-    rc, o, _ = _predecode_layout(ok, consts, 80, 14, 16, 4)
+    rc, o, _ = _predecode_layout(ok, consts, 80, 4, 16, 5)
     assert rc == 0 and o[1, 1] & 0xFF == 24 and (o[1, 1] >> 16) & 0xFF == 8      # a = W3 x 8, dst = W1 x 8
-    wdst = ok[:-4] + e("MOV_W", 256, isa.encode_dst("W", 4), 1) + e("END", 0, isa.encode_dst(None))
-    wsrc = ok[:-4] + e("W_NOT", 256, isa.encode_dst("W", 0), 5) + e("END", 0, isa.encode_dst(None))
+    wdst = ok[:-4] + e("MOV_W", 256, isa.encode_dst("W", 5), 1) + e("END", 0, isa.encode_dst(None))
+    wsrc = ok[:-4] + e("W_NOT", 256, isa.encode_dst("W", 0), 6) + e("END", 0, isa.encode_dst(None))
     nsrc = ok[:-4] + e("N_NOT", 8, isa.encode_dst("N", 2), 16) + e("END", 0, isa.encode_dst(None))
     for bad in (wdst, wsrc, nsrc):
-        assert _predecode_layout(bad, consts, 80, 14, 16, 4)[0] == -2
+        assert _predecode_layout(bad, consts, 80, 4, 16, 5)[0] == -2
         assert _predecode_layout(bad, consts, 88, 14, 24, 0)[0] == 0      # the narrow layout holds them
 
 
@@ -277,7 +277,7 @@ def test_corpus_fits_the_quarter_layout_in_part():
     """About half of the LASER corpus (as compiled) keeps its registers in the
     quarter layout's files."""
     progs = [p for f, p in _corpus_programs() if ".gz" in f]
-    fit = sum(_predecode_layout(p.code, p.consts, 80, 14, 16, 4)[0] == 0 for p in progs)
+    fit = sum(_predecode_layout(p.code, p.consts, 80, 4, 16, 5)[0] == 0 for p in progs)
     assert fit >= 0.35 * len(progs), (fit, len(progs))
 
 
