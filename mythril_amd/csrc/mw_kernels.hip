@@ -213,9 +213,13 @@ __global__ __launch_bounds__(kBlock, 2) void mw_search_kernel(const ProgDev* __r
   const u32 lane = threadIdx.x & 63u;
   u64 evals = 0, lsteps = 0, lfull = 0, lshort = 0, lgen = 0;   // division paths x lanes
   bool reported = false;   // this wave's later chunks hold only larger indices
+  u32 iter = 0;
   for (u64 ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const u64 base = begin + ch * kBlock;
-    if (flags & MW_FLAG_STOP_AFTER_HIT) {
+    // every 16th chunk of the block, not its first: every block reading the
+    // one witness word at every chunk queues them all at one memory channel
+    // (the asm interpreter's poll, mythril_amd/asmgen.py POLL_EVERY)
+    if ((flags & MW_FLAG_STOP_AFTER_HIT) && (++iter & 15u) == 0u) {
       u64 m = __hip_atomic_load(&out_min[blockIdx.y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (m <= base) break;
     }

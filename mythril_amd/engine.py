@@ -215,9 +215,10 @@ PROBE_CANDIDATES = 1 << 16
 def search_phased(dev, dps, seed: int, begin: int, count: int, flags: int, long_programs=None):
     """dev.search(dps, seed, begin, count, flags) with the probe launch above
     (stop-after-hit searches longer than twice the probe); the statistics of
-    both launches summed.  long_programs: per program, a callable giving the
-    program the launch after the probe runs instead (Query.long_program: the
-    same candidates; loaded here and freed after that launch)."""
+    both launches summed.  long_programs: per program, a callable of the
+    candidates left giving the program the launch after the probe runs
+    instead (search_program: the same candidates; loaded here and freed
+    after that launch)."""
     if not (flags & isa.FLAG_STOP_AFTER_HIT) or count <= 2 * PROBE_CANDIDATES:
         return dev.search(dps, seed, begin, count, flags)
     found, st = dev.search(dps, seed, begin, PROBE_CANDIDATES, flags)
@@ -226,7 +227,7 @@ def search_phased(dev, dps, seed: int, begin: int, count: int, flags: int, long_
         rdps, extra = [], []
         try:
             for i in rest:
-                lp = long_programs[i]() if long_programs is not None else None
+                lp = long_programs[i](count - PROBE_CANDIDATES) if long_programs is not None else None
                 if lp is not None and lp is not dps[i].prog:
                     extra.append(dev.load(lp))
                     rdps.append(extra[-1])
@@ -275,6 +276,11 @@ def _prebuild_witness_programs(queries) -> bool:
 # most QUARTER_MAX_GROWTH in instructions (profiles/r5c: the quarter kernel
 # runs the LASER group 1.28x as fast as the narrow and wide ones).
 QUARTER_SLOTS = (5, 16)
+# ... and only when the search left is long enough to repay that compile
+# (~0.3 ms host, the quarter kernel ~25 % faster): candidates x instructions
+# at least this (profiles/r5f: for a 2^22-candidate LASER miss, 0.32 ms of
+# kernel, the recompile cost more than it saved)
+LONG_PROGRAM_MIN_WORK = 1 << 31
 QUARTER_LDS_WORDS = 40
 QUARTER_MAX_GROWTH = 1.3
 
@@ -312,6 +318,14 @@ def _quarter_program(q: "Query") -> Program:
             or not np.array_equal(qp.leaves, p.leaves) or not np.array_equal(qp.pool, p.pool)):
         return p
     return qp
+
+
+def search_program(q: "Query", candidates: int) -> Program:
+    """The program a search of `candidates` candidates runs: q.long_program
+    when the work repays its compile (LONG_PROGRAM_MIN_WORK), else q.program."""
+    if candidates * max(1, q.program.n_insn) >= LONG_PROGRAM_MIN_WORK:
+        return q.long_program
+    return q.program
 
 
 def _witness_program(prog: Program, traced: List[Node]) -> Program:
@@ -391,7 +405,7 @@ class WitnessEngine:
                         and count * sum(q.ops_per_eval for q in queries) >= self.asmjit_min_ops):
                     self._assemble(dps)
                 found, st = search_phased(self.dev, dps, self.seed, begin, count, flags,
-                                          [lambda q=q: q.long_program for q in queries])
+                                          [lambda n, q=q: search_program(q, n) for q in queries])
             self.stats["searches"] += 1
             self.stats["programs"] += len(queries)
             self.stats["evals"] += st["evals"]

@@ -72,11 +72,34 @@ def test_the_launch_after_the_probe_runs_the_long_program():
         return loaded[-1]
     dev.load = load
     dev.ranges.clear()
-    found, _ = engine.search_phased(dev, [dp], syn.seed, begin, count, FLAGS, [lambda: long_prog])
+    found, _ = engine.search_phased(dev, [dp], syn.seed, begin, count, FLAGS, [lambda n: long_prog])
     assert found == [want] == [WITNESS]
     assert len(loaded) == 1 and loaded[0].prog is long_prog
     assert len(dev.ranges) == 2
     # a program that is its own long program is not loaded again
     loaded.clear()
-    engine.search_phased(dev, [dp], syn.seed, begin, count, FLAGS, [lambda: dp.prog])
+    engine.search_phased(dev, [dp], syn.seed, begin, count, FLAGS, [lambda n: dp.prog])
     assert loaded == []
+
+
+def test_search_program_repays_its_compile():
+    """engine.search_program: the quarter layout's compile only for searches
+    whose candidates x instructions reach LONG_PROGRAM_MIN_WORK (a default
+    LASER search of 2^22 candidates does not repay it); it keeps the search
+    program's leaf table and pools (the same candidates)."""
+    import os
+
+    import numpy as np
+
+    from mythril_amd.smt2 import parse_file
+    f = os.path.join(os.path.dirname(__file__), "golden", "laser",
+                     "calls_t2_fixed_address_q14_EtherThief_unknown.smt2.gz")
+    s = parse_file(f)
+    q = engine.prepare(s.asserts, s.ctx)
+    n = q.program.n_insn
+    assert engine.search_program(q, 1 << 22) is q.program
+    long_ = engine.search_program(q, engine.LONG_PROGRAM_MIN_WORK // n + 1)
+    assert long_ is q.long_program and long_ is not q.program
+    assert np.array_equal(long_.leaves, q.program.leaves) and np.array_equal(long_.pool, q.program.pool)
+    w, nn = engine._slots_used(long_)
+    assert w <= engine.QUARTER_SLOTS[0] and nn <= engine.QUARTER_SLOTS[1]

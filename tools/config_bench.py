@@ -92,9 +92,10 @@ def main():
         if a.only and name not in a.only.split(","):
             continue
         for gfiles, g in _groups(files, together):
-            # the program a long search runs (engine.search_phased after the
-            # probe: Query.long_program, the quarter layout's compile when it pays)
-            dps = [dev.load(q.long_program) for q in g]
+            # the program a search of this length runs (engine.search_program:
+            # the quarter layout's compile when the work repays it)
+            from mythril_amd.engine import search_program
+            dps = [dev.load(search_program(q, 1 << log2)) for q in g]
             ops = sum(q.ops_per_eval for q in g)
             count = 1 << log2
             # time to first witness (interpreter, early exit)

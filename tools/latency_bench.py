@@ -38,7 +38,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-device", action="store_true")
     a = ap.parse_args()
-    from mythril_amd.engine import WitnessEngine, _gil_handoff, _prebuild_witness_programs, prepare, search_phased
+    from mythril_amd.engine import (WitnessEngine, _gil_handoff, _prebuild_witness_programs, prepare,
+                                     search_phased, search_program)
     from mythril_amd.smt2 import parse_file
     eng = None if a.no_device else WitnessEngine(device=0)
     rows = []
@@ -66,7 +67,7 @@ def main():
                         # as WitnessEngine.search: the launch after the probe runs
                         # the query's long program (the quarter layout's compile)
                         (idx,), st = search_phased(eng.dev, [dp], eng.seed, 0, eng.launch_count([q]), 3,
-                                                   [lambda: q.long_program])
+                                                   [lambda n: search_program(q, n)])
                     row["search"] = (time.perf_counter() - t1) * 1e3
                     row["kernel"] = st["kernel_ms"]
                     if idx is not None:
