@@ -791,8 +791,20 @@ bool asm_eligible(const mg_prog_desc* d) {
 // waves per SIMD) fit a CU's 160 KiB; the quarter layout's 40 KiB (four).
 constexpr u32 kLdsSpillWordsByLayout[kAsmLayouts] = {kLdsSpillWords, 52, 40};
 
-bool asm_lds_fit(u32 max_spill, u32 max_pool, u32* nlds, u8 layout = kWide) {
-  const u32 words = kLdsSpillWordsByLayout[layout];
+// MYTHRIL_AMD_ASM_WIDE_LDS=n (81..160): the wide kernel's budget in words (A/B
+// runs: a program that spills past 80 words keeps them in LDS at one block,
+// one wave per SIMD, instead of two with the rest in global memory)
+u32 wide_lds_words() {
+  static const u32 w = [] {
+    const char* e = std::getenv("MYTHRIL_AMD_ASM_WIDE_LDS");
+    const long v = e ? std::strtol(e, nullptr, 10) : 0;
+    return v > (long)kLdsSpillWords && v <= 160 ? (u32)v : kLdsSpillWords;
+  }();
+  return w;
+}
+
+bool asm_lds_fit(u32 max_spill, u32 max_pool, u32* nlds, u8 layout = kWide, bool interp = false) {
+  const u32 words = layout == kWide && interp ? wide_lds_words() : kLdsSpillWordsByLayout[layout];
   const size_t budget = (size_t)words * kBlock * 4, pool_bytes = (size_t)max_pool * 4;
   if (pool_bytes > budget) return false;
   const u32 pool_words_lds = (u32)((pool_bytes + kBlock * 4 - 1) / (kBlock * 4));  // in spill-word rows
@@ -801,7 +813,7 @@ bool asm_lds_fit(u32 max_spill, u32 max_pool, u32* nlds, u8 layout = kWide) {
 }
 
 bool asm_lds_fit(const Prog* p, u32* nlds) {
-  return asm_lds_fit(p->dev.n_spill, p->dev.npool, nlds, p->asm_layout);
+  return asm_lds_fit(p->dev.n_spill, p->dev.npool, nlds, p->asm_layout, true);
 }
 
 // MYTHRIL_AMD_ASM=0 keeps every program on the compiled interpreter (A/B runs, tests)
@@ -953,8 +965,8 @@ int mg_init(int device, mg_ctx** out) {
           hipSuccess ||
       hipFuncSetAttribute((const void*)mw_eval_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
           hipSuccess ||
-      hipFuncSetAttribute((const void*)mw_search_asm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
-          hipSuccess ||
+      hipFuncSetAttribute((const void*)mw_search_asm_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)(wide_lds_words() * kBlock * sizeof(u32))) != hipSuccess ||
       hipFuncSetAttribute((const void*)mw_search_asm_kernel_n, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
           hipSuccess ||
       hipFuncSetAttribute((const void*)mw_search_asm_kernel_q, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
@@ -1275,7 +1287,7 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
       }
     }
     for (int L = 0; L < kAsmLayouts; ++L)
-      if (!glay[L].empty()) (void)asm_lds_fit(ms[L], mp[L], &lay_nlds[L], (u8)L);
+      if (!glay[L].empty()) (void)asm_lds_fit(ms[L], mp[L], &lay_nlds[L], (u8)L, true);
   }
   std::vector<size_t> interp;
   for (int L = 0; L < kAsmLayouts; ++L) interp.insert(interp.end(), glay[L].begin(), glay[L].end());
