@@ -579,13 +579,22 @@ def build_handlers():
         update_alive(g)
 
     def impeq(g):
-        """alive &= (a == 0) | (b == c) for the current bank's instruction"""
+        """alive &= (a == 0) | (b == c) for the current bank's instruction.
+        The premise a is an index equality of a congruence pair, false in
+        every lane for most pairs: then the check holds in every lane and b,
+        c are not read (the interpreter; an assembled body's check runs fold
+        the masks without branches)"""
         g.field("a", S[0]), g.field("b", S[1]), g.field("c", S[2])
         g.op_n(S[0], f"v_cmp_eq_u32_e64 {sr(MSK, 2)}, 0, {{a}}", T, "SRC1")
+        skip = g.L("iqskip") if g.chains else None
+        if skip:
+            g(f"s_cmp_eq_u64 {sr(MSK, 2)}, -1", f"s_cbranch_scc1 {skip}")
         g.fetch_n(S[2], T + 2)
         g.op_n(S[1], f"v_cmp_eq_u32_e32 vcc, {{a}}, {v(T + 2)}", T + 1)
         g(f"s_or_b64 vcc, vcc, {sr(MSK, 2)}")
         update_alive(g)
+        if skip:
+            g.label(skip)
 
     @handler("CHECK_IMPEQ")
     def _(g):
