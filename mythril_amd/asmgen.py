@@ -1020,7 +1020,7 @@ def build_handlers():
         g.label(ins)
         # no lane in range: the inserted byte is 0 in every lane (no leaf draw)
         nos = g.L("cdns")
-        g("s_nop 1", f"s_cmp_eq_u64 {sr(MSK2, 2)}, 0", f"s_cbranch_scc1 {nos}")
+        g(f"s_cmp_eq_u64 {sr(MSK2, 2)}, 0", f"s_cbranch_scc1 {nos}")
         g(f"s_and_b32 {s(S[3])}, {s(g.CUR + 3)}, 0xffff")
         if g.inline_leaf:   # no call / return jumps on the hottest leaf path (C2: 64 of 86 instructions)
             g(f"s_mov_b32 {s(S67)}, {s(S[3])}")
@@ -1212,6 +1212,54 @@ def drop_idx_offs(lines):
                 continue
         out.append(ln)
     return out
+
+
+_VCMP_CONSUMERS = ("s_cmp_", "s_and_b64", "s_or_b64", "s_mov_b64", "s_andn2_b64", "v_cndmask")
+
+
+def tidy_jumps(lines):
+    """Branch peepholes over a body: a branch (or conditional branch) to a
+    label whose first instruction is `s_branch Y` goes to Y; an `s_branch`
+    to the very next instruction is dropped; an `s_nop 1` between a `v_cmp`
+    and the scalar instruction or select that reads its mask is dropped (a
+    VALU-written SGPR needs no wait states before an SALU or VALU read; only
+    lane selects, VMEM and v_div_fmas do, which none of these are)."""
+    def first_insn(i):
+        while i < len(lines) and lines[i].endswith(":"):
+            i += 1
+        return i
+    at = {ln[:-1]: i for i, ln in enumerate(lines) if ln.endswith(":")}
+    out = list(lines)
+    for i, ln in enumerate(out):
+        if ln.startswith(("s_branch ", "s_cbranch_")):
+            op, tgt = ln.split(" ", 1)
+            for _ in range(8):
+                j = at.get(tgt)
+                if j is None:
+                    break
+                k = first_insn(j + 1)
+                if k < len(lines) and lines[k].startswith("s_branch "):
+                    tgt = lines[k].split(" ", 1)[1]
+                else:
+                    break
+            out[i] = f"{op} {tgt}"
+    res = []
+    n = len(out)
+    for i, ln in enumerate(out):
+        if ln.startswith("s_branch "):
+            tgt = ln.split(" ", 1)[1]
+            j = i + 1
+            labels = set()
+            while j < n and out[j].endswith(":"):
+                labels.add(out[j][:-1])
+                j += 1
+            if tgt in labels:
+                continue
+        if ln == "s_nop 1" and res and res[-1].startswith("v_cmp") and i + 1 < n \
+                and out[i + 1].startswith(_VCMP_CONSUMERS):
+            continue
+        res.append(ln)
+    return res
 
 
 def _hlabel(n, bank):
@@ -1423,6 +1471,8 @@ def gen(mode="interp"):
         g.label("Lbody_%=")
         g(MARKER)
         g.label("Ldone_%=")
+    if mode == "interp":
+        body[:] = tidy_jumps(body)
     return body
 
 

@@ -58,6 +58,7 @@ def c5(request, dev):
     if not jit.is_cached([prog], "x", BENCH_WAVES, BENCH_LDS):
         pytest.fail("C5 specialised kernel not in build/jit: run __graft_entry__.build() first")
     special = dev.load(prog)
+    _log(f"density {request.param}: program loaded ({dev.engine_of(special)})")
     jit.attach(dev, [special], variants="x", waves=BENCH_WAVES, lds_leaves=BENCH_LDS)
     _log(f"density {request.param}: kernel {special.kernel} attached")
     interp = dev.load(prog)
