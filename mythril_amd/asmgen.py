@@ -578,14 +578,18 @@ def build_handlers():
         g(f"s_or_b64 vcc, vcc, {sr(MSK, 2)}")
         update_alive(g)
 
-    def impeq(g):
-        """alive &= (a == 0) | (b == c) for the current bank's instruction.
-        The premise a is an index equality of a congruence pair, false in
-        every lane for most pairs: then the check holds in every lane and b,
-        c are not read (the interpreter; an assembled body's check runs fold
-        the masks without branches)"""
+    def impeq(g, keyed=False):
+        """alive &= (a == 0) | (b == c) for the current bank's instruction
+        (keyed, CHECK_IMPEQK: (a != imm) | (b == c)).  The premise is an
+        index equality of a congruence pair, false in every lane for most
+        pairs: then the check holds in every lane and b, c are not read (the
+        interpreter; an assembled body's check runs fold the masks without
+        branches)"""
         g.field("a", S[0]), g.field("b", S[1]), g.field("c", S[2])
-        g.op_n(S[0], f"v_cmp_eq_u32_e64 {sr(MSK, 2)}, 0, {{a}}", T, "SRC1")
+        if keyed:
+            g.op_n(S[0], f"v_cmp_ne_u32_e64 {sr(MSK, 2)}, {s(g.CUR + 3)}, {{a}}", T, "SRC1")
+        else:
+            g.op_n(S[0], f"v_cmp_eq_u32_e64 {sr(MSK, 2)}, 0, {{a}}", T, "SRC1")
         skip = g.L("iqskip") if g.chains else None
         if skip:
             g(f"s_cmp_eq_u64 {sr(MSK, 2)}, -1", f"s_cbranch_scc1 {skip}")
@@ -596,24 +600,24 @@ def build_handlers():
         if skip:
             g.label(skip)
 
-    @handler("CHECK_IMPEQ")
-    def _(g):
-        # congruence checks come in runs (a C3 program: 2 176 of its 3 218
+    def impeq_run(g, keyed):
+        # congruence checks come in runs (a C3 program: 2 176 of its 2 747
         # instructions): mw_asm_predecode flags a CHECK_IMPEQ followed by
-        # another with bit 31 of word 3 (its c field sits in the low bits),
-        # and the handler takes the next one itself - a branch not taken per
-        # link instead of a jump per instruction, two links per loop trip,
-        # one per bank, each with its own exit (as W_CDINS chains)
+        # another with bit 31 of word 3 (its c field sits in the low bits; a
+        # CHECK_IMPEQK, whose word 3 is the premise constant: bit 31 of word
+        # 1), and the handler takes the next one itself - a branch not taken
+        # per link instead of a jump per instruction, two links per loop
+        # trip, one per bank, each with its own exit (as W_CDINS chains)
         if not g.chains:
-            impeq(g)
+            impeq(g, keyed)
             return
         nlinks = 1 if DISPATCH == "single" else 2
         tops, exits = [g.L("iqtop") for _ in range(nlinks)], []
         for j in range(nlinks):
             g.label(tops[j])
-            impeq(g)
+            impeq(g, keyed)
             exits.append((g.L("iqlast"), g.CUR))
-            g(f"s_bitcmp1_b32 {s(g.CUR + 3)}, 31", f"s_cbranch_scc0 {exits[-1][0]}")
+            g(f"s_bitcmp1_b32 {s(g.CUR + (1 if keyed else 3))}, 31", f"s_cbranch_scc0 {exits[-1][0]}")
             g.consume()
         g(f"s_branch {tops[0]}")
         for lab, bank in exits[1:]:
@@ -622,6 +626,14 @@ def build_handlers():
             g.next()
         g.label(exits[0][0])
         g.CUR = exits[0][1]
+
+    @handler("CHECK_IMPEQ")
+    def _(g):
+        impeq_run(g, False)
+
+    @handler("CHECK_IMPEQK")
+    def _(g):
+        impeq_run(g, True)
 
     def eq8(g, a, b, dst_v):
         """dst_v = OR of the limb XORs (0 iff equal)"""
@@ -2181,7 +2193,7 @@ def _cdins_chain_static(g, links):
     g.write_w(XR)
 
 
-CHECK_OPS = ("CHECK", "CHECK_IMP", "CHECK_IMPEQ")
+CHECK_OPS = ("CHECK", "CHECK_IMP", "CHECK_IMPEQ", "CHECK_IMPEQK")
 ACC = JMP   # s[92:93]: a check run's lane mask (free in a static body)
 CMSK, CMSK2 = S[0], S[2]   # s[72:73], s[74:75]: a check's consequence mask (scratch in a static body)
 
@@ -2202,7 +2214,7 @@ def _nreg(g, f, tmp):
 
 
 def _check_run_static(g, run):
-    """A run of CHECK / CHECK_IMP / CHECK_IMPEQ as one lane mask: each check's
+    """A run of CHECK / CHECK_IMP / CHECK_IMPEQ(K) as one lane mask: each check's
     condition is formed in SGPRs (premise false OR consequence), ANDed into
     ACC, and ALIVE and the early-exit test are updated once at the end of the
     run.  The SALU combine of check k is emitted after check k+1's compares,
@@ -2221,7 +2233,11 @@ def _check_run_static(g, run):
             g(f"v_cmp_ne_u32_e64 {sr(m, 2)}, 0, {_nreg(g, a, T)}")
             combine = [f"s_and_b64 {sr(ACC, 2)}, {sr(ACC, 2)}, {sr(m, 2)}"]
         else:
-            g(f"v_cmp_eq_u32_e64 {sr(m, 2)}, 0, {_nreg(g, a, T)}")
+            if op == isa.OPCODES["CHECK_IMPEQK"]:   # premise a = imm (VOP3 takes no literal)
+                g(f"v_mov_b32_e32 {v(T + 3)}, {_lit(insn[3])}",
+                  f"v_cmp_ne_u32_e64 {sr(m, 2)}, {v(T + 3)}, {_nreg(g, a, T)}")
+            else:
+                g(f"v_cmp_eq_u32_e64 {sr(m, 2)}, 0, {_nreg(g, a, T)}")
             if op == isa.OPCODES["CHECK_IMP"]:
                 g(f"v_cmp_ne_u32_e64 {sr(mc, 2)}, 0, {_nreg(g, b, T + 1)}")
             else:

@@ -664,12 +664,40 @@ def _fuse_checks(insns: List[MInsn]) -> List[MInsn]:
             continue
         out.append(ins)
         i += 1
+    out = _fuse_keyed_premises(out)
     uses = _uses(out)
     for a, b in zip(out, out[1:]):
         if (a.op == "W_CDINS" and b.op == "W_CDINS" and a.dst is not None and uses.get(a.dst.id, 0) == 1
                 and _is(b.srcs[0], a)):
             a.chain = True
     return out
+
+
+def _fuse_keyed_premises(insns: List[MInsn]) -> List[MInsn]:
+    """``p = (key = K); CHECK_IMPEQ p, x, y`` -> ``CHECK_IMPEQK key, x, y, imm=K``
+    for K < isa.IMPEQK_LIMIT: a congruence premise over an index key
+    (lower._index_key) is compared inside the check, and the premise flags,
+    one per diagonal K - k of the pair grid and live across it, are dropped
+    once no other instruction reads them."""
+    defs = {ins.dst.id: ins for ins in insns if ins.dst is not None}
+    fused = set()
+    out: List[MInsn] = []
+    for ins in insns:
+        p = ins.srcs[0] if ins.op == "CHECK_IMPEQ" else None
+        d = defs.get(p.id) if isinstance(p, VReg) else None
+        if d is not None and d.op == "N_EQN" and d.width <= 32:
+            key, k = d.srcs
+            if isinstance(key, Const):
+                key, k = k, key
+            if isinstance(key, VReg) and isinstance(k, Const) and k.value < isa.IMPEQK_LIMIT:
+                out.append(MInsn("CHECK_IMPEQK", ins.width, None, [key, ins.srcs[1], ins.srcs[2]], imm=k.value))
+                fused.add(d.dst.id)
+                continue
+        out.append(ins)
+    if not fused:
+        return out
+    uses = _uses(out)
+    return [ins for ins in out if ins.dst is None or ins.dst.id not in fused or uses.get(ins.dst.id, 0)]
 
 
 def _schedule_narrow_early(insns: List[MInsn]) -> List[MInsn]:

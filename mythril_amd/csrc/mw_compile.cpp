@@ -662,6 +662,53 @@ struct Compiler {
     return u;
   }
 
+  // p = (key = K); CHECK_IMPEQ p, x, y -> CHECK_IMPEQK key, x, y, imm = K for
+  // K < 2^31 (compiler._fuse_keyed_premises): the premise flags of an index
+  // key (lower._index_key) are dropped once nothing else reads them
+  std::vector<Insn> fuse_keyed_premises(const std::vector<Insn>& in) {
+    std::vector<int> def(vcls.size(), -1);
+    for (size_t i = 0; i < in.size(); ++i)
+      if (in[i].dst >= 0) def[in[i].dst] = (int)i;
+    std::vector<char> fused(vcls.size(), 0);
+    bool any = false;
+    std::vector<Insn> out;
+    out.reserve(in.size());
+    for (const Insn& x : in) {
+      if (x.op == MW_CHECK_IMPEQ && is_v(x.s[0]) && def[x.s[0].v] >= 0) {
+        const Insn& d = in[def[x.s[0].v]];
+        Opnd key = d.s[0], k = d.s[1];
+        if (key.kind == O_CONST) std::swap(key, k);
+        if (d.op == MW_N_EQN && d.width <= 32 && is_v(key) && k.kind == O_CONST && k_small31(kv[k.v])) {
+          Insn c;
+          c.op = MW_CHECK_IMPEQK;
+          c.width = x.width;
+          c.ns = 3;
+          c.s[0] = key;
+          c.s[1] = x.s[1];
+          c.s[2] = x.s[2];
+          c.imm = kv[k.v].l[0];
+          out.push_back(c);
+          fused[d.dst] = 1;
+          any = true;
+          continue;
+        }
+      }
+      out.push_back(x);
+    }
+    if (!any) return out;
+    std::vector<int> uses = use_counts(out);
+    std::vector<Insn> kept;
+    kept.reserve(out.size());
+    for (const Insn& x : out)
+      if (x.dst < 0 || !fused[x.dst] || uses[x.dst]) kept.push_back(x);
+    return kept;
+  }
+  static bool k_small31(const K256& v) {
+    for (int q = 1; q < 8; ++q)
+      if (v.l[q]) return false;
+    return v.l[0] < 0x80000000u;
+  }
+
   std::vector<Insn> fuse_checks(const std::vector<Insn>& in0) {
     std::vector<int> uses = use_counts(in0);
     std::vector<Insn> a1;
@@ -730,6 +777,7 @@ struct Compiler {
       out.push_back(x);
       i += 1;
     }
+    out = fuse_keyed_premises(out);
     uses = use_counts(out);
     for (size_t i = 0; i + 1 < out.size(); ++i) {
       Insn& a = out[i];

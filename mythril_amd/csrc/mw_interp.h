@@ -187,6 +187,30 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
         break;
       }
+      case MW_CHECK_IMPEQK: {  // (N[a] = imm) => (b = c): a keyed congruence premise, runs as above
+#define MW_IMPEQK_STEP(fa, fb, fc, k)                                         \
+  do {                                                                        \
+    u32 _p, _b, _c;                                                           \
+    MW_FETCH_N(fa, _p);                                                       \
+    MW_FETCH_N(fb, _b);                                                       \
+    MW_FETCH_N(fc, _c);                                                       \
+    alive = alive && (_p != (k) || _b == _c);                                 \
+  } while (0)
+        MW_IMPEQK_STEP(oa, ob, oc, imm);
+        while ((n0 & 0xffu) == MW_CHECK_IMPEQK) {
+          asm volatile("" ::: "memory");
+          const u32x8v q = *(kptr8)(code + pc + 4);
+          MW_IMPEQK_STEP(n1 >> 16, n2 & 0xffffu, n2 >> 16, n3);
+          pc += 4;
+          if ((q[0] & 0xffu) != MW_CHECK_IMPEQK) { n0 = q[0]; n1 = q[1]; n2 = q[2]; n3 = q[3]; break; }
+          MW_IMPEQK_STEP(q[1] >> 16, q[2] & 0xffffu, q[2] >> 16, q[3]);
+          pc += 4;
+          n0 = q[4]; n1 = q[5]; n2 = q[6]; n3 = q[7];
+        }
+#undef MW_IMPEQK_STEP
+        if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
+        break;
+      }
       case MW_CHECK_IMPEQW: {
         u32 p;
         MW_FETCH_N(oa, p);

@@ -66,6 +66,7 @@ enum mw_opcode {
   MW_CHECK_IMP = 12,  // alive &= (N[a] == 0) | (N[b] != 0): a congruence conjunct a => b in one dispatch
   MW_CHECK_IMPEQ = 13,   // alive &= (N[a] == 0) | (N/K[b] == N/K[c])   (a => (b = c), narrow)
   MW_CHECK_IMPEQW = 14,  // alive &= (N[a] == 0) | (W/K[b] == W/K[c])   (a => (b = c), wide)
+  MW_CHECK_IMPEQK = 15,  // alive &= (N[a] != imm) | (N/K[b] == N/K[c]) (a keyed congruence premise, lower._index_key)
 
   // wide: W[dst] = f(W/K a, W/K b) at `width`
   MW_W_ADD = 16, MW_W_SUB = 17, MW_W_MUL = 18, MW_W_AND = 19, MW_W_OR = 20,

@@ -39,6 +39,7 @@ bool op_shape(u32 op, OpShape& s) {
     case MW_CHECK_IMP: s.a = 2; s.b = 2; return true;
     case MW_CHECK_IMPEQ: s.a = 2; s.b = 2; s.c = 2; return true;
     case MW_CHECK_IMPEQW: s.a = 2; s.b = 1; s.c = 1; return true;
+    case MW_CHECK_IMPEQK: s.a = 2; s.b = 2; s.c = 2; return true;
     case MW_W_CDINS: s.dst = 3; s.a = 1; s.b = 1; s.c = 1; s.wide = true; return true;
     case MW_LEAF_W: s.dst = 3; return true;
     case MW_LEAF_N: s.dst = 4; return true;
@@ -140,7 +141,7 @@ int mg_validate_desc(const mg_prog_desc* d) {
     if (s.dst == 3 || s.dst == 4 || s.a || s.b) {
       const u32 maxw = (s.wide || s.dst == 3) ? 256u : 32u;
       if (op != MW_CHECK && op != MW_CHECK_IMP && op != MW_CHECK_IMPEQ && op != MW_CHECK_IMPEQW &&
-          op != MW_STORE_W && op != MW_STORE_N && op != MW_SPILL_W &&
+          op != MW_CHECK_IMPEQK && op != MW_STORE_W && op != MW_STORE_N && op != MW_SPILL_W &&
           op != MW_SPILL_N && op != MW_FILL_W && op != MW_FILL_N && op != MW_MOV_W && op != MW_MOV_N &&
           op != MW_LEAF_W && op != MW_LEAF_N && (w < 1 || w > maxw))
         return fail(MG_E_PROG, "bad width " + std::to_string(w) + " at instruction " + std::to_string(i));
@@ -298,6 +299,11 @@ int mw_asm_predecode_layout(const u32* code, size_t nwords, const u32* consts, s
     // a CHECK_IMPEQ followed by another: the handler takes that one itself
     // (a chain, mythril_amd/asmgen.py), bit 31 above its c field
     if (op == MW_CHECK_IMPEQ && i + 7 < nwords && (code[i + 4] & 0xffu) == MW_CHECK_IMPEQ) O[3] |= 0x80000000u;
+    // CHECK_IMPEQK: word 3 is the premise constant, so its chain flag is bit
+    // 31 of word 1 (the width above a is not read by its handler)
+    if (op == MW_CHECK_IMPEQK)
+      O[1] = (O[1] & 0x7fffffffu) |
+             (i + 7 < nwords && (code[i + 4] & 0xffu) == MW_CHECK_IMPEQK ? 0x80000000u : 0u);
     if (op == MW_N_ADD || op == MW_N_SUB || op == MW_N_MUL || op == MW_N_NOT)
       O[3] = w >= 32u ? 0xffffffffu : (1u << w) - 1u;
   }

@@ -123,7 +123,7 @@ def _prepare(conjuncts, ctx, use_pools, timings) -> Query:
     t1 = time.perf_counter()
     # low.nodes: the topo of the flattened conjuncts, computed once by
     # lower_constraints; harvest collects the var leaves in the same loop
-    specs = harvest(low.conjuncts, None, nodes=low.nodes,
+    specs = harvest(low.harvest_conjuncts or low.conjuncts, None, nodes=low.harvest_nodes or low.nodes,
                     memo=ctx.__dict__.setdefault("_harvest", {}) if getattr(ctx, "long_lived", False) else None) \
         if use_pools else {}
     t2 = time.perf_counter()

@@ -22,7 +22,7 @@ LEAF_WIDTH, LEAF_KIND, LEAF_ID, LEAF_SHIFT, LEAF_BITS, LEAF_POOL, LEAF_INROW = r
 OPCODES = {
     "END": 0, "CHECK": 1, "LEAF_W": 2, "LEAF_N": 3, "STORE_W": 4, "STORE_N": 5,
     "SPILL_W": 6, "FILL_W": 7, "MOV_W": 8, "MOV_N": 9, "SPILL_N": 10, "FILL_N": 11, "CHECK_IMP": 12,
-    "CHECK_IMPEQ": 13, "CHECK_IMPEQW": 14,
+    "CHECK_IMPEQ": 13, "CHECK_IMPEQW": 14, "CHECK_IMPEQK": 15,
     "W_ADD": 16, "W_SUB": 17, "W_MUL": 18, "W_AND": 19, "W_OR": 20, "W_XOR": 21, "W_NOT": 22,
     "W_SHL": 23, "W_LSHR": 24, "W_ASHR": 25,
     "W_UDIV": 26, "W_UREM": 27, "W_SDIV": 28, "W_SREM": 29, "W_SMOD": 30,
@@ -43,6 +43,7 @@ OPCODES = {
 SHAPES = {
     "END": (None, []), "CHECK": (None, ["N"]), "CHECK_IMP": (None, ["N", "N"]),
     "CHECK_IMPEQ": (None, ["N", "N", "N"]), "CHECK_IMPEQW": (None, ["N", "W", "W"]),
+    "CHECK_IMPEQK": (None, ["N", "N", "N"]),   # (N[a] = imm) => (b = c)
     "W_CDINS": ("W", ["W", "W", "W"]),
     "LEAF_W": ("W", []), "LEAF_N": ("N", []),
     "STORE_W": (None, ["W"]), "STORE_N": (None, ["N"]),
@@ -70,6 +71,7 @@ FLAG_STOP_AFTER_HIT = 2
 
 
 # instruction flags, w0 bits [15:8] (csrc/mw_prog.h)
+IMPEQK_LIMIT = 1 << 31   # CHECK_IMPEQK premise constants (bit 31 of the word is free for a chain flag)
 FLAG_CHAIN = 1   # W_CDINS: result consumed only by the next W_CDINS's acc (kept in registers)
 
 
@@ -108,7 +110,7 @@ def encode(op: str, width: int = 0, dst: int = 0, a: int = 0, b: int = 0, c: int
 # tools/gen_asm_interp.py) has a handler for these opcodes and leaf kinds; a
 # program using anything else is searched by the compiled interpreter.
 ASM_OPCODES = [
-    "END", "CHECK", "CHECK_IMP", "CHECK_IMPEQ", "CHECK_IMPEQW", "LEAF_W", "LEAF_N", "MOV_W", "MOV_N",
+    "END", "CHECK", "CHECK_IMP", "CHECK_IMPEQ", "CHECK_IMPEQW", "CHECK_IMPEQK", "LEAF_W", "LEAF_N", "MOV_W", "MOV_N",
     "SPILL_W", "FILL_W", "SPILL_N", "FILL_N",
     "W_ADD", "W_SUB", "W_AND", "W_OR", "W_XOR", "W_NOT", "W_ITE", "W_SHLI", "W_LSHRI", "W_ZEXTN", "W_INSN",
     "W_CDINS", "W_MUL",

@@ -48,6 +48,7 @@ from dataclasses import dataclass, field
 from operator import attrgetter
 from typing import Dict, List, Optional, Tuple
 
+from . import isa
 from .compiler import Unsupported, _flatten
 from .ir import BOOL, Ctx, Node, topo
 
@@ -71,6 +72,9 @@ class Lowered:
     congruence: int = 0
     flat: List[Node] = field(default_factory=list)    # conjuncts with top-level `and` flattened, `true` dropped
     nodes: List[Node] = field(default_factory=list)   # topo(flat): every node the search program evaluates
+    # what harvest reads (the congruence premises unkeyed, _Rewriter.keyed): None = conjuncts / nodes
+    harvest_conjuncts: Optional[List[Node]] = None
+    harvest_nodes: Optional[List[Node]] = None
 
 
 class _Rewriter:
@@ -565,6 +569,57 @@ class _Rewriter:
                     out.append(r)
         return out
 
+    def keyed(self, cong: List[Node]) -> List[Node]:
+        """The congruence conjuncts with their index premises keyed: a wide
+        index against a constant (base = K - k, the bytes of an ABI word at
+        a symbolic calldata offset) becomes a 32-bit compare of the base's
+        index key with K - k + KEY_BIAS (_index_key), for bases with at least
+        KEY_MIN such premises (single-argument pairs: a premise that is an
+        `and` is not one flag the check can take): one narrow term per base instead of a wide
+        compare per diagonal of the pair grid, which compiler._fuse_checks
+        folds into the check itself (CHECK_IMPEQK), so no premise flag stays
+        live across the grid.  The harvest reads the unkeyed conjuncts."""
+        c = self.ctx
+        count: Dict[int, int] = {}
+        for n in cong:
+            bk = _wide_index_eq(n.args[0]) if n.op == "=>" else None
+            if bk is not None:
+                count[bk[0].id] = count.get(bk[0].id, 0) + 1
+        if not count or max(count.values()) < KEY_MIN:
+            return cong
+        out = []
+        for n in cong:
+            if n.op == "=>":
+                k = self._keyed_eq(n.args[0], count)
+                if k is not n.args[0]:
+                    n = c.app("=>", k, n.args[1])
+            out.append(n)
+        return out
+
+    def _keyed_eq(self, e: Node, count: Dict[int, int]) -> Node:
+        bk = _wide_index_eq(e)
+        if bk is None or count[bk[0].id] < KEY_MIN:
+            return e
+        b, k = bk
+        v = (k + KEY_BIAS) & ((1 << b.width) - 1)
+        if v >= KEY_LIMIT:
+            return e
+        return self.ctx.app("=", self._index_key(b), self.ctx.const(v, 32))
+
+    def _index_key(self, b: Node) -> Node:
+        """ite(hi(b + KEY_BIAS) = 0, lo32(b + KEY_BIAS), 0xffffffff): for
+        e < KEY_LIMIT, key = e holds exactly when b = e - KEY_BIAS (mod 2^w)
+        (e never equals the all-ones sentinel); the bias covers K < k too."""
+        key = self.__dict__.setdefault("_keys", {})
+        got = key.get(b.id)
+        if got is None:
+            c, w = self.ctx, b.width
+            s = c.app("bvadd", b, c.const(KEY_BIAS, w))
+            got = c.app("ite", c.app("=", self.extract(s, w - 1, 32), c.const(0, w - 32)),
+                        self.extract(s, 31, 0), c.const(0xFFFFFFFF, 32))
+            key[b.id] = got
+        return got
+
     def _pair(self, t: AckLeaf, u: AckLeaf) -> Optional[Node]:
         c = self.ctx
         if all(a.op == "const" for a in t.args) and all(a.op == "const" for a in u.args):
@@ -663,7 +718,10 @@ def _offset(n: Node):
     return n, 0
 
 
-PAIR_TILE = 12   # symbolic cells kept resident while the concrete cells stream past
+KEY_BIAS = 1 << 16      # _index_key: K - k + KEY_BIAS >= 0 for offsets k < 2^16
+KEY_LIMIT = isa.IMPEQK_LIMIT   # premise constants the fused check carries (CHECK_IMPEQK)
+KEY_MIN = 8             # premises a base needs before it is keyed (a key costs four instructions)
+PAIR_TILE = 32   # symbolic cells kept resident while the concrete cells stream past
 
 
 def _pair_order(reads):
@@ -672,7 +730,11 @@ def _pair_order(reads):
     pairs in tiles of PAIR_TILE symbolic reads.  Within a tile each concrete
     cell is used PAIR_TILE times in a row and the tile's symbolic cells stay
     in registers, instead of the narrow file refilling one of 32+ live cells at
-    every pair (C3: 2 371 -> ~300 fills)."""
+    every pair (C3: 2 371 -> ~300 fills).  With keyed premises (no premise
+    flags live across the grid, _Rewriter.keyed) one tile holds an ABI word's
+    32 bytes and each concrete cell dies after its 32 pairs (C3: 41 fills, one
+    per spilled word; tile 12: 80; LASER corpus 153.5 k -> 152.8 k
+    instructions)."""
     sym = [r for r in reads if not all(a.op == "const" for a in r.args)]
     con = [r for r in reads if all(a.op == "const" for a in r.args)]
     out = [(sym[i], sym[j]) for i in range(len(sym)) for j in range(i + 1, len(sym))]
@@ -680,6 +742,18 @@ def _pair_order(reads):
         tile = sym[k:k + PAIR_TILE]
         out += [(c, s) for c in con for s in tile]
     return out
+
+
+def _wide_index_eq(e: Node):
+    """(base, K) for e = (base = K) with a symbolic base of 33..MAXW bits, else None"""
+    if e.op != "=" or len(e.args) != 2:
+        return None
+    b, k = e.args
+    if b.op == "const":
+        b, k = k, b
+    if k.op != "const" or b.op == "const" or not 32 < b.width <= MAXW:
+        return None
+    return b, k.val
 
 
 def _fold_offsets(c: Ctx, x: Node, y: Node):
@@ -740,7 +814,12 @@ def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
     if nodes and max(map(_width, nodes)) > MAXW:   # every consumer chunks its wide operands; none may remain
         n = next(n for n in nodes if n.width > MAXW)
         raise Unsupported(f"{n.width}-bit {n.op} outside the legalised vocabulary")
-    return Lowered(out + cong, rw.ack, len(cong), flat, nodes)
+    keyed = rw.keyed(cong)
+    if keyed is cong:
+        return Lowered(out + cong, rw.ack, len(cong), flat, nodes)
+    kflat = _flatten(out + keyed)
+    return Lowered(out + keyed, rw.ack, len(cong), kflat, topo(kflat),
+                   harvest_conjuncts=out + cong, harvest_nodes=nodes)
 
 
 def needs_lowering(conjuncts: List[Node]) -> bool:

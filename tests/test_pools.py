@@ -122,10 +122,41 @@ def test_congruence_conjuncts_fuse_to_one_check():
     q = prepare(s.asserts, s.ctx)
     ops = [int(w) & 0xFF for w in q.program.code.reshape(-1, 4)[:, 0]]
     fused = ops.count(isa.OPCODES["CHECK_IMP"]) + ops.count(isa.OPCODES["CHECK_IMPEQ"]) + \
-        ops.count(isa.OPCODES["CHECK_IMPEQW"])
+        ops.count(isa.OPCODES["CHECK_IMPEQW"]) + ops.count(isa.OPCODES["CHECK_IMPEQK"])
     assert fused >= 2000
-    assert ops.count(isa.OPCODES["CHECK_IMPEQ"]) >= 2000   # (i = j) => (v = w): one dispatch
+    # (key = K) => (v = w): one dispatch, the premise compared inside the check
+    # (lower._Rewriter.keyed): no premise flags, so no wide compare per diagonal
+    assert ops.count(isa.OPCODES["CHECK_IMPEQK"]) >= 2000
+    assert ops.count(isa.OPCODES["N_EQ"]) < 60
+    assert q.program.n_spill <= 48
     assert all(not i.op.startswith("CHECK_IMP") for i in q.program.machine_ir())
+
+
+def test_index_keys_are_exact():
+    """lower._index_key: for a premise constant e < KEY_LIMIT, key(b) = e holds
+    exactly when b = e - KEY_BIAS (mod 2^w), at the wrap-around, at the
+    sentinel's neighbours and for random words (the keyed premise replaces
+    b = K - k in the congruence conjuncts)."""
+    import random
+    from mythril_amd.ir import Ctx
+    from mythril_amd.lower import _Rewriter, KEY_BIAS, KEY_LIMIT
+    from oracle.dag_eval import eval_nodes
+    rng = random.Random(7)
+    c = Ctx()
+    w = 256
+    b = c.var("b", w)
+    rw = _Rewriter(c)
+    key = rw._index_key(b)
+    M = (1 << w) - 1
+    for d in (0, 1, 4, 31, 1234, M, M - 30, KEY_LIMIT - KEY_BIAS - 1):
+        e = (d + KEY_BIAS) & M
+        if e >= KEY_LIMIT:
+            continue
+        prem = c.app("=", key, c.const(e, 32))
+        for v in (d, (d + 1) & M, (d - 1) & M, d ^ (1 << 40), (d + (1 << 32)) & M, M, 0,
+                  (0xFFFFFFFF - KEY_BIAS) & M, rng.getrandbits(w)):
+            vals = eval_nodes([prem], {"b": v})
+            assert bool(vals[prem.id]) == (v == d), (d, v)
 
 
 def test_check_imp_verdicts_all_input_combinations():
@@ -158,5 +189,5 @@ def test_check_imp_verdicts_all_input_combinations():
         got, _ = emu_eval(prog, pack_inputs(prog, models), len(models))
         assert list(map(int, got)) == want, conj
         if not any(k.args[0].op == "const" or k.args[1].op == "const" for k in conj):
-            assert ops & {isa.OPCODES["CHECK_IMP"], isa.OPCODES["CHECK_IMPEQ"], isa.OPCODES["CHECK_IMPEQW"]}, conj
+            assert ops & {isa.OPCODES[n] for n in ("CHECK_IMP", "CHECK_IMPEQ", "CHECK_IMPEQW", "CHECK_IMPEQK")}, conj
     assert [int(all(eval_nodes(shapes[0], m)[k.id] for k in shapes[0])) for m in models] == [1, 1, 0, 1]
