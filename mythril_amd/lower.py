@@ -87,6 +87,9 @@ class _Rewriter:
         self.inner_apply: Dict[int, tuple] = {}   # leaf id of f(x) -> (f, x)
         self.seg_memo: Dict[int, List[Node]] = {}
         self.chunk_memo: Dict[int, List[Node]] = {}
+        # leaves a top-level conjunct fixes (leaf = K): the congruence reads K
+        # in their place (equivalent under that conjunct, candidate by candidate)
+        self.pins: Dict[str, Node] = {}
 
     # -- extract simplification (pushes extracts towards leaves) ------------------
     def extract(self, x: Node, hi: int, lo: int) -> Node:
@@ -557,14 +560,17 @@ class _Rewriter:
         for (kind, base), reads in self.by_base.items():
             for t, u in _pair_order(reads):
                 if memo is not None:
-                    got = memo.get((t.name, u.name), 0)
+                    pt, pu = self.pins.get(t.name), self.pins.get(u.name)
+                    key = (t.name, u.name) if pt is None and pu is None else \
+                        (t.name, u.name, pt and pt.val, pu and pu.val)
+                    got = memo.get(key, 0)
                     if got != 0:
                         if got is not None:
                             out.append(got)
                         continue
                 r = self._pair(t, u)
                 if memo is not None:
-                    memo[(t.name, u.name)] = r
+                    memo[key] = r
                 if r is not None:
                     out.append(r)
         return out
@@ -574,22 +580,22 @@ class _Rewriter:
         index against a constant (base = K - k, the bytes of an ABI word at
         a symbolic calldata offset) becomes a 32-bit compare of the base's
         index key with K - k + KEY_BIAS (_index_key), for bases with at least
-        KEY_MIN such premises (single-argument pairs: a premise that is an
-        `and` is not one flag the check can take): one narrow term per base instead of a wide
+        KEY_MIN such premises (single-argument pairs of narrow values,
+        _narrow_imp): one narrow term per base instead of a wide
         compare per diagonal of the pair grid, which compiler._fuse_checks
         folds into the check itself (CHECK_IMPEQK), so no premise flag stays
         live across the grid.  The harvest reads the unkeyed conjuncts."""
         c = self.ctx
         count: Dict[int, int] = {}
         for n in cong:
-            bk = _wide_index_eq(n.args[0]) if n.op == "=>" else None
+            bk = _wide_index_eq(n.args[0]) if _narrow_imp(n) else None
             if bk is not None:
                 count[bk[0].id] = count.get(bk[0].id, 0) + 1
         if not count or max(count.values()) < KEY_MIN:
             return cong
         out = []
         for n in cong:
-            if n.op == "=>":
+            if _narrow_imp(n):
                 k = self._keyed_eq(n.args[0], count)
                 if k is not n.args[0]:
                     n = c.app("=>", k, n.args[1])
@@ -620,16 +626,25 @@ class _Rewriter:
             key[b.id] = got
         return got
 
+    def _value(self, t: AckLeaf) -> Node:
+        if t.value is not None:
+            return t.value
+        pin = self.pins.get(t.name)
+        return pin if pin is not None else self.wide_var(t.name, t.width)
+
     def _pair(self, t: AckLeaf, u: AckLeaf) -> Optional[Node]:
         c = self.ctx
         if all(a.op == "const" for a in t.args) and all(a.op == "const" for a in u.args):
             return None   # distinct concrete cells: nothing to relate
         if any(_never_equal(x, y) for x, y in zip(t.args, u.args)):
             return None   # e.g. cells base+3 and base+7 of one symbolic offset
-        same = [self.eq(*_fold_offsets(c, x, y)) for x, y in zip(t.args, u.args)]
+        # an argument both reads share (Power(256, k) and Power(256, i): the same
+        # constant node) adds nothing to the premise
+        same = [self.eq(*_fold_offsets(c, x, y)) for x, y in zip(t.args, u.args) if x is not y]
+        vt, vu = self._value(t), self._value(u)
+        if not same:
+            return self.eq(vt, vu)
         prem = c.app("and", *same) if len(same) > 1 else same[0]
-        vt = t.value if t.value is not None else self.wide_var(t.name, t.width)
-        vu = u.value if u.value is not None else self.wide_var(u.name, u.width)
         return c.app("=>", prem, self.eq(vt, vu))
 
 
@@ -744,6 +759,33 @@ def _pair_order(reads):
     return out
 
 
+def _pins(conjuncts: List[Node], ack: Dict[str, AckLeaf]) -> Dict[str, Node]:
+    """{read name: K} for the top-level conjuncts (read = K) over a read's
+    value leaf (Mythril's Power(256, k) = 256^k, keccak values of constant
+    preimages): the congruence compares K instead of keeping the leaf live
+    from that conjunct to the pair grid at the end of the program."""
+    pins: Dict[str, Node] = {}
+    for cj in _flatten(conjuncts):
+        if cj.op != "=" or len(cj.args) != 2:
+            continue
+        x, k = cj.args
+        if x.op == "const":
+            x, k = k, x
+        if k.op == "const" and x.op == "var" and x.name in ack and x.name not in pins:
+            pins[x.name] = k
+    return pins
+
+
+def _narrow_imp(n: Node) -> bool:
+    """n = (p => (x = y)) over narrow x, y: the shape CHECK_IMPEQK takes (a
+    keyed premise before a wide compare would stay a flag, and its premise
+    constant one of the asm interpreter's few narrow constant registers)"""
+    if n.op != "=>":
+        return False
+    q = n.args[1]
+    return q.op == "=" and len(q.args) == 2 and q.args[0].width <= 32
+
+
 def _wide_index_eq(e: Node):
     """(base, K) for e = (base = K) with a symbolic base of 33..MAXW bits, else None"""
     if e.op != "=" or len(e.args) != 2:
@@ -808,6 +850,7 @@ def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
         rw.ack = ack
         for al in ack.values():
             rw.by_base.setdefault((al.kind, al.base), []).append(al)
+    rw.pins = _pins(out, rw.ack)
     cong = rw.congruence(ctx.__dict__.setdefault("_pairs", {}) if lowered is not None else None)
     flat = _flatten(out + cong)
     nodes = topo(flat)
