@@ -293,3 +293,20 @@ def test_predecode_chains_check_impeq_runs():
     o, _ = _predecode(code, [0])
     assert [int(x) >> 31 for x in o[:, 3]] == [0, 1, 1, 0, 0, 0, 0]
     assert [int(x) & 0xFFFF for x in o[1:4, 3]] == [5, 7, 9]      # c in the low bits, as before
+
+
+def test_predecode_chains_keyed_checks():
+    """CHECK_IMPEQK keeps its premise constant whole in word 3: a keyed check
+    followed by another gets bit 31 of word 1 instead (above the width, which
+    its handler does not read), and a following unkeyed check ends the chain."""
+    e = isa.encode
+    none = isa.encode_dst(None)
+    K = 0x7FFFFFFF
+    code = (e("CHECK_IMPEQK", 8, none, 1, 4, 5, imm=0x10020) + e("CHECK_IMPEQK", 255, none, 1, 6, 7, imm=K)
+            + e("CHECK_IMPEQK", 200, none, 1, 8, 9, imm=3) + e("CHECK_IMPEQ", 0, none, 1, 2, 3)
+            + e("CHECK_IMPEQK", 8, none, 1, 2, 3, imm=4) + e("END", 0, none))
+    o, _ = _predecode(code, [0])
+    assert [int(o[i, 1]) >> 31 for i in (0, 1, 2, 4)] == [1, 1, 0, 0]   # (the other rows' width bits)
+    assert [int(x) for x in o[:3, 3]] == [0x10020, K, 3]         # the premise constants, whole
+    assert [int(x) & 0xFF for x in o[:3, 1]] == [1, 1, 1]           # the key's register
+    assert [int(x) for x in o[:3, 2]] == [4 | 5 << 16, 6 | 7 << 16, 8 | 9 << 16]

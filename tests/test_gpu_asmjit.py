@@ -174,8 +174,38 @@ def test_check_runs_with_true_premises(dev):
     q = prepare(s.asserts, s.ctx)
     p = q.program
     ops = [int(w) & 0xFF for w in p.code[0::4]]
+    # round 5: the congruence premises are keyed (lower._Rewriter.keyed), the
+    # runs CHECK_IMPEQK; the unkeyed CHECK_IMPEQ runs are test_check_runs_unkeyed's
+    imp = isa.OPCODES["CHECK_IMPEQK"]
+    assert any(a == b == imp for a, b in zip(ops, ops[1:])), "no run of CHECK_IMPEQK"
+    n = 1 << 14
+    di, da = pair(dev, p)
+    try:
+        va, _ = dev.eval_generated(da, DEFAULT_SEED, 0, n, trace=False)
+        vi, _ = dev.eval_generated(di, DEFAULT_SEED, 0, n, trace=False)
+    finally:
+        di.free()
+        da.free()
+    _, _, vo = cdag.evaluate(q.lowered.conjuncts, DEFAULT_SEED, 0, n, want_verdict=True,
+                             specs=cdag.program_specs(p))
+    assert np.array_equal(vi.astype(np.uint8), vo)
+    assert np.array_equal(va.astype(np.uint8), vo), int(np.count_nonzero(va.astype(np.uint8) != vo))
+
+
+def test_check_runs_unkeyed(dev, monkeypatch):
+    """The same query with keying off (lower.KEY_MIN out of reach): runs of
+    CHECK_IMPEQ over premise flags, on both engines, against the oracle."""
+    from mythril_amd import lower
+    monkeypatch.setattr(lower, "KEY_MIN", 1 << 30)
+    f = os.path.join(os.path.dirname(__file__), "golden", "laser",
+                     "environments_t1_batch_transfer_q09_unknown.smt2.gz")
+    s = parse_file(f)
+    q = prepare(s.asserts, s.ctx)
+    p = q.program
+    ops = [int(w) & 0xFF for w in p.code[0::4]]
     imp = isa.OPCODES["CHECK_IMPEQ"]
     assert any(a == b == imp for a, b in zip(ops, ops[1:])), "no run of CHECK_IMPEQ"
+    assert isa.OPCODES["CHECK_IMPEQK"] not in ops
     n = 1 << 14
     di, da = pair(dev, p)
     try:
@@ -252,7 +282,7 @@ def test_asmjit_long_check_runs(dev, seed):
         q = prepare(conj, c, use_pools=pools)
         p = q.program
         ops = [int(w) & 0xFF for w in p.code[0::4]]
-        checks = {isa.OPCODES[n] for n in ("CHECK", "CHECK_IMP", "CHECK_IMPEQ")}
+        checks = {isa.OPCODES[n] for n in ("CHECK", "CHECK_IMP", "CHECK_IMPEQ", "CHECK_IMPEQK")}
         run = best = 0
         for o in ops:
             run = run + 1 if o in checks else 0
