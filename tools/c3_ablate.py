@@ -42,12 +42,12 @@ def main():
     s = parse_file(a.file)
     p = prepare(s.asserts, s.ctx).program
     ops = sorted({INV[int(r[0]) & 0xFF] for r in p.code.reshape(-1, 4)})
-    checks = {"CHECK", "CHECK_IMP", "CHECK_IMPEQ", "CHECK_IMPEQW"}
+    checks = {"CHECK", "CHECK_IMP", "CHECK_IMPEQ", "CHECK_IMPEQW", "CHECK_IMPEQK"}
     spills = {"SPILL_W", "SPILL_N", "FILL_W", "FILL_N"}
     leaves = {"LEAF_W", "LEAF_N", "W_CDINS"}
     variants = {
         "full": set(),
-        "no_impeq": {"CHECK_IMPEQ"},
+        "no_impeq": {"CHECK_IMPEQ", "CHECK_IMPEQK"},
         "no_checks": checks,
         "no_spills": spills,
         "no_checks_spills": checks | spills,

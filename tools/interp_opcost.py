@@ -86,6 +86,7 @@ def variants(p):
         "CHECK": [e("CHECK", 1, 0, 4)],
         "CHECK_IMPEQ_regs": [e("CHECK_IMPEQ", 8, 0, 4, 1, 2)],
         "CHECK_IMPEQ_const": [e("CHECK_IMPEQ", 8, 0, 4, 1, kn(p))],
+        "CHECK_IMPEQK_regs": [e("CHECK_IMPEQK", 8, 0, 4, 1, 2, imm=0x10000)],
         "N_ADD": [e("N_ADD", 8, 5, 0, 1)],
         "N_EQN": [e("N_EQN", 1, 5, 0, 1)],
         "MOV_N": [e("MOV_N", 8, 5, 1)],
