@@ -575,42 +575,56 @@ class _Rewriter:
                     out.append(r)
         return out
 
-    def keyed(self, cong: List[Node]) -> List[Node]:
+    def keyed(self, cong: List[Node], memo: Optional[dict] = None) -> List[Node]:
         """The congruence conjuncts with their index premises keyed: a wide
         index against a constant (base = K - k, the bytes of an ABI word at
         a symbolic calldata offset) becomes a 32-bit compare of the base's
         index key with K - k + KEY_BIAS (_index_key), for bases with at least
         KEY_MIN such premises (single-argument pairs of narrow values,
-        _narrow_imp): one narrow term per base instead of a wide
-        compare per diagonal of the pair grid, which compiler._fuse_checks
-        folds into the check itself (CHECK_IMPEQK), so no premise flag stays
-        live across the grid.  The harvest reads the unkeyed conjuncts."""
-        c = self.ctx
+        _narrow_imp): one narrow term per base instead of a wide compare per
+        diagonal of the pair grid, which compiler._fuse_checks folds into the
+        check itself (CHECK_IMPEQK), so no premise flag stays live across the
+        grid.  The harvest reads the unkeyed conjuncts.
+        memo (a long-lived context's): per conjunct id, (base, K) or None and
+        its keyed form - the same in every set whose count keys that base."""
+        shapes = [self._shape(n, memo) for n in cong]
         count: Dict[int, int] = {}
-        for n in cong:
-            bk = _wide_index_eq(n.args[0]) if _narrow_imp(n) else None
-            if bk is not None:
-                count[bk[0].id] = count.get(bk[0].id, 0) + 1
+        for sh in shapes:
+            if sh is not None:
+                bid = sh[0].id
+                count[bid] = count.get(bid, 0) + 1
         if not count or max(count.values()) < KEY_MIN:
             return cong
+        c = self.ctx
         out = []
-        for n in cong:
-            if _narrow_imp(n):
-                k = self._keyed_eq(n.args[0], count)
-                if k is not n.args[0]:
-                    n = c.app("=>", k, n.args[1])
+        for n, sh in zip(cong, shapes):
+            if sh is not None and count[sh[0].id] >= KEY_MIN:
+                got = memo.get(("k", n.id)) if memo is not None else None
+                if got is None:
+                    got = self._keyed_imp(n, sh)
+                    if memo is not None:
+                        memo[("k", n.id)] = got
+                n = got
             out.append(n)
         return out
 
-    def _keyed_eq(self, e: Node, count: Dict[int, int]) -> Node:
-        bk = _wide_index_eq(e)
-        if bk is None or count[bk[0].id] < KEY_MIN:
-            return e
-        b, k = bk
+    def _shape(self, n: Node, memo: Optional[dict]):
+        if memo is not None:
+            got = memo.get(n.id, 0)
+            if got != 0:
+                return got
+        sh = _wide_index_eq(n.args[0]) if _narrow_imp(n) else None
+        if memo is not None:
+            memo[n.id] = sh
+        return sh
+
+    def _keyed_imp(self, n: Node, sh) -> Node:
+        b, k = sh
         v = (k + KEY_BIAS) & ((1 << b.width) - 1)
         if v >= KEY_LIMIT:
-            return e
-        return self.ctx.app("=", self._index_key(b), self.ctx.const(v, 32))
+            return n
+        c = self.ctx
+        return c.app("=>", c.app("=", self._index_key(b), c.const(v, 32)), n.args[1])
 
     def _index_key(self, b: Node) -> Node:
         """ite(hi(b + KEY_BIAS) = 0, lo32(b + KEY_BIAS), 0xffffffff): for
@@ -852,16 +866,20 @@ def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
             rw.by_base.setdefault((al.kind, al.base), []).append(al)
     rw.pins = _pins(out, rw.ack)
     cong = rw.congruence(ctx.__dict__.setdefault("_pairs", {}) if lowered is not None else None)
-    flat = _flatten(out + cong)
-    nodes = topo(flat)
+    fmain = _flatten(out)
+    seen: set = set()
+    nmain = topo(fmain, seen)
+    keyed = rw.keyed(cong, ctx.__dict__.setdefault("_keyed", {}) if lowered is not None else None)
+    seen_main = set(seen) if keyed is not cong else None
+    fcong = _flatten(cong)
+    flat, nodes = fmain + fcong, nmain + topo(fcong, seen)   # = topo(_flatten(out + cong))
     if nodes and max(map(_width, nodes)) > MAXW:   # every consumer chunks its wide operands; none may remain
         n = next(n for n in nodes if n.width > MAXW)
         raise Unsupported(f"{n.width}-bit {n.op} outside the legalised vocabulary")
-    keyed = rw.keyed(cong)
     if keyed is cong:
         return Lowered(out + cong, rw.ack, len(cong), flat, nodes)
-    kflat = _flatten(out + keyed)
-    return Lowered(out + keyed, rw.ack, len(cong), kflat, topo(kflat),
+    fkeyed = _flatten(keyed)
+    return Lowered(out + keyed, rw.ack, len(cong), fmain + fkeyed, nmain + topo(fkeyed, seen_main),
                    harvest_conjuncts=out + cong, harvest_nodes=nodes)
 
 
