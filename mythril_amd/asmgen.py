@@ -651,6 +651,40 @@ def build_handlers():
           "s_nop 1", f"s_or_b64 vcc, vcc, {sr(MSK, 2)}")
         update_alive(g)
 
+    @handler("CHECK_GRID")
+    def _(g):
+        """One row of a congruence grid (compiler.py _form_grids): j = imm - key;
+        the live lanes with j < n read word T0 + j of their own spill area (LDS
+        [word][lane] below nlds, else the global buffer, as spill_word) and
+        must find b there.  c (raw): T0 = c & 1023, n - 1 = c >> 10 & 31."""
+        g.field("a", S[0]), g.field("b", S[1])
+        done, nolds, noglob = g.L("gd"), g.L("gl"), g.L("gg")
+        if g.static_imm() is not None:     # an assembled body: the field is known
+            g(f"s_mov_b32 {s(S[2])}, {_lit(g.cur['c'])}")
+        else:
+            g(f"s_lshr_b32 {s(S[2])}, {s(g.CUR + 2)}, 16")
+        g.op_n(S[0], f"v_sub_u32_e32 {v(T)}, {s(g.CUR + 3)}, {{a}}", T + 4, "SRC1")
+        g(f"s_and_b32 {s(S[3])}, {s(S[2])}, 1023", f"s_bfe_u32 {s(S[4])}, {s(S[2])}, 0x5000a",
+          f"v_cmp_ge_u32_e32 vcc, {s(S[4])}, {v(T)}", f"s_and_b64 {sr(MSK2, 2)}, vcc, {sr(AM, 2)}",
+          f"s_cbranch_scc0 {done}",
+          f"v_add_u32_e32 {v(T + 1)}, {s(S[3])}, {v(T)}",
+          f"s_mov_b64 {sr(EXECSV, 2)}, exec",
+          f"v_cmp_gt_u32_e32 vcc, {s(NLDS)}, {v(T + 1)}",
+          f"s_and_b64 exec, {sr(MSK2, 2)}, vcc", f"s_cbranch_scc0 {nolds}",
+          f"v_lshlrev_b32_e32 {v(T + 2)}, 10, {v(T + 1)}", f"v_add_u32_e32 {v(T + 2)}, {v(T + 2)}, {v(LDSOFF)}",
+          f"ds_read_b32 {v(T + 3)}, {v(T + 2)}")
+        g.label(nolds)
+        g(f"s_andn2_b64 exec, {sr(MSK2, 2)}, vcc", f"s_cbranch_scc0 {noglob}",
+          f"v_subrev_u32_e32 {v(T + 2)}, {s(NLDS)}, {v(T + 1)}",
+          f"v_mul_lo_u32 {v(T + 2)}, {v(T + 2)}, {s(GSTRIDE)}", f"v_add_u32_e32 {v(T + 2)}, {v(T + 2)}, {v(GOFF)}",
+          f"global_load_dword {v(T + 3)}, {v(T + 2)}, {sr(GSP, 2)}")
+        g.label(noglob)
+        g(f"s_mov_b64 exec, {sr(MSK2, 2)}", "s_waitcnt vmcnt(0) lgkmcnt(0)")
+        g.op_n(S[1], f"v_cmp_ne_u32_e32 vcc, {{a}}, {v(T + 3)}", T + 4)
+        g(f"s_mov_b64 exec, {sr(EXECSV, 2)}", f"s_andn2_b64 {sr(AM, 2)}, {sr(AM, 2)}, vcc")
+        g.all_dead_exit()
+        g.label(done)
+
     # -------------------------------------------------------- wide -> narrow
     # N_EQ / N_ULT / N_ULE read operand a (N_ULE: b) as the VALU source
     # itself (Gen.w_indexed): no eight-move copy out of the W file

@@ -664,7 +664,7 @@ def _fuse_checks(insns: List[MInsn]) -> List[MInsn]:
             continue
         out.append(ins)
         i += 1
-    out = _fuse_keyed_premises(out)
+    out = _form_grids(_fuse_keyed_premises(out))
     uses = _uses(out)
     for a, b in zip(out, out[1:]):
         if (a.op == "W_CDINS" and b.op == "W_CDINS" and a.dst is not None and uses.get(a.dst.id, 0) == 1
@@ -698,6 +698,137 @@ def _fuse_keyed_premises(insns: List[MInsn]) -> List[MInsn]:
         return out
     uses = _uses(out)
     return [ins for ins in out if ins.dst is None or ins.dst.id not in fused or uses.get(ins.dst.id, 0)]
+
+
+GRID_MIN = 64      # keyed checks of one key before they become a table (_form_grids)
+GRID_MAX_N = 32    # table entries: CHECK_GRID's c field holds n - 1 in 5 bits, the table's word in 10
+
+
+def _okey(o):
+    return ("v", o.id) if isinstance(o, VReg) else ("k", o.value, o.cls)
+
+
+def _grid_plan(insns: List[MInsn], pos: List[int]):
+    """(table operands in offset order, {row operand key: (operand, E, last position)}) for
+    the keyed checks at `pos` (one key), or None unless they form a complete grid
+    e(r, t) = E_r - k_t with the k_t distinct in [0, n)."""
+    first: Dict[tuple, object] = {}
+    adj: Dict[tuple, List[tuple]] = {}
+    for p in pos:
+        x, y = insns[p].srcs[1], insns[p].srcs[2]
+        kx, ky = _okey(x), _okey(y)
+        if kx == ky:
+            return None
+        for k, o in ((kx, x), (ky, y)):
+            if k not in first:
+                first[k] = o
+                adj[k] = []
+        adj[kx].append(ky)
+        adj[ky].append(kx)
+    # 2-colour the operands (a complete bipartite graph is connected); colour 0
+    # holds the first operand met
+    colour: Dict[tuple, int] = {}
+    order = list(first)
+    colour[order[0]] = 0
+    stack = [order[0]]
+    while stack:
+        k = stack.pop()
+        for m in adj[k]:
+            if m not in colour:
+                colour[m] = 1 - colour[k]
+                stack.append(m)
+            elif colour[m] == colour[k]:
+                return None
+    if len(colour) != len(order):
+        return None
+    sides = [[k for k in order if colour[k] == c] for c in (0, 1)]
+    # the larger side that fits is the table: a store per entry is cheaper than a row
+    for tside in ((0, 1) if len(sides[0]) >= len(sides[1]) else (1, 0)):
+        tkeys, rkeys = sides[tside], sides[1 - tside]
+        n, m = len(tkeys), len(rkeys)
+        if n > GRID_MAX_N or n * m != len(pos):
+            continue
+        tset = set(tkeys)
+        e: Dict[Tuple[tuple, tuple], int] = {}
+        last: Dict[tuple, int] = {}
+        ok = True
+        for p in pos:
+            ins = insns[p]
+            kx, ky = _okey(ins.srcs[1]), _okey(ins.srcs[2])
+            t, r = (kx, ky) if kx in tset else (ky, kx)
+            if (t, r) in e:
+                ok = False
+                break
+            e[(t, r)] = ins.imm
+            last[r] = p
+        if not ok or len(e) != n * m:
+            continue
+        r0 = rkeys[0]
+        top = max(e[(t, r0)] for t in tkeys)
+        off = {t: top - e[(t, r0)] for t in tkeys}
+        if sorted(off.values()) != list(range(n)):
+            continue
+        rows = {}
+        for r in rkeys:
+            E = {e[(t, r)] + off[t] for t in tkeys}
+            if len(E) != 1:
+                ok = False
+                break
+            rows[r] = (first[r], E.pop(), last[r])
+        if not ok:
+            continue
+        table = sorted(tkeys, key=lambda t: off[t])
+        return [first[t] for t in table], rows
+    return None
+
+
+def _form_grids(insns: List[MInsn]) -> List[MInsn]:
+    """A complete grid of keyed congruence checks over one key (C3: an ABI
+    word's 32 bytes S_k at a symbolic offset against 68 concrete cells v_K,
+    ``(key = E_K - k) => (S_k = v_K)``) becomes a table and one lookup per
+    row: the S_k are stored to n consecutive spill words (GRID_PUT, an
+    SPILL_N to a fixed word; the tables precede the spill slots) right after
+    the last of them is defined, and each row is ``CHECK_GRID key, v_K`` with
+    imm E_K and c = table word | (n - 1) << 10: j = E_K - key; j < n =>
+    table[j] = v_K (mw_isa.h).  The row goes where the row's last check was.
+    Same verdict as the checks, lane by lane: key = E_K - j holds for exactly
+    the pair (K, k = j)."""
+    groups: Dict[int, List[int]] = {}
+    for i, ins in enumerate(insns):
+        if ins.op == "CHECK_IMPEQK" and isinstance(ins.srcs[0], VReg):
+            groups.setdefault(ins.srcs[0].id, []).append(i)
+    defpos = {ins.dst.id: i for i, ins in enumerate(insns) if ins.dst is not None}
+    drop: set = set()
+    after: Dict[int, List[MInsn]] = {}
+    t0 = 0
+    for kid, pos in groups.items():
+        if len(pos) < GRID_MIN:
+            continue
+        plan = _grid_plan(insns, pos)
+        if plan is None:
+            continue
+        table, rows = plan
+        n = len(table)
+        if t0 + n > 1024:
+            break
+        key = insns[pos[0]].srcs[0]
+        put = max([defpos[key.id]] + [defpos[t.id] for t in table if isinstance(t, VReg)])
+        after.setdefault(put, []).extend(MInsn("GRID_PUT", 0, None, [t], imm=t0 + k) for k, t in enumerate(table))
+        width = insns[pos[0]].width
+        for r, (opnd, E, lastp) in rows.items():
+            at = lastp if lastp > put else put
+            after.setdefault(at, []).append(MInsn("CHECK_GRID", width, None, [key, opnd, ("raw", t0 | (n - 1) << 10)],
+                                                  imm=E))
+        drop.update(pos)
+        t0 += n
+    if not drop:
+        return insns
+    out: List[MInsn] = []
+    for i, ins in enumerate(insns):
+        if i not in drop:
+            out.append(ins)
+        out.extend(after.get(i, ()))
+    return out
 
 
 def _schedule_narrow_early(insns: List[MInsn]) -> List[MInsn]:
@@ -859,15 +990,17 @@ def _layout_spills(insns: List[MInsn], slot_cls: List[str]):
     rest in global memory (mw_kernels.hip), so slots are placed by traffic:
     most SPILL/FILL accesses per word first.  C3 (129 narrow slots) keeps its
     hottest 80 in LDS instead of the first 10 W-sized slots."""
+    # the grid tables (_form_grids) come first, at the words their GRID_PUTs name
+    tables = 1 + max((ins.imm for ins in insns if ins.op == "GRID_PUT"), default=-1)
     if not slot_cls:
-        return insns, 0
+        return insns, tables
     hits = [0] * len(slot_cls)
     for ins in insns:
         if ins.op in ("SPILL_W", "SPILL_N", "FILL_W", "FILL_N"):
             hits[ins.imm] += 1
     size = [8 if c == "W" else 1 for c in slot_cls]
     order = sorted(range(len(slot_cls)), key=lambda k: (-hits[k] / size[k], k))
-    off, words = {}, 0
+    off, words = {}, tables
     for k in order:
         off[k] = words
         words += size[k]
@@ -1041,7 +1174,8 @@ def compile_program(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, Le
         nxt = insns[k + 1] if k + 1 < len(insns) else None
         flags = isa.FLAG_CHAIN if (ins.chain and nxt is not None and nxt.op == "W_CDINS" and nxt.srcs
                                    and nxt.srcs[0] == ins.dst) else 0
-        code.extend(isa.encode(ins.op, ins.width, dst, fields[0], fields[1], fields[2], imm, flags))
+        op = "SPILL_N" if ins.op == "GRID_PUT" else ins.op
+        code.extend(isa.encode(op, ins.width, dst, fields[0], fields[1], fields[2], imm, flags))
     if len(consts) > 0x7FFF:
         raise Unsupported("constant pool overflow")
 

@@ -105,7 +105,7 @@ K256 kshl(const K256& v, int s) {   // callers keep the result below 2^256 (comp
 }
 
 // operands: a virtual register, a constant, or (after allocation) a physical slot
-enum { O_NONE = 0, O_VREG = 1, O_CONST = 2, O_PHYS = 3 };
+enum { O_NONE = 0, O_VREG = 1, O_CONST = 2, O_PHYS = 3, O_RAW = 4 };   // O_RAW: v is the field itself
 struct Opnd {
   int kind = O_NONE;
   int v = 0;
@@ -119,6 +119,7 @@ struct Insn {
   int ns = 0;
   long long imm = 0;  // STORE_*: the traced record until encode
   bool chain = false;
+  bool grid = false;  // SPILL_N of a grid table entry (form_grids): a fixed word, not a spill slot
 };
 
 int dst_cls(int op) {   // 'W', 'N' or 0 (isa.SHAPES[op][0])
@@ -709,6 +710,190 @@ struct Compiler {
     return v.l[0] < 0x80000000u;
   }
 
+  // ------------------------------------------------------------------ grids (compiler.py _form_grids)
+  static constexpr size_t GRID_MIN = 64, GRID_MAX_N = 32;
+  struct OKey {
+    int kind, v;
+    char cls;
+    K256 val;
+  };
+  OKey okey(const Opnd& o) const {
+    OKey k{o.kind, o.v, 0, K256{}};
+    if (o.kind == O_CONST) {
+      k.v = 0;
+      k.cls = kc[o.v];
+      k.val = kv[o.v];
+    }
+    return k;
+  }
+  static bool okey_eq(const OKey& a, const OKey& b) {
+    if (a.kind != b.kind) return false;
+    if (a.kind != O_CONST) return a.v == b.v;
+    return a.cls == b.cls && memcmp(a.val.l, b.val.l, sizeof a.val.l) == 0;
+  }
+  struct GridPlan {
+    std::vector<Opnd> table, rowop;
+    std::vector<long long> rowE;
+    std::vector<int> rowlast;
+  };
+  bool grid_plan(const std::vector<Insn>& in, const std::vector<int>& pos, GridPlan& gp) const {
+    std::vector<OKey> keys;
+    std::vector<Opnd> firsto;
+    std::vector<std::vector<int>> adj;
+    auto idx_of = [&](const Opnd& o) -> int {
+      OKey k = okey(o);
+      for (size_t q = 0; q < keys.size(); ++q)
+        if (okey_eq(keys[q], k)) return (int)q;
+      keys.push_back(k);
+      firsto.push_back(o);
+      adj.emplace_back();
+      return (int)keys.size() - 1;
+    };
+    std::vector<std::pair<int, int>> pr(pos.size());
+    for (size_t q = 0; q < pos.size(); ++q) {
+      const Insn& x = in[pos[q]];
+      if (okey_eq(okey(x.s[1]), okey(x.s[2]))) return false;
+      int a = idx_of(x.s[1]), b = idx_of(x.s[2]);
+      adj[a].push_back(b);
+      adj[b].push_back(a);
+      pr[q] = {a, b};
+    }
+    std::vector<int> col(keys.size(), -1);
+    col[0] = 0;
+    std::vector<int> st{0};
+    while (!st.empty()) {
+      int k = st.back();
+      st.pop_back();
+      for (int m : adj[k]) {
+        if (col[m] < 0) {
+          col[m] = 1 - col[k];
+          st.push_back(m);
+        } else if (col[m] == col[k]) {
+          return false;
+        }
+      }
+    }
+    for (int c : col)
+      if (c < 0) return false;
+    size_t n0 = 0;
+    for (int c : col) n0 += c == 0;
+    const int first_side = n0 >= keys.size() - n0 ? 0 : 1;   // the larger side that fits is the table
+    for (int ts = 0; ts < 2; ++ts) {
+      const int tside = ts == 0 ? first_side : 1 - first_side;
+      std::vector<int> tk, rk;
+      for (size_t q = 0; q < keys.size(); ++q) (col[q] == tside ? tk : rk).push_back((int)q);
+      size_t n = tk.size(), m = rk.size();
+      if (n > GRID_MAX_N || n * m != pos.size()) continue;
+      std::vector<int> tix(keys.size(), -1), rix(keys.size(), -1);
+      for (size_t q = 0; q < n; ++q) tix[tk[q]] = (int)q;
+      for (size_t q = 0; q < m; ++q) rix[rk[q]] = (int)q;
+      std::vector<long long> e(n * m, -1);
+      std::vector<int> last(m, -1);
+      bool ok = true;
+      for (size_t q = 0; q < pos.size() && ok; ++q) {
+        int a = pr[q].first, b = pr[q].second;
+        int t = col[a] == tside ? a : b, r = col[a] == tside ? b : a;
+        long long& slot = e[(size_t)tix[t] * m + rix[r]];
+        if (slot >= 0) ok = false;
+        slot = in[pos[q]].imm;
+        last[rix[r]] = pos[q];
+      }
+      if (!ok) continue;
+      long long top = -1;
+      for (size_t q = 0; q < n; ++q) top = std::max(top, e[q * m]);
+      std::vector<long long> off(n);
+      std::vector<char> seen(n, 0);
+      for (size_t q = 0; q < n && ok; ++q) {
+        off[q] = top - e[q * m];
+        if (off[q] < 0 || off[q] >= (long long)n || seen[off[q]]) ok = false;
+        else seen[off[q]] = 1;
+      }
+      if (!ok) continue;
+      gp = GridPlan{};
+      for (size_t r = 0; r < m && ok; ++r) {
+        long long E = e[r] + off[0];
+        for (size_t q = 1; q < n && ok; ++q) ok = e[q * m + r] + off[q] == E;
+        gp.rowop.push_back(firsto[rk[r]]);
+        gp.rowE.push_back(E);
+        gp.rowlast.push_back(last[r]);
+      }
+      if (!ok) continue;
+      gp.table.assign(n, Opnd{});
+      for (size_t q = 0; q < n; ++q) gp.table[off[q]] = firsto[tk[q]];
+      return true;
+    }
+    return false;
+  }
+
+  std::vector<Insn> form_grids(const std::vector<Insn>& in) {
+    std::vector<int> gkey, gidx(vcls.size(), -1);
+    std::vector<std::vector<int>> gpos;
+    for (size_t i = 0; i < in.size(); ++i) {
+      const Insn& x = in[i];
+      if (x.op == MW_CHECK_IMPEQK && is_v(x.s[0])) {
+        int k = x.s[0].v;
+        if (gidx[k] < 0) {
+          gidx[k] = (int)gkey.size();
+          gkey.push_back(k);
+          gpos.emplace_back();
+        }
+        gpos[gidx[k]].push_back((int)i);
+      }
+    }
+    std::vector<int> defpos(vcls.size(), -1);
+    for (size_t i = 0; i < in.size(); ++i)
+      if (in[i].dst >= 0) defpos[in[i].dst] = (int)i;
+    std::vector<char> drop(in.size(), 0);
+    std::vector<std::vector<Insn>> after(in.size());
+    int t0 = 0;
+    bool any = false;
+    for (size_t g = 0; g < gkey.size(); ++g) {
+      const std::vector<int>& pos = gpos[g];
+      if (pos.size() < GRID_MIN) continue;
+      GridPlan gp;
+      if (!grid_plan(in, pos, gp)) continue;
+      int n = (int)gp.table.size();
+      if (t0 + n > 1024) break;
+      Opnd key = in[pos[0]].s[0];
+      int put = defpos[key.v];
+      for (const Opnd& t : gp.table)
+        if (is_v(t)) put = std::max(put, defpos[t.v]);
+      for (int k = 0; k < n; ++k) {
+        Insn p;
+        p.op = MW_SPILL_N;
+        p.grid = true;
+        p.ns = 1;
+        p.s[0] = gp.table[k];
+        p.imm = t0 + k;
+        after[put].push_back(p);
+      }
+      int width = in[pos[0]].width;
+      for (size_t r = 0; r < gp.rowop.size(); ++r) {
+        int at = gp.rowlast[r] > put ? gp.rowlast[r] : put;
+        Insn c;
+        c.op = MW_CHECK_GRID;
+        c.width = width;
+        c.ns = 3;
+        c.s[0] = key;
+        c.s[1] = gp.rowop[r];
+        c.s[2] = Opnd{O_RAW, t0 | (n - 1) << 10};
+        c.imm = gp.rowE[r];
+        after[at].push_back(c);
+      }
+      for (int p : pos) drop[p] = 1;
+      t0 += n;
+      any = true;
+    }
+    if (!any) return in;
+    std::vector<Insn> out;
+    out.reserve(in.size());
+    for (size_t i = 0; i < in.size(); ++i) {
+      if (!drop[i]) out.push_back(in[i]);
+      for (const Insn& a : after[i]) out.push_back(a);
+    }
+    return out;
+  }
+
   std::vector<Insn> fuse_checks(const std::vector<Insn>& in0) {
     std::vector<int> uses = use_counts(in0);
     std::vector<Insn> a1;
@@ -777,7 +962,7 @@ struct Compiler {
       out.push_back(x);
       i += 1;
     }
-    out = fuse_keyed_premises(out);
+    out = form_grids(fuse_keyed_premises(out));
     uses = use_counts(out);
     for (size_t i = 0; i + 1 < out.size(); ++i) {
       Insn& a = out[i];
@@ -927,12 +1112,20 @@ struct Compiler {
       }
       out.push_back(y);
     }
-    // spill slot layout: most accesses per word first (compiler.py _layout_spills)
+    // spill slot layout: the grid tables first (form_grids' words), then the
+    // slots, most accesses per word first (compiler.py _layout_spills)
+    long long tables = 0;
+    for (const Insn& x : out)
+      if (x.grid) tables = std::max(tables, x.imm + 1);
+    n_spill_words = (u64)tables;
+    auto slot_op = [](const Insn& x) {
+      return !x.grid && (x.op == MW_SPILL_W || x.op == MW_SPILL_N || x.op == MW_FILL_W || x.op == MW_FILL_N);
+    };
     if (!slot_cls.empty()) {
       size_t ns = slot_cls.size();
       std::vector<long long> hits(ns, 0);
       for (const Insn& x : out)
-        if (x.op == MW_SPILL_W || x.op == MW_SPILL_N || x.op == MW_FILL_W || x.op == MW_FILL_N) ++hits[x.imm];
+        if (slot_op(x)) ++hits[x.imm];
       std::vector<int> order(ns);
       for (size_t q = 0; q < ns; ++q) order[q] = (int)q;
       auto size = [&](int q) -> long long { return slot_cls[q] == 'W' ? 8 : 1; };
@@ -942,13 +1135,13 @@ struct Compiler {
         return a < b;
       });
       std::vector<long long> off(ns, 0);
-      long long words = 0;
+      long long words = tables;
       for (int q : order) {
         off[q] = words;
         words += size(q);
       }
       for (Insn& x : out)
-        if (x.op == MW_SPILL_W || x.op == MW_SPILL_N || x.op == MW_FILL_W || x.op == MW_FILL_N) x.imm = off[x.imm];
+        if (slot_op(x)) x.imm = off[x.imm];
       n_spill_words = (u64)words;
     }
     return out;
@@ -1033,7 +1226,7 @@ struct Compiler {
       code.push_back((dst & 0xffff) | ((f[0] & 0xffff) << 16));
       code.push_back((f[1] & 0xffff) | ((f[2] & 0xffff) << 16));
       code.push_back((u32)(imm & 0xffffffffLL));
-      if (x.op == MW_SPILL_W || x.op == MW_SPILL_N) ++n_spills;
+      if ((x.op == MW_SPILL_W || x.op == MW_SPILL_N) && !x.grid) ++n_spills;
       if (x.op == MW_FILL_W || x.op == MW_FILL_N) ++n_fills;
     }
     if (consts.size() > 0x7fff) throw Unsupported{"constant pool overflow"};

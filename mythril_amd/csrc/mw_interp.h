@@ -211,6 +211,18 @@ MW_HD bool mw_run(const u32* __restrict__ code_, const u32* __restrict__ cpool_,
         if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
         break;
       }
+      case MW_CHECK_GRID: {  // one row of a congruence grid (compiler.py _form_grids)
+        u32 key, v;
+        MW_FETCH_N(oa, key);
+        MW_FETCH_N(ob, v);
+        const u32 j = imm - key;
+        if (j <= ((oc >> 10) & 31u)) {
+          env.fill((oc & 1023u) + j, x, 1);   // a per-lane word (fill writes x[0..7])
+          alive = alive && x[0] == v;
+        }
+        if (flags & MW_FLAG_EARLY_EXIT) stop = env.none(alive);
+        break;
+      }
       case MW_CHECK_IMPEQW: {
         u32 p;
         MW_FETCH_N(oa, p);

@@ -83,6 +83,9 @@ enum mw_opcode {
   MW_W_CDINS = 38, // W[dst] = W/K a | ((K[c] <s W[b] (256-bit) ? leaf(imm & 0xffff) : 0) << (imm >> 16)):
                    // one guarded calldata byte ite(i <s size, cd[i], 0) inserted into a word
                    // (state/calldata.py:218-231), four dispatches in one
+  MW_CHECK_GRID = 39,  // j = imm - N[a]; alive &= j >= n | (spill word T0 + j == N/K[b]),
+                       // c a raw field: T0 = c & 1023, n = (c >> 10 & 31) + 1 (a congruence grid's row,
+                       // compiler.py _form_grids; the table's words are stored by SPILL_N)
 
   // wide -> narrow
   MW_N_EXTRACTW = 48, // N[dst] = (a >> imm) masked to width (<= 32)

@@ -40,6 +40,7 @@ bool op_shape(u32 op, OpShape& s) {
     case MW_CHECK_IMPEQ: s.a = 2; s.b = 2; s.c = 2; return true;
     case MW_CHECK_IMPEQW: s.a = 2; s.b = 1; s.c = 1; return true;
     case MW_CHECK_IMPEQK: s.a = 2; s.b = 2; s.c = 2; return true;
+    case MW_CHECK_GRID: s.a = 2; s.b = 2; return true;   // c: the table's word and size, raw
     case MW_W_CDINS: s.dst = 3; s.a = 1; s.b = 1; s.c = 1; s.wide = true; return true;
     case MW_LEAF_W: s.dst = 3; return true;
     case MW_LEAF_N: s.dst = 4; return true;
@@ -141,7 +142,7 @@ int mg_validate_desc(const mg_prog_desc* d) {
     if (s.dst == 3 || s.dst == 4 || s.a || s.b) {
       const u32 maxw = (s.wide || s.dst == 3) ? 256u : 32u;
       if (op != MW_CHECK && op != MW_CHECK_IMP && op != MW_CHECK_IMPEQ && op != MW_CHECK_IMPEQW &&
-          op != MW_CHECK_IMPEQK && op != MW_STORE_W && op != MW_STORE_N && op != MW_SPILL_W &&
+          op != MW_CHECK_IMPEQK && op != MW_CHECK_GRID && op != MW_STORE_W && op != MW_STORE_N && op != MW_SPILL_W &&
           op != MW_SPILL_N && op != MW_FILL_W && op != MW_FILL_N && op != MW_MOV_W && op != MW_MOV_N &&
           op != MW_LEAF_W && op != MW_LEAF_N && (w < 1 || w > maxw))
         return fail(MG_E_PROG, "bad width " + std::to_string(w) + " at instruction " + std::to_string(i));
@@ -172,6 +173,10 @@ int mg_validate_desc(const mg_prog_desc* d) {
         break;
       case MW_W_SEXT: case MW_W_SEXTN: case MW_N_SEXT:
         if (I[3] < 1 || I[3] > w) return fail(MG_E_PROG, "bad sign-extension source width");
+        break;
+      case MW_CHECK_GRID:   // the table's words lie in the spill area
+        if (c >= 0x8000u || (u64)(c & 1023u) + ((c >> 10) & 31u) + 1 > d->n_spill)
+          return fail(MG_E_PROG, "grid table out of range");
         break;
       default: break;
     }

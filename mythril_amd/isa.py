@@ -27,7 +27,7 @@ OPCODES = {
     "W_SHL": 23, "W_LSHR": 24, "W_ASHR": 25,
     "W_UDIV": 26, "W_UREM": 27, "W_SDIV": 28, "W_SREM": 29, "W_SMOD": 30,
     "W_ITE": 31, "W_SHLI": 32, "W_LSHRI": 33, "W_ZEXTN": 34, "W_SEXT": 35, "W_SEXTN": 36,
-    "W_INSN": 37, "W_CDINS": 38,
+    "W_INSN": 37, "W_CDINS": 38, "CHECK_GRID": 39,
     "N_EXTRACTW": 48, "N_ULT": 49, "N_ULE": 50, "N_SLT": 51, "N_SLE": 52, "N_EQ": 53,
     "N_UMULNO": 54, "N_ADDC": 55,
     "N_ADD": 64, "N_SUB": 65, "N_MUL": 66, "N_AND": 67, "N_OR": 68, "N_XOR": 69, "N_NOT": 70,
@@ -44,6 +44,8 @@ SHAPES = {
     "END": (None, []), "CHECK": (None, ["N"]), "CHECK_IMP": (None, ["N", "N"]),
     "CHECK_IMPEQ": (None, ["N", "N", "N"]), "CHECK_IMPEQW": (None, ["N", "W", "W"]),
     "CHECK_IMPEQK": (None, ["N", "N", "N"]),   # (N[a] = imm) => (b = c)
+    # j = imm - N[a]; j < n => spill word (c & 1023) + j = b, n = (c >> 10 & 31) + 1 (c: a raw field)
+    "CHECK_GRID": (None, ["N", "N"]),
     "W_CDINS": ("W", ["W", "W", "W"]),
     "LEAF_W": ("W", []), "LEAF_N": ("N", []),
     "STORE_W": (None, ["W"]), "STORE_N": (None, ["N"]),
@@ -120,6 +122,7 @@ ASM_OPCODES = [
     "W_UDIV", "W_UREM",
     "STORE_W", "STORE_N",   # trace rows (witness programs, mg_eval_generated)
     "W_SHL", "W_LSHR", "W_ASHR",   # shifts by a per-lane amount (a barrel shifter)
+    "CHECK_GRID",   # a congruence grid's row (compiler.py _form_grids)
 ]
 ASM_LEAF_KINDS = [0, 1, 2, 3]
 # The asm engines divide bit-serially (256 steps per wide division); a program

@@ -174,10 +174,11 @@ def test_check_runs_with_true_premises(dev):
     q = prepare(s.asserts, s.ctx)
     p = q.program
     ops = [int(w) & 0xFF for w in p.code[0::4]]
-    # round 5: the congruence premises are keyed (lower._Rewriter.keyed), the
-    # runs CHECK_IMPEQK; the unkeyed CHECK_IMPEQ runs are test_check_runs_unkeyed's
-    imp = isa.OPCODES["CHECK_IMPEQK"]
-    assert any(a == b == imp for a, b in zip(ops, ops[1:])), "no run of CHECK_IMPEQK"
+    # round 5: the congruence premises are keyed (lower._Rewriter.keyed) and
+    # complete grids of them are table rows (compiler._form_grids): CHECK_GRID
+    # and the remaining CHECK_IMPEQK; the unkeyed CHECK_IMPEQ runs are
+    # test_check_runs_unkeyed's
+    assert isa.OPCODES["CHECK_GRID"] in ops and isa.OPCODES["CHECK_IMPEQK"] in ops
     n = 1 << 14
     di, da = pair(dev, p)
     try:
@@ -190,6 +191,46 @@ def test_check_runs_with_true_premises(dev):
                              specs=cdag.program_specs(p))
     assert np.array_equal(vi.astype(np.uint8), vo)
     assert np.array_equal(va.astype(np.uint8), vo), int(np.count_nonzero(va.astype(np.uint8) != vo))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_grid_rows_on_every_engine(dev, seed, monkeypatch):
+    """Congruence grids (tests/test_grid.py's sets: an ABI word's bytes at a
+    symbolic offset against concrete cells, with the symbolic bytes partly or
+    wholly past the concrete ones): the asm interpreter in each register
+    layout the program fits (the quarter layout's 40-word LDS budget puts
+    table words in the global buffer), the compiled interpreter, the
+    assembled kernel and the oracle agree on every candidate."""
+    from tests.test_gpu_asm import both
+    from tests.test_grid import _grid_rows, _word_dag
+    shift = (0, 0, 7, 40, 3, 0)[seed]
+    c, conj = _word_dag(9700 + seed, nsym=16 + 16 * (seed & 1), ncon=24 + 16 * (seed & 1), shift=shift)
+    n = 1 << 14
+    for pools in (False, True):
+        q = prepare(conj, c, use_pools=pools)
+        p = q.program
+        assert _grid_rows(p)
+        _, _, vo = cdag.evaluate(q.lowered.conjuncts, DEFAULT_SEED + seed, 0, n, want_verdict=True,
+                                 specs=cdag.program_specs(p) if pools else None)
+        for env in ({}, {"MYTHRIL_AMD_ASM_QUARTER": "0"},
+                    {"MYTHRIL_AMD_ASM_QUARTER": "0", "MYTHRIL_AMD_ASM_NARROW": "0"}):
+            for k in ("MYTHRIL_AMD_ASM_QUARTER", "MYTHRIL_AMD_ASM_NARROW"):
+                if k in env:
+                    monkeypatch.setenv(k, env[k])
+                else:
+                    monkeypatch.delenv(k, raising=False)
+            va, vi = both(dev, p, DEFAULT_SEED + seed, 0, n)
+            assert np.array_equal(va, vo), (seed, pools, env, int(np.count_nonzero(va != vo)))
+            assert np.array_equal(vi, vo), (seed, pools, env, int(np.count_nonzero(vi != vo)))
+        monkeypatch.delenv("MYTHRIL_AMD_ASM_QUARTER", raising=False)
+        monkeypatch.delenv("MYTHRIL_AMD_ASM_NARROW", raising=False)
+        di, da = pair(dev, p)
+        try:
+            vj, _ = dev.eval_generated(da, DEFAULT_SEED + seed, 0, n, trace=False)
+        finally:
+            di.free()
+            da.free()
+        assert np.array_equal(vj.astype(np.uint8), vo), (seed, pools, int(np.count_nonzero(vj.astype(np.uint8) != vo)))
 
 
 def test_check_runs_unkeyed(dev, monkeypatch):

@@ -121,14 +121,16 @@ def test_congruence_conjuncts_fuse_to_one_check():
                                 "c3_bec_batchtransfer_overflow.smt2"))
     q = prepare(s.asserts, s.ctx)
     ops = [int(w) & 0xFF for w in q.program.code.reshape(-1, 4)[:, 0]]
-    fused = ops.count(isa.OPCODES["CHECK_IMP"]) + ops.count(isa.OPCODES["CHECK_IMPEQ"]) + \
-        ops.count(isa.OPCODES["CHECK_IMPEQW"]) + ops.count(isa.OPCODES["CHECK_IMPEQK"])
-    assert fused >= 2000
-    # (key = K) => (v = w): one dispatch, the premise compared inside the check
-    # (lower._Rewriter.keyed): no premise flags, so no wide compare per diagonal
-    assert ops.count(isa.OPCODES["CHECK_IMPEQK"]) >= 2000
+    # (key = K) => (v = w) with keyed premises (lower._Rewriter.keyed): no premise
+    # flags; over one key they form complete grids (compiler._form_grids), one
+    # CHECK_GRID per concrete cell over a table of the symbolic bytes
+    code = q.program.code.reshape(-1, 4)
+    rows = [r for r in code if int(r[0]) & 0xFF == isa.OPCODES["CHECK_GRID"]]
+    pairs = sum(((int(r[2]) >> 26) & 31) + 1 for r in rows)    # n of each row's table (c = T0 | (n-1) << 10)
+    assert pairs == 2176, pairs
+    assert ops.count(isa.OPCODES["CHECK_IMPEQK"]) == 0
     assert ops.count(isa.OPCODES["N_EQ"]) < 60
-    assert q.program.n_spill <= 48
+    assert len(ops) < 800 and q.program.n_spill <= 80
     assert all(not i.op.startswith("CHECK_IMP") for i in q.program.machine_ir())
 
 
