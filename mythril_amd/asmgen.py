@@ -2297,6 +2297,51 @@ def lds_spill_words(n_spill: int, npool: int) -> int:
     return max(0, min(n_spill, LDS_SPILL_WORDS - rows))
 
 
+def _grid_static(g, insn, nlds):
+    """A CHECK_GRID row in an assembled body (no exec writes there): the
+    lanes out of range read the table's first word instead (j clamped to 0),
+    and with the table split between LDS and the global buffer every lane
+    reads both places at clamped words and selects (nlds None: the kernel's
+    NLDS register; only for text, asmjit passes nlds)."""
+    g.set_insn(insn)
+    c = g.cur["c"]
+    t0, nm1 = c & 1023, (c >> 10) & 31
+    key = _nreg(g, g.cur["a"], T + 4)
+    skip = g.L("gs")
+    g(f"v_sub_u32_e32 {v(T)}, {_lit(insn[3])}, {key}", f"v_cmp_ge_u32_e32 vcc, {nm1}, {v(T)}",
+      f"s_and_b64 {sr(CMSK, 2)}, vcc, {sr(AM, 2)}", f"s_cbranch_scc0 {skip}",
+      f"v_cndmask_b32_e32 {v(T)}, 0, {v(T)}, vcc")
+    if nlds is not None and t0 + nm1 + 1 <= nlds:        # the whole table in LDS
+        g(f"v_lshlrev_b32_e32 {v(T + 2)}, 10, {v(T)}", f"v_add_u32_e32 {v(T + 2)}, {v(T + 2)}, {v(LDSOFF)}")
+        if t0 * 1024 < 65536:
+            g(f"ds_read_b32 {v(T + 3)}, {v(T + 2)} offset:{t0 * 1024}")
+        else:
+            g(f"v_add_u32_e32 {v(T + 2)}, {_lit(t0 * 1024)}, {v(T + 2)}", f"ds_read_b32 {v(T + 3)}, {v(T + 2)}")
+    elif nlds is not None and t0 >= nlds:                 # the whole table in the global buffer
+        g(f"v_add_u32_e32 {v(T + 2)}, {_lit(t0 - nlds)}, {v(T)}",
+          f"v_mul_lo_u32 {v(T + 2)}, {v(T + 2)}, {s(GSTRIDE)}", f"v_add_u32_e32 {v(T + 2)}, {v(T + 2)}, {v(GOFF)}",
+          f"global_load_dword {v(T + 3)}, {v(T + 2)}, {sr(GSP, 2)}")
+    else:
+        nl = _lit(nlds) if nlds is not None else s(NLDS)
+        g(f"v_add_u32_e32 {v(T + 1)}, {_lit(t0)}, {v(T)}",                 # the word
+          f"v_cmp_gt_u32_e64 {sr(CMSK2, 2)}, {nl}, {v(T + 1)}",            # lanes whose word is in LDS
+          f"v_cndmask_b32_e64 {v(T + 2)}, 0, {v(T + 1)}, {sr(CMSK2, 2)}",
+          f"v_lshlrev_b32_e32 {v(T + 2)}, 10, {v(T + 2)}", f"v_add_u32_e32 {v(T + 2)}, {v(T + 2)}, {v(LDSOFF)}",
+          f"ds_read_b32 {v(T + 3)}, {v(T + 2)}",
+          f"v_subrev_u32_e32 {v(T + 5)}, {nl}, {v(T + 1)}",
+          f"v_cndmask_b32_e64 {v(T + 5)}, {v(T + 5)}, 0, {sr(CMSK2, 2)}",
+          f"v_mul_lo_u32 {v(T + 5)}, {v(T + 5)}, {s(GSTRIDE)}", f"v_add_u32_e32 {v(T + 5)}, {v(T + 5)}, {v(GOFF)}",
+          f"global_load_dword {v(T + 5)}, {v(T + 5)}, {sr(GSP, 2)}",
+          "s_waitcnt vmcnt(0) lgkmcnt(0)",
+          f"v_cndmask_b32_e64 {v(T + 3)}, {v(T + 5)}, {v(T + 3)}, {sr(CMSK2, 2)}")
+    g("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    g(f"v_cmp_ne_u32_e64 {sr(CMSK2, 2)}, {_nreg(g, g.cur['b'], T + 5)}, {v(T + 3)}",
+      f"s_and_b64 {sr(CMSK2, 2)}, {sr(CMSK2, 2)}, {sr(CMSK, 2)}",
+      f"s_andn2_b64 {sr(AM, 2)}, {sr(AM, 2)}, {sr(CMSK2, 2)}")
+    g.all_dead_exit()
+    g.label(skip)
+
+
 def _spill_static(g, name, insn, nlds):
     """SPILL/FILL with the word's place known: LDS [word][lane] below nlds,
     else the global buffer [word][thread] (mw_kernels.hip)."""
@@ -2395,6 +2440,11 @@ def static_body(code, consts, leaves, forward: bool = True, nlds: int = None, po
                 _cdins_static(g)
         elif name == "W_CDINS":
             _cdins_static(g)
+        elif name == "CHECK_GRID":
+            g.chain_open = False
+            g.summary_b = None
+            g.digit_spec = None
+            _grid_static(g, insn, nlds)
         elif name in ("SPILL_W", "SPILL_N", "FILL_W", "FILL_N") and nlds is not None:
             g.chain_open = False
             g.summary_b = None

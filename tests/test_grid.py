@@ -127,3 +127,32 @@ def test_incomplete_grid_stays_checks():
             k = syms.index(i.srcs[1])
             for K, b in enumerate(cons):
                 assert (i.imm - (100 + K - k)) & 0xFFFFFFFF == puts[id(b)], (k, K)
+
+
+@pytest.mark.parametrize("nlds", [None, 0, 8, 80])
+def test_grid_rows_assemble(nlds):
+    """An assembled body's rows (asmgen._grid_static: no exec writes, the
+    table wholly in LDS, wholly global, or split) assemble for gfx950, and the
+    kernel reads the table the way the split puts it."""
+    from mythril_amd import asmgen, asmjit
+    c, conj = _word_dag(9701, nsym=32, ncon=40)
+    q = prepare(conj, c, use_pools=True)
+    p = q.program
+    body = asmgen.static_body(p.code, p.consts, p.leaves, nlds=nlds, pool=p.pool)
+    assert not any("exec" in ln for ln in body)
+    sect, lds, glob = None, 0, 0
+    for ln in body:
+        if ln.startswith("; "):
+            sect = ln.split(": ", 1)[-1]
+        elif sect == "CHECK_GRID":
+            lds += "ds_read_b32" in ln
+            glob += "global_load_dword" in ln
+    rows = len(_grid_rows(p))
+    if nlds == 80:
+        assert (lds, glob) == (rows, 0)
+    if nlds == 0:
+        assert (lds, glob) == (0, rows)
+    if nlds in (None, 8):
+        assert (lds, glob) == (rows, rows)
+    co, name, _ = asmjit.assemble(p, cache=False)
+    assert len(co) > 0 and name.startswith("mwa_")
