@@ -737,14 +737,19 @@ def _zeros(c: Ctx, n: int) -> List[Node]:
 
 
 def _offset(n: Node):
-    """(base, k) with n == base + k (mod 2^w), for a const k; (n, 0) otherwise."""
-    if n.op == "bvadd" and len(n.args) == 2:
+    """(base, k) with n == base + k (mod 2^w), for a const k, through nested
+    constant additions (calldata offset + 4 + k: one base for every byte of
+    the word); (n, 0) otherwise."""
+    k = 0
+    while n.op == "bvadd" and len(n.args) == 2:
         a, b = n.args
         if b.op == "const" and a.op != "const":
-            return a, b.val
-        if a.op == "const" and b.op != "const":
-            return b, a.val
-    return n, 0
+            n, k = a, k + b.val
+        elif a.op == "const" and b.op != "const":
+            n, k = b, k + a.val
+        else:
+            break
+    return n, k & ((1 << n.width) - 1)
 
 
 KEY_BIAS = 1 << 16      # _index_key: K - k + KEY_BIAS >= 0 for offsets k < 2^16
