@@ -175,10 +175,9 @@ def test_check_runs_with_true_premises(dev):
     p = q.program
     ops = [int(w) & 0xFF for w in p.code[0::4]]
     # round 5: the congruence premises are keyed (lower._Rewriter.keyed) and
-    # complete grids of them are table rows (compiler._form_grids): CHECK_GRID
-    # and the remaining CHECK_IMPEQK; the unkeyed CHECK_IMPEQ runs are
-    # test_check_runs_unkeyed's
-    assert isa.OPCODES["CHECK_GRID"] in ops and isa.OPCODES["CHECK_IMPEQK"] in ops
+    # complete grids of them are table rows (compiler._form_grids): CHECK_GRID;
+    # the unkeyed CHECK_IMPEQ runs are test_check_runs_unkeyed's
+    assert isa.OPCODES["CHECK_GRID"] in ops
     n = 1 << 14
     di, da = pair(dev, p)
     try:
