@@ -691,28 +691,12 @@ def build_handlers():
     @handler("N_EQ")
     def _(g):
         g.field("a", S[0]), g.field("b", S[1])
-        small = g.static_imm() is None     # the interpreter: mw_asm_predecode's small-constant form
-        if small:
-            # a register against a constant below 2^32 (84 % of the corpus's
-            # N_EQ have a constant, half of them that small): predecode puts the
-            # register in a, the constant in word 3 and flags bit 16 of word 2
-            # - no constant-pool load
-            fast, merge = g.L("eqk"), g.L("eqm")
-            g(f"s_bitcmp1_b32 {s(g.CUR + 2)}, 16", f"s_cbranch_scc1 {fast}")
         g.fetch_w(S[1], XB)
         g.w_indexed(S[0], "SRC0", lambda base: g(*[f"v_xor_b32_e32 {v(T + k)}, {v(base + k)}, {v(XB + k)}"
                                                    for k in range(8)]))
         g(f"v_or3_b32 {v(T)}, {v(T)}, {v(T + 1)}, {v(T + 2)}", f"v_or3_b32 {v(T + 3)}, {v(T + 3)}, {v(T + 4)}, {v(T + 5)}",
           f"v_or3_b32 {v(XC)}, {v(T + 6)}, {v(T + 7)}, {v(T)}", f"v_or_b32_e32 {v(XC)}, {v(XC)}, {v(T + 3)}")
         g(f"v_cmp_eq_u32_e32 vcc, 0, {v(XC)}")
-        if small:
-            g(f"s_branch {merge}")
-            g.label(fast)
-            g(f"v_mov_b32_e32 {v(T + 1)}, {s(g.CUR + 3)}")
-            g.w_indexed(S[0], "SRC0", lambda base: g(f"v_xor_b32_e32 {v(T)}, {v(base)}, {v(T + 1)}",
-                                                     *[f"v_or_b32_e32 {v(T)}, {v(base + k)}, {v(T)}" for k in range(1, 8)]))
-            g(f"v_cmp_eq_u32_e32 vcc, 0, {v(T)}")
-            g.label(merge)
         g.bool_from_vcc(XR)
         g.write_n(XR)
 

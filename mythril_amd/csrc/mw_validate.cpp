@@ -304,28 +304,6 @@ int mw_asm_predecode_layout(const u32* code, size_t nwords, const u32* consts, s
     // a CHECK_IMPEQ followed by another: the handler takes that one itself
     // (a chain, mythril_amd/asmgen.py), bit 31 above its c field
     if (op == MW_CHECK_IMPEQ && i + 7 < nwords && (code[i + 4] & 0xffu) == MW_CHECK_IMPEQ) O[3] |= 0x80000000u;
-    // N_EQ of a W register with a constant below 2^32 (upper limbs zero): the
-    // register in a, the constant in word 3, bit 16 of word 2 set (asmgen.py
-    // N_EQ's small-constant path: no constant-pool load); otherwise bit 16 clear
-    if (op == MW_N_EQ) {
-      auto small = [&](u32 f) {
-        if (!(f & MW_KBIT)) return false;
-        const size_t o = f & 0x7fffu;
-        if (o + 8 > nconst) return false;
-        for (int k = 1; k < 8; ++k)
-          if (consts[o + k]) return false;
-        return true;
-      };
-      O[2] &= 0xffffu;
-      if (small(b) && !(a & MW_KBIT)) {
-        O[3] = consts[b & 0x7fffu];
-        O[2] |= 1u << 16;
-      } else if (small(a) && !(b & MW_KBIT)) {
-        O[1] = (O[1] & ~0xffffu) | b2;
-        O[3] = consts[a & 0x7fffu];
-        O[2] = b2 | (1u << 16);
-      }
-    }
     // CHECK_IMPEQK: word 3 is the premise constant, so its chain flag is bit
     // 31 of word 1 (the width above a is not read by its handler)
     if (op == MW_CHECK_IMPEQK)

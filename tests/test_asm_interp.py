@@ -310,22 +310,3 @@ def test_predecode_chains_keyed_checks():
     assert [int(x) for x in o[:3, 3]] == [0x10020, K, 3]         # the premise constants, whole
     assert [int(x) & 0xFF for x in o[:3, 1]] == [1, 1, 1]           # the key's register
     assert [int(x) for x in o[:3, 2]] == [4 | 5 << 16, 6 | 7 << 16, 8 | 9 << 16]
-
-
-def test_predecode_small_constant_n_eq():
-    """N_EQ of a W register with a constant below 2^32: predecode puts the
-    register in a (either operand order), the constant in word 3 and sets bit
-    16 of word 2 (asmgen.py N_EQ's small-constant path); a wide constant or
-    two registers keep the pool path with bit 16 clear."""
-    e = isa.encode
-    N = lambda k: isa.encode_dst("N", k)   # noqa: E731
-    K = isa.KBIT
-    consts = [0] * 8 + [0x12345678] + [0] * 7 + [5, 0, 0, 0, 0, 1, 0, 0]   # K|0: 0, K|8: small, K|16: wide
-    code = (e("N_EQ", 256, N(1), 3, K | 8) + e("N_EQ", 256, N(2), K | 8, 5) + e("N_EQ", 256, N(3), 3, K | 16)
-            + e("N_EQ", 256, N(4), 3, 4) + e("N_EQ", 256, N(5), 2, K | 0) + e("END", 0, isa.encode_dst(None)))
-    o, _ = _predecode(code, consts)
-    assert o is not None
-    flags = [(int(r[2]) >> 16) & 1 for r in o[:5]]
-    assert flags == [1, 1, 0, 0, 1]
-    assert [int(o[i, 3]) for i in (0, 1, 4)] == [0x12345678, 0x12345678, 0]
-    assert [int(o[i, 1]) & 0xFFFF for i in (0, 1, 4)] == [3 * 8, 5 * 8, 2 * 8]   # the register, as a W index
