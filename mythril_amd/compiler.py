@@ -654,8 +654,14 @@ def _fuse_checks(insns: List[MInsn]) -> List[MInsn]:
                 and q[2].srcs[1].value == 0 and _is(q[2].srcs[2], q[0])
                 and ((q[3].op == "W_INSN" and _is(q[3].srcs[1], q[2]))
                      or (q[3].op == "W_ZEXTN" and _is(q[3].srcs[0], q[2])))
-                and all(uses.get(x.dst.id, 0) == 1 for x in q[:3])
+                and uses.get(q[0].dst.id, 0) == 1 and uses.get(q[2].dst.id, 0) == 1
                 and q[1].imm < (1 << 16)):
+            if uses.get(q[1].dst.id, 0) > 1:
+                # the byte's leaf has other uses (a congruence grid's table or
+                # rows): it stays, and W_CDINS draws the same leaf again
+                # itself; _hoist_cdins_leaves keeps the chain unbroken
+                q[1].cdleaf = True
+                out.append(q[1])
             acc = q[3].srcs[0] if q[3].op == "W_INSN" else Const(0, "W")
             off = q[3].imm if q[3].op == "W_INSN" else 0
             out.append(MInsn("W_CDINS", q[3].width, q[3].dst, [acc, q[0].srcs[1], Const(q[0].srcs[0].value, "W")],
@@ -664,12 +670,33 @@ def _fuse_checks(insns: List[MInsn]) -> List[MInsn]:
             continue
         out.append(ins)
         i += 1
+    out = _hoist_cdins_leaves(out)
     out = _form_grids(_fuse_keyed_premises(out))
     uses = _uses(out)
     for a, b in zip(out, out[1:]):
         if (a.op == "W_CDINS" and b.op == "W_CDINS" and a.dst is not None and uses.get(a.dst.id, 0) == 1
                 and _is(b.srcs[0], a)):
             a.chain = True
+    return out
+
+
+def _hoist_cdins_leaves(insns: List[MInsn]) -> List[MInsn]:
+    """In a run of W_CDINS links and the leaves kept beside them (_fuse_checks:
+    a leaf with other uses), the leaves move to the run's start, so the links
+    stay adjacent and chain (a leaf has no operands: it can move earlier)."""
+    out: List[MInsn] = []
+    i = 0
+    while i < len(insns):
+        if insns[i].op == "W_CDINS" or getattr(insns[i], "cdleaf", False):
+            j = i
+            while j < len(insns) and (insns[j].op == "W_CDINS" or getattr(insns[j], "cdleaf", False)):
+                j += 1
+            seg = insns[i:j]
+            out += [x for x in seg if x.op != "W_CDINS"] + [x for x in seg if x.op == "W_CDINS"]
+            i = j
+        else:
+            out.append(insns[i])
+            i += 1
     return out
 
 

@@ -120,6 +120,7 @@ struct Insn {
   long long imm = 0;  // STORE_*: the traced record until encode
   bool chain = false;
   bool grid = false;  // SPILL_N of a grid table entry (form_grids): a fixed word, not a spill slot
+  bool cdleaf = false;  // a LEAF_N kept beside the W_CDINS that draws it again (fuse_checks)
 };
 
 int dst_cls(int op) {   // 'W', 'N' or 0 (isa.SHAPES[op][0])
@@ -710,6 +711,28 @@ struct Compiler {
     return v.l[0] < 0x80000000u;
   }
 
+  // a run of W_CDINS links and the leaves kept beside them: the leaves first,
+  // so the links stay adjacent and chain (compiler.py _hoist_cdins_leaves)
+  static std::vector<Insn> hoist_cdins_leaves(const std::vector<Insn>& in) {
+    std::vector<Insn> out;
+    out.reserve(in.size());
+    size_t i = 0;
+    while (i < in.size()) {
+      if (in[i].op == MW_W_CDINS || in[i].cdleaf) {
+        size_t j = i;
+        while (j < in.size() && (in[j].op == MW_W_CDINS || in[j].cdleaf)) ++j;
+        for (size_t k = i; k < j; ++k)
+          if (in[k].op != MW_W_CDINS) out.push_back(in[k]);
+        for (size_t k = i; k < j; ++k)
+          if (in[k].op == MW_W_CDINS) out.push_back(in[k]);
+        i = j;
+      } else {
+        out.push_back(in[i++]);
+      }
+    }
+    return out;
+  }
+
   // ------------------------------------------------------------------ grids (compiler.py _form_grids)
   static constexpr size_t GRID_MIN = 64, GRID_MAX_N = 32;
   struct OKey {
@@ -940,9 +963,14 @@ struct Compiler {
                   q1.op == MW_LEAF_N && q2.op == MW_N_ITE && is_def(q2.s[0], q1) && q2.s[1].kind == O_CONST &&
                   kv[q2.s[1].v].zero() && is_def(q2.s[2], q0) &&
                   ((q3.op == MW_W_INSN && is_def(q3.s[1], q2)) || (q3.op == MW_W_ZEXTN && is_def(q3.s[0], q2)));
-        ok = ok && q0.dst >= 0 && q1.dst >= 0 && q2.dst >= 0 && uses[q0.dst] == 1 && uses[q1.dst] == 1 &&
-             uses[q2.dst] == 1 && q1.imm < (1 << 16);
+        ok = ok && q0.dst >= 0 && q1.dst >= 0 && q2.dst >= 0 && uses[q0.dst] == 1 && uses[q2.dst] == 1 &&
+             q1.imm < (1 << 16);
         if (ok) {
+          if (uses[q1.dst] > 1) {   // the leaf has other uses: it stays, W_CDINS draws it again
+            Insn l = q1;
+            l.cdleaf = true;
+            out.push_back(l);
+          }
           Opnd acc = q3.op == MW_W_INSN ? q3.s[0] : mkconst(K256{}, 'W');
           long long off = q3.op == MW_W_INSN ? q3.imm : 0;
           Insn c;
@@ -962,7 +990,7 @@ struct Compiler {
       out.push_back(x);
       i += 1;
     }
-    out = form_grids(fuse_keyed_premises(out));
+    out = form_grids(fuse_keyed_premises(hoist_cdins_leaves(out)));
     uses = use_counts(out);
     for (size_t i = 0; i + 1 < out.size(); ++i) {
       Insn& a = out[i];

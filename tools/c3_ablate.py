@@ -48,6 +48,9 @@ def main():
     variants = {
         "full": set(),
         "no_impeq": {"CHECK_IMPEQ", "CHECK_IMPEQK"},
+        "no_grid_rows": {"CHECK_GRID"},
+        "no_leaf_n": {"LEAF_N"},
+        "no_byte_inserts": {"N_SLT", "N_ITE", "W_INSN"},
         "no_checks": checks,
         "no_spills": spills,
         "no_checks_spills": checks | spills,
