@@ -825,8 +825,11 @@ def _form_grids(insns: List[MInsn]) -> List[MInsn]:
         if ins.op == "CHECK_IMPEQK" and isinstance(ins.srcs[0], VReg):
             groups.setdefault(ins.srcs[0].id, []).append(i)
     defpos = {ins.dst.id: i for i, ins in enumerate(insns) if ins.dst is not None}
+    nextid = 1 + max((v.id for ins in insns for v in ([ins.dst] if ins.dst is not None else []) + list(ins.srcs)
+                      if isinstance(v, VReg)), default=-1)
     drop: set = set()
     after: Dict[int, List[MInsn]] = {}
+    redrawn: set = set()
     t0 = 0
     for kid, pos in groups.items():
         if len(pos) < GRID_MIN:
@@ -844,6 +847,15 @@ def _form_grids(insns: List[MInsn]) -> List[MInsn]:
         width = insns[pos[0]].width
         for r, (opnd, E, lastp) in rows.items():
             at = lastp if lastp > put else put
+            d = insns[defpos[opnd.id]] if isinstance(opnd, VReg) else None
+            if d is not None and d.op == "LEAF_N" and defpos[opnd.id] < put:
+                # a leaf defined before the table: drawn again at its row rather
+                # than kept live (a spill and a fill) across the program
+                fresh = VReg(nextid, "N")
+                nextid += 1
+                after.setdefault(at, []).append(MInsn("LEAF_N", d.width, fresh, [], imm=d.imm))
+                redrawn.add(opnd.id)
+                opnd = fresh
             after.setdefault(at, []).append(MInsn("CHECK_GRID", width, None, [key, opnd, ("raw", t0 | (n - 1) << 10)],
                                                   imm=E))
         drop.update(pos)
@@ -855,6 +867,10 @@ def _form_grids(insns: List[MInsn]) -> List[MInsn]:
         if i not in drop:
             out.append(ins)
         out.extend(after.get(i, ()))
+    if redrawn:   # the leaves drawn again that nothing else reads any more
+        uses = _uses(out)
+        out = [ins for ins in out if not (ins.op == "LEAF_N" and ins.dst is not None and ins.dst.id in redrawn
+                                          and not uses.get(ins.dst.id, 0))]
     return out
 
 

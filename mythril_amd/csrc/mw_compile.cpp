@@ -868,6 +868,8 @@ struct Compiler {
       if (in[i].dst >= 0) defpos[in[i].dst] = (int)i;
     std::vector<char> drop(in.size(), 0);
     std::vector<std::vector<Insn>> after(in.size());
+    std::vector<char> redrawn(vcls.size(), 0);
+    bool any_redrawn = false;
     int t0 = 0;
     bool any = false;
     for (size_t g = 0; g < gkey.size(); ++g) {
@@ -893,12 +895,29 @@ struct Compiler {
       int width = in[pos[0]].width;
       for (size_t r = 0; r < gp.rowop.size(); ++r) {
         int at = gp.rowlast[r] > put ? gp.rowlast[r] : put;
+        Opnd opnd = gp.rowop[r];
+        if (is_v(opnd) && in[defpos[opnd.v]].op == MW_LEAF_N && defpos[opnd.v] < put) {
+          // a leaf defined before the table: drawn again at its row rather than
+          // kept live (a spill and a fill) across the program
+          const Insn& d = in[defpos[opnd.v]];
+          Insn l;
+          l.op = MW_LEAF_N;
+          l.width = d.width;
+          l.dst = (int)vcls.size();
+          vcls.push_back('N');
+          l.ns = 0;
+          l.imm = d.imm;
+          after[at].push_back(l);
+          redrawn[opnd.v] = 1;
+          any_redrawn = true;
+          opnd = Opnd{O_VREG, l.dst};
+        }
         Insn c;
         c.op = MW_CHECK_GRID;
         c.width = width;
         c.ns = 3;
         c.s[0] = key;
-        c.s[1] = gp.rowop[r];
+        c.s[1] = opnd;
         c.s[2] = Opnd{O_RAW, t0 | (n - 1) << 10};
         c.imm = gp.rowE[r];
         after[at].push_back(c);
@@ -913,6 +932,15 @@ struct Compiler {
     for (size_t i = 0; i < in.size(); ++i) {
       if (!drop[i]) out.push_back(in[i]);
       for (const Insn& a : after[i]) out.push_back(a);
+    }
+    if (any_redrawn) {   // the leaves drawn again that nothing else reads any more
+      std::vector<int> u = use_counts(out);
+      std::vector<Insn> kept;
+      kept.reserve(out.size());
+      for (const Insn& x : out)
+        if (!(x.op == MW_LEAF_N && x.dst >= 0 && x.dst < (int)redrawn.size() && redrawn[x.dst] && u[x.dst] == 0))
+          kept.push_back(x);
+      out.swap(kept);
     }
     return out;
   }

@@ -121,10 +121,14 @@ def test_incomplete_grid_stays_checks():
     assert sum(i.op == "CHECK_GRID" for i in out) == len(syms)
     assert not any(i.op == "CHECK_IMPEQK" for i in out)
     puts = {id(i.srcs[0]): i.imm for i in out if i.op == "GRID_PUT"}
+    # the rows' leaves are drawn again at the row (defined before the table):
+    # the fresh register's LEAF_N names the original leaf (imm = its id here)
+    drawn = {i.dst.id: i.imm for i in out if i.op == "LEAF_N"}
+    assert sum(i.op == "LEAF_N" for i in out) == 1 + len(syms) + len(cons)   # key, cells, redrawn bytes
     # row of t_k: (key = 100 + K - k) <=> j = E - key = table offset of cell K
     for i in out:
         if i.op == "CHECK_GRID":
-            k = syms.index(i.srcs[1])
+            k = [t.id for t in syms].index(drawn[i.srcs[1].id])
             for K, b in enumerate(cons):
                 assert (i.imm - (100 + K - k)) & 0xFFFFFFFF == puts[id(b)], (k, K)
 
