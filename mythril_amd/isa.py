@@ -142,9 +142,10 @@ ASM_FUSED_MAX = 4
 ASM_FUSED = [
     ("N_SLT", "LEAF_N", "N_ITE", "N_SHLI"),   # a calldata byte behind its bounds guard, shifted into place
     # round 5: the same byte inserted into its word when the leaf has another
-    # use (a congruence grid's row: no W_CDINS), and a row after its value's fill
+    # use, and a grid row after its value's leaf (drawn again there) or fill
     ("N_SLT", "LEAF_N", "N_ITE", "W_INSN"),
     ("LEAF_N", "N_ITE", "W_INSN"),
+    ("LEAF_N", "CHECK_GRID"),
     ("FILL_N", "CHECK_GRID"),
     ("N_EQ", "N_EQ", "N_OR", "N_EQ"),
     ("LEAF_W", "LEAF_W", "N_ULE", "CHECK"),
