@@ -276,6 +276,7 @@ def _prebuild_witness_programs(queries) -> bool:
 # most QUARTER_MAX_GROWTH in instructions (profiles/r5c: the quarter kernel
 # runs the LASER group 1.28x as fast as the narrow and wide ones).
 QUARTER_SLOTS = (5, 16)
+NARROW_SLOTS = (8, 24)      # the narrow layout's files (asmgen.py variant "narrow")
 # ... and only when the search left is long enough to repay that compile
 # (~0.3 ms host, the quarter kernel ~25 % faster): candidates x instructions
 # at least this (profiles/r5f: for a 2^22-candidate LASER miss, 0.32 ms of
@@ -316,8 +317,28 @@ def _quarter_program(q: "Query") -> Program:
         return p
     if (qp.n_insn > QUARTER_MAX_GROWTH * p.n_insn or qp.n_spill + _pool_rows(qp) > QUARTER_LDS_WORDS
             or not np.array_equal(qp.leaves, p.leaves) or not np.array_equal(qp.pool, p.pool)):
-        return p
+        return _narrow_program(q, fixed)
     return qp
+
+
+def _narrow_program(q: "Query", fixed) -> Program:
+    """A wide-layout program recompiled into the narrow layout's 24 N slots
+    (three waves per SIMD instead of two) when that costs at most
+    QUARTER_MAX_GROWTH in instructions (C3 with grids: 35 N slots -> 24,
+    460 -> 480 instructions)."""
+    p = q.program
+    w, n = _slots_used(p)
+    if w <= NARROW_SLOTS[0] and n <= NARROW_SLOTS[1]:
+        return p
+    try:
+        np_ = compile_query(q.lowered.conjuncts, leaf_specs=fixed, reach=(q.lowered.flat, q.lowered.nodes),
+                            slots=NARROW_SLOTS)
+    except Exception:   # noqa: BLE001 - the program as it is
+        return p
+    if (np_.n_insn > QUARTER_MAX_GROWTH * p.n_insn
+            or not np.array_equal(np_.leaves, p.leaves) or not np.array_equal(np_.pool, p.pool)):
+        return p
+    return np_
 
 
 def search_program(q: "Query", candidates: int) -> Program:
