@@ -227,10 +227,16 @@ def search_phased(dev, dps, seed: int, begin: int, count: int, flags: int, long_
         rdps, extra = [], []
         try:
             for i in rest:
-                lp = long_programs[i](count - PROBE_CANDIDATES) if long_programs is not None else None
+                # a program with an assembled kernel attached keeps it (ADVICE r5:
+                # the long program would run on the interpreter instead)
+                lp = long_programs[i](count - PROBE_CANDIDATES) \
+                    if long_programs is not None and not getattr(dps[i], "assembled", None) else None
                 if lp is not None and lp is not dps[i].prog:
-                    extra.append(dev.load(lp))
-                    rdps.append(extra[-1])
+                    d = dev.load(lp)
+                    extra.append(d)
+                    # the recompile is for the asm interpreter; on any other
+                    # engine it is only longer (engine_of is the loader's choice)
+                    rdps.append(d if not hasattr(dev, "engine_of") or dev.engine_of(d) == "asm" else dps[i])
                 else:
                     rdps.append(dps[i])
             f2, st2 = dev.search(rdps, seed, begin + PROBE_CANDIDATES, count - PROBE_CANDIDATES, flags)
@@ -282,8 +288,9 @@ NARROW_SLOTS = (8, 24)      # the narrow layout's files (asmgen.py variant "narr
 # at least this (profiles/r5f: for a 2^22-candidate LASER miss, 0.32 ms of
 # kernel, the recompile cost more than it saved)
 LONG_PROGRAM_MIN_WORK = 1 << 31
-QUARTER_LDS_WORDS = 40
+QUARTER_LDS_WORDS = isa.ASM_LDS_WORDS["quarter"]
 QUARTER_MAX_GROWTH = 1.3
+NARROW_MAX_GLOBAL_SPILL = 8
 
 
 def _slots_used(p: Program) -> Tuple[int, int]:
@@ -304,18 +311,47 @@ def _pool_rows(p: Program) -> int:
     return (int(p.pool.size) + 255) // 256 if p.pool is not None else 0
 
 
+def _lands_on(p: Program, layout: str) -> bool:
+    """Whether the loader (mw_prog_load) puts p on the asm kernel of this
+    register layout: its narrow constants fit the layout's constant
+    registers, and its pool (the quarter layout: its spill words too) fits
+    the layout's LDS budget.  Register files are the compile's own slots."""
+    if len(isa.asm_narrow_constants(p.code, p.consts)) > isa.ASM_NK_BY_LAYOUT[layout]:
+        return False
+    rows = _pool_rows(p)
+    if layout == "quarter":
+        return p.n_spill + rows <= isa.ASM_LDS_WORDS["quarter"]
+    return rows <= isa.ASM_LDS_WORDS[layout]
+
+
+def _global_spill(p: Program, layout: str) -> int:
+    """Spill words per thread that fall outside the layout's LDS budget (the global spill buffer)."""
+    return max(0, p.n_spill + _pool_rows(p) - isa.ASM_LDS_WORDS[layout])
+
+
 def _quarter_program(q: "Query") -> Program:
+    """q.long_program's compile: only programs the asm
+    interpreter runs are recompiled, only into layouts whose switch is on,
+    and a recompiled program is kept only if the loader will put it on the
+    kernel it was compiled for (_lands_on) - otherwise it would run with more
+    instructions on a wider kernel or the compiled interpreter, a pure loss."""
     p = q.program
+    sw = isa.asm_switches()
+    if not sw["narrow"] or not isa.asm_eligible(p.code, p.leaves, p.consts):
+        return p
     w, n = _slots_used(p)
     if (w <= QUARTER_SLOTS[0] and n <= QUARTER_SLOTS[1]) or _pool_rows(p) >= QUARTER_LDS_WORDS:
         return p       # fits already (the loader picks the quarter kernel), or its pool alone fills the budget
     fixed = {s.name: dataclasses.replace(s, pool=None if s.pool is None else list(s.pool)) for s in p.leaf_specs}
+    if not sw["quarter"]:
+        return _narrow_program(q, fixed)
     try:
         qp = compile_query(q.lowered.conjuncts, leaf_specs=fixed, reach=(q.lowered.flat, q.lowered.nodes),
                            slots=QUARTER_SLOTS)
     except Exception:   # noqa: BLE001 - the program as it is
         return p
-    if (qp.n_insn > QUARTER_MAX_GROWTH * p.n_insn or qp.n_spill + _pool_rows(qp) > QUARTER_LDS_WORDS
+    if (qp.n_insn > QUARTER_MAX_GROWTH * p.n_insn or not _lands_on(qp, "quarter")
+            or not isa.asm_eligible(qp.code, qp.leaves, qp.consts)
             or not np.array_equal(qp.leaves, p.leaves) or not np.array_equal(qp.pool, p.pool)):
         return _narrow_program(q, fixed)
     return qp
@@ -325,7 +361,10 @@ def _narrow_program(q: "Query", fixed) -> Program:
     """A wide-layout program recompiled into the narrow layout's 24 N slots
     (three waves per SIMD instead of two) when that costs at most
     QUARTER_MAX_GROWTH in instructions (C3 with grids: 35 N slots -> 24,
-    460 -> 480 instructions)."""
+    460 -> 480 instructions), lands on the narrow kernel, and puts at most
+    NARROW_MAX_GLOBAL_SPILL more spill words in global memory than the
+    original does on the wide one (C3: 6 words past the 52-word budget, and
+    still 1.27x as fast, profiles/r5zd)."""
     p = q.program
     w, n = _slots_used(p)
     if w <= NARROW_SLOTS[0] and n <= NARROW_SLOTS[1]:
@@ -335,7 +374,9 @@ def _narrow_program(q: "Query", fixed) -> Program:
                             slots=NARROW_SLOTS)
     except Exception:   # noqa: BLE001 - the program as it is
         return p
-    if (np_.n_insn > QUARTER_MAX_GROWTH * p.n_insn
+    if (np_.n_insn > QUARTER_MAX_GROWTH * p.n_insn or not _lands_on(np_, "narrow")
+            or not isa.asm_eligible(np_.code, np_.leaves, np_.consts)
+            or _global_spill(np_, "narrow") > _global_spill(p, "wide") + NARROW_MAX_GLOBAL_SPILL
             or not np.array_equal(np_.leaves, p.leaves) or not np.array_equal(np_.pool, p.pool)):
         return p
     return np_

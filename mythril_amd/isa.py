@@ -192,6 +192,22 @@ def asm_fused_dispatch(code):
 
 # narrow (N-class) constants the asm interpreter holds in VGPRs (mw_isa.h MW_ASM_NK)
 ASM_NK = 16
+# per register layout of the asm interpreter (asmgen.py NKN, mw_asm_interp.inc
+# MW_ASM_NK_N / MW_ASM_NK_Q): how many narrow constants fit its constant
+# registers, and its LDS budget in words per thread (mw_kernels.hip
+# kLdsSpillWordsByLayout: pool rows plus spill words)
+ASM_NK_BY_LAYOUT = {"wide": ASM_NK, "narrow": ASM_NK - 2, "quarter": 4}
+ASM_LDS_WORDS = {"wide": 80, "narrow": 52, "quarter": 40}
+
+
+def asm_switches() -> dict:
+    """The loader's layout switches (mw_kernels.hip asm_enabled /
+    asm_narrow_enabled / asm_quarter_enabled), read from the same variables."""
+    import os
+    off = lambda k: os.environ.get(k, "1")[:1] == "0"   # noqa: E731
+    asm = not off("MYTHRIL_AMD_ASM")
+    narrow = asm and not off("MYTHRIL_AMD_ASM_NARROW")
+    return {"asm": asm, "narrow": narrow, "quarter": narrow and not off("MYTHRIL_AMD_ASM_QUARTER")}
 
 
 def asm_narrow_constants(code, consts):

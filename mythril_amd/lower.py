@@ -320,8 +320,20 @@ class _Rewriter:
             nm = f"{base}@" + ",".join(f"{a.val:x}" for a in args)
         else:
             key = (base,) + tuple(("t", a.id) for a in args)
-            nm = f"{base}@s{_shash_args(self.ctx, args):016x}"
+            nm = self._unique_name(f"{base}@s{_shash_args(self.ctx, args):016x}", args)
         return key, nm
+
+    def _unique_name(self, nm: str, args: Tuple[Node, ...]) -> str:
+        """nm for these argument terms, made unique in the context: a 64-bit
+        structural hash that collides for two different argument tuples gets a
+        suffix, so two reads never merge into one leaf (the context
+        is hash-consed, so equal terms have equal ids)."""
+        names = self.ctx.__dict__.setdefault("_ack_names", {})
+        ids, base, k = tuple(a.id for a in args), nm, 0
+        while names.setdefault(nm, ids) != ids:
+            k += 1
+            nm = f"{base}~{k}"
+        return nm
 
     def read_leaf(self, kind: str, base: str, args: Tuple[Node, ...], width: int) -> Node:
         key, nm = self._key_name(base, args)
@@ -338,7 +350,7 @@ class _Rewriter:
         """An application whose value is a term (no free leaf); still congruence-checked."""
         key = ("def", base) + tuple(("t", a.id) for a in args)
         if key not in self.leaf_of_key:
-            nm = f"{base}@d{_shash_args(self.ctx, args):016x}"
+            nm = self._unique_name(f"{base}@d{_shash_args(self.ctx, args):016x}", args)
             al = AckLeaf(nm, "apply", base, args, width, value=value)
             self.ack[nm] = al
             self.by_base.setdefault(("apply", base), []).append(al)

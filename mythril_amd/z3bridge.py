@@ -89,7 +89,7 @@ class ConjunctCache:
                 self.walker = z3walk.Z3Walker(z3, self.ctx)
                 self.decls = self.walker.decls     # one table: the walker declares what it meets
 
-    def to_ir(self, raws: Sequence) -> Script:
+    def to_ir(self, raws: Sequence, _retried: bool = False) -> Script:
         if len(self.ctx.nodes) > self.max_nodes or len(self.entries) > self.max_entries:
             self.reset()
             self.stats["resets"] += 1
@@ -108,9 +108,18 @@ class ConjunctCache:
             new = [raws[i] for i in missing]
             nodes = None
             if self.walker is not None:
+                from .z3walk import SortConflict
                 try:
                     nodes = [self.walker.term(r) for r in new]
                     self.stats["walked"] += len(new)
+                except SortConflict:
+                    # a name this context holds with another sort: once on a fresh
+                    # context, then the reference solver
+                    if _retried:
+                        raise
+                    self.reset()
+                    self.stats["resets"] += 1
+                    return self.to_ir(raws, _retried=True)
                 except Unsupported as e:       # the text route below answers (and fails closed itself)
                     log.debug("z3walk: %s; printing the conjuncts instead", e)
             if nodes is None:
@@ -121,9 +130,14 @@ class ConjunctCache:
                 for name, d in sc.decls.items():
                     old = self.decls.get(name)
                     if old is not None and (old.sort != d.sort or old.args != d.args):
-                        # one name, two sorts: the shared context cannot hold both
+                        # one name, two sorts: the shared context cannot hold both.
+                        # One retry on a fresh context; a set that conflicts with
+                        # itself goes to the reference solver (no loop)
+                        if _retried:
+                            raise Unsupported(f"z3bridge: '{name}' declared with two sorts in one set")
                         self.reset()
-                        return self.to_ir(raws)
+                        self.stats["resets"] += 1
+                        return self.to_ir(raws, _retried=True)
                     self.decls[name] = d
                 nodes = sc.asserts
             for i, r, n in zip(missing, new, nodes):
@@ -139,6 +153,11 @@ class ConjunctCache:
 _cache: Optional[ConjunctCache] = None
 CACHE_CONJUNCTS = os.environ.get("MYTHRIL_AMD_CONJUNCT_CACHE", "1") != "0"
 WALK_ASTS = os.environ.get("MYTHRIL_AMD_Z3_WALK", "1") != "0"     # z3walk, else print + parse
+# a witness z3 confirms only past the pinned budget: "confirm" (default) keeps
+# it, with the rest of the query's budget for that second check; "reference"
+# hands the query to the reference solver instead, whose own check on the
+# unpinned formula may time out there (unknown -> UnsatError, model.py:58-63)
+SLOW_RECHECK = os.environ.get("MYTHRIL_AMD_SLOW_RECHECK", "confirm")
 
 
 def to_ir(raws: Sequence, ctx: Optional[Ctx] = None) -> Script:
@@ -171,7 +190,11 @@ def recheck(raws: Sequence, script: Script, w: Witness, timeout_ms: int, pinned_
     m = model_from_witness(raws, script, w, min(timeout_ms, pinned_ms))
     if m is not None or pinned_ms >= timeout_ms or last_check().get("result") != "unknown":
         return m, False
-    m = model_from_witness(raws, script, w, timeout_ms)
+    if SLOW_RECHECK == "reference":
+        return None, False      # the reference solver answers the query
+    # the second check gets what is left of the query's own budget, so the
+    # two z3 calls together stay within it
+    m = model_from_witness(raws, script, w, timeout_ms - pinned_ms)
     return m, m is not None
 
 

@@ -26,6 +26,10 @@ from .compiler import Unsupported
 from .ir import BOOL, Ctx, Node
 from .smt2 import Decl, Sort
 
+
+class SortConflict(Unsupported):
+    """One symbol name met with two sorts (z3 allows it; one IR context cannot hold both)."""
+
 # z3 operator kind name -> IR op (SMT-LIB names; the _I division variants as
 # the parser's ALIASES read them)
 _OPS = {
@@ -91,7 +95,7 @@ class Z3Walker:
         if old is None:
             self.decls[name] = Decl(name, args, sort)
         elif old.sort != sort or old.args != args:
-            raise Unsupported(f"z3walk: {name} declared with two sorts")
+            raise SortConflict(f"z3walk: {name} declared with two sorts")
 
     def term(self, root) -> Node:
         """The IR term of one z3 expression (operands first, iteratively)."""

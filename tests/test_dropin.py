@@ -477,9 +477,18 @@ def test_slow_recheck_is_counted_and_logged(mythril, monkeypatch, caplog):
     with caplog.at_level("WARNING"):
         res = dropin.get_model(SAT)
     assert res.raw[0][0] == "z3"
-    assert calls == [dropin.PINNED_CHECK_MS, mythril.args.solver_timeout]
+    # the second check gets the rest of the query's budget
+    assert calls == [dropin.PINNED_CHECK_MS, mythril.args.solver_timeout - dropin.PINNED_CHECK_MS]
     assert dropin.STATS["slow_rechecks"] == n0 + 1
     assert "pinned re-check budget" in caplog.text
+    # MYTHRIL_AMD_SLOW_RECHECK=reference: the reference solver answers instead
+    dropin.get_model.cache_clear()
+    dropin._memo.clear()
+    calls.clear()
+    monkeypatch.setattr(z3bridge, "SLOW_RECHECK", "reference")
+    assert dropin.get_model(SAT).raw[0] == "ref"
+    assert calls == [dropin.PINNED_CHECK_MS]
+    monkeypatch.setattr(z3bridge, "SLOW_RECHECK", "confirm")
     # an unsat answer under the pinned budget is final: no second check
     dropin.get_model.cache_clear()
     dropin._memo.clear()

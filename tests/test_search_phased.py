@@ -103,3 +103,68 @@ def test_search_program_repays_its_compile():
     assert np.array_equal(long_.leaves, q.program.leaves) and np.array_equal(long_.pool, q.program.pool)
     w, nn = engine._slots_used(long_)
     assert w <= engine.QUARTER_SLOTS[0] and nn <= engine.QUARTER_SLOTS[1]
+
+
+def test_an_assembled_program_keeps_its_kernel():
+    """when WitnessEngine._assemble attached an assembled kernel,
+    the launch after the probe keeps that program (the long program would run
+    on the interpreter); a long program the loader puts on another engine
+    than the asm interpreter is not used either."""
+    syn, dev, dp = _setup()
+    begin = WITNESS - engine.PROBE_CANDIDATES - 5000
+    count = 1 << 18
+    long_prog = compile_program(syn.conjuncts, slots=(4, 16))
+    asked = []
+
+    def lp(n):
+        asked.append(n)
+        return long_prog
+    dp.assembled = "mw_asmjit_test"
+    dev.ranges.clear()
+    found, _ = engine.search_phased(dev, [dp], syn.seed, begin, count, FLAGS, [lp])
+    assert found == [WITNESS] and asked == []
+    dp.assembled = None
+    searched = []
+    real_search = dev.search
+
+    def search(dps, *a, **k):
+        searched.append([d.prog for d in dps])
+        return real_search(dps, *a, **k)
+    dev.search = search
+    dev.engine_of = lambda d: "interp"
+    found, _ = engine.search_phased(dev, [dp], syn.seed, begin, count, FLAGS, [lp])
+    assert found == [WITNESS] and asked and searched[-1] == [dp.prog]
+    dev.engine_of = lambda d: "asm"
+    engine.search_phased(dev, [dp], syn.seed, begin, count, FLAGS, [lp])
+    assert searched[-1] == [long_prog]
+
+
+def test_long_program_respects_layout_switches(monkeypatch):
+    """ADVICE r5: MYTHRIL_AMD_ASM=0 / _NARROW=0 keep the program as it is;
+    _QUARTER=0 allows the narrow layout only; a recompiled program always
+    fits the layout it was compiled for (narrow constants, LDS budget)."""
+    import os
+
+    from mythril_amd.smt2 import parse_file
+    from mythril_amd import isa
+    f = os.path.join(os.path.dirname(__file__), "golden", "laser",
+                     "calls_t2_fixed_address_q14_EtherThief_unknown.smt2.gz")
+    s = parse_file(f)
+    for var in ("MYTHRIL_AMD_ASM", "MYTHRIL_AMD_ASM_NARROW"):
+        monkeypatch.setenv(var, "0")
+        q = engine.prepare(s.asserts, s.ctx)
+        assert q.long_program is q.program, var
+        monkeypatch.delenv(var)
+    monkeypatch.setenv("MYTHRIL_AMD_ASM_QUARTER", "0")
+    q = engine.prepare(s.asserts, s.ctx)
+    lp = q.long_program
+    w, n = engine._slots_used(lp)
+    assert w <= engine.NARROW_SLOTS[0] and n <= engine.NARROW_SLOTS[1]
+    if lp is not q.program:
+        assert engine._lands_on(lp, "narrow") and not engine._lands_on(lp, "quarter") or \
+            (w > engine.QUARTER_SLOTS[0] or n > engine.QUARTER_SLOTS[1])
+    monkeypatch.delenv("MYTHRIL_AMD_ASM_QUARTER")
+    q = engine.prepare(s.asserts, s.ctx)
+    lp = q.long_program
+    assert lp is not q.program and engine._lands_on(lp, "quarter")
+    assert len(isa.asm_narrow_constants(lp.code, lp.consts)) <= isa.ASM_NK_BY_LAYOUT["quarter"]

@@ -121,3 +121,25 @@ def test_decls_of_a_long_lived_cache_pin_the_witness(monkeypatch):
     assert z3bridge.model_from_witness(["raw"], script, Witness(0, {name: 5, "cd@3": 1})) is not None
     pinned = [p for p in fz.pins if isinstance(p, tuple) and p[0] == "pin"]
     assert [p[1] for p in pinned] == [name]
+
+
+def test_sort_conflicts_reset_once_and_fail_closed(monkeypatch):
+    """one name with two sorts across queries resets the cache once
+    and translates the new set; a set that uses one name with two sorts
+    itself is refused after that one retry (the reference solver answers),
+    not retried until a RecursionError."""
+    z = fakez3.module()
+    monkeypatch.setitem(sys.modules, "z3", z)
+    c1, c2 = Ctx(), Ctx()
+    a8 = c1.app("bvugt", c1.var("x", 8), c1.const(1, 8))
+    a16 = c2.app("bvugt", c2.var("x", 16), c2.const(1, 16))
+    cache = z3bridge.ConjunctCache()
+    s = cache.to_ir([z.ast(a8)])
+    assert s.asserts[0].args[0].width == 8
+    s = cache.to_ir([z.ast(a16)])
+    assert s.asserts[0].args[0].width == 16 and cache.stats["resets"] <= 1
+    resets = cache.stats["resets"]
+    with pytest.raises(Exception) as ei:
+        cache.to_ir([z.ast(a8), z.ast(a16)])
+    assert not isinstance(ei.value, RecursionError)
+    assert cache.stats["resets"] <= resets + 1
