@@ -176,6 +176,14 @@ int mg_validate_desc(const mg_prog_desc* desc);
 
 const char* mg_last_error(void);
 
+/* Debugging (not a reference crossing): the C-ABI calls in flight on every
+ * thread, one line each ("tid=... <call>/<step> arg=N call_ms=T step_ms=T"),
+ * written NUL-terminated into buf (at most n bytes); returns how many calls
+ * are in flight.  Lock-free: safe from a watchdog thread while another thread
+ * is stuck inside a call.  A step slower than MYTHRIL_AMD_SLOW_STEP_MS
+ * (default 2000) also prints one line on stderr when it ends. */
+int mg_debug_inflight(char* buf, size_t n);
+
 #ifdef __cplusplus
 }
 #endif

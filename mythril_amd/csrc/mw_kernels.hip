@@ -27,6 +27,7 @@
 #include "mw_asm_abi.h"
 #include "mw_asm_interp.inc"
 #include "mw_handles.h"
+#include "mw_inflight.h"
 #include "mw_interp.h"
 #include "mw_keccak.h"
 #include "mw_leaf.h"
@@ -604,8 +605,10 @@ void* pool_get(Ctx* c, size_t bytes, size_t* cls) {
     return q;
   }
   void* q = nullptr;
+  mw::inflight_step("pool_get/hipMalloc", k);
   if (hipMalloc(&q, k) == hipSuccess) return q;
   (void)hipGetLastError();
+  mw::inflight_step("pool_get/drain", c->pool_cached);
   pool_drain(c);   // memory pressure: give the cached buffers back and try once more
   if (hipMalloc(&q, k) == hipSuccess) return q;
   (void)hipGetLastError();
@@ -616,6 +619,7 @@ void pool_put(Ctx* c, void* q, size_t cls) {
   if (!q) return;
   if (g_pool_cached.fetch_add(cls) + cls > pool_cache_limit()) {
     g_pool_cached -= cls;
+    mw::inflight_step("pool_put/hipFree", cls);
     hipFree(q);
     return;
   }
@@ -641,6 +645,7 @@ struct Scratch {
 
 void release_prog(Prog& p) {
   hipSetDevice(p.ctx->dev);
+  mw::inflight_step("release_prog/unload");
   p.unload();
   // every call on the context synchronises before it returns (and this runs
   // under the context's mu): no kernel still reads the buffer.  Only
@@ -652,8 +657,11 @@ void release_prog(Prog& p) {
 
 void release_ctx(Ctx& c) {
   hipSetDevice(c.dev);
+  mw::inflight_step("release_ctx/sync");
   if (c.stream) hipStreamSynchronize(c.stream);
+  mw::inflight_step("release_ctx/drain", c.pool_cached);
   pool_drain(&c);
+  mw::inflight_step("release_ctx/free");
   if (c.d_spill) hipFree(c.d_spill);
   if (c.d_blk) hipFree(c.d_blk);
   if (c.h_blk) hipHostFree(c.h_blk);
@@ -692,6 +700,7 @@ int ensure_launch(Ctx* c, size_t nmin, size_t nargs) {
   const size_t off_progs = up(off_min + nmin * sizeof(u64));
   const size_t off_args = up(off_progs + nmin * sizeof(ProgDev));
   const size_t bytes = up(off_args + nargs * sizeof(AsmArgs));
+  mw::inflight_step("ensure_launch/realloc", bytes);
   if (c->d_blk) HIPCHK(hipFree(c->d_blk));
   if (c->h_blk) HIPCHK(hipHostFree(c->h_blk));
   c->d_blk = c->h_blk = nullptr;
@@ -752,6 +761,7 @@ int launch_assembled(Ctx* c, const Prog* p, u32 gx, const ProgDev* dprog, const 
 
 int ensure_spill(Ctx* c, size_t bytes) {
   if (bytes <= c->spill_bytes) return 0;
+  mw::inflight_step("ensure_spill/realloc", bytes);
   if (c->d_spill) HIPCHK(hipFree(c->d_spill));
   c->d_spill = nullptr;
   c->spill_bytes = 0;
@@ -940,6 +950,7 @@ int mg_device_count(int* n) {
 }
 
 int mg_init(int device, mg_ctx** out) {
+  mw::CallMark mark("mg_init");
   if (!out) return fail(MG_E_ARG, "null out");
   *out = nullptr;
   int n = 0;
@@ -948,9 +959,11 @@ int mg_init(int device, mg_ctx** out) {
   HIPCHK(hipSetDevice(device));
   auto c = std::make_shared<Ctx>();
   c->dev = device;
+  mark.step("properties");
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->ncu = prop.multiProcessorCount;
+  mark.step("stream");
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
       ensure_launch(c.get(), 16, 4) != 0) {
@@ -959,6 +972,7 @@ int mg_init(int device, mg_ctx** out) {
   }
   // allow the LDS spill area (up to kLdsSpillWords x 1 KiB) beyond the 64 KiB default
   const int lds_max = (int)(kLdsSpillWords * kBlock * sizeof(u32));
+  mark.step("attributes");
   if (hipFuncSetAttribute((const void*)mw_search_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
           hipSuccess ||
       hipFuncSetAttribute((const void*)mw_search_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_max) !=
@@ -973,6 +987,7 @@ int mg_init(int device, mg_ctx** out) {
           hipSuccess) {
     (void)hipGetLastError();  // older runtimes: the default limit already covers it
   }
+  mark.step("asm offsets");
   if (asm_enabled() && asm_handler_offsets(c->dev, c->stream) != 0) {
     (void)hipGetLastError();  // the asm interpreter stays off: the compiled interpreter runs every program
     std::fprintf(stderr, "[mythril_amd] asm interpreter disabled: %s\n", mg_last_error());
@@ -983,6 +998,8 @@ int mg_init(int device, mg_ctx** out) {
 
 int mg_free(mg_ctx* h) {
   if (!h) return 0;
+  mw::CallMark mark("mg_free");
+  mark.step("lock");
   // programs still loaded in this context are freed with it; a call in flight
   // on another thread finishes first (mw_handles.h free_ctx)
   if (!mw::free_ctx(g_reg, hid(h), release_prog, release_ctx)) return fail(MG_E_ARG, "mg_free: not a live context");
@@ -1008,11 +1025,14 @@ static bool trace_rows_covered(const mg_prog_desc* d) {
 int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   if (!h || !d || !out) return fail(MG_E_ARG, "null argument");
   *out = nullptr;
+  mw::CallMark mark("mg_prog_load");
   std::shared_ptr<Ctx> cref = g_reg.ctx(hid(h));
   if (!cref) return fail(MG_E_ARG, "mg_prog_load: not a live context");
+  mark.step("validate", d->ncode_words);
   int rc = mg_validate_desc(d);
   if (rc) return rc;
   Ctx* c = cref.get();
+  mark.step("lock");
   std::lock_guard<std::mutex> lk(c->mu);
   if (c->dead) return fail(MG_E_ARG, "mg_prog_load: the context was freed during the call");
   HIPCHK(hipSetDevice(c->dev));
@@ -1029,17 +1049,21 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   p->ctx = cref;
   p->desc = *d;
   p->ops_per_eval = d->ops_per_eval;
+  mark.step("signature", total);
   p->sig = prog_signature(d);
   p->trace_full = trace_rows_covered(d);
+  mark.step("pool_get", total * 4);
   p->d_buf = (u32*)pool_get(c, total * sizeof(u32), &p->buf_cls);
   if (!p->d_buf) return fail(MG_E_NOMEM, "program upload allocation failed");
   // stage in the context's pinned buffer (after the previous upload from it has landed)
+  mark.step("sync previous upload");
   if (c->up_pending && hipStreamSynchronize(c->stream) != hipSuccess) {
     release_prog(*p);
     return fail(MG_E_HIP, "program upload: stream synchronize failed");
   }
   c->up_pending = false;
   if (total * 4 > c->up_bytes) {
+    mark.step("staging regrow", total * 4);
     if (c->h_up) hipHostFree(c->h_up);
     c->h_up = nullptr;
     c->up_bytes = 0;
@@ -1050,6 +1074,7 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
     }
     c->up_bytes = want;
   }
+  mark.step("stage + predecode", total * 4);
   u32* hbuf = (u32*)c->h_up;
   std::memset(hbuf, 0, total * 4);
   std::memcpy(hbuf, d->code, nc * 4);
@@ -1083,6 +1108,7 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   }
   // queued on the context's stream: every launch that reads the program is
   // queued after it on the same stream
+  mark.step("upload", total * 4);
   if (hipMemcpyAsync(p->d_buf, hbuf, total * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
     release_prog(*p);
     return fail(MG_E_HIP, "program upload copy failed");
@@ -1113,6 +1139,8 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
 
 int mg_prog_free(mg_prog* h) {
   if (!h) return 0;
+  mw::CallMark mark("mg_prog_free");
+  mark.step("lock");
   if (!mw::free_prog(g_reg, hid(h), release_prog))
     return fail(MG_E_ARG, "mg_prog_free: not a live program (already freed, or freed with its context)");
   return 0;
@@ -1121,8 +1149,11 @@ int mg_prog_free(mg_prog* h) {
 int mg_prog_attach_kernel(mg_prog* h, const void* image, size_t size, const char* name) {
   if (!h || !image || !size || !name) return fail(MG_E_ARG, "null argument");
   if (std::strlen(name) > 200) return fail(MG_E_ARG, "kernel name too long");
+  mw::CallMark mark("mg_prog_attach_kernel");
+  mark.step("lock");
   CallG call;
   if (const char* why = mw::enter_prog(g_reg, hid(h), call)) return fail(MG_E_ARG, std::string("mg_prog_attach_kernel: ") + why);
+  mark.step("hipModuleLoadData", size);
   Ctx* c = call.c.get();
   Prog* p = call.ps[0].get();
   HIPCHK(hipSetDevice(c->dev));
@@ -1199,8 +1230,11 @@ int mg_prog_engine(const mg_prog* h) {
 int mg_prog_attach_asm(mg_prog* h, const void* image, size_t size, const char* name) {
   if (!h || !image || !size || !name) return fail(MG_E_ARG, "null argument");
   if (std::strlen(name) > 200) return fail(MG_E_ARG, "kernel name too long");
+  mw::CallMark mark("mg_prog_attach_asm");
+  mark.step("lock");
   CallG call;
   if (const char* why = mw::enter_prog(g_reg, hid(h), call)) return fail(MG_E_ARG, std::string("mg_prog_attach_asm: ") + why);
+  mark.step("hipModuleLoadData", size);
   Ctx* c = call.c.get();
   Prog* p = call.ps[0].get();
   if (!p->asm_ok) return fail(MG_E_PROG, "mg_prog_attach_asm: the program has opcodes the asm engines lack");
@@ -1240,11 +1274,14 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   if (count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad candidate range");
   std::vector<u64> ids(nprog);
   for (size_t i = 0; i < nprog; ++i) ids[i] = hid(hprogs[i]);
+  mw::CallMark mark("mg_search");
+  mark.step("lock", nprog);
   CallG call;   // resolved, reference-held and locked for the whole call (mw_handles.h)
   if (const char* why = mw::enter(g_reg, hid(h), ids.data(), nprog, call)) return fail(MG_E_ARG, std::string("mg_search: ") + why);
   Ctx* c = call.c.get();
   std::vector<const Prog*> progs(nprog);
   for (size_t i = 0; i < nprog; ++i) progs[i] = call.ps[i].get();
+  mark.step("plan", nprog);
   const double t0 = now_ms();
   HIPCHK(hipSetDevice(c->dev));
   (void)hipGetLastError();  // start from a clean error state: launch errors are read back below
@@ -1362,6 +1399,7 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     spill_need = std::max(spill_need, (size_t)(d.n_spill - r.nlds) * agx * kBlock * sizeof(u32));
   }
   const bool need_args = nasm || !gasb.empty();
+  mark.step("buffers", nprog);
   rc = ensure_launch(c, nprog, need_args ? ha.size() : 0);
   if (rc) return rc;
   if (nia) {
@@ -1384,6 +1422,7 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     aa.verdict = nullptr;
   }
   // one upload: zeroed counters, d_min at MG_NONE, the ProgDev and AsmArgs records
+  mark.step("enqueue", count);
   HIPCHK(stage_upload(c, nprog, hp.data(), nia, ha.data(), need_args ? ha.size() : 0));
   HIPCHK(hipEventRecord(c->e0, c->stream));
   for (int gi = 0; gi < kAsmLayouts; ++gi) {
@@ -1425,6 +1464,7 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   }
   HIPCHK(hipEventRecord(c->e1, c->stream));
   HIPCHK(stage_readback(c, nprog));   // counters and d_min, one copy
+  mark.step("sync", count);
   HIPCHK(hipStreamSynchronize(c->stream));
   const u64* stripes = (const u64*)c->h_blk;
   const u64* mins = (const u64*)(c->h_blk + c->off_min);
@@ -1459,6 +1499,7 @@ constexpr size_t kReadbackMax = (size_t)1 << 20;
 
 static bool ensure_readback(Ctx* c, size_t bytes) {
   if (bytes <= c->rb_bytes) return true;
+  mw::inflight_step("ensure_readback/realloc", bytes);
   if (c->h_rb) hipHostFree(c->h_rb);
   c->h_rb = nullptr;
   c->rb_bytes = 0;
@@ -1499,6 +1540,7 @@ static int eval_common(Ctx* c, const Prog* p, const uint32_t* leaves_soa, size_t
     if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, vb, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess && ntr) e = hipMemcpyAsync(trace, d_t, tb, hipMemcpyDeviceToHost, c->stream);
   }
+  mw::inflight_step("eval/sync", ncand);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   s_in.synced = s_vt.synced = e == hipSuccess;
   if (e != hipSuccess) return fail(MG_E_HIP, std::string("eval: ") + hipGetErrorString(e));
@@ -1514,8 +1556,11 @@ int mg_eval(mg_ctx* h, const mg_prog* hp, const uint32_t* leaves_soa, size_t nca
             uint32_t* trace) {
   if (!h || !hp) return fail(MG_E_ARG, "null argument");
   const u64 id = hid(hp);
+  mw::CallMark mark("mg_eval");
+  mark.step("lock", ncand);
   CallG call;
   if (const char* why = mw::enter(g_reg, hid(h), &id, 1, call)) return fail(MG_E_ARG, std::string("mg_eval: ") + why);
+  mark.step("eval", ncand);
   const Prog* p = call.ps[0].get();
   if (p->desc.nleaves && p->desc.n_input_rows && !leaves_soa) return fail(MG_E_ARG, "leaves_soa required");
   if (p->desc.nleaves && !p->desc.n_input_rows) return fail(MG_E_ARG, "program has no input rows");
@@ -1580,6 +1625,7 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
     if (e == hipSuccess) e = hipMemcpyAsync(verdict, d_v, vb, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess && ntr) e = hipMemcpyAsync(trace, d_t, tb, hipMemcpyDeviceToHost, c->stream);
   }
+  mw::inflight_step("eval_asm/sync", count);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   s_v.synced = e == hipSuccess;
   if (e != hipSuccess)
@@ -1597,9 +1643,12 @@ int mg_eval_generated(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t begi
                       uint32_t* verdict, uint32_t* trace) {
   if (!h || !hp) return fail(MG_E_ARG, "null argument");
   const u64 id = hid(hp);
+  mw::CallMark mark("mg_eval_generated");
+  mark.step("lock", count);
   CallG call;
   if (const char* why = mw::enter(g_reg, hid(h), &id, 1, call))
     return fail(MG_E_ARG, std::string("mg_eval_generated: ") + why);
+  mark.step("eval", count);
   Ctx* c = call.c.get();
   const Prog* p = call.ps[0].get();
   if (!p->jit_ready() && verdict && count) {
@@ -1630,9 +1679,12 @@ int mg_eval_generated(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t begi
 int mg_witness_leaves(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t index, uint32_t* out) {
   if (!h || !hp || !out) return fail(MG_E_ARG, "null argument");
   const u64 id = hid(hp);
+  mw::CallMark mark("mg_witness_leaves");
+  mark.step("lock");
   CallG call;
   if (const char* why = mw::enter(g_reg, hid(h), &id, 1, call))
     return fail(MG_E_ARG, std::string("mg_witness_leaves: ") + why);
+  mark.step("launch + sync");
   Ctx* c = call.c.get();
   const Prog* p = call.ps[0].get();
   const u32 nl = (u32)p->desc.nleaves;
@@ -1677,6 +1729,8 @@ int mg_valu_peak(mg_ctx* h, uint32_t mul, double* ops_per_s, double* kernel_ms) 
 int mg_keccak256_device(mg_ctx* h, const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len, size_t n,
                         uint8_t* d_out32, mg_stats* st) {
   if (!h || (!n)) return fail(MG_E_ARG, "bad argument");
+  mw::CallMark mark("mg_keccak256_device");
+  mark.step("lock", n);
   CallG call;
   if (const char* why = mw::enter(g_reg, hid(h), nullptr, 0, call)) return fail(MG_E_ARG, std::string("mg_keccak256: ") + why);
   Ctx* c = call.c.get();
@@ -1706,6 +1760,8 @@ int mg_keccak256_device(mg_ctx* h, const uint8_t* d_data, const uint64_t* d_off,
 int mg_keccak256(mg_ctx* h, const uint8_t* data, size_t ndata, const uint64_t* off, const uint32_t* len, size_t n,
                  uint8_t* out32, mg_stats* st) {
   if (!h || !off || !len || !out32) return fail(MG_E_ARG, "null argument");
+  mw::CallMark mark("mg_keccak256");
+  mark.step("copy in", ndata);
   std::shared_ptr<Ctx> cref = g_reg.ctx(hid(h));   // its device, for the staging buffers
   if (!cref) return fail(MG_E_ARG, "mg_keccak256: not a live context");
   const Ctx* c = cref.get();
@@ -1740,5 +1796,9 @@ int mg_keccak256(mg_ctx* h, const uint8_t* data, size_t ndata, const uint64_t* o
   cleanup();
   return rc;
 }
+
+// The C-ABI calls in flight on every thread, one line each (mw_inflight.h):
+// for a watchdog that finds a call that does not return.  Never blocks.
+int mg_debug_inflight(char* buf, size_t n) { return mw::inflight_report(buf, n); }
 
 }  // extern "C"

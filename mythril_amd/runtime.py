@@ -80,6 +80,7 @@ SIGNATURES = {
     "mg_valu_peak": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
                                     ctypes.POINTER(ctypes.c_double)]),
     "mg_last_error": (ctypes.c_char_p, []),
+    "mg_debug_inflight": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
 }
 
 
@@ -145,8 +146,16 @@ class DeviceProgram:
         self.handle = None
 
     def __del__(self):  # pragma: no cover - best effort
+        # A finalizer runs on whichever thread the garbage collector happens
+        # to run (the witness-program thread, in the middle of another call's
+        # Python wrapper): it only queues the handle, and the device frees it
+        # at the start of its next call from its own caller (Device._reap),
+        # so no library call (mg_prog_free: a module unload, hipFree) ever
+        # runs from a collection.
         try:
-            self.free()
+            if self.handle and self.dev.handle:
+                self.dev._reap_queue.append(self.handle)
+            self.handle = None
         except Exception:
             pass
 
@@ -165,9 +174,22 @@ class Device:
         self.handle = h.value
         self.device = device
         self._live = weakref.WeakSet()   # programs loaded and not yet freed
+        self._reap_queue: List[int] = []    # handles of programs collected without free() (DeviceProgram.__del__)
+
+    def _reap(self):
+        """Free the programs the garbage collector queued (list.pop is atomic)."""
+        q = self._reap_queue
+        while q:
+            try:
+                h = q.pop()
+            except IndexError:
+                break
+            if self.handle:
+                self.lib.mg_prog_free(h)
 
     def close(self):
         if self.handle:
+            self._reap()
             for dp in list(self._live):
                 dp.free()
             self.lib.mg_free(self.handle)
@@ -176,6 +198,8 @@ class Device:
     def load(self, p: Program) -> DeviceProgram:
         if not self.handle:
             raise EngineError("device context is closed")
+        if self._reap_queue:
+            self._reap()
         d, keep = make_desc(p)
         h = _P()
         _check(self.lib, self.lib.mg_prog_load(self.handle, ctypes.byref(d), ctypes.byref(h)), "mg_prog_load")
@@ -209,6 +233,8 @@ class Device:
 
     def search(self, progs: Sequence[DeviceProgram], seed: int, begin: int, count: int,
                flags: int = 0) -> Tuple[List[Optional[int]], dict]:
+        if self._reap_queue:
+            self._reap()
         arr = (_P * len(progs))(*[dp.handle for dp in progs])
         out = (ctypes.c_uint64 * len(progs))()
         st = MgStats()
@@ -274,6 +300,17 @@ class Device:
         _check(self.lib, self.lib.mg_valu_peak(self.handle, 1 if mul else 0, ctypes.byref(ops), ctypes.byref(ms)),
                "mg_valu_peak")
         return ops.value, ms.value
+
+
+def inflight() -> str:
+    """The C-ABI calls in flight on every thread, with the step each is in
+    (mg_debug_inflight; for watchdogs: it never blocks), or "" if the
+    library is not loaded."""
+    if _lib is None:
+        return ""
+    buf = ctypes.create_string_buffer(8192)
+    _lib.mg_debug_inflight(buf, len(buf))
+    return buf.value.decode(errors="replace")
 
 
 def validate(p: Program) -> None:

@@ -57,6 +57,7 @@ def c5(request, dev):
     _log(f"density {request.param}: program built in {time.perf_counter() - t0:.1f} s")
     if not jit.is_cached([prog], "x", BENCH_WAVES, BENCH_LDS):
         pytest.fail("C5 specialised kernel not in build/jit: run __graft_entry__.build() first")
+    _log(f"density {request.param}: specialised kernel cached; loading the program")
     special = dev.load(prog)
     _log(f"density {request.param}: program loaded ({dev.engine_of(special)})")
     jit.attach(dev, [special], variants="x", waves=BENCH_WAVES, lds_leaves=BENCH_LDS)
