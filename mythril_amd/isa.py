@@ -243,3 +243,82 @@ def asm_eligible(code, leaves, consts=None) -> bool:
     if not all(k in ASM_LEAF_KINDS for k in kinds):
         return False
     return consts is None or len(asm_narrow_constants(code, consts)) <= ASM_NK
+
+
+# ---------------------------------------------------------------- executed work
+# u32 ops one evaluation of a program executes, priced per instruction of the
+# final bytecode with SURVEY §8(d)'s units (compiler.node_cost: L = limbs of
+# the operand width).  ops_per_eval prices the lowered DAG instead; the two
+# agree where each DAG node is one instruction, and differ where the compiler
+# executes less than the DAG states: a congruence grid row (CHECK_GRID, one
+# table lookup) stands for n pair checks, a keyed check
+# (CHECK_IMPEQK) for its premise compare and its pair.  Data movement (leaf
+# draws, spills, fills, moves, trace stores) is not algorithmic work: 0.
+def _limbs(width: int) -> int:
+    return max(1, (width + 31) // 32)
+
+
+def _log2c(n: int) -> int:
+    k = 0
+    while (1 << k) < n:
+        k += 1
+    return k
+
+
+def insn_ops(op: str, width: int) -> int:
+    """u32 ops one instruction executes (width: the instruction's width field,
+    the operand width of compares and checks)."""
+    L = _limbs(width)
+    if op in ("END", "LEAF_W", "LEAF_N", "STORE_W", "STORE_N", "SPILL_W", "FILL_W", "SPILL_N", "FILL_N",
+              "MOV_W", "MOV_N", "CHECK"):
+        return 0
+    if op == "CHECK_IMP":
+        return 2                          # =>
+    if op == "CHECK_IMPEQ":
+        return 2 + 2                      # narrow = and =>
+    if op in ("CHECK_IMPEQW", "CHECK_IMPEQK"):
+        return 2 * L + 2 + (2 if op == "CHECK_IMPEQK" else 0)   # = (the premise compare too), =>
+    if op == "CHECK_GRID":
+        return 1 + 2 + 2 * L + 2          # j = E - key, j < n, table[j] = v, =>
+    if op in ("W_ADD", "W_SUB", "W_AND", "W_OR", "W_XOR", "W_NOT", "W_ITE", "W_SHLI", "W_LSHRI", "W_ZEXTN",
+              "W_SEXT", "W_SEXTN", "N_ADDC"):
+        return L
+    if op == "W_MUL":
+        return 2 * L * (L + 1)
+    if op in ("W_SHL", "W_LSHR", "W_ASHR"):
+        return 2 * L + L * max(1, _log2c(L)) if L > 1 else 2
+    if op in ("W_UDIV", "W_UREM", "W_SDIV", "W_SREM", "W_SMOD"):
+        base = L * (6 * L + 20) + 3 * (2 * L + L * max(1, _log2c(L))) if L > 1 else 20
+        return base + (4 * L if op in ("W_SDIV", "W_SREM", "W_SMOD") else 0)
+    if op == "W_INSN":
+        return 1                          # one narrow part of a concat
+    if op == "W_CDINS":
+        return 8 + 1 + 1 + 1              # a calldata byte: signed 256-bit bound (L+1), ite, its part of the word
+    if op in ("N_ULT", "N_ULE", "N_SLT", "N_SLE"):
+        return L + 1
+    if op == "N_EQ":
+        return 2 * L
+    if op == "N_UMULNO":
+        return 4 * L * L + L
+    if op in ("N_AND", "N_OR", "N_XOR"):
+        return 2 if width == 1 else 1     # a Bool connective: one per operand
+    if op in ("N_MUL",):
+        return 4
+    if op in ("N_SHL", "N_LSHR", "N_ASHR", "N_ULTN", "N_ULEN", "N_SLTN", "N_SLEN", "N_EQN"):
+        return 2
+    if op in ("N_UDIV", "N_UREM"):
+        return 20
+    if op in ("N_SDIV", "N_SREM", "N_SMOD"):
+        return 24
+    if op == "N_UMULNON":
+        return 5
+    return 1                              # N_ADD/SUB/NOT/ITE/SHLI/LSHRI/SEXT/EXTRACTW, N_ADDCN
+
+
+_OPNAME = {v: k for k, v in OPCODES.items()}
+
+
+def executed_ops_per_eval(code) -> int:
+    """Sum of insn_ops over a program's bytecode (4 words per instruction)."""
+    w = [int(x) for x in list(code)[0::4]]
+    return sum(insn_ops(_OPNAME[x & 0xFF], x >> 16) for x in w)

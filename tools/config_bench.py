@@ -16,7 +16,14 @@ these programs), the compiled interpreter (MYTHRIL_AMD_ASM=0) and the
 specialised kernel (mythril_amd/jit.py).  Time to first witness (early exit + stop-after-hit,
 interpreter) is reported beside it.  evals/s = programs x candidates / wall
 time of the mg_search call; the roofline uses the kernel time from the library's
-HIP events and the compiler's ops_per_eval.
+HIP events.  Two op counts are reported: the compiler's ops_per_eval (SURVEY.md
+§8(d) priced on the lowered DAG) and executed_ops_per_eval (the same units
+priced per instruction of the program the engine runs, isa.insn_ops: a
+congruence grid row is one table lookup, not the n pair checks the DAG
+states).  frac_peak uses the smaller of the two, so no
+engine claims more work than its instructions execute; frac_peak_nominal
+keeps the DAG count.  The hipcc-specialised tier compiles the unfused SSA
+(no grids): its executed count is the DAG's.
 
     python tools/config_bench.py [--out FILE] [--no-jit]
 """
@@ -97,6 +104,7 @@ def main():
             from mythril_amd.engine import search_program
             dps = [dev.load(search_program(q, 1 << log2)) for q in g]
             ops = sum(q.ops_per_eval for q in g)
+            exec_ops = sum(isa.executed_ops_per_eval(dp.prog.code) for dp in dps)
             count = 1 << log2
             # time to first witness (interpreter, early exit)
             t0 = time.perf_counter()
@@ -130,13 +138,16 @@ def main():
                     kms += st["kernel_ms"]
                     evals += st["evals"]
                 wall = time.perf_counter() - t0
-                achieved = ops * count / (kms / 1e3)
+                nominal = ops * count / (kms / 1e3)
+                ex = ops if engine == "jit" else exec_ops      # hipcc compiles the unfused SSA
+                achieved = min(ops, ex) * count / (kms / 1e3)
                 line = {"config": name, "files": gfiles, "engine": engine + (f" ({dps[0].kernel})" if dps[0].kernel else ""),
                         "kernels": ran,
                         "programs": len(g), "candidates": count, "evals": evals,
                         "evals_per_s": len(g) * count / wall, "kernel_ms": kms, "ops_per_eval": ops,
-                        "tops": achieved / 1e12, "frac_peak": achieved / peak, "jit_compile_s": compile_s,
-                        "first_witness": first, "ttfw_s": ttfw}
+                        "executed_ops_per_eval": ex,
+                        "tops": achieved / 1e12, "frac_peak": achieved / peak, "frac_peak_nominal": nominal / peak,
+                        "jit_compile_s": compile_s, "first_witness": first, "ttfw_s": ttfw}
                 print(json.dumps(line), flush=True)
                 lines.append(line)
             for dp in dps:
