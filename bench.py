@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ttfw", action="store_true", help="skip the time-to-first-witness search")
+    ap.add_argument("--no-recount", action="store_true",
+                    help="skip the untimed counting pass (profiling runs: every dispatch of the kernel is then a "
+                         "timed-form launch; the division-path counts and the executed roofline are not reported)")
     ap.add_argument("--ttfw-slice-log2", type=int, default=24, help="candidates per rank per stop-after-hit slice")
     ap.add_argument("--ttfw-max-slices", type=int, default=128)
     ap.add_argument("--ttfw-begin", type=int, default=0, help="first index of the time-to-first-witness sweep")
@@ -192,18 +195,25 @@ def main():
             mdp.parts[0].free()
             mdp.parts[0] = dp   # device 0's copy is the program the kernel was attached to above
     batch = 1 << args.batch_log2
+    from mythril_amd import isa
+    # The timed launches write no launch counters (isa.FLAG_NO_COUNT: the
+    # specialised kernel's per-wave atomics were 11 MiB of HBM writes per
+    # launch, profiles/pmc_traffic.json r4ad); the same steps run again after
+    # the timed region with the counters on, for the division-path counts the
+    # executed-work roofline is priced from.
+    TIMED_FLAGS = isa.FLAG_NO_COUNT
 
-    def step(k):
+    def step(k, flags=0):
         if multi is not None:   # one process: every device searches its slice of the step
             begin = (args.begin + k * args.devices * batch) % (1 << 62)
-            (found,), st = multi.search([mdp], syn.seed, begin, batch * args.devices, 0)
+            (found,), st = multi.search([mdp], syn.seed, begin, batch * args.devices, flags)
             return found, st
         begin = (args.begin + (k * world + rank) * batch) % (1 << 62)
-        (found,), st = dev.search([dp], syn.seed, begin, batch, 0)
+        (found,), st = dev.search([dp], syn.seed, begin, batch, flags)
         return found, st
 
     for k in range(args.warmup):
-        step(k)
+        step(k, TIMED_FLAGS)
 
     def barrier():
         if dist is not None:
@@ -218,14 +228,25 @@ def main():
     dcounts = []
     found_any = None
     t0 = time.perf_counter()
+    timed_evals = 0
     for k in range(args.warmup, args.warmup + args.steps):
-        found, st = step(k)
+        found, st = step(k, TIMED_FLAGS)
         kms.append(st.get("kernel_ms", 0.0))
-        dcounts.append(st)
+        timed_evals += st.get("evals", 0)
         if found is not None:
             found_any = found if found_any is None else min(found_any, found)
     barrier()
     elapsed = time.perf_counter() - t0
+    # the counting pass (untimed): the same K launches with the counters on
+    recount = found_any if args.no_recount else None
+    for k in (range(args.warmup, args.warmup + args.steps) if not args.no_recount else ()):
+        found, st = step(k, 0)
+        dcounts.append(st)
+        if found is not None:
+            recount = found if recount is None else min(recount, found)
+    if recount != found_any:
+        print(f"[bench] PARITY FAILURE: the counting pass found {recount}, the timed launches {found_any}",
+              file=sys.stderr)
     rccl_world = 1
     if dist is not None:
         import torch
@@ -243,7 +264,8 @@ def main():
     # path each wave took (mg_stats.lane_div_*; compiler.DIV_PRICE_*), and the
     # division-free floor beside it
     from mythril_amd.multidev import DIV_COUNTS
-    per_launch = {k: sum(st.get(k, 0) for st in dcounts) / len(dcounts) / max(1, args.devices) for k in DIV_COUNTS}
+    per_launch = {k: sum(st.get(k, 0) for st in dcounts) / max(1, len(dcounts)) / max(1, args.devices)
+                  for k in DIV_COUNTS}
     ops_launch = prog.executed_ops(batch, per_launch)
     ops_floor = prog.executed_ops(batch, None)
     achieved = ops_launch / avg_kernel_s if avg_kernel_s > 0 else 0.0
@@ -301,6 +323,10 @@ def main():
             "dist_backend": args.dist_backend if dist is not None else None,
             "candidate_begin": args.begin,
             "witness_found_in_timed_range": found_any,
+            "timed_launch_flags": "no launch counters (isa.FLAG_NO_COUNT); division paths from an untimed "
+                                  "recount of the same launches",
+            "evals_timed": timed_evals,
+            "evals_counted": sum(st.get("evals", 0) for st in dcounts),
             "time_to_first_witness": ttfw,
         },
         "roofline": {

@@ -48,6 +48,9 @@ extern "C" {
 /* search flags (same values as MW_FLAG_* in mw_isa.h) */
 #define MG_FLAG_EARLY_EXIT 1u
 #define MG_FLAG_STOP_AFTER_HIT 2u
+/* specialised kernels write no launch counters (division-path counts stay 0;
+ * evals = count per program); ignored together with MG_FLAG_STOP_AFTER_HIT */
+#define MG_FLAG_NO_COUNT 4u
 
 typedef struct mg_ctx mg_ctx;
 typedef struct mg_prog mg_prog;

@@ -109,3 +109,7 @@ enum mw_opcode {
 // mg_search flags
 #define MW_FLAG_EARLY_EXIT 1u   // per-wave ballot exit after a failing CHECK
 #define MW_FLAG_STOP_AFTER_HIT 2u  // blocks stop once a lower witness is known
+// specialised kernels skip the launch counters (evals, division paths): a
+// timed exhaustive launch writes nothing but its witness minimum; the host
+// reports evals = count per program.  Ignored with STOP_AFTER_HIT.
+#define MW_FLAG_NO_COUNT 4u

@@ -313,9 +313,11 @@ __device__ __attribute__((always_inline)) inline void search(const u32* __restri
   DivCount dc;
   const bool ok = BODY(pool, seed, cand, in, flags, nullptr, 0, 0, dc);
   const u64 nvalid = (u64)__popcll(__ballot(valid));
+  // MW_FLAG_NO_COUNT (a timed exhaustive launch): no counter atomics at all
+  const bool counting = !(flags & MW_FLAG_NO_COUNT);
   // this block's counter stripe (mw_alu.h MW_CTR_STRIPES)
   counter += MW_CTR_STRIPE_WORDS * (1u + (blockIdx.x & (MW_CTR_STRIPES - 1u)));
-  if (lane == 0 && nvalid)   // division paths x lanes (mg_stats.lane_div_*)
+  if (counting && lane == 0 && nvalid)   // division paths x lanes (mg_stats.lane_div_*)
     add_div_counts(counter, dc, nvalid);
   if (!(stage & MW_JIT_LAST)) {
     if (valid) alivebuf[cand - begin] = ok ? 1u : 0u;
@@ -330,7 +332,7 @@ __device__ __attribute__((always_inline)) inline void search(const u32* __restri
     if (lane == first && cand < __hip_atomic_load(out_min, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
       atomicMin((unsigned long long*)out_min, (unsigned long long)cand);
   }
-  if (lane == 0 && nvalid) atomicAdd((unsigned long long*)counter, (unsigned long long)nvalid);
+  if (counting && lane == 0 && nvalid) atomicAdd((unsigned long long*)counter, (unsigned long long)nvalid);
 }
 
 // <name>_x: exhaustive; <name>_e: per-wave early exit after a failing CHECK.

@@ -1272,6 +1272,7 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   if (!h || !hprogs || !out_min_idx || nprog == 0) return fail(MG_E_ARG, "null argument");
   if (nprog > 65535) return fail(MG_E_ARG, "too many programs per launch");
   if (count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad candidate range");
+  if (flags & MW_FLAG_STOP_AFTER_HIT) flags &= ~MW_FLAG_NO_COUNT;   // blocks may skip: only the counters know
   std::vector<u64> ids(nprog);
   for (size_t i = 0; i < nprog; ++i) ids[i] = hid(hprogs[i]);
   mw::CallMark mark("mg_search");
@@ -1471,7 +1472,9 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   u64 ctr[kNCounters] = {0, 0, 0, 0, 0};
   for (size_t sidx = 0; sidx <= MW_CTR_STRIPES; ++sidx)
     for (int k = 0; k < kNCounters; ++k) ctr[k] += stripes[sidx * MW_CTR_STRIPE_WORDS + k];
-  const u64 evals = ctr[0];
+  // specialised launches under MW_FLAG_NO_COUNT counted nothing: every
+  // candidate of the range was evaluated (no stop-after-hit)
+  const u64 evals = ctr[0] + ((flags & MW_FLAG_NO_COUNT) ? (u64)count * special.size() : 0u);
   for (size_t j = 0; j < nia; ++j) out_min_idx[interp[j]] = mins[j];
   for (size_t j = 0; j < special.size(); ++j) out_min_idx[special[j]] = mins[nia + j];
   if (st) {

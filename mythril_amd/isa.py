@@ -70,6 +70,7 @@ for _n in ("N_ADD", "N_SUB", "N_MUL", "N_AND", "N_OR", "N_XOR", "N_SHL", "N_LSHR
 
 FLAG_EARLY_EXIT = 1
 FLAG_STOP_AFTER_HIT = 2
+FLAG_NO_COUNT = 4      # specialised kernels skip the launch counters (mw_isa.h MW_FLAG_NO_COUNT)
 
 
 # instruction flags, w0 bits [15:8] (csrc/mw_prog.h)

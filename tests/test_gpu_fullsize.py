@@ -170,3 +170,24 @@ def test_division_dag_path_counts_match_oracle(dev):
     orc = cdag.div_paths(conj, 0x5EED, 0, SWEEP, wave=64)
     assert {k: st[k] for k in DIV_KEYS} == orc
     assert orc["lane_div_general"] > 0 and orc["lane_div_steps"] > 0
+
+
+def test_c5_uncounted_launch(c5, dev):
+    """bench.py's timed launches (isa.FLAG_NO_COUNT): the
+    specialised kernel writes no counters - no division-path counts - and
+    finds the same witness; the host reports every candidate evaluated.  The
+    interpreter ignores the flag (it counts once per wave per launch)."""
+    dens, syn, prog, special, interp = c5
+    w = syn.witness_index
+    begin, count = w - (1 << 18), (1 << 18) + 1
+    (fc,), stc = dev.search([special], syn.seed, begin, count, 0)
+    (fn,), stn = dev.search([special], syn.seed, begin, count, isa.FLAG_NO_COUNT)
+    assert fc == fn and (dens != 24 or fn == w)
+    assert stn["evals"] == stc["evals"] == count
+    assert all(stn[k] == 0 for k in DIV_KEYS) and stc["lane_div_full"] > 0
+    (fi,), sti = dev.search([interp], syn.seed, begin, count, isa.FLAG_NO_COUNT)
+    assert fi == fc and sti["evals"] == count and sti["lane_div_full"] == stc["lane_div_full"]
+    # with stop-after-hit the flag is ignored: only the counters know what ran
+    (fs,), sts = dev.search([special], syn.seed, begin, count,
+                            isa.FLAG_NO_COUNT | isa.FLAG_STOP_AFTER_HIT | isa.FLAG_EARLY_EXIT)
+    assert fs == fc and 0 < sts["evals"] <= count

@@ -1,3 +1,7 @@
+"""isa.py's mirrors of the library's constants (the opcode table itself is
+checked against mw_isa.h by tests/test_build.py)."""
+
+
 
 
 def test_layout_limits_match_the_library():

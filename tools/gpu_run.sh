@@ -33,7 +33,7 @@ TAG=$1
 shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-ttfw ${BENCH_ARGS:-}"
+B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-ttfw --no-recount ${BENCH_ARGS:-}"
 
 run() {  # run LIMIT LOG CMD...: one GPU step, bounded; print the log tail on failure
   local lim=$1 log=$2
@@ -59,13 +59,13 @@ for step in "$@"; do
     tests|tests=*)
       K=()
       [ "$step" != tests ] && K=(-k "${step#tests=}")
-      run 1000 "$OUT/gpu_tests.log" python3 -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread "${K[@]}"
+      run 1000 "$OUT/gpu_tests.log" python3 -u -m pytest tests -m gpu -x -v -s --timeout 150 --timeout-method thread "${K[@]}"
       tail -3 "$OUT/gpu_tests.log" ;;
     bench)
       run 500 "$OUT/bench.err" bash -c "python3 bench.py > $OUT/bench.json"
       cat "$OUT/bench.json" ;;
     bench1)
-      run 300 "$OUT/bench1.err" bash -c "$B > $OUT/bench1.json"
+      run 300 "$OUT/bench1.err" bash -c "${B/--no-recount/} > $OUT/bench1.json"
       cat "$OUT/bench1.json" ;;
     prof)
       run 400 "$OUT/prof.log" rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- $B
@@ -77,7 +77,7 @@ for step in "$@"; do
                  "FETCH_SIZE" "WRITE_SIZE"; do
         i=$((i + 1))
         run 150 "$OUT/pmc$i.log" timeout -s KILL 140 rocprofv3 --pmc $set --output-format csv -d "$OUT/pmc/p$i" -o run -- \
-          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ttfw
+          python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-ttfw --no-recount
       done
       find "$OUT/pmc" -name "*counter_collection*" ;;
     config)

@@ -42,6 +42,16 @@ def main():
                                      search_phased, search_program)
     from mythril_amd.smt2 import parse_file
     eng = None if a.no_device else WitnessEngine(device=0)
+    calls = []    # every mg_search of the current query: (call wall, library wall, kernel) ms
+    if eng is not None:
+        real_search = eng.dev.search
+
+        def timed_search(*args, **kw):
+            t = time.perf_counter()
+            res = real_search(*args, **kw)
+            calls.append(((time.perf_counter() - t) * 1e3, res[1].get("wall_ms", 0.0), res[1].get("kernel_ms", 0.0)))
+            return res
+        eng.dev.search = timed_search
     rows = []
     for corpus in ("solver_log", "laser"):
         files = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", corpus, "*.smt2*")))
@@ -60,8 +70,11 @@ def main():
                 # as WitnessEngine.search: the witness program compiles on the
                 # host thread while the program uploads and the device searches
                 queued = _prebuild_witness_programs([q])
+                t_q = time.perf_counter()
                 with _gil_handoff(queued):
                     dp = eng.dev.load(q.program)
+                t_l = time.perf_counter()
+                calls.clear()
                 try:
                     with _gil_handoff(queued):
                         # as WitnessEngine.search: the launch after the probe runs
@@ -70,6 +83,11 @@ def main():
                                                    [lambda n: search_program(q, n)])
                     row["search"] = (time.perf_counter() - t1) * 1e3
                     row["kernel"] = st["kernel_ms"]
+                    # where the search's time goes: queueing the witness compile,
+                    # the upload call, and per mg_search call its Python/ctypes
+                    # wall, the library's own wall and the kernel time
+                    row["search_parts"] = {"prebuild": (t_q - t1) * 1e3, "load": (t_l - t_q) * 1e3,
+                                           "calls": [[round(x, 4) for x in c] for c in calls]}
                     if idx is not None:
                         # as WitnessEngine.search does: the search program is still
                         # loaded (mg_witness_leaves when every cell index is constant)
