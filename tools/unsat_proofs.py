@@ -19,9 +19,17 @@ UFs Ackermannised):
   tautology     a conjunct folds to false once `x <u 0` (never) and
                 `x >=u 0` (always) are folded, as solc 0.4's `a - b >= 0`
                 underflow checks on uints make them;
-  open          neither applies (the reason is argued by hand in DESIGN.md).
+  rewriting     on the query as stated (store chains intact): facts
+                substituted, reads over writes resolved, no-op stores
+                dropped, constants folded, until a conjunct is false;
+  contradiction a literal met with both polarities once comparisons are put
+                in one form (a <u b, a <s b);
+  bounds        unsigned intervals from the literals comparing terms with
+                constants, carried through + - * & / >> concat extract
+                zero_extend ite, decide a literal false (abstract() below);
+  open          none applies (the reason is argued by hand in DESIGN.md).
 
-    python tools/unsat_proofs.py GROUND_TRUTH.json [--out FILE]
+    python tools/unsat_proofs.py GROUND_TRUTH.json[.gz] [--out FILE] [--update]
 """
 import argparse
 import json
@@ -153,19 +161,363 @@ def interval(conj):
     return None
 
 
+# ---------------------------------------------------------------------------
+# Rewriting, complementary literals and unsigned bounds (round 6, VERDICT r5
+# item 5) - on the query as LASER states it (the parsed script: arrays and
+# store chains intact, no Ackermannisation).  Every step is an equivalence or
+# a sound over-approximation, so "false" means UNSAT:
+#   * facts `v = K` (also through `ite(c, 1, 0) = 0/1` and `not`) substitute;
+#   * read over write: select(store(a, i, v), j) is v when i and j are the same
+#     term or equal constants, select(a, j) when they are different constants;
+#     store(a, i, select(a, i)) is a (the no-op stores LASER's CALL makes:
+#     world_state.py:33 / account.py:26-29 copy the balance map);
+#     x + 0, x - 0, x / 1, x & ~0 are x; ite(c, t, t) is t; t = t is true,
+#     t < t false; constant subterms fold (the oracle's evaluator);
+#   * complementary literals: comparisons put in one form (a <u b, a <s b, a = b)
+#     and a literal met with both polarities;
+#   * unsigned bounds: every literal comparing a term with a constant bounds
+#     that term; bounds flow up through +, -, *, concat, extract, zero_extend,
+#     &, >>, / and ite (interval arithmetic, no wrap-around assumed: an
+#     operation that could wrap gets the full range), and a literal the bounds
+#     decide false makes the set UNSAT.
+
+def _ops():
+    from oracle.dag_eval import _eval1
+    return _eval1
+
+
+_FLIP = {"bvugt": ("bvult", True), "bvuge": ("bvult", False), "bvule": ("bvult", True),
+         "bvsgt": ("bvslt", True), "bvsge": ("bvslt", False), "bvsle": ("bvslt", True)}
+
+
+class _Simp:
+    def __init__(self, ctx, fixed):
+        self.c, self.fixed, self.memo = ctx, fixed, {}
+        self.ev = _ops()
+
+    def const(self, n):
+        return n.op == "const"
+
+    def is_val(self, n, v):
+        return n.op == "const" and n.val == v
+
+    def __call__(self, root):
+        from mythril_amd.ir import topo
+        memo, c = self.memo, self.c
+        for n in topo([root]):
+            if n.id in memo:
+                continue
+            args = tuple(memo[a.id] for a in n.args)
+            memo[n.id] = self.rule(n, args)
+        return memo[root.id]
+
+    def mk(self, n, args):
+        if all(a is b for a, b in zip(args, n.args)):
+            return n
+        return self.c._mk(n.op, n.width, args, n.params, n.val, n.name, n.dom)
+
+    def rule(self, n, args):
+        c, op = self.c, n.op
+        if op == "var" and n.name in self.fixed:
+            return c.const(self.fixed[n.name], n.width)
+        if op in ("const", "var", "array"):
+            return n
+        if op == "select":
+            a, j = args
+            while a.op == "store":
+                b, i, v = a.args
+                if i is j or (self.const(i) and self.const(j) and i.val == j.val):
+                    return v
+                if self.const(i) and self.const(j):
+                    a = b
+                    continue
+                break
+            return self.mk(n, (a, j))
+        if op == "store":
+            a, i, v = args
+            if v.op == "select" and v.args[0] is a and v.args[1] is i:
+                return a
+            return self.mk(n, args)
+        if op == "ite":
+            cond, t, e = args
+            if self.const(cond):
+                return t if cond.val else e
+            if t is e:
+                return t
+            return self.mk(n, args)
+        if op in ("=", "bvult", "bvslt", "bvugt", "bvsgt") and len(args) == 2 and args[0] is args[1]:
+            return c.const(op == "=", 0)
+        if op in ("bvule", "bvuge", "bvsle", "bvsge") and args[0] is args[1]:
+            return c.true()
+        if op == "=" and len(args) == 2:
+            a, b = args
+            if a.op == "const":
+                a, b = b, a
+            # ite(c, 1, 0) = 1 / = 0: the flag's condition, or its negation
+            if a.op == "ite" and b.op == "const" and all(x.op == "const" for x in a.args[1:]) and \
+                    a.args[1].val != a.args[2].val and b.val in (a.args[1].val, a.args[2].val):
+                cond = a.args[0]
+                return cond if b.val == a.args[1].val else self.rule(c.app("not", cond), (cond,))
+        if op == "not" and args[0].op == "not":
+            return args[0].args[0]
+        if op in ("and", "or"):
+            unit, zero = (1, 0) if op == "and" else (0, 1)
+            keep = []
+            for a in args:
+                if self.const(a):
+                    if a.val == zero:
+                        return c.const(zero, 0)
+                    continue
+                keep.append(a)
+            if not keep:
+                return c.const(unit, 0)
+            if len(keep) == 1:
+                return keep[0]
+            return c.app(op, *keep)
+        if op in ("bvadd", "bvsub") and len(args) == 2 and self.is_val(args[1], 0):
+            return args[0]
+        if op == "bvadd" and len(args) == 2 and self.is_val(args[0], 0):
+            return args[1]
+        if op == "bvudiv" and self.is_val(args[1], 1):
+            return args[0]
+        if op == "bvand" and len(args) == 2:
+            for x, y in (args, args[::-1]):
+                if self.is_val(y, (1 << n.width) - 1):
+                    return x
+        if args and all(self.const(a) for a in args) and op not in ("apply", "select", "store", "const_array"):
+            try:
+                return c.const(self.ev(n, [a.val for a in args], {}), n.width)
+            except Exception:   # noqa: BLE001 - not foldable here
+                pass
+        return self.mk(n, args)
+
+
+def _literals(conj, ctx):
+    """Top-level literals (atom, polarity): `and` flattened, `not` peeled, and
+    comparisons in one form (a <u b, a <s b)."""
+    out, stack = [], [(x, True) for x in conj]
+    while stack:
+        n, pol = stack.pop()
+        if n.op == "and" and pol:
+            stack.extend((a, True) for a in n.args)
+        elif n.op == "or" and not pol:
+            stack.extend((a, False) for a in n.args)
+        elif n.op == "not":
+            stack.append((n.args[0], not pol))
+        elif n.op in _FLIP:
+            base, swap = _FLIP[n.op]
+            a, b = n.args
+            atom = ctx.app(base, b, a) if swap else ctx.app(base, a, b)
+            # a >u b == b <u a; a >=u b == not a <u b; a <=u b == not b <u a
+            stack.append((atom, pol if n.op in ("bvugt", "bvsgt") else not pol))
+        else:
+            out.append((n, pol))
+    return out
+
+
+def _facts_of(lits):
+    fixed = {}
+    for n, pol in lits:
+        if n.op == "var" and n.width == BOOL:
+            fixed[n.name] = 1 if pol else 0
+        elif pol and n.op == "=" and len(n.args) == 2:
+            a, b = n.args
+            if a.op == "const":
+                a, b = b, a
+            if a.op == "var" and b.op == "const" and a.width != BOOL:
+                fixed[a.name] = b.val
+    return fixed
+
+
+class _Bounds:
+    """Unsigned intervals of terms, from the literals' bounds (fact[id])."""
+
+    def __init__(self, fact):
+        self.fact, self.memo = fact, {}
+
+    def full(self, n):
+        return (0, (1 << n.width) - 1)
+
+    def get(self, n):
+        r = self.memo.get(n.id)
+        if r is None:
+            r = self.memo[n.id] = self._meet(n, self.compute(n))
+        return r
+
+    def _meet(self, n, r):
+        f = self.fact.get(n.id)
+        if f is None or r is None:
+            return r if f is None else f
+        return (max(r[0], f[0]), min(r[1], f[1]))
+
+    def compute(self, n):
+        op, w = n.op, n.width
+        if w == BOOL or n.is_array:
+            return None
+        top = (1 << w) - 1
+        if op == "const":
+            return (n.val, n.val)
+        a = [self.get(x) if x.width != BOOL and not x.is_array else None for x in n.args]
+        if op == "zero_extend":
+            return a[0]
+        if op == "bvadd" and all(a):
+            lo, hi = sum(x[0] for x in a), sum(x[1] for x in a)
+            return (lo, hi) if hi <= top else self.full(n)
+        if op == "bvsub" and all(a) and len(a) == 2:
+            return (a[0][0] - a[1][1], a[0][1] - a[1][0]) if a[0][0] >= a[1][1] else self.full(n)
+        if op == "bvmul" and all(a):
+            lo, hi = 1, 1
+            for x in a:
+                lo, hi = lo * x[0], hi * x[1]
+            return (lo, hi) if hi <= top else self.full(n)
+        if op == "bvand" and all(a):
+            return (0, min(x[1] for x in a))
+        if op == "bvudiv" and all(a) and a[1][0] > 0:
+            return (a[0][0] // a[1][1], a[0][1] // a[1][0])
+        if op == "bvlshr" and all(a) and a[1][0] == a[1][1]:
+            k = a[1][0]
+            return (a[0][0] >> k, a[0][1] >> k) if k < w else (0, 0)
+        if op == "concat" and all(a):
+            lo = hi = 0
+            for x, arg in zip(a, n.args):
+                lo, hi = (lo << arg.width) | x[0], (hi << arg.width) | x[1]
+            # the parts are disjoint bit fields: the least value is every part at
+            # its least, the greatest every part at its greatest
+            return (lo, hi)
+        if op == "extract" and a[0]:
+            h, l = n.params
+            lo, hi = a[0]
+            if (lo >> (h + 1)) == (hi >> (h + 1)):
+                m = (1 << (h - l + 1)) - 1
+                return ((lo >> l) & m, (hi >> l) & m)
+            return self.full(n)
+        if op == "ite" and a[1] and a[2]:
+            t = self.truth(n.args[0])
+            if t is True:
+                return a[1]
+            if t is False:
+                return a[2]
+            return (min(a[1][0], a[2][0]), max(a[1][1], a[2][1]))
+        return self.full(n)
+
+    def truth(self, n):
+        """True / False when the bounds decide the Bool term, else None."""
+        op = n.op
+        if op == "const":
+            return bool(n.val)
+        if op == "not":
+            t = self.truth(n.args[0])
+            return None if t is None else not t
+        if op in ("and", "or"):
+            ts = [self.truth(x) for x in n.args]
+            if op == "and":
+                return False if False in ts else (True if all(t is True for t in ts) else None)
+            return True if True in ts else (False if all(t is False for t in ts) else None)
+        if op in ("bvult", "bvule", "bvugt", "bvuge", "=", "bvumul_noovfl") and len(n.args) == 2 \
+                and n.args[0].width != BOOL and not n.args[0].is_array:
+            (alo, ahi), (blo, bhi) = self.get(n.args[0]), self.get(n.args[1])
+            if op == "=":
+                if ahi < blo or bhi < alo:
+                    return False
+                return True if alo == ahi == blo == bhi else None
+            if op == "bvumul_noovfl":
+                top = 1 << n.args[0].width
+                return True if ahi * bhi < top else (False if alo * blo >= top else None)
+            if op in ("bvugt", "bvuge"):
+                (alo, ahi), (blo, bhi) = (blo, bhi), (alo, ahi)
+            strict = op in ("bvult", "bvugt")
+            if (ahi < blo) if strict else (ahi <= blo):
+                return True
+            if (alo >= bhi) if strict else (alo > bhi):
+                return False
+        return None
+
+
+def _bounds_from(lits):
+    fact = {}
+
+    def meet(t, lo, hi):
+        if t.width == BOOL or t.is_array:
+            return
+        old = fact.get(t.id, (0, (1 << t.width) - 1))
+        fact[t.id] = (max(old[0], lo), min(old[1], hi))
+    for n, pol in lits:
+        if n.op == "=" and pol and len(n.args) == 2:
+            a, b = n.args
+            if a.op == "const":
+                a, b = b, a
+            if b.op == "const":
+                meet(a, b.val, b.val)
+        elif n.op == "bvult" and len(n.args) == 2:
+            a, b = n.args
+            top = (1 << a.width) - 1 if a.width != BOOL else 1
+            if b.op == "const":        # a < K  /  a >= K
+                if pol:
+                    meet(a, 0, b.val - 1)
+                else:
+                    meet(a, b.val, top)
+            elif a.op == "const":      # K < b  /  b <= K
+                if pol:
+                    meet(b, a.val + 1, top)
+                else:
+                    meet(b, 0, a.val)
+    return fact
+
+
+def abstract(asserts, ctx):
+    """Rewriting, complementary literals, then unsigned bounds (above), to a fixpoint of facts."""
+    sys.setrecursionlimit(max(sys.getrecursionlimit(), 20000))
+    conj = list(asserts)
+    fixed = {}
+    for _ in range(8):
+        simp = _Simp(ctx, fixed)
+        conj = [simp(x) for x in conj]
+        for i, x in enumerate(conj):
+            if x.op == "const" and not x.val:
+                return {"reason": "rewriting", "false_conjunct": i}
+        lits = _literals(conj, ctx)
+        seen = {}
+        for n, pol in lits:
+            if n.op == "const":
+                if not (n.val if pol else not n.val):
+                    return {"reason": "rewriting", "false_literal": repr(n)[:80]}
+                continue
+            if seen.get(n.id, pol) != pol:
+                return {"reason": "contradiction", "literal": repr(n)[:120]}
+            seen[n.id] = pol
+        more = _facts_of(lits)
+        if all(fixed.get(k) == v for k, v in more.items()):
+            break
+        fixed.update(more)
+    fact = _bounds_from(lits)
+    for tid, (lo, hi) in fact.items():
+        if lo > hi:       # e.g. x <u 0, or x <u 5 beside x >=u 9
+            return {"reason": "bounds", "empty_term": tid}
+    bounds = _Bounds(fact)
+    for n, pol in lits:
+        if n.width == BOOL and bounds.truth(n) is (not pol):
+            return {"reason": "bounds", "literal": repr(n)[:120]}
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("ground_truth")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--update", action="store_true",
+                    help="write the reasons into the ground-truth file itself (.json or .json.gz)")
     a = ap.parse_args()
-    gt = json.load(open(a.ground_truth))
+    import gzip
+    opener = gzip.open if a.ground_truth.endswith(".gz") else open
+    gt = json.loads(opener(a.ground_truth, "rt").read())
     man = {m["file"]: m for m in json.load(open(os.path.join(CORPUS, "manifest.json")))}
     out = {}
     for f in gt["no_witness"]:
         s = parse_file(os.path.join(CORPUS, f))
         q = prepare(s.asserts, s.ctx)
         conj = _flatten(q.lowered.conjuncts)
-        why = propagation(conj) or interval(conj) or tautology(conj, q.ctx) or {"reason": "open"}
+        why = propagation(conj) or interval(conj) or tautology(conj, q.ctx) or abstract(s.asserts, s.ctx) \
+            or {"reason": "open"}
         why["kind"] = man[f]["kind"]
         out[f] = why
     counts = {}
@@ -177,6 +529,10 @@ def main():
             print("open:", f, w["kind"])
     if a.out:
         json.dump(out, open(a.out, "w"), indent=1, sort_keys=True)
+    if a.update:
+        gt["no_witness"] = out
+        with opener(a.ground_truth, "wt") as fh:
+            fh.write(json.dumps(gt, indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":
