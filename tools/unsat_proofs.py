@@ -497,6 +497,12 @@ def abstract(asserts, ctx):
     for n, pol in lits:
         if n.width == BOOL and bounds.truth(n) is (not pol):
             return {"reason": "bounds", "literal": repr(n)[:120]}
+        # a term whose computed range misses the range the literals give it
+        # (every literal holds in a model, so the term lies in both)
+        for a in n.args:
+            r = bounds.get(a) if a.width != BOOL and not a.is_array else None
+            if r is not None and r[0] > r[1]:
+                return {"reason": "bounds", "empty_term": repr(a)[:120]}
     return None
 
 
