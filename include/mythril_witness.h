@@ -187,6 +187,12 @@ const char* mg_last_error(void);
  * (default 2000) also prints one line on stderr when it ends. */
 int mg_debug_inflight(char* buf, size_t n);
 
+/* Debugging: with MYTHRIL_AMD_STEP_TIMES=1 in the environment, the wall time
+ * (ms) and count of every call and step since the last read, one
+ * "call/step ms count" line each (the whole call as "call/(call)"); the
+ * table is then cleared.  Returns the number of lines (0 when off). */
+int mg_debug_step_times(char* buf, size_t n);
+
 #ifdef __cplusplus
 }
 #endif

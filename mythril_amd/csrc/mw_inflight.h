@@ -21,6 +21,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
+#include <map>
+#include <mutex>
+#include <string>
 #include <thread>
 
 namespace mw {
@@ -66,6 +69,32 @@ inline InflightSlot* inflight_slot() {
   return k < kInflightSlots ? &inflight_table()[k] : nullptr;
 }
 
+// Step-time accounting (MYTHRIL_AMD_STEP_TIMES=1; tools/dropin_profile.py):
+// wall time and count per "call/step", summed over the process until read
+// (mw::step_times_report, mg_debug_step_times).  Off by default: one getenv.
+inline bool step_times_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MYTHRIL_AMD_STEP_TIMES");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+struct StepTimes {
+  std::mutex mu;
+  std::map<std::string, std::pair<double, uint64_t>> t;   // "call/step" -> (ms, count)
+};
+inline StepTimes& step_times() {
+  static StepTimes st;
+  return st;
+}
+inline void step_times_add(const char* call, const char* step, double ms) {
+  StepTimes& st = step_times();
+  std::lock_guard<std::mutex> lk(st.mu);
+  auto& e = st.t[std::string(call) + "/" + step];
+  e.first += ms;
+  e.second += 1;
+}
+
 class CallMark;
 inline CallMark*& current_mark() {
   thread_local CallMark* m = nullptr;
@@ -78,6 +107,8 @@ class CallMark {
     if (current_mark()) return;   // a call made by another call (mg_keccak256): the outer one reports
     current_mark() = this;
     outer_ = true;
+    step_ = "enter";
+    t_call_ = t_step_;
     s_ = inflight_slot();
     if (s_) {
       s_->t_call.store(t_step_, std::memory_order_relaxed);
@@ -108,6 +139,7 @@ class CallMark {
   ~CallMark() {
     if (!outer_) return;
     finish_step();
+    if (step_times_on()) step_times_add(call_, "(call)", inflight_now_ms() - t_call_);
     if (s_) s_->call.store(nullptr, std::memory_order_release);
     current_mark() = nullptr;
   }
@@ -116,6 +148,7 @@ class CallMark {
   void finish_step() {
     if (!step_) return;
     const double d = inflight_now_ms() - t_step_;
+    if (step_times_on()) step_times_add(call_, step_, d);
     if (d > slow_step_ms())
       std::fprintf(stderr, "[mythril_amd] slow step: %s/%s (%llu) took %.0f ms\n", call_, step_,
                    (unsigned long long)arg_, d);
@@ -125,7 +158,7 @@ class CallMark {
   const char* call_;
   const char* step_ = nullptr;
   uint64_t arg_ = 0;
-  double t_step_;
+  double t_step_, t_call_ = 0.0;
 };
 
 // Name the current step of this thread's call from inside a helper
@@ -157,6 +190,26 @@ inline int inflight_report(char* buf, size_t n) {
     }
   }
   return calls;
+}
+
+// "call/step ms count" per line, then the table is cleared; returns the
+// number of lines (0 when MYTHRIL_AMD_STEP_TIMES is off).
+inline int step_times_report(char* buf, size_t n) {
+  StepTimes& st = step_times();
+  std::lock_guard<std::mutex> lk(st.mu);
+  size_t used = 0;
+  int lines = 0;
+  if (buf && n) buf[0] = 0;
+  for (auto& kv : st.t) {
+    if (buf && used + 1 < n) {
+      const int w = std::snprintf(buf + used, n - used, "%s %.6f %llu\n", kv.first.c_str(), kv.second.first,
+                                  (unsigned long long)kv.second.second);
+      if (w > 0) used = std::min(n - 1, used + (size_t)w);
+    }
+    ++lines;
+  }
+  st.t.clear();
+  return lines;
 }
 
 }  // namespace mw

@@ -1467,6 +1467,7 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   HIPCHK(stage_readback(c, nprog));   // counters and d_min, one copy
   mark.step("sync", count);
   HIPCHK(hipStreamSynchronize(c->stream));
+  c->up_pending = false;   // the stream drained: a queued program upload has landed
   const u64* stripes = (const u64*)c->h_blk;
   const u64* mins = (const u64*)(c->h_blk + c->off_min);
   u64 ctr[kNCounters] = {0, 0, 0, 0, 0};
@@ -1803,5 +1804,9 @@ int mg_keccak256(mg_ctx* h, const uint8_t* data, size_t ndata, const uint64_t* o
 // The C-ABI calls in flight on every thread, one line each (mw_inflight.h):
 // for a watchdog that finds a call that does not return.  Never blocks.
 int mg_debug_inflight(char* buf, size_t n) { return mw::inflight_report(buf, n); }
+
+// Wall time per call and step since the last read (MYTHRIL_AMD_STEP_TIMES=1;
+// "call/step ms count" lines), then cleared; 0 lines when off.
+int mg_debug_step_times(char* buf, size_t n) { return mw::step_times_report(buf, n); }
 
 }  // extern "C"

@@ -81,6 +81,7 @@ SIGNATURES = {
                                     ctypes.POINTER(ctypes.c_double)]),
     "mg_last_error": (ctypes.c_char_p, []),
     "mg_debug_inflight": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
+    "mg_debug_step_times": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
 }
 
 
@@ -311,6 +312,19 @@ def inflight() -> str:
     buf = ctypes.create_string_buffer(8192)
     _lib.mg_debug_inflight(buf, len(buf))
     return buf.value.decode(errors="replace")
+
+
+def step_times() -> dict:
+    """{"call/step": (ms, count)} since the last read (MYTHRIL_AMD_STEP_TIMES=1), then cleared."""
+    if _lib is None:
+        return {}
+    buf = ctypes.create_string_buffer(1 << 16)
+    _lib.mg_debug_step_times(buf, len(buf))
+    out = {}
+    for ln in buf.value.decode(errors="replace").splitlines():
+        k, ms, n = ln.rsplit(" ", 2)
+        out[k] = (float(ms), int(n))
+    return out
 
 
 def validate(p: Program) -> None:

@@ -14,6 +14,7 @@
 #   config         tools/config_bench.py (C2-C4 queries) -> config_bench.json
 #   gt[=LOG2]      tools/ground_truth.py: the corpus's unknown queries searched up to 2^LOG2 (32)
 #   latency        tools/latency_bench.py (drop-in prepare/search/materialise per query)
+#   dropinprof     tools/dropin_profile.py (library step times per drop-in query)
 #   replay         python -m mythril_amd.replay tests/golden/solver_log
 #   replaylat      tools/replay_latency.py (LASER-order translation + preparation, host only)
 #   opbench        tools/opbench.py jit
@@ -91,6 +92,9 @@ for step in "$@"; do
     latency)
       run 600 "$OUT/latency.log" python3 tools/latency_bench.py --out "$OUT/latency.json"
       tail -20 "$OUT/latency.log" ;;
+    dropinprof)
+      run 300 "$OUT/dropin_profile.log" python3 tools/dropin_profile.py --out "$OUT/dropin_profile.json"
+      head -60 "$OUT/dropin_profile.log" ;;
     replay)
       run 300 "$OUT/replay.txt" python3 -m mythril_amd.replay tests/golden/solver_log
       tail -12 "$OUT/replay.txt" ;;
