@@ -957,6 +957,11 @@ int mg_init(int device, mg_ctx** out) {
   HIPCHK(hipGetDeviceCount(&n));
   if (device < 0 || device >= n) return fail(MG_E_ARG, "no such device");
   HIPCHK(hipSetDevice(device));
+  // MYTHRIL_AMD_SPIN=1 (A/B runs, tools/dropin_profile.py): synchronising
+  // threads spin instead of yielding (lower wake-up latency per call)
+  if (const char* e = std::getenv("MYTHRIL_AMD_SPIN"); e && e[0] == '1') {
+    if (hipSetDeviceFlags(hipDeviceScheduleSpin) != hipSuccess) (void)hipGetLastError();
+  }
   auto c = std::make_shared<Ctx>();
   c->dev = device;
   mark.step("properties");

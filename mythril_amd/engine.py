@@ -155,6 +155,21 @@ def _prepare(conjuncts, ctx, use_pools, timings) -> Query:
     return q
 
 
+# Python-side phase times of WitnessEngine.search (tools/dropin_profile.py):
+# a dict to accumulate {phase: [seconds, count]} into, or None (off)
+PROFILE: Optional[dict] = None
+
+
+def _tick(prof: dict, key: str, t0: float) -> float:
+    t = time.perf_counter()
+    e = prof.get(key)
+    if e is None:
+        e = prof[key] = [0.0, 0]
+    e[0] += t - t0
+    e[1] += 1
+    return t
+
+
 _PREBUILD = None   # one host thread for witness-program compiles (_prebuild_witness_programs)
 _PREBUILD_LOCK = threading.Lock()
 
@@ -166,6 +181,15 @@ def _build_witness_program(q: "Query") -> None:
         pass
     time.sleep(0)   # hand the GIL back between queries (the search caller waits for it)
 
+
+# MYTHRIL_AMD_WITNESS_THREAD=1: compile the witness programs on a host thread
+# while the search runs (rounds 4-5).  Off by default since round 6: the
+# compile is mostly Python, so the thread holds the GIL the searching caller
+# needs back after each library call; without it a LASER query costs 0.36
+# instead of 0.44 ms on the device path (profiles/r6e, tools/dropin_profile.py
+# --ab), and a witness program compiles only when a search found a witness.
+import os as _os
+WITNESS_THREAD = _os.environ.get("MYTHRIL_AMD_WITNESS_THREAD", "0") == "1"
 
 # Larger witness programs compile in materialize: their Python part (record
 # stream, leaf table) would hold the GIL the returning search call waits for.
@@ -258,6 +282,8 @@ def _prebuild_witness_programs(queries) -> bool:
     Query.trace_program takes a finished one, waits for a running one and
     compiles a not yet started one itself, so nothing is compiled twice and
     no search waits for the compiles of queries that found nothing."""
+    if not WITNESS_THREAD:
+        return False
     todo = [q for q in queries if q._trace is None and q._trace_future is None
             and len(q.arg_terms) <= PREBUILD_MAX_TERMS and not all(t.op == "const" for t in q.arg_terms)]
     if not todo:
@@ -455,19 +481,27 @@ class WitnessEngine:
         count = count or self.launch_count(queries)
         dps = []
         hits = set()
+        prof = PROFILE
+        t0 = time.perf_counter() if prof is not None else 0.0
         # the witness programs compile on a host thread while the programs
         # upload and the device searches (those calls release the GIL): a
         # witness then costs one upload and one launch (materialize)
         queued = _prebuild_witness_programs(queries)
         try:
             with _gil_handoff(queued):
+                if prof is not None:
+                    _tick(prof, "prebuild", t0)
                 for q in queries:   # a failed load frees the programs already loaded
                     dps.append(self.dev.load(q.program))
+                if prof is not None:
+                    t0 = _tick(prof, "load", t0)
                 if (self.asmjit_min_ops and hasattr(self.dev, "attach_asm")
                         and count * sum(q.ops_per_eval for q in queries) >= self.asmjit_min_ops):
                     self._assemble(dps)
                 found, st = search_phased(self.dev, dps, self.seed, begin, count, flags,
                                           [lambda n, q=q: search_program(q, n) for q in queries])
+                if prof is not None:
+                    t0 = _tick(prof, "search", t0)
             self.stats["searches"] += 1
             self.stats["programs"] += len(queries)
             self.stats["evals"] += st["evals"]
@@ -485,6 +519,8 @@ class WitnessEngine:
                     self.stats["hits"] += 1
                     hits.add(id(q))
                 out.append(w)
+            if prof is not None:
+                t0 = _tick(prof, "materialize", t0)
         finally:
             for dp in dps:
                 dp.free()
@@ -498,6 +534,8 @@ class WitnessEngine:
                     if f is not None and id(q) not in hits:
                         f.cancel()
                         q._trace_future = None
+            if prof is not None:
+                _tick(prof, "free", t0)
         return out
 
     def _assemble(self, dps) -> None:
@@ -586,7 +624,10 @@ class WitnessEngine:
     def _materialize_traced(self, q: Query, index: int, search_dp=None) -> Optional[Witness]:
         from .runtime import EngineError, trace_column
         t0 = time.perf_counter()
+        waited = q._trace is None
         p = q.trace_program
+        if PROFILE is not None:
+            _tick(PROFILE, "materialize/witness program" + (" (waited)" if waited else ""), t0)
         # a witness program built from the search program's stream shares its
         # leaf table (compile_trace_native checked the leaf order).  Otherwise
         # the search program's leaves must lead the witness program's in the
@@ -607,6 +648,9 @@ class WitnessEngine:
         t3 = time.perf_counter()
         # seconds per step of the last traced witness (tools/latency_bench.py)
         self.last_materialize = {"program": t1 - t0, "load": t2 - t1, "eval": t3 - t2}
+        if PROFILE is not None:
+            PROFILE.setdefault("materialize/load (mg_prog_load)", [0.0, 0])[0] += t2 - t1
+            PROFILE.setdefault("materialize/eval (mg_eval_generated)", [0.0, 0])[0] += t3 - t2
         col = trace_column(trace)   # the one candidate's rows, read per node below
         tmap, frm = p.trace_map, int.from_bytes
         values = {}

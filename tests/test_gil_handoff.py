@@ -62,9 +62,11 @@ def test_a_change_made_meanwhile_is_kept():
         sys.setswitchinterval(before)
 
 
-def test_search_withdraws_queued_compiles_of_misses():
+def test_search_withdraws_queued_compiles_of_misses(monkeypatch):
     """a search that finds nothing leaves no witness-program
-    compile queued on the host thread (nor when the device raises)."""
+    compile queued on the host thread (nor when the device raises).  The
+    thread is off by default since round 6 (MYTHRIL_AMD_WITNESS_THREAD=1)."""
+    monkeypatch.setattr(engine, "WITNESS_THREAD", True)
     from mythril_amd.engine import WitnessEngine, prepare
     from mythril_amd.ir import Ctx
     from tests.fakedev import FakeDevice

@@ -23,7 +23,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--every", type=int, default=2, help="profile every K-th query of the corpus")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--ab", action="store_true",
+                    help="run the profile once per A/B environment (a child process each) and compare")
     a = ap.parse_args()
+    if a.ab:
+        return ab(a)
     from mythril_amd import runtime
     from mythril_amd.engine import WitnessEngine, prepare
     from mythril_amd.smt2 import parse_file
@@ -36,6 +40,8 @@ def main():
     for q in qs[:8]:      # warm-up: pools, pinned buffers, code paths
         eng.search([q])
     runtime.step_times()
+    from mythril_amd import engine
+    engine.PROFILE = {}
     py = {"engine.search": 0.0}
     t0 = time.perf_counter()
     hits = 0
@@ -48,12 +54,43 @@ def main():
     lib = runtime.step_times()
     n = len(qs)
     rows = sorted(((k, ms / n, c / n) for k, (ms, c) in lib.items()), key=lambda r: -r[1])
+    phases = {k: {"ms": round(v[0] * 1e3 / n, 5), "calls": round(v[1] / n, 3)} for k, v in engine.PROFILE.items()}
+    engine.PROFILE = None
     out = {"queries": n, "hits": hits, "wall_ms_per_query": wall * 1e3 / n,
            "python_ms_per_query": {k: v * 1e3 / n for k, v in py.items()},
+           "engine_search_phases_ms_per_query": phases,
            "library_ms_per_query": {k: {"ms": round(ms, 5), "calls": round(c, 3)} for k, ms, c in rows}}
     print(json.dumps(out, indent=1))
     if a.out:
         json.dump(out, open(a.out, "w"), indent=1)
+
+
+AB = {
+    "base": {},
+    "no_witness_thread": {"MYTHRIL_AMD_WITNESS_THREAD": "0"},
+    "nt_spin": {"MYTHRIL_AMD_WITNESS_THREAD": "0", "MYTHRIL_AMD_SPIN": "1"},
+    "nt_nosdma": {"MYTHRIL_AMD_WITNESS_THREAD": "0", "HSA_ENABLE_SDMA": "0"},
+    "nt_spin_nosdma": {"MYTHRIL_AMD_WITNESS_THREAD": "0", "MYTHRIL_AMD_SPIN": "1", "HSA_ENABLE_SDMA": "0"},
+}
+
+
+def ab(a):
+    import subprocess
+    import tempfile
+    res = {}
+    for name, env in AB.items():
+        with tempfile.NamedTemporaryFile(suffix=".json") as f:
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--every", str(a.every), "--out", f.name],
+                               env=dict(os.environ, **env), capture_output=True, text=True, timeout=280)
+            if r.returncode != 0:
+                print(name, "failed", r.stderr[-2000:], flush=True)
+                continue
+            d = json.load(open(f.name))
+        res[name] = d
+        print(f"{name:18s} {d['wall_ms_per_query']:.4f} ms/query  "
+              + "  ".join(f"{k} {v['ms']:.4f}" for k, v in d["engine_search_phases_ms_per_query"].items()), flush=True)
+    if a.out:
+        json.dump(res, open(a.out, "w"), indent=1)
 
 
 if __name__ == "__main__":

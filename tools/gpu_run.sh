@@ -95,6 +95,9 @@ for step in "$@"; do
     dropinprof)
       run 300 "$OUT/dropin_profile.log" python3 tools/dropin_profile.py --out "$OUT/dropin_profile.json"
       head -60 "$OUT/dropin_profile.log" ;;
+    dropinab)   # the same under each A/B environment (tools/dropin_profile.py --ab)
+      run 900 "$OUT/dropin_ab.log" python3 tools/dropin_profile.py --ab --out "$OUT/dropin_ab.json"
+      tail -30 "$OUT/dropin_ab.log" ;;
     replay)
       run 300 "$OUT/replay.txt" python3 -m mythril_amd.replay tests/golden/solver_log
       tail -12 "$OUT/replay.txt" ;;
