@@ -62,6 +62,10 @@ class KeccakService:
         self.min_batch = min_batch
         self.memo: Dict[bytes, bytes] = {}
         self.stats = {"requests": 0, "memo_hits": 0, "launches": 0, "gpu_hashes": 0, "reference_hashes": 0}
+        # one record per batch of more than one message (a prefetch, a
+        # _replace_with_actual_sha): its size, the digests it had to compute,
+        # and whether the device computed them (tests/test_keccak_batches.py)
+        self.batches: List[Dict[str, object]] = []
 
     # -- batch entry -------------------------------------------------------
     def hash_many(self, msgs: Iterable[bytes]) -> List[bytes]:
@@ -72,13 +76,16 @@ class KeccakService:
         if todo:
             if len(self.memo) + len(todo) > MEMO_MAX:
                 self.memo.clear()
-            if self.device is not None and len(todo) >= self.min_batch:
+            on_device = self.device is not None and len(todo) >= self.min_batch
+            if on_device:
                 digests, _ = self.device.keccak256(todo)
                 self.stats["launches"] += 1
                 self.stats["gpu_hashes"] += len(todo)
             else:
                 digests = [self._reference(m) for m in todo]
             self.memo.update(zip(todo, digests))
+        if len(msgs) > 1 and len(self.batches) < 4096:
+            self.batches.append({"size": len(msgs), "new": len(todo), "device": bool(todo) and on_device})
         return [self.memo[m] for m in msgs]
 
     def digest(self, msg: bytes) -> bytes:

@@ -204,7 +204,10 @@ def _state(q):
         assert cons[-1] is q.keccak_cond
         kc = FakeBool(cons.pop())
     c = Constraints([FakeBool(n) for n in cons], kc)
-    return types.SimpleNamespace(world_state=types.SimpleNamespace(constraints=c))
+    # a LASER world state holds the target contract's account (its address is
+    # a storage key the plugin's Keccak speculation hashes, mythril_plugin.storage_keys)
+    from tests.laser_concolic import CONTRACT
+    return types.SimpleNamespace(world_state=types.SimpleNamespace(constraints=c, accounts={CONTRACT: None}))
 
 
 def install_standins(monkeypatch, model_for, ctx):
