@@ -130,6 +130,15 @@ int mg_eval_generated(mg_ctx* ctx, const mg_prog* prog, uint64_t seed, uint64_t 
  * (mythril/laser/smt/solver/solver.py:68-77) for the free symbols. */
 int mg_witness_leaves(mg_ctx* ctx, const mg_prog* prog, uint64_t seed, uint64_t index, uint32_t* out);
 
+/* One-shot evaluation of a program description that is not kept: upload,
+ * mg_eval_generated's evaluation of candidates [begin, begin+count) and the
+ * release, in one call (a witness program read once at the found index).
+ * Same validation, results and trace layout as mg_prog_load +
+ * mg_eval_generated + mg_prog_free.  Replaces the reference's model
+ * evaluation of the witness (z3 ModelRef.eval, mythril/support/model.py:58-60). */
+int mg_eval_program(mg_ctx* ctx, const mg_prog_desc* desc, uint64_t seed, uint64_t begin, size_t count,
+                    uint32_t* verdict, uint32_t* trace);
+
 /* Attach a specialised kernel to a loaded program: `image` is a gfx950 code
  * object generated from this program's own IR by mythril_amd/jit.py (one
  * straight-line kernel per program, csrc/mw_jit.h).  It must export

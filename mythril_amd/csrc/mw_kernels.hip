@@ -1027,20 +1027,12 @@ static bool trace_rows_covered(const mg_prog_desc* d) {
   return left == 0;
 }
 
-int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
-  if (!h || !d || !out) return fail(MG_E_ARG, "null argument");
-  *out = nullptr;
-  mw::CallMark mark("mg_prog_load");
-  std::shared_ptr<Ctx> cref = g_reg.ctx(hid(h));
-  if (!cref) return fail(MG_E_ARG, "mg_prog_load: not a live context");
-  mark.step("validate", d->ncode_words);
-  int rc = mg_validate_desc(d);
-  if (rc) return rc;
+// The upload of a validated program into context c (its mu held, the
+// device set): device buffer from the pool, staged through the pinned
+// buffer, predecoded for the smallest asm layout that holds it, copy queued.
+static int load_locked(const std::shared_ptr<Ctx>& cref, const mg_prog_desc* d, std::shared_ptr<Prog>& out) {
   Ctx* c = cref.get();
-  mark.step("lock");
-  std::lock_guard<std::mutex> lk(c->mu);
-  if (c->dead) return fail(MG_E_ARG, "mg_prog_load: the context was freed during the call");
-  HIPCHK(hipSetDevice(c->dev));
+  mw::CallMark mark("load_locked");   // nested: its steps are the caller's
   // constants padded to >= MW_KPAD words: the interpreter's branch-free narrow
   // operand fetch reads cpool[slot] (slot < 64) before selecting the register
   const size_t nc = d->ncode_words, nk = (d->nconst_words + 8 > MW_KPAD ? d->nconst_words + 8 : MW_KPAD), nl = d->nleaves * MW_LEAF_WORDS + 8,
@@ -1138,6 +1130,27 @@ int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
   p->desc.consts = nullptr;
   p->desc.leaves = nullptr;
   p->desc.pool = nullptr;
+  out = std::move(p);
+  return 0;
+}
+
+int mg_prog_load(mg_ctx* h, const mg_prog_desc* d, mg_prog** out) {
+  if (!h || !d || !out) return fail(MG_E_ARG, "null argument");
+  *out = nullptr;
+  mw::CallMark mark("mg_prog_load");
+  std::shared_ptr<Ctx> cref = g_reg.ctx(hid(h));
+  if (!cref) return fail(MG_E_ARG, "mg_prog_load: not a live context");
+  mark.step("validate", d->ncode_words);
+  int rc = mg_validate_desc(d);
+  if (rc) return rc;
+  Ctx* c = cref.get();
+  mark.step("lock");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->dead) return fail(MG_E_ARG, "mg_prog_load: the context was freed during the call");
+  HIPCHK(hipSetDevice(c->dev));
+  std::shared_ptr<Prog> p;
+  rc = load_locked(cref, d, p);
+  if (rc) return rc;
   *out = (mg_prog*)(uintptr_t)g_reg.add_prog(std::move(p));   // published under c->mu (mw_handles.h)
   return 0;
 }
@@ -1683,6 +1696,38 @@ int mg_eval_generated(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t begi
   s_v.synced = e == hipSuccess;
   if (e != hipSuccess) return fail(MG_E_HIP, std::string("eval (specialised): ") + hipGetErrorString(e));
   return 0;
+}
+
+// One-shot evaluation of a program that is not kept (a witness program:
+// engine.WitnessEngine._materialize_traced): upload, evaluation and release
+// in one call under one lock, the upload's buffer back to the pool after the
+// evaluation's synchronisation.  Same results as mg_prog_load +
+// mg_eval_generated + mg_prog_free.
+int mg_eval_program(mg_ctx* h, const mg_prog_desc* d, uint64_t seed, uint64_t begin, size_t count, uint32_t* verdict,
+                    uint32_t* trace) {
+  if (!h || !d || !verdict || count == 0) return fail(MG_E_ARG, "null argument");
+  mw::CallMark mark("mg_eval_program");
+  std::shared_ptr<Ctx> cref = g_reg.ctx(hid(h));
+  if (!cref) return fail(MG_E_ARG, "mg_eval_program: not a live context");
+  mark.step("validate", d->ncode_words);
+  int rc = mg_validate_desc(d);
+  if (rc) return rc;
+  Ctx* c = cref.get();
+  mark.step("lock");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->dead) return fail(MG_E_ARG, "mg_eval_program: the context was freed during the call");
+  HIPCHK(hipSetDevice(c->dev));
+  std::shared_ptr<Prog> p;
+  rc = load_locked(cref, d, p);
+  if (rc) return rc;
+  mark.step("eval", count);
+  rc = eval_asm(c, p.get(), seed, begin, count, verdict, trace);
+  if (rc == 1) rc = eval_common(c, p.get(), nullptr, count, seed, begin, verdict, trace);
+  if (rc != 0) hipStreamSynchronize(c->stream);   // a failed launch: nothing may still read the buffer
+  mark.step("release");
+  release_prog(*p);
+  p->dead = true;
+  return rc;
 }
 
 int mg_witness_leaves(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t index, uint32_t* out) {

@@ -639,12 +639,17 @@ class WitnessEngine:
             # an EngineError, so get_model's handler sends the query to z3
             raise EngineError("witness program's leaf layout differs from the search program's")
         t1 = time.perf_counter()
-        dp = self.dev.load(p)
-        t2 = time.perf_counter()
-        try:
-            _, trace = self.dev.eval_generated(dp, self.seed, index, 1)
-        finally:
-            dp.free()
+        if hasattr(self.dev, "eval_program"):
+            # upload, evaluation and release in one library call (mg_eval_program)
+            t2 = t1
+            _, trace = self.dev.eval_program(p, self.seed, index, 1)
+        else:
+            dp = self.dev.load(p)
+            t2 = time.perf_counter()
+            try:
+                _, trace = self.dev.eval_generated(dp, self.seed, index, 1)
+            finally:
+                dp.free()
         t3 = time.perf_counter()
         # seconds per step of the last traced witness (tools/latency_bench.py)
         self.last_materialize = {"program": t1 - t0, "load": t2 - t1, "eval": t3 - t2}

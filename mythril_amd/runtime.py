@@ -74,6 +74,8 @@ SIGNATURES = {
     "mg_eval": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t, _P, _P]),
     "mg_eval_generated": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, _P, _P]),
     "mg_witness_leaves": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, _P]),
+    "mg_eval_program": (ctypes.c_int, [_P, ctypes.POINTER(MgProgDesc), ctypes.c_uint64, ctypes.c_uint64,
+                                       ctypes.c_size_t, _P, _P]),
     "mg_keccak256": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _P, _P, ctypes.c_size_t, _P, ctypes.POINTER(MgStats)]),
     "mg_keccak256_device": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_size_t, _P, ctypes.POINTER(MgStats)]),
     "mg_validate_desc": (ctypes.c_int, [ctypes.POINTER(MgProgDesc)]),
@@ -261,6 +263,20 @@ class Device:
                                                     v.ctypes.data, _ptr(t) if t is not None else None),
                "mg_eval_generated")
         return v, (t.reshape(dp.prog.n_trace_rows, count) if t is not None else None)
+
+    def eval_program(self, p: Program, seed: int, begin: int, count: int = 1,
+                     trace: bool = True) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+        """load + eval_generated + free of a program that is not kept, in one
+        library call (mg_eval_program)."""
+        if not self.handle:
+            raise EngineError("device context is closed")
+        d, keep = make_desc(p)
+        v = np.zeros(count, dtype=np.uint32)
+        t = np.zeros(p.n_trace_rows * count, dtype=np.uint32) if trace and p.n_trace_rows else None
+        _check(self.lib, self.lib.mg_eval_program(self.handle, ctypes.byref(d), seed & ((1 << 64) - 1), begin, count,
+                                                  v.ctypes.data, _ptr(t) if t is not None else None),
+               "mg_eval_program")
+        return v, (t.reshape(p.n_trace_rows, count) if t is not None else None)
 
     def witness_leaves(self, dp: DeviceProgram, seed: int, index: int) -> List[int]:
         """The value of every leaf of dp's program at candidate index, in

@@ -43,7 +43,7 @@ def test_library_exports_the_report():
 def test_every_device_call_is_marked():
     src = (ROOT / "mythril_amd" / "csrc" / "mw_kernels.hip").read_text()
     for fn in ("mg_init", "mg_free", "mg_prog_load", "mg_prog_free", "mg_search", "mg_eval", "mg_eval_generated",
-               "mg_witness_leaves", "mg_prog_attach_kernel", "mg_prog_attach_asm", "mg_keccak256",
+               "mg_witness_leaves", "mg_eval_program", "mg_prog_attach_kernel", "mg_prog_attach_asm", "mg_keccak256",
                "mg_keccak256_device"):
         body = src[src.index(f"int {fn}("):]
         body = body[:body.index("\n}\n")]
