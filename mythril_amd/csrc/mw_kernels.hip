@@ -401,6 +401,9 @@ struct Ctx {
   int ncu = 256;
   hipStream_t stream = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipEvent_t ea = nullptr, eb = nullptr;   // step-time accounting only (MYTHRIL_AMD_STEP_TIMES=1)
+  hipEvent_t eu = nullptr;                 // ... recorded before a program upload's copy
+  bool eu_live = false;
   u32* d_spill = nullptr;
   size_t spill_bytes = 0;
   // One call's launch records, in one device block mirrored by a pinned host
@@ -675,6 +678,10 @@ void release_ctx(Ctx& c) {
   if (c.d_alive) hipFree(c.d_alive);
   if (c.e0) hipEventDestroy(c.e0);
   if (c.e1) hipEventDestroy(c.e1);
+  if (c.ea) hipEventDestroy(c.ea);
+  if (c.eb) hipEventDestroy(c.eb);
+  if (c.eu) hipEventDestroy(c.eu);
+  c.ea = c.eb = c.eu = nullptr;
   if (c.stream) hipStreamDestroy(c.stream);
   c.d_spill = nullptr;
   c.d_blk = c.h_blk = nullptr;
@@ -971,6 +978,8 @@ int mg_init(int device, mg_ctx** out) {
   mark.step("stream");
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->e0) != hipSuccess || hipEventCreate(&c->e1) != hipSuccess ||
+      (mw::step_times_on() && (hipEventCreate(&c->ea) != hipSuccess || hipEventCreate(&c->eb) != hipSuccess ||
+                               hipEventCreate(&c->eu) != hipSuccess)) ||
       ensure_launch(c.get(), 16, 4) != 0) {
     release_ctx(*c);
     return fail(MG_E_HIP, "context setup failed");
@@ -1106,6 +1115,7 @@ static int load_locked(const std::shared_ptr<Ctx>& cref, const mg_prog_desc* d, 
   // queued on the context's stream: every launch that reads the program is
   // queued after it on the same stream
   mark.step("upload", total * 4);
+  if (c->eu && !c->eu_live) c->eu_live = hipEventRecord(c->eu, c->stream) == hipSuccess;
   if (hipMemcpyAsync(p->d_buf, hbuf, total * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
     release_prog(*p);
     return fail(MG_E_HIP, "program upload copy failed");
@@ -1442,6 +1452,10 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   }
   // one upload: zeroed counters, d_min at MG_NONE, the ProgDev and AsmArgs records
   mark.step("enqueue", count);
+  // step-time accounting: the stream's own time before the records upload
+  // (a queued program upload), the upload, the kernels and the readback
+  const bool gpu_steps = mw::step_times_on() && c->ea && c->eb;
+  if (gpu_steps) HIPCHK(hipEventRecord(c->ea, c->stream));
   HIPCHK(stage_upload(c, nprog, hp.data(), nia, ha.data(), need_args ? ha.size() : 0));
   HIPCHK(hipEventRecord(c->e0, c->stream));
   for (int gi = 0; gi < kAsmLayouts; ++gi) {
@@ -1483,9 +1497,23 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   }
   HIPCHK(hipEventRecord(c->e1, c->stream));
   HIPCHK(stage_readback(c, nprog));   // counters and d_min, one copy
+  if (gpu_steps) HIPCHK(hipEventRecord(c->eb, c->stream));
   mark.step("sync", count);
   HIPCHK(hipStreamSynchronize(c->stream));
   c->up_pending = false;   // the stream drained: a queued program upload has landed
+  if (gpu_steps) {
+    float a = 0.f, k = 0.f, b = 0.f;
+    if (hipEventElapsedTime(&a, c->ea, c->e0) == hipSuccess && hipEventElapsedTime(&k, c->e0, c->e1) == hipSuccess &&
+        hipEventElapsedTime(&b, c->e1, c->eb) == hipSuccess) {
+      mw::step_times_add("mg_search", "gpu: records upload", a);
+      mw::step_times_add("mg_search", "gpu: kernels", k);
+      mw::step_times_add("mg_search", "gpu: readback", b);
+    }
+    float u = 0.f;
+    if (c->eu_live && hipEventElapsedTime(&u, c->eu, c->ea) == hipSuccess)
+      mw::step_times_add("mg_search", "gpu: queued program uploads", u);
+  }
+  c->eu_live = false;
   const u64* stripes = (const u64*)c->h_blk;
   const u64* mins = (const u64*)(c->h_blk + c->off_min);
   u64 ctr[kNCounters] = {0, 0, 0, 0, 0};

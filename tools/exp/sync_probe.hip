@@ -30,6 +30,14 @@
 __global__ void k_empty(unsigned* out) {
   if (threadIdx.x == 0 && blockIdx.x == 0 && out) out[0] += 1u;
 }
+extern __shared__ unsigned lds_buf[];
+// a search-shaped launch: many blocks, large dynamic LDS, ~iters dependent ALU steps per lane
+__global__ __launch_bounds__(256, 2) void k_big(unsigned* out, unsigned iters) {
+  unsigned x = threadIdx.x;
+  lds_buf[threadIdx.x] = x;
+  for (unsigned i = 0; i < iters; ++i) x = x * 1664525u + 1013904223u;
+  if (x == 0x12345678u) out[blockIdx.x] = x + lds_buf[threadIdx.x];
+}
 __global__ void k_rw(const unsigned long long* in, unsigned long long* out) {
   if (threadIdx.x == 0 && blockIdx.x == 0) out[0] = in[0] + 1ull;
 }
@@ -102,6 +110,31 @@ int main() {
     hipLaunchKernelGGL(k_rw, dim3(1), dim3(64), 0, s, d, h + 16);
     (void)hipStreamSynchronize(s);
   });
+  (void)hipFuncSetAttribute((const void*)k_big, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+  unsigned long long* hb = nullptr;
+  CK(hipHostMalloc(&hb, 1 << 16, hipHostMallocDefault));
+  for (unsigned iters : {0u, 2000u, 8000u}) {
+    for (unsigned blocks : {256u, 2048u}) {
+      char nm[64];
+      std::snprintf(nm, sizeof nm, "big%u/%u", blocks, iters);
+      run(nm, [&] {
+        hipLaunchKernelGGL(k_big, dim3(blocks), dim3(256), 80 * 1024, s, (unsigned*)d, iters);
+        (void)hipStreamSynchronize(s);
+      });
+      std::snprintf(nm, sizeof nm, "big%u/%u+ev+cp", blocks, iters);
+      float kms = 0.f;
+      run(nm, [&] {
+        (void)hipMemcpyAsync(d, hb, 1024, hipMemcpyHostToDevice, s);
+        (void)hipEventRecord(e0, s);
+        hipLaunchKernelGGL(k_big, dim3(blocks), dim3(256), 80 * 1024, s, (unsigned*)d, iters);
+        (void)hipEventRecord(e1, s);
+        (void)hipMemcpyAsync(hb + 1024, d, 8320, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        (void)hipEventElapsedTime(&kms, e0, e1);
+      });
+      std::printf("   (kernel by events: %.1f us)\n", kms * 1e3);
+    }
+  }
   std::printf("check %llu\n", h[16]);
   return 0;
 }
