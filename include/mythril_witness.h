@@ -106,6 +106,23 @@ int mg_search(mg_ctx* ctx, mg_prog* const* progs, size_t nprog, uint64_t seed,
               uint64_t begin, uint64_t count, uint32_t flags, uint64_t* out_min_idx,
               mg_stats* stats);
 
+/* mg_search in two calls, so the caller can work on the host while the device
+ * searches (engine.WitnessEngine compiles the witness programs meanwhile).
+ * mg_search_begin validates, plans and enqueues the search and returns; until
+ * mg_search_end every other call that launches work on this context is
+ * refused (MG_E_ARG), and a program of the search freed meanwhile waits for it.
+ * mg_search_end completes it: the same out_min_idx and stats as mg_search.
+ * witness (nullable): per program, a witness program description (or NULL);
+ * each is uploaded and evaluated at the index its program's search found,
+ * queued after the search, read back with the same synchronisation into
+ * out_trace[i] (its n_trace_rows words; traced[i] = 1), or left for the caller
+ * (traced[i] = 0: no witness found, or a program the asm interpreter does not
+ * run).  Replaces Optimize.check + model() of mythril/support/model.py:58-60. */
+int mg_search_begin(mg_ctx* ctx, mg_prog* const* progs, size_t nprog, uint64_t seed, uint64_t begin,
+                    uint64_t count, uint32_t flags);
+int mg_search_end(mg_ctx* ctx, uint64_t* out_min_idx, mg_stats* stats, const mg_prog_desc* const* witness,
+                  uint32_t* const* out_trace, int32_t* traced);
+
 /* Evaluate one program on explicit assignments: leaves_soa has n_input_rows
  * rows of ncand u32 (row r, candidate i at [r*ncand + i]).  verdict[i] = 0/1;
  * trace (may be NULL) receives n_trace_rows rows of ncand u32. */

@@ -315,6 +315,20 @@ __global__ __launch_bounds__(kBlock, 2) void mw_eval_kernel(ProgDev P, const u32
 
 // The leaf values of one candidate: one thread per leaf, the candidate
 // generator of every search engine (mw_leaf.h leaf_value), for mg_witness_leaves.
+// The witness evaluations of mg_search_end read the candidate index the
+// search found, on the device: record k evaluates index dmin[slot[k]] (0 when
+// that search found nothing; the host ignores that trace).
+__global__ __launch_bounds__(kBlock) void mw_witness_index_kernel(const u64* __restrict__ dmin,
+                                                                   const u32* __restrict__ slot, AsmArgs* args,
+                                                                   u32 n) {
+  const u32 k = blockIdx.x * kBlock + threadIdx.x;
+  if (k >= n) return;
+  u64 m = dmin[slot[k]];
+  if (m == MG_NONE) m = 0;
+  args[k].begin = m;
+  args[k].end = m + 1;
+}
+
 __global__ __launch_bounds__(kBlock) void mw_leaf_kernel(const u32* __restrict__ leaves, const u32* __restrict__ pool,
                                                          u32 nleaves, u64 seed, u64 cand, u32* __restrict__ out) {
   const u32 l = blockIdx.x * kBlock + threadIdx.x;
@@ -396,6 +410,26 @@ double now_ms() {
 
 }  // namespace
 
+struct Prog;
+
+// A search between its enqueue and its completion: mg_search does both in
+// one call; mg_search_begin returns after the enqueue so the caller can work
+// on the host (compile the witness programs) while the device searches, and
+// mg_search_end completes it.  Meanwhile the context's launch records stay
+// untouched: every other call that uses them is refused (context_busy).
+struct Pending {
+  bool active = false;
+  std::vector<std::shared_ptr<Prog>> ps;   // the programs, alive until the end
+  std::vector<size_t> slot;                // program i's word in d_min
+  std::vector<size_t> interp, special;     // d_min order (search_complete)
+  size_t nia = 0;
+  u64 count = 0, ops = 0, seed = 0;
+  u32 flags = 0;
+  size_t nlaunches = 0;
+  double t0 = 0.0;
+  bool gpu_steps = false;
+};
+
 struct Ctx {
   int dev = 0;
   int ncu = 256;
@@ -436,6 +470,9 @@ struct Ctx {
   // class (pool_get / pool_put below; guarded by mu)
   std::map<size_t, std::vector<void*>> pool;
   size_t pool_cached = 0;
+  Pending pending;               // a begun search (mg_search_begin), guarded by mu
+  uint8_t* h_wit = nullptr;      // pinned staging of the witness records (mg_search_end)
+  size_t wit_bytes = 0;
 };
 
 struct Prog {
@@ -654,6 +691,8 @@ void release_prog(Prog& p) {
   // under the context's mu): no kernel still reads the buffer.  Only
   // mg_prog_load returns with its upload queued; whatever reuses the buffer
   // next is queued after that copy on the same stream
+  // ... except a begun search (mg_search_begin): let it finish first
+  if (p.d_buf && p.ctx->pending.active) hipStreamSynchronize(p.ctx->stream);
   if (p.d_buf) pool_put(p.ctx.get(), p.d_buf, p.buf_cls);
   p.d_buf = nullptr;
 }
@@ -670,6 +709,10 @@ void release_ctx(Ctx& c) {
   if (c.h_blk) hipHostFree(c.h_blk);
   if (c.h_up) hipHostFree(c.h_up);
   if (c.h_rb) hipHostFree(c.h_rb);
+  if (c.h_wit) hipHostFree(c.h_wit);
+  c.h_wit = nullptr;
+  c.wit_bytes = 0;
+  c.pending = Pending();
   c.h_rb = nullptr;
   c.rb_bytes = 0;
   c.h_up = nullptr;
@@ -1295,21 +1338,32 @@ int mg_prog_attach_asm(mg_prog* h, const void* image, size_t size, const char* n
   return 0;
 }
 
-int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, uint64_t begin,
-              uint64_t count, uint32_t flags, uint64_t* out_min_idx, mg_stats* st) {
-  if (!h || !hprogs || !out_min_idx || nprog == 0) return fail(MG_E_ARG, "null argument");
-  if (nprog > 65535) return fail(MG_E_ARG, "too many programs per launch");
-  if (count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad candidate range");
-  if (flags & MW_FLAG_STOP_AFTER_HIT) flags &= ~MW_FLAG_NO_COUNT;   // blocks may skip: only the counters know
-  std::vector<u64> ids(nprog);
-  for (size_t i = 0; i < nprog; ++i) ids[i] = hid(hprogs[i]);
-  mw::CallMark mark("mg_search");
-  mark.step("lock", nprog);
-  CallG call;   // resolved, reference-held and locked for the whole call (mw_handles.h)
-  if (const char* why = mw::enter(g_reg, hid(h), ids.data(), nprog, call)) return fail(MG_E_ARG, std::string("mg_search: ") + why);
-  Ctx* c = call.c.get();
+// The eval paths below run inside a call (the context's mu held, handles live).
+// Readbacks up to this size land in the context's pinned buffer with one copy
+// and are handed over with a host memcpy (a copy straight into pageable
+// memory costs a staged transfer per buffer).
+constexpr size_t kReadbackMax = (size_t)1 << 20;
+
+static bool ensure_readback(Ctx* c, size_t bytes) {
+  if (bytes <= c->rb_bytes) return true;
+  mw::inflight_step("ensure_readback/realloc", bytes);
+  if (c->h_rb) hipHostFree(c->h_rb);
+  c->h_rb = nullptr;
+  c->rb_bytes = 0;
+  const size_t want = std::max<size_t>(bytes, (size_t)1 << 16);
+  if (hipHostMalloc(&c->h_rb, want, hipHostMallocDefault) != hipSuccess) return false;
+  c->rb_bytes = want;
+  return true;
+}
+
+// Plan and enqueue a search of ps (the context's mu held): the launch
+// records upload, the kernels, the readback of counters and d_min; P gets what
+// search_complete needs.  Nothing here waits for the device.
+static int search_enqueue(Ctx* c, const std::vector<std::shared_ptr<Prog>>& ps, uint64_t seed, uint64_t begin,
+                          uint64_t count, uint32_t flags, mw::CallMark& mark, Pending& P) {
+  const size_t nprog = ps.size();
   std::vector<const Prog*> progs(nprog);
-  for (size_t i = 0; i < nprog; ++i) progs[i] = call.ps[i].get();
+  for (size_t i = 0; i < nprog; ++i) progs[i] = ps[i].get();
   mark.step("plan", nprog);
   const double t0 = now_ms();
   HIPCHK(hipSetDevice(c->dev));
@@ -1498,10 +1552,32 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   HIPCHK(hipEventRecord(c->e1, c->stream));
   HIPCHK(stage_readback(c, nprog));   // counters and d_min, one copy
   if (gpu_steps) HIPCHK(hipEventRecord(c->eb, c->stream));
+  P.ps = ps;
+  P.interp = interp;
+  P.special = special;
+  P.nia = nia;
+  P.slot.assign(nprog, 0);
+  for (size_t j = 0; j < nia; ++j) P.slot[interp[j]] = j;
+  for (size_t j = 0; j < special.size(); ++j) P.slot[special[j]] = nia + j;
+  P.count = count;
+  P.seed = seed;
+  P.ops = ops;
+  P.flags = flags;
+  P.nlaunches = gasb.size() + special.size();
+  for (const Group& G : groups) P.nlaunches += G.n ? 1 : 0;
+  P.t0 = t0;
+  P.gpu_steps = gpu_steps;
+  return 0;
+}
+
+// Wait for a search enqueued by search_enqueue (and anything queued after it)
+// and read its results (the context's mu held).
+static int search_complete(Ctx* c, Pending& P, uint64_t* out_min_idx, mg_stats* st, mw::CallMark& mark) {
+  const u64 count = P.count;
   mark.step("sync", count);
   HIPCHK(hipStreamSynchronize(c->stream));
   c->up_pending = false;   // the stream drained: a queued program upload has landed
-  if (gpu_steps) {
+  if (P.gpu_steps) {
     float a = 0.f, k = 0.f, b = 0.f;
     if (hipEventElapsedTime(&a, c->ea, c->e0) == hipSuccess && hipEventElapsedTime(&k, c->e0, c->e1) == hipSuccess &&
         hipEventElapsedTime(&b, c->e1, c->eb) == hipSuccess) {
@@ -1521,18 +1597,17 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
     for (int k = 0; k < kNCounters; ++k) ctr[k] += stripes[sidx * MW_CTR_STRIPE_WORDS + k];
   // specialised launches under MW_FLAG_NO_COUNT counted nothing: every
   // candidate of the range was evaluated (no stop-after-hit)
-  const u64 evals = ctr[0] + ((flags & MW_FLAG_NO_COUNT) ? (u64)count * special.size() : 0u);
-  for (size_t j = 0; j < nia; ++j) out_min_idx[interp[j]] = mins[j];
-  for (size_t j = 0; j < special.size(); ++j) out_min_idx[special[j]] = mins[nia + j];
+  const u64 evals = ctr[0] + ((P.flags & MW_FLAG_NO_COUNT) ? P.count * P.special.size() : 0u);
+  for (size_t j = 0; j < P.nia; ++j) out_min_idx[P.interp[j]] = mins[j];
+  for (size_t j = 0; j < P.special.size(); ++j) out_min_idx[P.special[j]] = mins[P.nia + j];
   if (st) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, c->e0, c->e1));
     st->kernel_ms = ms;
-    st->wall_ms = now_ms() - t0;
+    st->wall_ms = now_ms() - P.t0;
     st->evals = evals;  // summed over every program's blocks
-    st->launches = gasb.size() + special.size();
-    for (const Group& G : groups) st->launches += G.n ? 1 : 0;
-    st->ops = (double)evals / (double)nprog * (double)ops;
+    st->launches = P.nlaunches;
+    st->ops = (double)evals / (double)P.ps.size() * (double)P.ops;
     st->lane_div_steps = ctr[1];
     st->lane_div_full = ctr[2];
     st->lane_div_short = ctr[3];
@@ -1541,22 +1616,206 @@ int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, ui
   return 0;
 }
 
-// The eval paths below run inside a call (the context's mu held, handles live).
-// Readbacks up to this size land in the context's pinned buffer with one copy
-// and are handed over with a host memcpy (a copy straight into pageable
-// memory costs a staged transfer per buffer).
-constexpr size_t kReadbackMax = (size_t)1 << 20;
+int mg_search(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, uint64_t begin,
+              uint64_t count, uint32_t flags, uint64_t* out_min_idx, mg_stats* st) {
+  if (!h || !hprogs || !out_min_idx || nprog == 0) return fail(MG_E_ARG, "null argument");
+  if (nprog > 65535) return fail(MG_E_ARG, "too many programs per launch");
+  if (count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad candidate range");
+  if (flags & MW_FLAG_STOP_AFTER_HIT) flags &= ~MW_FLAG_NO_COUNT;   // blocks may skip: only the counters know
+  std::vector<u64> ids(nprog);
+  for (size_t i = 0; i < nprog; ++i) ids[i] = hid(hprogs[i]);
+  mw::CallMark mark("mg_search");
+  mark.step("lock", nprog);
+  CallG call;   // resolved, reference-held and locked for the whole call (mw_handles.h)
+  if (const char* why = mw::enter(g_reg, hid(h), ids.data(), nprog, call)) return fail(MG_E_ARG, std::string("mg_search: ") + why);
+  Ctx* c = call.c.get();
+  if (c->pending.active) return fail(MG_E_ARG, "mg_search: a search begun with mg_search_begin is pending");
+  Pending P;
+  int rc = search_enqueue(c, call.ps, seed, begin, count, flags, mark, P);
+  if (rc) return rc;
+  return search_complete(c, P, out_min_idx, st, mark);
+}
 
-static bool ensure_readback(Ctx* c, size_t bytes) {
-  if (bytes <= c->rb_bytes) return true;
-  mw::inflight_step("ensure_readback/realloc", bytes);
-  if (c->h_rb) hipHostFree(c->h_rb);
-  c->h_rb = nullptr;
-  c->rb_bytes = 0;
-  const size_t want = std::max<size_t>(bytes, (size_t)1 << 16);
-  if (hipHostMalloc(&c->h_rb, want, hipHostMallocDefault) != hipSuccess) return false;
-  c->rb_bytes = want;
-  return true;
+int mg_search_begin(mg_ctx* h, mg_prog* const* hprogs, size_t nprog, uint64_t seed, uint64_t begin,
+                    uint64_t count, uint32_t flags) {
+  if (!h || !hprogs || nprog == 0) return fail(MG_E_ARG, "null argument");
+  if (nprog > 65535) return fail(MG_E_ARG, "too many programs per launch");
+  if (count == 0 || begin + count < begin) return fail(MG_E_ARG, "bad candidate range");
+  if (flags & MW_FLAG_STOP_AFTER_HIT) flags &= ~MW_FLAG_NO_COUNT;
+  std::vector<u64> ids(nprog);
+  for (size_t i = 0; i < nprog; ++i) ids[i] = hid(hprogs[i]);
+  mw::CallMark mark("mg_search_begin");
+  mark.step("lock", nprog);
+  CallG call;
+  if (const char* why = mw::enter(g_reg, hid(h), ids.data(), nprog, call))
+    return fail(MG_E_ARG, std::string("mg_search_begin: ") + why);
+  Ctx* c = call.c.get();
+  if (c->pending.active) return fail(MG_E_ARG, "mg_search_begin: a search begun earlier is pending");
+  Pending P;
+  int rc = search_enqueue(c, call.ps, seed, begin, count, flags, mark, P);
+  if (rc) {
+    hipStreamSynchronize(c->stream);
+    return rc;
+  }
+  P.active = true;
+  c->pending = std::move(P);
+  return 0;
+}
+
+// The witness evaluations of mg_search_end: each witness program is uploaded,
+// its index patched in on the device from the search's d_min word, and
+// evaluated for that one candidate on the asm interpreter, queued after the
+// search; traced[i] = 1 for the programs whose trace will be read back.
+struct WitPlan {
+  std::vector<std::shared_ptr<Prog>> wps;
+  std::vector<size_t> prog_of, trace_off;   // per witness record: its search program, its trace rows' offset
+  size_t rb_bytes = 0, verd_off = 0;
+};
+
+static int witness_enqueue(Ctx* c, const std::shared_ptr<Ctx>& cref, Pending& P, const mg_prog_desc* const* wd,
+                           int32_t* traced, WitPlan& W, std::unique_ptr<Scratch>& blk, mw::CallMark& mark) {
+  const size_t nprog = P.ps.size();
+  mark.step("witness loads", nprog);
+  for (size_t i = 0; i < nprog; ++i) {
+    traced[i] = 0;
+    if (!wd[i]) continue;
+    int rc = mg_validate_desc(wd[i]);
+    if (rc) return rc;
+    if (!wd[i]->n_trace_rows) continue;
+    std::shared_ptr<Prog> wp;
+    rc = load_locked(cref, wd[i], wp);
+    if (rc) return rc;
+    u32 nlds = 0;
+    if (!wp->asm_ok || !asm_enabled() || !asm_lds_fit(wp.get(), &nlds)) {   // the caller evaluates it later
+      release_prog(*wp);
+      continue;
+    }
+    W.wps.push_back(std::move(wp));
+    W.prog_of.push_back(i);
+  }
+  const size_t nw = W.wps.size();
+  if (!nw) return 0;
+  // device block: slots | ProgDev records | AsmArgs records | counter sink |
+  // verdicts | trace rows
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_prog = up(nw * 4), o_args = up(o_prog + nw * sizeof(ProgDev)),
+               o_ctr = up(o_args + nw * sizeof(AsmArgs)), o_verd = up(o_ctr + 8 * sizeof(u64));
+  size_t rows = 0;
+  for (auto& wp : W.wps) {
+    W.trace_off.push_back(rows);
+    rows += wp->desc.n_trace_rows;
+  }
+  const size_t o_tr = o_verd + nw * 4, total = o_tr + rows * 4, head = o_ctr;
+  W.verd_off = o_verd;
+  W.rb_bytes = total - o_verd;
+  if (W.rb_bytes > kReadbackMax || !ensure_readback(c, W.rb_bytes)) {   // too big to read back in one copy
+    for (auto& wp : W.wps) release_prog(*wp);
+    W.wps.clear();
+    return 0;
+  }
+  size_t spill = 4;
+  for (auto& wp : W.wps) {
+    u32 nlds = 0;
+    (void)asm_lds_fit(wp.get(), &nlds);
+    spill = std::max(spill, (size_t)(wp->dev.n_spill - nlds) * kBlock * sizeof(u32));
+  }
+  int rc = ensure_spill(c, spill);   // (a regrow frees the old buffer: hipFree waits for the search)
+  if (rc) return rc;
+  blk.reset(new Scratch(c, total));
+  if (!blk->p) return fail(MG_E_NOMEM, "witness evaluation buffer");
+  uint8_t* d = (uint8_t*)blk->p;
+  if (head > c->wit_bytes) {
+    if (c->h_wit) hipHostFree(c->h_wit);
+    c->h_wit = nullptr;
+    c->wit_bytes = 0;
+    if (hipHostMalloc(&c->h_wit, std::max<size_t>(head, 4096), hipHostMallocDefault) != hipSuccess)
+      return fail(MG_E_NOMEM, "witness staging allocation failed");
+    c->wit_bytes = std::max<size_t>(head, 4096);
+  }
+  uint8_t* hw = c->h_wit;
+  std::memset(hw, 0, head);
+  u32* hslot = (u32*)hw;
+  ProgDev* hprog = (ProgDev*)(hw + o_prog);
+  AsmArgs* hargs = (AsmArgs*)(hw + o_args);
+  for (size_t k = 0; k < nw; ++k) {
+    const Prog* wp = W.wps[k].get();
+    hslot[k] = (u32)P.slot[W.prog_of[k]];
+    hprog[k] = wp->adev;
+    AsmArgs& a = hargs[k];
+    a.seed = 0;   // set below: the search's seed
+    a.begin = 0;
+    a.end = 1;    // patched on the device (mw_witness_index_kernel)
+    a.flags = 0;
+    (void)asm_lds_fit(wp, &a.nlds);
+    a.gstride = kBlock * 4;
+    a.nchunks = 1;
+    a.gdx = 1;
+    a.nprog = 0;
+    a.spillbuf = c->d_spill;
+    a.verdict = (u32*)(d + o_verd) + k;
+    a.trace = (u32*)(d + o_tr) + W.trace_off[k];
+    a.ncand = 1;
+  }
+  for (size_t k = 0; k < nw; ++k) hargs[k].seed = P.seed;
+  mark.step("witness enqueue", nw);
+  HIPCHK(hipMemcpyAsync(d, hw, head, hipMemcpyHostToDevice, c->stream));
+  for (size_t k = 0; k < nw; ++k)
+    if (!W.wps[k]->trace_full)
+      HIPCHK(hipMemsetAsync(d + o_tr + W.trace_off[k] * 4, 0, W.wps[k]->desc.n_trace_rows * 4, c->stream));
+  hipLaunchKernelGGL(mw_witness_index_kernel, dim3((u32)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, c->stream,
+                     (const u64*)c->d_min, (const u32*)d, (AsmArgs*)(d + o_args), (u32)nw);
+  HIPCHK(hipGetLastError());
+  for (size_t k = 0; k < nw; ++k) {
+    const Prog* wp = W.wps[k].get();
+    const u32 nlds = hargs[k].nlds;
+    const size_t lds = (size_t)nlds * kBlock * 4 + (size_t)wp->dev.npool * 4;
+    hipLaunchKernelGGL(kAsmKernel[wp->asm_layout], dim3(1u, 1u), dim3(kBlock), lds, c->stream,
+                       (const ProgDev*)(d + o_prog) + k, (const AsmArgs*)(d + o_args) + k,
+                       (u64*)(d + o_ctr) + 1, (u64*)(d + o_ctr), nlds);
+    HIPCHK(hipGetLastError());
+  }
+  HIPCHK(hipMemcpyAsync(c->h_rb, d + o_verd, W.rb_bytes, hipMemcpyDeviceToHost, c->stream));
+  for (size_t k = 0; k < nw; ++k) traced[W.prog_of[k]] = 1;
+  return 0;
+}
+
+int mg_search_end(mg_ctx* h, uint64_t* out_min_idx, mg_stats* st, const mg_prog_desc* const* witness,
+                  uint32_t* const* out_trace, int32_t* traced) {
+  if (!h || !out_min_idx) return fail(MG_E_ARG, "null argument");
+  if (witness && (!out_trace || !traced)) return fail(MG_E_ARG, "witness programs need out_trace and traced");
+  mw::CallMark mark("mg_search_end");
+  mark.step("lock");
+  CallG call;
+  if (const char* why = mw::enter(g_reg, hid(h), nullptr, 0, call)) return fail(MG_E_ARG, std::string("mg_search_end: ") + why);
+  Ctx* c = call.c.get();
+  if (!c->pending.active) return fail(MG_E_ARG, "mg_search_end: no search begun on this context");
+  Pending P = std::move(c->pending);
+  c->pending = Pending();
+  HIPCHK(hipSetDevice(c->dev));
+  WitPlan W;
+  std::unique_ptr<Scratch> blk;
+  int rc = 0;
+  if (witness) rc = witness_enqueue(c, call.c, P, witness, traced, W, blk, mark);
+  if (rc) {
+    hipStreamSynchronize(c->stream);
+    for (auto& wp : W.wps) release_prog(*wp);
+    return rc;
+  }
+  rc = search_complete(c, P, out_min_idx, st, mark);   // one synchronisation for the search and the witnesses
+  if (blk) blk->synced = rc == 0;
+  if (rc == 0) {
+    for (size_t k = 0; k < W.wps.size(); ++k) {
+      const size_t i = W.prog_of[k];
+      if (out_min_idx[i] == MG_NONE) {
+        traced[i] = 0;
+        continue;
+      }
+      // h_rb: the verdicts (one word per witness), then the trace rows
+      std::memcpy(out_trace[i], c->h_rb + W.wps.size() * 4 + W.trace_off[k] * 4, W.wps[k]->desc.n_trace_rows * 4);
+    }
+  }
+  for (auto& wp : W.wps) release_prog(*wp);
+  return rc;
 }
 
 static int eval_common(Ctx* c, const Prog* p, const uint32_t* leaves_soa, size_t ncand, uint64_t seed,
@@ -1610,6 +1869,7 @@ int mg_eval(mg_ctx* h, const mg_prog* hp, const uint32_t* leaves_soa, size_t nca
   mark.step("lock", ncand);
   CallG call;
   if (const char* why = mw::enter(g_reg, hid(h), &id, 1, call)) return fail(MG_E_ARG, std::string("mg_eval: ") + why);
+  if (call.c->pending.active) return fail(MG_E_ARG, "a search begun with mg_search_begin is pending on this context");
   mark.step("eval", ncand);
   const Prog* p = call.ps[0].get();
   if (p->desc.nleaves && p->desc.n_input_rows && !leaves_soa) return fail(MG_E_ARG, "leaves_soa required");
@@ -1698,6 +1958,7 @@ int mg_eval_generated(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t begi
   CallG call;
   if (const char* why = mw::enter(g_reg, hid(h), &id, 1, call))
     return fail(MG_E_ARG, std::string("mg_eval_generated: ") + why);
+  if (call.c->pending.active) return fail(MG_E_ARG, "a search begun with mg_search_begin is pending on this context");
   mark.step("eval", count);
   Ctx* c = call.c.get();
   const Prog* p = call.ps[0].get();
@@ -1744,6 +2005,7 @@ int mg_eval_program(mg_ctx* h, const mg_prog_desc* d, uint64_t seed, uint64_t be
   mark.step("lock");
   std::lock_guard<std::mutex> lk(c->mu);
   if (c->dead) return fail(MG_E_ARG, "mg_eval_program: the context was freed during the call");
+  if (c->pending.active) return fail(MG_E_ARG, "a search begun with mg_search_begin is pending on this context");
   HIPCHK(hipSetDevice(c->dev));
   std::shared_ptr<Prog> p;
   rc = load_locked(cref, d, p);
@@ -1766,6 +2028,7 @@ int mg_witness_leaves(mg_ctx* h, const mg_prog* hp, uint64_t seed, uint64_t inde
   CallG call;
   if (const char* why = mw::enter(g_reg, hid(h), &id, 1, call))
     return fail(MG_E_ARG, std::string("mg_witness_leaves: ") + why);
+  if (call.c->pending.active) return fail(MG_E_ARG, "a search begun with mg_search_begin is pending on this context");
   mark.step("launch + sync");
   Ctx* c = call.c.get();
   const Prog* p = call.ps[0].get();
@@ -1790,6 +2053,7 @@ int mg_valu_peak(mg_ctx* h, uint32_t mul, double* ops_per_s, double* kernel_ms) 
   if (!h || !ops_per_s) return fail(MG_E_ARG, "null argument");
   CallG call;
   if (const char* why = mw::enter(g_reg, hid(h), nullptr, 0, call)) return fail(MG_E_ARG, std::string("mg_valu_peak: ") + why);
+  if (call.c->pending.active) return fail(MG_E_ARG, "a search begun with mg_search_begin is pending on this context");
   Ctx* c = call.c.get();
   HIPCHK(hipSetDevice(c->dev));
   const u32 blocks = (u32)c->ncu * 8, iters = 4096;
@@ -1815,6 +2079,7 @@ int mg_keccak256_device(mg_ctx* h, const uint8_t* d_data, const uint64_t* d_off,
   mark.step("lock", n);
   CallG call;
   if (const char* why = mw::enter(g_reg, hid(h), nullptr, 0, call)) return fail(MG_E_ARG, std::string("mg_keccak256: ") + why);
+  if (call.c->pending.active) return fail(MG_E_ARG, "a search begun with mg_search_begin is pending on this context");
   Ctx* c = call.c.get();
   HIPCHK(hipSetDevice(c->dev));
   const double t0 = now_ms();

@@ -190,6 +190,7 @@ def _build_witness_program(q: "Query") -> None:
 # --ab), and a witness program compiles only when a search found a witness.
 import os as _os
 WITNESS_THREAD = _os.environ.get("MYTHRIL_AMD_WITNESS_THREAD", "0") == "1"
+_os_env = _os.environ.get
 
 # Larger witness programs compile in materialize: their Python part (record
 # stream, leaf table) would hold the GIL the returning search call waits for.
@@ -272,6 +273,67 @@ def search_phased(dev, dps, seed: int, begin: int, count: int, flags: int, long_
             found[i] = f
         st = {k: (v + st2[k] if isinstance(v, (int, float)) and k in st2 else v) for k, v in st.items()}
     return found, st
+
+
+# MYTHRIL_AMD_WITNESS_IN_LAUNCH=0: read witnesses with a launch of their own
+# after the search (mg_eval_program) instead of in the search's synchronisation
+WITNESS_IN_LAUNCH = _os_env("MYTHRIL_AMD_WITNESS_IN_LAUNCH", "1") != "0"
+
+
+def search_with_witnesses(dev, dps, queries, seed: int, begin: int, count: int, flags: int, long_programs=None):
+    """search_phased, with each query's witness read in the search's own
+    synchronisation: the search is enqueued
+    (mg_search_begin), the witness programs compile on the host while the
+    device searches, and mg_search_end evaluates each at the index its search
+    found, queued after the search, one synchronisation for all of it.
+    Returns (found, stats, traces): traces[i] is query i's witness trace
+    column, or None (no witness; or the caller evaluates it)."""
+    n = len(dps)
+    probe = bool(flags & isa.FLAG_STOP_AFTER_HIT) and count > 2 * PROBE_CANDIDATES
+    first = PROBE_CANDIDATES if probe else count
+    dev.search_begin(dps, seed, begin, first, flags)
+    wps = None
+    try:
+        wps = [q.trace_program for q in queries]
+        # only a witness program with the search program's leaf layout reads
+        # the same candidate (else materialize refuses it: z3 answers)
+        wps = [p if _same_leaves(q, p) else None for q, p in zip(queries, wps)]
+    finally:
+        if wps is None:          # the compile raised: complete the search, then re-raise
+            dev.search_end(None)
+    found, st, traces = dev.search_end(wps)
+    rest = [i for i, f in enumerate(found) if f is None]
+    if not probe or not rest:
+        return found, st, traces
+    rdps, extra = [], []
+    try:
+        for i in rest:
+            lp = long_programs[i](count - PROBE_CANDIDATES) \
+                if long_programs is not None and not getattr(dps[i], "assembled", None) else None
+            if lp is not None and lp is not dps[i].prog:
+                d = dev.load(lp)
+                extra.append(d)
+                rdps.append(d if not hasattr(dev, "engine_of") or dev.engine_of(d) == "asm" else dps[i])
+            else:
+                rdps.append(dps[i])
+        dev.search_begin(rdps, seed, begin + PROBE_CANDIDATES, count - PROBE_CANDIDATES, flags)
+        f2, st2, t2 = dev.search_end([wps[i] for i in rest])
+    finally:
+        for d in extra:
+            d.free()
+    found, traces = list(found), list(traces)
+    for k, i in enumerate(rest):
+        found[i], traces[i] = f2[k], t2[k]
+    st = {k: (v + st2[k] if isinstance(v, (int, float)) and k in st2 else v) for k, v in st.items()}
+    return found, st, traces
+
+
+def _same_leaves(q: "Query", p: Program) -> bool:
+    """The witness program p draws the search program's leaves in its order
+    (compile_trace_native shares the leaf table itself; a fresh compile must
+    lead with the same names)."""
+    return p.leaves is q.program.leaves or \
+        [n.name for n in p.leaf_nodes[:len(q.program.leaf_nodes)]] == [n.name for n in q.program.leaf_nodes]
 
 
 def _prebuild_witness_programs(queries) -> bool:
@@ -498,8 +560,13 @@ class WitnessEngine:
                 if (self.asmjit_min_ops and hasattr(self.dev, "attach_asm")
                         and count * sum(q.ops_per_eval for q in queries) >= self.asmjit_min_ops):
                     self._assemble(dps)
-                found, st = search_phased(self.dev, dps, self.seed, begin, count, flags,
-                                          [lambda n, q=q: search_program(q, n) for q in queries])
+                longs = [lambda n, q=q: search_program(q, n) for q in queries]
+                traces = [None] * len(queries)
+                if WITNESS_IN_LAUNCH and not queued and hasattr(self.dev, "search_begin"):
+                    found, st, traces = search_with_witnesses(self.dev, dps, queries, self.seed, begin, count, flags,
+                                                              longs)
+                else:
+                    found, st = search_phased(self.dev, dps, self.seed, begin, count, flags, longs)
                 if prof is not None:
                     t0 = _tick(prof, "search", t0)
             self.stats["searches"] += 1
@@ -507,8 +574,13 @@ class WitnessEngine:
             self.stats["evals"] += st["evals"]
             self.stats["kernel_ms"] += st["kernel_ms"]
             out: List[Optional[Witness]] = []
-            for q, dp, idx in zip(queries, dps, found):
-                w = self.materialize(q, idx, dp) if idx is not None else None
+            for q, dp, idx, tr in zip(queries, dps, found, traces):
+                if idx is None:
+                    w = None
+                elif tr is not None:     # read in the search's synchronisation
+                    w = self._decode_trace(q, q.trace_program, idx, tr)
+                else:
+                    w = self.materialize(q, idx, dp)
                 if w is not None and self.verify:
                     v, _ = self.dev.eval_generated(dp, self.seed, idx, 1, trace=False)
                     if not int(v[0]):
@@ -634,8 +706,7 @@ class WitnessEngine:
         # same order; it may have more: variables only a cell index reads and
         # no conjunct (a DependencyPruner tuple `f(x) == 1` reads no x), whose
         # values no verdict depends on
-        if p.leaves is not q.program.leaves and \
-                [n.name for n in p.leaf_nodes[:len(q.program.leaf_nodes)]] != [n.name for n in q.program.leaf_nodes]:
+        if not _same_leaves(q, p):
             # an EngineError, so get_model's handler sends the query to z3
             raise EngineError("witness program's leaf layout differs from the search program's")
         t1 = time.perf_counter()
@@ -656,6 +727,11 @@ class WitnessEngine:
         if PROFILE is not None:
             PROFILE.setdefault("materialize/load (mg_prog_load)", [0.0, 0])[0] += t2 - t1
             PROFILE.setdefault("materialize/eval (mg_eval_generated)", [0.0, 0])[0] += t3 - t2
+        return self._decode_trace(q, p, index, trace)
+
+    def _decode_trace(self, q: Query, p: Program, index: int, trace) -> Witness:
+        """The witness from the witness program p's trace column at index."""
+        from .runtime import trace_column
         col = trace_column(trace)   # the one candidate's rows, read per node below
         tmap, frm = p.trace_map, int.from_bytes
         values = {}

@@ -71,6 +71,11 @@ SIGNATURES = {
     "mg_search": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                  ctypes.c_uint64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
                                  ctypes.POINTER(MgStats)]),
+    "mg_search_begin": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
+                                       ctypes.c_uint64, ctypes.c_uint32]),
+    "mg_search_end": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(MgStats),
+                                     ctypes.POINTER(ctypes.POINTER(MgProgDesc)), ctypes.POINTER(_P),
+                                     ctypes.POINTER(ctypes.c_int32)]),
     "mg_eval": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t, _P, _P]),
     "mg_eval_generated": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, _P, _P]),
     "mg_witness_leaves": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, _P]),
@@ -245,6 +250,49 @@ class Device:
                                             flags, out, ctypes.byref(st)), "mg_search")
         res = [None if v == MG_NONE else int(v) for v in out]
         return res, st.as_dict()
+
+    def search_begin(self, progs: Sequence[DeviceProgram], seed: int, begin: int, count: int,
+                     flags: int = 0) -> None:
+        """mg_search_begin: enqueue a search and return at once; search_end
+        completes it (the caller may compile witness programs meanwhile)."""
+        if self._reap_queue:
+            self._reap()
+        arr = (_P * len(progs))(*[dp.handle for dp in progs])
+        _check(self.lib, self.lib.mg_search_begin(self.handle, arr, len(progs), seed & ((1 << 64) - 1), begin, count,
+                                                  flags), "mg_search_begin")
+        self._begun = len(progs)
+
+    def search_end(self, witness: Optional[Sequence[Optional[Program]]] = None):
+        """mg_search_end: (lowest satisfying index per program or None, stats,
+        traces): traces[i] is the trace rows of witness[i] evaluated at
+        program i's index (one column, as eval_generated(..., count=1)
+        returns it), or None (no witness program, no hit, or not on the asm
+        interpreter: the caller evaluates it)."""
+        n = getattr(self, "_begun", 0)
+        self._begun = 0
+        out = (ctypes.c_uint64 * max(1, n))()
+        st = MgStats()
+        traces = [None] * n
+        if witness is not None:
+            descs = (ctypes.POINTER(MgProgDesc) * n)()
+            bufs = (_P * n)()
+            traced = (ctypes.c_int32 * n)()
+            keep, arrays = [], [None] * n
+            for i, p in enumerate(witness):
+                if p is None or not p.n_trace_rows:
+                    continue
+                d, k = make_desc(p)
+                keep.append((d, k))
+                descs[i] = ctypes.pointer(d)
+                arrays[i] = np.zeros(p.n_trace_rows, dtype=np.uint32)
+                bufs[i] = arrays[i].ctypes.data
+            _check(self.lib, self.lib.mg_search_end(self.handle, out, ctypes.byref(st), descs, bufs, traced),
+                   "mg_search_end")
+            traces = [arrays[i].reshape(-1, 1) if traced[i] else None for i in range(n)]
+        else:
+            _check(self.lib, self.lib.mg_search_end(self.handle, out, ctypes.byref(st), None, None, None),
+                   "mg_search_end")
+        return [None if out[i] == MG_NONE else int(out[i]) for i in range(n)], st.as_dict(), traces
 
     def eval(self, dp: DeviceProgram, leaves_soa: Optional[np.ndarray], ncand: int,
              trace: bool = True) -> Tuple[np.ndarray, Optional[np.ndarray]]:

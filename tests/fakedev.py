@@ -40,6 +40,26 @@ class FakeDevice:
             out.append(found)
         return out, {"evals": evals, "kernel_ms": 0.0}
 
+    def search_begin(self, dps, seed, begin, count, flags=0):
+        """Device.search_begin on the host build: the search runs at the end."""
+        assert getattr(self, "_begun", None) is None, "a search is pending"
+        self._begun = (list(dps), seed, begin, count, flags)
+        self.begin_calls = getattr(self, "begin_calls", 0) + 1
+
+    def search_end(self, witness=None):
+        """Device.search_end: the search, then each witness program evaluated
+        at its program's index (the trace column), as mg_search_end does."""
+        dps, seed, begin, count, flags = self._begun
+        self._begun = None
+        found, st = self.search(dps, seed, begin, count, flags)
+        traces = [None] * len(dps)
+        if witness is not None:
+            for i, (p, f) in enumerate(zip(witness, found)):
+                if p is not None and f is not None and p.n_trace_rows:
+                    _, tr = emu_eval(p, None, 1, seed=seed, begin=f)
+                    traces[i] = tr
+        return found, st, traces
+
     def eval_generated(self, dp, seed, begin, count, trace=True):
         return emu_eval(dp.prog, None, count, seed=seed, begin=begin)
 

@@ -447,11 +447,21 @@ def test_witness_layout_mismatch_falls_back_to_reference(mythril, monkeypatch):
     assert dropin.STATS["device_errors"] >= 1
 
 
-def test_constant_cells_materialise_from_leaves(mythril):
-    """A witness whose array cells all have constant indices is read from the
-    search program's leaves (mg_witness_leaves), without a witness program."""
+def test_constant_cells_materialise_from_leaves(mythril, monkeypatch):
+    """A witness is read in the search's own synchronisation (mg_search_end
+    evaluates the witness program at the found index; round 6): no witness
+    call of its own.  With MYTHRIL_AMD_WITNESS_IN_LAUNCH=0, a witness whose
+    array cells all have constant indices is read from the search program's
+    leaves (mg_witness_leaves), without a witness program."""
+    from mythril_amd import engine as engine_mod
     dev = dropin._engine.dev
-    n0 = getattr(dev, "witness_leaf_calls", 0)
+    n0, b0 = getattr(dev, "witness_leaf_calls", 0), getattr(dev, "begin_calls", 0)
+    res = dropin.get_model(SAT)
+    assert res.raw[0][0] == "z3"
+    assert getattr(dev, "witness_leaf_calls", 0) == n0 and getattr(dev, "begin_calls", 0) == b0 + 1
+    monkeypatch.setattr(engine_mod, "WITNESS_IN_LAUNCH", False)
+    dropin.get_model.cache_clear()
+    dropin._memo.clear()
     res = dropin.get_model(SAT)
     assert res.raw[0][0] == "z3"
     assert getattr(dev, "witness_leaf_calls", 0) == n0 + 1
