@@ -40,6 +40,7 @@ def main():
     a = ap.parse_args()
     from mythril_amd.engine import (WitnessEngine, _gil_handoff, _prebuild_witness_programs, prepare,
                                      search_phased, search_program)
+    from mythril_amd import engine as engine_mod
     from mythril_amd.smt2 import parse_file
     eng = None if a.no_device else WitnessEngine(device=0)
     calls = []    # every mg_search of the current query: (call wall, library wall, kernel) ms
@@ -76,11 +77,19 @@ def main():
                 t_l = time.perf_counter()
                 calls.clear()
                 try:
+                    tr = None
                     with _gil_handoff(queued):
                         # as WitnessEngine.search: the launch after the probe runs
-                        # the query's long program (the quarter layout's compile)
-                        (idx,), st = search_phased(eng.dev, [dp], eng.seed, 0, eng.launch_count([q]), 3,
-                                                   [lambda n: search_program(q, n)])
+                        # the query's long program (the quarter layout's compile);
+                        # since round 6 the witness program compiles while the
+                        # device searches and is evaluated in the search's own
+                        # synchronisation (engine.search_with_witnesses)
+                        longs = [lambda n: search_program(q, n)]
+                        if engine_mod.WITNESS_IN_LAUNCH and not queued:
+                            (idx,), st, (tr,) = engine_mod.search_with_witnesses(
+                                eng.dev, [dp], [q], eng.seed, 0, eng.launch_count([q]), 3, longs)
+                        else:
+                            (idx,), st = search_phased(eng.dev, [dp], eng.seed, 0, eng.launch_count([q]), 3, longs)
                     row["search"] = (time.perf_counter() - t1) * 1e3
                     row["kernel"] = st["kernel_ms"]
                     # where the search's time goes: queueing the witness compile,
@@ -93,7 +102,10 @@ def main():
                         # loaded (mg_witness_leaves when every cell index is constant)
                         t2 = time.perf_counter()
                         eng.last_materialize = None
-                        eng.materialize(q, idx, dp)
+                        if tr is not None:     # the trace came back with the search: decode only
+                            eng._decode_trace(q, q.trace_program, idx, tr)
+                        else:
+                            eng.materialize(q, idx, dp)
                         row["materialise"] = (time.perf_counter() - t2) * 1e3
                         if getattr(eng, "last_materialize", None):
                             row["materialise_parts"] = {k: v * 1e3 for k, v in eng.last_materialize.items()}
