@@ -457,10 +457,14 @@ struct Ctx {
   size_t alive_cap = 0;
   // pinned staging of program uploads (mg_prog_load): the copy is queued on
   // the stream, ahead of every launch that reads the program; the next upload
-  // waits for it before reusing the buffer (up_pending)
-  uint8_t* h_up = nullptr;
-  size_t up_bytes = 0;
-  bool up_pending = false;
+  // waits for it before reusing the buffer (up_pending).  Two buffers, used
+  // in turn: a second upload right after the first (the witness programs of
+  // mg_search_end after the search's) needs no synchronisation
+  uint8_t* h_up[2] = {nullptr, nullptr};
+  size_t up_bytes[2] = {0, 0};
+  bool up_pending[2] = {false, false};
+  int up_next = 0;
+  void uploads_landed() { up_pending[0] = up_pending[1] = false; }
   // pinned landing area of small readbacks (eval verdicts and traces)
   uint8_t* h_rb = nullptr;
   size_t rb_bytes = 0;
@@ -484,6 +488,7 @@ struct Prog {
   mg_prog_desc desc{};
   u64 ops_per_eval = 0;
   u64 sig = 0;                  // FNV-1a 64 of the program words (mythril_amd/jit.py signature)
+  bool sig_ready = false;       // computed on the first attach (program_signature), not at load
   bool asm_ok = false;          // every opcode and leaf kind has a handler in mw_search_asm_kernel
   u8 asm_layout = kWide;        // the asm kernel adev is predecoded for (kAsmKernel)
   bool trace_full = false;      // STOREs cover every trace row: an evaluation needs no zeroed trace block
@@ -527,12 +532,33 @@ u64 fnv1a(u64 h, const u32* w, size_t n) {
   return h;
 }
 
-u64 prog_signature(const mg_prog_desc* d) {
+
+// A loaded program's signature (the context's mu held), from its words read
+// back from the device on the first attach: only the specialised and
+// assembled kernels check it, so an upload does not hash every program
+// (mg_prog_load's FNV pass was a fifth of a LASER load, tools/dropin_profile.py).
+u64 program_signature(Ctx* c, Prog* p) {
+  if (p->sig_ready) return p->sig;
+  const mg_prog_desc& d = p->desc;
+  const size_t nl = d.nleaves * MW_LEAF_WORDS;
+  std::vector<u32> w(d.ncode_words + d.nconst_words + nl + d.npool_words);
+  u32* o = w.data();
+  hipStreamSynchronize(c->stream);   // the upload may still be queued
+  bool ok = hipMemcpy(o, p->dev.code, d.ncode_words * 4, hipMemcpyDeviceToHost) == hipSuccess;
+  o += d.ncode_words;
+  if (ok && d.nconst_words) ok = hipMemcpy(o, p->dev.consts, d.nconst_words * 4, hipMemcpyDeviceToHost) == hipSuccess;
+  o += d.nconst_words;
+  if (ok && nl) ok = hipMemcpy(o, p->dev.leaves, nl * 4, hipMemcpyDeviceToHost) == hipSuccess;
+  o += nl;
+  if (ok && d.npool_words) ok = hipMemcpy(o, p->dev.pool, d.npool_words * 4, hipMemcpyDeviceToHost) == hipSuccess;
+  if (!ok) {
+    (void)hipGetLastError();
+    return ~0ull;   // matches no code object: the attach is refused
+  }
   u64 h = 0xcbf29ce484222325ull;
-  h = fnv1a(h, d->code, d->ncode_words);
-  if (d->consts) h = fnv1a(h, d->consts, d->nconst_words);
-  if (d->leaves) h = fnv1a(h, d->leaves, d->nleaves * MW_LEAF_WORDS);
-  if (d->pool) h = fnv1a(h, d->pool, d->npool_words);
+  h = fnv1a(h, w.data(), w.size());
+  p->sig = h;
+  p->sig_ready = true;
   return h;
 }
 
@@ -707,7 +733,8 @@ void release_ctx(Ctx& c) {
   if (c.d_spill) hipFree(c.d_spill);
   if (c.d_blk) hipFree(c.d_blk);
   if (c.h_blk) hipHostFree(c.h_blk);
-  if (c.h_up) hipHostFree(c.h_up);
+  for (int k = 0; k < 2; ++k)
+    if (c.h_up[k]) hipHostFree(c.h_up[k]);
   if (c.h_rb) hipHostFree(c.h_rb);
   if (c.h_wit) hipHostFree(c.h_wit);
   c.h_wit = nullptr;
@@ -715,9 +742,9 @@ void release_ctx(Ctx& c) {
   c.pending = Pending();
   c.h_rb = nullptr;
   c.rb_bytes = 0;
-  c.h_up = nullptr;
-  c.up_bytes = 0;
-  c.up_pending = false;
+  c.h_up[0] = c.h_up[1] = nullptr;
+  c.up_bytes[0] = c.up_bytes[1] = 0;
+  c.uploads_landed();
   if (c.d_alive) hipFree(c.d_alive);
   if (c.e0) hipEventDestroy(c.e0);
   if (c.e1) hipEventDestroy(c.e1);
@@ -1098,33 +1125,33 @@ static int load_locked(const std::shared_ptr<Ctx>& cref, const mg_prog_desc* d, 
   p->ctx = cref;
   p->desc = *d;
   p->ops_per_eval = d->ops_per_eval;
-  mark.step("signature", total);
-  p->sig = prog_signature(d);
   p->trace_full = trace_rows_covered(d);
   mark.step("pool_get", total * 4);
   p->d_buf = (u32*)pool_get(c, total * sizeof(u32), &p->buf_cls);
   if (!p->d_buf) return fail(MG_E_NOMEM, "program upload allocation failed");
   // stage in the context's pinned buffer (after the previous upload from it has landed)
   mark.step("sync previous upload");
-  if (c->up_pending && hipStreamSynchronize(c->stream) != hipSuccess) {
+  const int ub = c->up_next;
+  c->up_next ^= 1;
+  if (c->up_pending[ub] && hipStreamSynchronize(c->stream) != hipSuccess) {
     release_prog(*p);
     return fail(MG_E_HIP, "program upload: stream synchronize failed");
   }
-  c->up_pending = false;
-  if (total * 4 > c->up_bytes) {
+  if (c->up_pending[ub]) c->uploads_landed();   // the stream drained
+  if (total * 4 > c->up_bytes[ub]) {
     mark.step("staging regrow", total * 4);
-    if (c->h_up) hipHostFree(c->h_up);
-    c->h_up = nullptr;
-    c->up_bytes = 0;
+    if (c->h_up[ub]) hipHostFree(c->h_up[ub]);
+    c->h_up[ub] = nullptr;
+    c->up_bytes[ub] = 0;
     const size_t want = std::max<size_t>(total * 4, (size_t)1 << 18);
-    if (hipHostMalloc(&c->h_up, want, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(&c->h_up[ub], want, hipHostMallocDefault) != hipSuccess) {
       release_prog(*p);
       return fail(MG_E_NOMEM, "program upload staging allocation failed");
     }
-    c->up_bytes = want;
+    c->up_bytes[ub] = want;
   }
   mark.step("stage + predecode", total * 4);
-  u32* hbuf = (u32*)c->h_up;
+  u32* hbuf = (u32*)c->h_up[ub];
   std::memset(hbuf, 0, total * 4);
   std::memcpy(hbuf, d->code, nc * 4);
   if (d->nconst_words) std::memcpy(hbuf + nc, d->consts, d->nconst_words * 4);
@@ -1163,7 +1190,7 @@ static int load_locked(const std::shared_ptr<Ctx>& cref, const mg_prog_desc* d, 
     release_prog(*p);
     return fail(MG_E_HIP, "program upload copy failed");
   }
-  c->up_pending = true;
+  c->up_pending[ub] = true;
   p->dev.code = p->d_buf;
   p->dev.consts = p->d_buf + nc;
   p->dev.leaves = p->d_buf + nc + nk;
@@ -1249,7 +1276,7 @@ int mg_prog_attach_kernel(mg_prog* h, const void* image, size_t size, const char
     hipModuleUnload(mod);
     return fail(MG_E_PROG, "code object has no program signature " + base + "_sig");
   }
-  if (sig != p->sig) {
+  if (sig != program_signature(c, p)) {
     hipModuleUnload(mod);
     return fail(MG_E_PROG, "code object was generated for another program (signature mismatch)");
   }
@@ -1322,7 +1349,7 @@ int mg_prog_attach_asm(mg_prog* h, const void* image, size_t size, const char* n
     hipModuleUnload(mod);
     return fail(MG_E_PROG, "code object has no program signature " + base + "_sig");
   }
-  if (sig != p->sig) {
+  if (sig != program_signature(c, p)) {
     hipModuleUnload(mod);
     return fail(MG_E_PROG, "code object was assembled for another program (signature mismatch)");
   }
@@ -1576,7 +1603,7 @@ static int search_complete(Ctx* c, Pending& P, uint64_t* out_min_idx, mg_stats* 
   const u64 count = P.count;
   mark.step("sync", count);
   HIPCHK(hipStreamSynchronize(c->stream));
-  c->up_pending = false;   // the stream drained: a queued program upload has landed
+  c->uploads_landed();   // the stream drained: a queued program upload has landed
   if (P.gpu_steps) {
     float a = 0.f, k = 0.f, b = 0.f;
     if (hipEventElapsedTime(&a, c->ea, c->e0) == hipSuccess && hipEventElapsedTime(&k, c->e0, c->e1) == hipSuccess &&
@@ -1853,7 +1880,7 @@ static int eval_common(Ctx* c, const Prog* p, const uint32_t* leaves_soa, size_t
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   s_in.synced = s_vt.synced = e == hipSuccess;
   if (e != hipSuccess) return fail(MG_E_HIP, std::string("eval: ") + hipGetErrorString(e));
-  c->up_pending = false;   // the stream drained: a queued program upload has landed
+  c->uploads_landed();   // the stream drained: a queued program upload has landed
   if (pinned) {
     std::memcpy(verdict, c->h_rb, vb);
     if (ntr) std::memcpy(trace, c->h_rb + vb, tb);
@@ -1941,7 +1968,7 @@ static int eval_asm(Ctx* c, const Prog* p, uint64_t seed, uint64_t begin, size_t
   if (e != hipSuccess)
     return fail(MG_E_HIP, std::string(assembled ? "eval (assembled kernel): " : "eval (asm interpreter): ") +
                               hipGetErrorString(e));
-  c->up_pending = false;   // the stream drained: a queued program upload has landed
+  c->uploads_landed();   // the stream drained: a queued program upload has landed
   if (pinned) {
     std::memcpy(verdict, c->h_rb, vb);
     if (ntr) std::memcpy(trace, c->h_rb + vb, tb);
