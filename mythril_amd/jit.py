@@ -52,6 +52,10 @@ SPLIT_KIND = os.environ.get("MW_JIT_SPLIT", "branch")
 # experiments (tools/ab_c5.py): a workgroup barrier after every conjunct of the
 # exhaustive variant, keeping a block's waves at the same place in the code
 CHECK_SYNC = os.environ.get("MW_JIT_CHECK_SYNC", "0") == "1"
+# 256-bit products of two register operands by columns (mw_jit.h mul8_cols:
+# v_mad_u64_u32 carry-outs counted per column) instead of mul8's rows; C5
+# 17.51 -> 17.40 ms per 2^22 launch (profiles/r6k/ab_c5_mulcols.json)
+MUL_COLS = os.environ.get("MW_JIT_MUL_COLS", "1") == "1"
 M32 = 0xFFFFFFFF
 
 _WBIN = {"W_ADD": "w_add", "W_SUB": "w_sub", "W_MUL": "w_mul", "W_AND": "w_and", "W_OR": "w_or",
@@ -145,8 +149,9 @@ class _Gen:
     """Emit the body of one program as straight-line HIP."""
 
     def __init__(self, p: Program, name: str, fence_first: bool = False, lds_leaves: int = 0,
-                 insns: Optional[List[MInsn]] = None, interleave: int = 1):
+                 insns: Optional[List[MInsn]] = None, interleave: int = 1, mul_cols: Optional[bool] = None):
         self.fence_first = fence_first  # diagnostics (tools/opbench.py): no folding across nodes
+        self.mul_cols = MUL_COLS if mul_cols is None else mul_cols
         self.p = p
         self.insns = interleave_conjuncts(p.machine_ir() if insns is None else insns, interleave)
         # the lds_leaves most-used wide leaves live in LDS (mw_jit.h lds_put8/lds_get8)
@@ -248,6 +253,8 @@ class _Gen:
             out(f"u32 {dn}[8]; jit::w_mov({A[0]}, {w}u, {dn});")
         elif op == "MOV_N":
             out(f"const u32 {dn} = {A[0]};")
+        elif op == "W_MUL" and self.mul_cols and all(isinstance(s, VReg) for s in S):
+            out(f"u32 {dn}[8]; jit::w_mulv({A[0]}, {A[1]}, {w}u, {dn});")
         elif op in _WBIN:
             out(f"u32 {dn}[8]; jit::{_WBIN[op]}({A[0]}, {A[1]}, {w}u, {dn});")
         elif op.startswith("W_") and op[2:] in _DIV:
@@ -390,7 +397,8 @@ def split_ssa(p: Program, part_weight: int = PART_WEIGHT) -> List[List[MInsn]]:
 
 def generate(progs: Sequence[Program], names: Sequence[str], variants: str = "xe",
              fence_first: bool = False, lds_leaves: int = 0,
-             parts: Optional[Sequence[Tuple[List[MInsn], int, int]]] = None, interleave: int = 1) -> str:
+             parts: Optional[Sequence[Tuple[List[MInsn], int, int]]] = None, interleave: int = 1,
+             mul_cols: Optional[bool] = None) -> str:
     """HIP source for a module holding one specialised kernel set per program
     (with `parts`: per program, its (instructions, part index, part count))."""
     out = ["// generated by mythril_amd/jit.py: specialised witness-search kernels"]
@@ -416,7 +424,7 @@ def generate(progs: Sequence[Program], names: Sequence[str], variants: str = "xe
         part = parts[k] if parts else None
         out.append(f"// program {name}: {p.n_insn} bytecode insns, {p.ops_per_eval} u32 ops/eval"
                    + (f", part {part[1]} of {part[2]}" if part else ""))
-        out.append(_Gen(p, name, fence_first, lds_leaves, part[0] if part else None, interleave).body())
+        out.append(_Gen(p, name, fence_first, lds_leaves, part[0] if part else None, interleave, mul_cols).body())
         out.append(f"MW_JIT_SIG({name}, {signature(p):#x}ull)")
         if part:
             out.append(f"MW_JIT_PART({name}, {part[1]}u, {part[2]}u)")
@@ -493,22 +501,23 @@ def _compile(src: str, flags: Sequence[str], suffix: str, ext: str) -> Tuple[Pat
 
 
 def is_cached(progs: Sequence[Program], variants: str = "xe", waves: int = 2, lds_leaves: int = 0,
-              interleave: int = 1) -> bool:
+              interleave: int = 1, mul_cols: Optional[bool] = None) -> bool:
     """Whether compile_device(...) with these arguments would be a cache hit."""
     names = [kernel_name(p) for p in progs]
-    src = generate(progs, names, variants, lds_leaves=lds_leaves, interleave=interleave)
+    src = generate(progs, names, variants, lds_leaves=lds_leaves, interleave=interleave, mul_cols=mul_cols)
     return (_cache_dir() / f"{_key(src, _device_flags(waves))}.hsaco").exists()
 
 
 def compile_device(progs: Sequence[Program], variants: str = "xe", fence_first: bool = False,
-                   waves: int = 2, lds_leaves: int = 0, interleave: int = 1) -> Tuple[bytes, List[str], float]:
+                   waves: int = 2, lds_leaves: int = 0, interleave: int = 1,
+                   mul_cols: Optional[bool] = None) -> Tuple[bytes, List[str], float]:
     """gfx950 code object for `progs`; returns (image, kernel names, compile seconds; 0 if cached).
 
     waves: waves per SIMD the kernels are built for (launch bounds): 2 gives
     each lane 256 registers, 1 gives 512 (AGPRs become spill space instead of
     scratch memory) at half the latency hiding."""
     names = [kernel_name(p) for p in progs]
-    src = generate(progs, names, variants, fence_first, lds_leaves, interleave=interleave)
+    src = generate(progs, names, variants, fence_first, lds_leaves, interleave=interleave, mul_cols=mul_cols)
     path, dt = _compile(src, _device_flags(waves), ".hsaco", ".hip")
     return path.read_bytes(), names, dt
 

@@ -44,6 +44,7 @@ for (:class:`AckLeaf`) so a witness can be turned back into a model.
 from __future__ import annotations
 
 import zlib
+from itertools import chain
 from dataclasses import dataclass, field
 from operator import attrgetter
 from typing import Dict, List, Optional, Tuple
@@ -851,6 +852,41 @@ def _never_equal(x: Node, y: Node) -> bool:
     return bx is by and x.width == y.width and (kx - ky) % (1 << x.width) != 0
 
 
+def _topo_memo(roots: List[Node], seen: set, memo: dict, table: List[Node], whole: bool = False) -> List[Node]:
+    """topo(roots, seen) from walks kept in ``memo`` (a long-lived context's):
+    each root's own walk (whole=False: the main conjuncts, which share few
+    nodes), or the fresh walk of the whole root list, keyed by its root ids
+    (whole=True: the congruence conjuncts, thousands of small roots over the
+    same few shared reads, identical while a set's reads are).  The same
+    list as topo: a node ``seen`` before has its whole operand tree seen, so
+    dropping the seen nodes from a fresh walk leaves exactly what the walk
+    with ``seen`` emits, and a root's walk after earlier roots is its own
+    walk without the nodes they emitted.  The merge is C-level
+    (dict.fromkeys over ids; table is the context's node list, by id)."""
+    if whole:
+        key = tuple([r.id for r in roots])
+        ids = memo.get(key)
+        if ids is None:
+            if len(memo) > _TOPO_MEMO_MAX:
+                memo.clear()
+            ids = memo[key] = tuple([n.id for n in topo(roots)])
+    else:
+        get = memo.get
+        lists = []
+        for r in roots:
+            t = get(r.id)
+            if t is None:
+                t = memo[r.id] = tuple([n.id for n in topo([r])])
+            lists.append(t)
+        ids = dict.fromkeys(chain.from_iterable(lists))
+    out = [i for i in ids if i not in seen] if seen else list(ids)
+    seen.update(out)
+    return list(map(table.__getitem__, out))
+
+
+_TOPO_MEMO_MAX = 1 << 14
+
+
 def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
     """Rewrite every conjunct, Ackermannise, add the congruence conjuncts.
 
@@ -885,18 +921,27 @@ def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
     cong = rw.congruence(ctx.__dict__.setdefault("_pairs", {}) if lowered is not None else None)
     fmain = _flatten(out)
     seen: set = set()
-    nmain = topo(fmain, seen)
+    if lowered is not None:        # per-root walks kept with the context (_topo_memo)
+        tmemo = ctx.__dict__.setdefault("_topo", {})
+        lmemo = ctx.__dict__.setdefault("_topo_lists", {})
+
+        def walk(roots, seen_):
+            return _topo_memo(roots, seen_, lmemo, ctx.nodes, whole=True)
+        nmain = _topo_memo(fmain, seen, tmemo, ctx.nodes)
+    else:
+        walk = topo
+        nmain = topo(fmain, seen)
     keyed = rw.keyed(cong, ctx.__dict__.setdefault("_keyed", {}) if lowered is not None else None)
     seen_main = set(seen) if keyed is not cong else None
     fcong = _flatten(cong)
-    flat, nodes = fmain + fcong, nmain + topo(fcong, seen)   # = topo(_flatten(out + cong))
+    flat, nodes = fmain + fcong, nmain + walk(fcong, seen)   # = topo(_flatten(out + cong))
     if nodes and max(map(_width, nodes)) > MAXW:   # every consumer chunks its wide operands; none may remain
         n = next(n for n in nodes if n.width > MAXW)
         raise Unsupported(f"{n.width}-bit {n.op} outside the legalised vocabulary")
     if keyed is cong:
         return Lowered(out + cong, rw.ack, len(cong), flat, nodes)
     fkeyed = _flatten(keyed)
-    return Lowered(out + keyed, rw.ack, len(cong), fmain + fkeyed, nmain + topo(fkeyed, seen_main),
+    return Lowered(out + keyed, rw.ack, len(cong), fmain + fkeyed, nmain + walk(fkeyed, seen_main),
                    harvest_conjuncts=out + cong, harvest_nodes=nodes)
 
 

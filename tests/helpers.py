@@ -207,6 +207,43 @@ def division_check_programs(npairs: int = 256, seed: int = 11):
     return progs
 
 
+def mul_stress_pairs(n: int, seed: int = 13):
+    """256-bit operand pairs for the column multiply (mw_jit.h mul8_cols):
+    limbs from the carry-heavy set (all ones, 2^32 - 2, the top bit, 0, 1)
+    mixed with random limbs, whole-word edge values, and random pairs."""
+    rng = random.Random(seed)
+    M = (1 << 256) - 1
+    edge = [0xFFFFFFFF, 0xFFFFFFFE, 0x80000000, 0, 1, 0x7FFFFFFF]
+
+    def word(mode):
+        if mode == 0:
+            return rng.getrandbits(256)
+        if mode == 1:
+            return M - rng.getrandbits(rng.choice([0, 1, 8, 32, 64, 200]))
+        return sum((rng.choice(edge) if rng.random() < 0.7 else rng.getrandbits(32)) << (32 * k) for k in range(8))
+    out = [(M, M), (M, 1), (1 << 255, M), (M, (1 << 32) - 1)]
+    while len(out) < n:
+        out.append((word(rng.randrange(3)), word(rng.randrange(3))))
+    return out[:n]
+
+
+def mul_check_programs(npairs: int = 4096, seed: int = 13):
+    """One program asserting bvmul(a, b) == e and bvmul(b, a) == e, where
+    candidate i draws (a, b, e) = pair i of mul_stress_pairs and its oracle
+    product from bit-field pools: every verdict over [0, npairs) must be 1."""
+    from mythril_amd.compiler import LeafSpec, compile_program
+    from oracle import bvsem
+    pairs = mul_stress_pairs(npairs, seed)
+    k = (npairs - 1).bit_length()
+    ctx = Ctx()
+    a, b, e = ctx.var("a", 256), ctx.var("b", 256), ctx.var("e", 256)
+    exp = [bvsem.bvmul(256, x, y) for x, y in pairs]
+    specs = {nm: LeafSpec(nm, 256, pool=list(vals), shift=0, bits=k)
+             for nm, vals in (("a", [x for x, _ in pairs]), ("b", [y for _, y in pairs]), ("e", exp))}
+    conj = [ctx.app("=", ctx.app("bvmul", a, b), e), ctx.app("=", ctx.app("bvmul", b, a), e)]
+    return [compile_program(conj, leaf_specs=specs)]
+
+
 def full_width_division_models(seed: int, n: int) -> List[Dict[str, int]]:
     """Operand pairs whose divisor has a nonzero top limb (y >= 2^224), with the
     quotient-estimate edge cases of mw_alu.h udivrem8_full: digits near 2^32-1,

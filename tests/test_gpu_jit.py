@@ -202,3 +202,25 @@ def test_constant_divisors_specialised(dev):
             v, _ = dev.eval_generated(dp, 1, 0, 256, trace=False)
             assert int(v.sum()) == 256, (name, special)
             dp.free()
+
+
+def test_mul_cols_against_oracle(dev):
+    """mw_jit.h mul8_cols (the column multiply of two register operands) on
+    carry-heavy operand pairs: every candidate asserts bvmul(a, b) == e with e
+    the oracle's product (tests/helpers.mul_check_programs), so every verdict
+    over the pool must be 1, on the kernel built with and without the columns
+    and on the interpreter."""
+    from tests.helpers import mul_check_programs
+    (p,) = mul_check_programs()
+    src = jit.generate([p], [jit.kernel_name(p)], mul_cols=True)
+    assert "jit::w_mulv(" in src
+    n = 4096
+    for cols in (True, False):
+        image, names, _ = jit.compile_device([p], mul_cols=cols)
+        a, b = _pair(dev, p, image, names[0])
+        va, _ = dev.eval_generated(a, 1, 0, n, trace=False)
+        vb, _ = dev.eval_generated(b, 1, 0, n, trace=False)
+        assert int(va.sum()) == n, "interpreter"
+        assert int(vb.sum()) == n, f"specialised kernel, mul_cols={cols}: {n - int(vb.sum())} wrong products"
+        a.free()
+        b.free()

@@ -38,8 +38,14 @@ def main():
         print("tests/test_gpu_jit.py constant divisors:", jit.compile_device(constant_divisor_programs())[2], "s",
               flush=True)
 
+    def mul_cols():
+        from tests.helpers import mul_check_programs
+        for cols in (True, False):
+            print("tests/test_gpu_jit.py mul_cols=%s:" % cols,
+                  jit.compile_device(mul_check_programs(), mul_cols=cols)[2], "s", flush=True)
+
     from config_bench import warm_jobs as config_jobs   # tools/config_bench.py (C2-C4 solver-log queries)
-    jobs += config_jobs() + [gpu_jit_modules, constant_divisors]
+    jobs += config_jobs() + [gpu_jit_modules, constant_divisors, mul_cols]
     if "--opbench" in sys.argv:
         from opbench import OPS, chain
 
