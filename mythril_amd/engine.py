@@ -124,7 +124,8 @@ def _prepare(conjuncts, ctx, use_pools, timings) -> Query:
     # low.nodes: the topo of the flattened conjuncts, computed once by
     # lower_constraints; harvest collects the var leaves in the same loop
     specs = harvest(low.harvest_conjuncts or low.conjuncts, None, nodes=low.harvest_nodes or low.nodes,
-                    memo=ctx.__dict__.setdefault("_harvest", {}) if getattr(ctx, "long_lived", False) else None) \
+                    memo=ctx.__dict__.setdefault("_harvest", {}) if getattr(ctx, "long_lived", False) else None,
+                    split=low.harvest_split) \
         if use_pools else {}
     t2 = time.perf_counter()
     prog = compile_query(low.conjuncts, leaf_specs=specs, reach=(low.flat, low.nodes))

@@ -76,6 +76,10 @@ class Lowered:
     # what harvest reads (the congruence premises unkeyed, _Rewriter.keyed): None = conjuncts / nodes
     harvest_conjuncts: Optional[List[Node]] = None
     harvest_nodes: Optional[List[Node]] = None
+    # long-lived contexts: (length of the main conjuncts' part of the harvest
+    # nodes, the congruence part's node ids) - harvest keeps its scan of that
+    # part, identical while a set's reads are (pools.harvest segments)
+    harvest_split: Optional[Tuple[int, tuple]] = None
 
 
 class _Rewriter:
@@ -885,6 +889,7 @@ def _topo_memo(roots: List[Node], seen: set, memo: dict, table: List[Node], whol
 
 
 _TOPO_MEMO_MAX = 1 << 14
+_ID = attrgetter("id")
 
 
 def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
@@ -934,15 +939,17 @@ def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
     keyed = rw.keyed(cong, ctx.__dict__.setdefault("_keyed", {}) if lowered is not None else None)
     seen_main = set(seen) if keyed is not cong else None
     fcong = _flatten(cong)
-    flat, nodes = fmain + fcong, nmain + walk(fcong, seen)   # = topo(_flatten(out + cong))
+    ncong = walk(fcong, seen)
+    flat, nodes = fmain + fcong, nmain + ncong   # = topo(_flatten(out + cong))
+    split = (len(nmain), tuple(map(_ID, ncong))) if lowered is not None and len(ncong) >= 256 else None
     if nodes and max(map(_width, nodes)) > MAXW:   # every consumer chunks its wide operands; none may remain
         n = next(n for n in nodes if n.width > MAXW)
         raise Unsupported(f"{n.width}-bit {n.op} outside the legalised vocabulary")
     if keyed is cong:
-        return Lowered(out + cong, rw.ack, len(cong), flat, nodes)
+        return Lowered(out + cong, rw.ack, len(cong), flat, nodes, harvest_split=split)
     fkeyed = _flatten(keyed)
     return Lowered(out + keyed, rw.ack, len(cong), fmain + fkeyed, nmain + walk(fkeyed, seen_main),
-                   harvest_conjuncts=out + cong, harvest_nodes=nodes)
+                   harvest_conjuncts=out + cong, harvest_nodes=nodes, harvest_split=split)
 
 
 def needs_lowering(conjuncts: List[Node]) -> bool:

@@ -52,7 +52,7 @@ Pools are laid out as index bit-fields while the 40 field bits last
 from __future__ import annotations
 
 import itertools
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 from .compiler import LeafSpec
 from .ir import BOOL, Node, topo
@@ -439,9 +439,69 @@ def _cmp_effect(n: Node):
     return props, words, part
 
 
+_SEG_MEMO_MAX = 64
+
+
+def _scan(nodes: List[Node], memo: Optional[dict]):
+    """harvest's walk over one segment of the node list, as lists in node
+    order: constants, vars, concats, the comparisons' contributions
+    (_cmp_effect, non-empty ones), alignment facts (leaf, K) and leaf
+    unions (name, name).  The unions of a segment are reduced to one edge
+    per merged name (same partition: harvest's proposals depend on the
+    partition alone, not on its union order)."""
+    consts, vars_, concats, effs, align, unions = [], [], [], [], [], []
+    for n in nodes:
+        op = n.op
+        if op == "const":
+            if n.width != BOOL:
+                consts.append(n.val)
+            continue
+        if op == "var":
+            vars_.append(n)
+            continue
+        if op == "concat":
+            concats.append(n)
+            continue
+        if op in _CMP and len(n.args) == 2:
+            eff = memo.get(n.id) if memo is not None else None
+            if eff is None:
+                eff = _cmp_effect(n)
+                if memo is not None:
+                    memo[n.id] = eff
+            if eff[0] or eff[1] or eff[2]:
+                effs.append(eff)
+            if op == "=":
+                a, b = n.args
+                for x, k in ((a, b), (b, a)):
+                    al = _align_of(x) if (k.op == "const" and k.val == 0) else None
+                    if al is not None:
+                        align.append(al)
+                # x = y, also through the masks and zero-padding of an address
+                # compare (concat(0, extract(159, 0, x)), bvand(mask, x)): a stored
+                # owner equated with msg.sender gets the actors
+                xa, xb = _bare_leaf(a), _bare_leaf(b)
+                if xa is not None and xb is not None and xa.width == xb.width and xa is not xb:
+                    unions.append((xa.name, xb.name))
+    if len(unions) > 8:
+        parent: Dict[str, str] = {}
+
+        def find(x):
+            while parent.get(x, x) != x:
+                parent[x] = parent.get(parent[x], parent[x])
+                x = parent[x]
+            return x
+        for na, nb in unions:
+            ra, rb = find(na), find(nb)
+            if ra != rb:
+                parent[ra] = rb
+        unions = [(x, find(x)) for x in parent]
+    return consts, vars_, concats, effs, align, unions
+
+
 def harvest(conjuncts: List[Node], leaves: Optional[List[Node]], pool_size: int = 32,
             random_share: float = 0.25, restrict: bool = True,
-            nodes: Optional[List[Node]] = None, memo: Optional[dict] = None) -> Dict[str, LeafSpec]:
+            nodes: Optional[List[Node]] = None, memo: Optional[dict] = None,
+            split: Optional[Tuple[int, tuple]] = None) -> Dict[str, LeafSpec]:
     """nodes: topo(conjuncts) when the caller has it (prepare: Lowered.nodes,
     the same walk without the top-level `and` nodes, which no rule reads).
     leaves None: every var of `nodes`, first occurrence of each name in walk
@@ -477,31 +537,37 @@ def harvest(conjuncts: List[Node], leaves: Optional[List[Node]], pool_size: int 
     word_props: Dict[int, List[int]] = {}
     consts = []
     dm: List[Dict[str, List[int]]] = []
-    eq2: List[Node] = []      # binary equalities (alignment, leaf unions), in walk order
     concats: List[Node] = []  # word candidates (_tie_words)
-    for n in nodes:
-        op = n.op
-        if op == "const":
-            if n.width != BOOL:
-                consts.append(n.val)
-            continue
-        if op == "var":
-            if collect and n.name not in seen_leaf:
-                seen_leaf.add(n.name)
-                leaves.append(n)
-            continue
-        if op == "concat":
-            concats.append(n)
-            continue
-        if op in _CMP and len(n.args) == 2:
-            if op == "=":
-                eq2.append(n)
-            eff = memo.get(n.id) if memo is not None else None
-            if eff is None:
-                eff = _cmp_effect(n)
-                if memo is not None:
-                    memo[n.id] = eff
-            props, words, part = eff
+    align: Dict[str, int] = {}
+    unions: List[Tuple[str, str]] = []
+    # the node list in segments: (start, end, memo key or None).  A keyed
+    # segment's scan (_scan) is kept in the context's memo and replayed: the
+    # accumulators below only ever append in node order, so replaying a
+    # segment's lists equals scanning its nodes again (split: engine.prepare
+    # passes Lowered.harvest_split, the congruence part of a long-lived set)
+    if split is not None and memo is not None:
+        segs = [(0, split[0], None), (split[0], len(nodes), ("seg", split[1]))]
+    else:
+        segs = [(0, len(nodes), None)]
+    for a, b, key in segs:
+        sc = memo.get(key) if key is not None else None
+        if sc is None:
+            sc = _scan(nodes[a:b] if (a, b) != (0, len(nodes)) else nodes, memo)
+            if key is not None:
+                segm = memo.setdefault("segments", [])
+                if len(segm) >= _SEG_MEMO_MAX:      # bounded: a long run meets many read sets
+                    memo.pop(segm.pop(0), None)
+                segm.append(key)
+                memo[key] = sc
+        s_consts, s_vars, s_concats, s_effs, s_align, s_unions = sc
+        consts.extend(s_consts)
+        if collect:
+            for n in s_vars:
+                if n.name not in seen_leaf:
+                    seen_leaf.add(n.name)
+                    leaves.append(n)
+        concats.extend(s_concats)
+        for props, words, part in s_effs:
             for name, vs in props.items():
                 got = proposals.get(name)
                 if got is None:
@@ -515,16 +581,12 @@ def harvest(conjuncts: List[Node], leaves: Optional[List[Node]], pool_size: int 
                 else:
                     got.extend(vs)
             dm.extend(part)                    # facts fixing only part of some leaf's bits
+        for name, K in s_align:
+            align[name] = K
+        unions.extend(s_unions)
     # packed-array indexing: t / K == c and t % K == r -> t = c*K + r, tried first
     combos = _combine_partial(dm)
-    # alignment facts: (= (bvurem x K) 0)  ->  x should be a multiple of K
-    align: Dict[str, int] = {}
-    for n in eq2:
-        a, b = n.args
-        for x, k in ((a, b), (b, a)):
-            al = _align_of(x) if (k.op == "const" and k.val == 0) else None
-            if al is not None:
-                align[al[0]] = al[1]
+    # alignment facts: (= (bvurem x K) 0)  ->  x should be a multiple of K (_scan)
     for name, K in align.items():
         props = proposals.get(name, [])
         aligned = []
@@ -541,15 +603,10 @@ def harvest(conjuncts: List[Node], leaves: Optional[List[Node]], pool_size: int 
             x = parent[x]
         return x
 
-    for n in eq2:
-        # x = y, also through the masks and zero-padding of an address
-        # compare (concat(0, extract(159, 0, x)), bvand(mask, x)): a stored
-        # owner equated with msg.sender gets the actors
-        xa, xb = _bare_leaf(n.args[0]), _bare_leaf(n.args[1])
-        if xa is not None and xb is not None and xa.width == xb.width and xa is not xb:
-            ra, rb = find(xa.name), find(xb.name)
-            if ra != rb:
-                parent[ra] = rb
+    for na, nb in unions:     # x = y between two leaves (_scan)
+        ra, rb = find(na), find(nb)
+        if ra != rb:
+            parent[ra] = rb
     if parent:
         groups: Dict[str, List[int]] = {}
         for name, props in list(proposals.items()):

@@ -1,6 +1,8 @@
 """Candidate pools (mythril_amd/pools.py): domain restriction and word-tied
 calldata bytes.  The generated candidates are checked with the oracle's leaf
 generator (tests/helpers.oracle_models), which mirrors csrc/mw_leaf.h."""
+import os
+
 from mythril_amd.compiler import compile_program
 from mythril_amd.ir import Ctx
 from mythril_amd.pools import ACTORS, domains, harvest
@@ -193,3 +195,43 @@ def test_check_imp_verdicts_all_input_combinations():
         if not any(k.args[0].op == "const" or k.args[1].op == "const" for k in conj):
             assert ops & {isa.OPCODES[n] for n in ("CHECK_IMP", "CHECK_IMPEQ", "CHECK_IMPEQW", "CHECK_IMPEQK")}, conj
     assert [int(all(eval_nodes(shapes[0], m)[k.id] for k in shapes[0])) for m in models] == [1, 1, 0, 1]
+
+
+def test_long_lived_prepare_replays_memoised_walks_and_scans():
+    """C3 through a long-lived context (z3bridge.ConjunctCache's): its parent
+    set, the full set and the full set again (the kept topo walks and the
+    harvest's congruence-segment scan replayed, lower._topo_memo /
+    pools._scan) compile to the program a fresh context gives."""
+    from mythril_amd import z3bridge
+    from mythril_amd.engine import prepare
+    from mythril_amd.smt2 import parse_script, to_smt2
+    from tests import fakez3
+    from tools.replay_latency import program_bytes
+    import sys as _sys
+    z = fakez3.module()
+    old = _sys.modules.get("z3")
+    _sys.modules["z3"] = z
+    saved = z3bridge.solver_sexpr
+    z3bridge.solver_sexpr = lambda raws: to_smt2([r.node for r in raws])
+    try:
+        text = open(os.path.join(os.path.dirname(__file__), "golden", "solver_log",
+                                 "c3_bec_batchtransfer_overflow.smt2")).read()
+        fresh = parse_script(text)
+        want = program_bytes(prepare(fresh.asserts, fresh.ctx).program)
+        ws = parse_script(text)
+        raws = [z.ast(n) for n in ws.asserts]
+        cache = z3bridge.ConjunctCache()
+        sp = cache.to_ir(raws[:-1])
+        prepare(sp.asserts, sp.ctx)
+        for _ in range(2):
+            sc = cache.to_ir(raws)
+            q = prepare(sc.asserts, sc.ctx)
+            assert q.lowered.harvest_split is not None
+            assert program_bytes(q.program) == want
+        assert any(isinstance(k, tuple) and k and k[0] == "seg" for k in sc.ctx._harvest)
+    finally:
+        z3bridge.solver_sexpr = saved
+        if old is None:
+            _sys.modules.pop("z3", None)
+        else:
+            _sys.modules["z3"] = old
