@@ -17,6 +17,7 @@
 #   dropinprof     tools/dropin_profile.py (library step times per drop-in query)
 #   replay         python -m mythril_amd.replay tests/golden/solver_log
 #   replaylat      tools/replay_latency.py (LASER-order translation + preparation, host only)
+#   c3prep         tools/c3_prepare.py (C3 through the per-conjunct cache, host only)
 #   opbench        tools/opbench.py jit
 #   keccak         tools/keccak_bench.py
 #   ipmc=FILE      PMC passes on one exhaustive interpreter launch of FILE (tools/interp_once.py)
@@ -101,6 +102,9 @@ for step in "$@"; do
     replay)
       run 300 "$OUT/replay.txt" python3 -m mythril_amd.replay tests/golden/solver_log
       tail -12 "$OUT/replay.txt" ;;
+    c3prep)
+      run 300 "$OUT/c3_prepare.log" python3 -u tools/c3_prepare.py --reps 40 --out "$OUT/c3_prepare.json"
+      tail -2 "$OUT/c3_prepare.log" ;;
     replaylat)
       run 400 "$OUT/replay_latency.log" python3 -u tools/replay_latency.py --out "$OUT/replay_latency.json"
       tail -3 "$OUT/replay_latency.log" ;;
