@@ -923,7 +923,19 @@ def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
         for al in ack.values():
             rw.by_base.setdefault((al.kind, al.base), []).append(al)
     rw.pins = _pins(out, rw.ack)
-    cong = rw.congruence(ctx.__dict__.setdefault("_pairs", {}) if lowered is not None else None)
+    lists = None
+    if lowered is not None:
+        # the congruence and its keyed form depend on the reads per base (in
+        # order) and the pinned values alone: kept per such key (a successor
+        # that adds no read reuses its parent's lists outright)
+        cmemo = ctx.__dict__.setdefault("_cong_lists", {})
+        ckey = (tuple([(kb, tuple([al.name for al in reads])) for kb, reads in rw.by_base.items()]),
+                tuple(sorted([(nm, k.id) for nm, k in rw.pins.items()])))
+        lists = cmemo.get(ckey)
+    if lists is None:
+        cong = rw.congruence(ctx.__dict__.setdefault("_pairs", {}) if lowered is not None else None)
+    else:
+        cong = lists[0]
     fmain = _flatten(out)
     seen: set = set()
     if lowered is not None:        # per-root walks kept with the context (_topo_memo)
@@ -936,18 +948,27 @@ def lower_constraints(conjuncts: List[Node], ctx: Ctx) -> Lowered:
     else:
         walk = topo
         nmain = topo(fmain, seen)
-    keyed = rw.keyed(cong, ctx.__dict__.setdefault("_keyed", {}) if lowered is not None else None)
+    if lists is None:
+        keyed = rw.keyed(cong, ctx.__dict__.setdefault("_keyed", {}) if lowered is not None else None)
+    else:
+        keyed = lists[1]
     seen_main = set(seen) if keyed is not cong else None
-    fcong = _flatten(cong)
+    fcong = _flatten(cong) if lists is None else lists[2]
     ncong = walk(fcong, seen)
     flat, nodes = fmain + fcong, nmain + ncong   # = topo(_flatten(out + cong))
     split = (len(nmain), tuple(map(_ID, ncong))) if lowered is not None and len(ncong) >= 256 else None
     if nodes and max(map(_width, nodes)) > MAXW:   # every consumer chunks its wide operands; none may remain
         n = next(n for n in nodes if n.width > MAXW)
         raise Unsupported(f"{n.width}-bit {n.op} outside the legalised vocabulary")
+    fkeyed = None
+    if keyed is not cong:
+        fkeyed = _flatten(keyed) if lists is None else lists[3]
+    if lists is None and lowered is not None:
+        if len(cmemo) >= _TOPO_MEMO_MAX:
+            cmemo.clear()
+        cmemo[ckey] = (cong, keyed, fcong, fkeyed)
     if keyed is cong:
         return Lowered(out + cong, rw.ack, len(cong), flat, nodes, harvest_split=split)
-    fkeyed = _flatten(keyed)
     return Lowered(out + keyed, rw.ack, len(cong), fmain + fkeyed, nmain + walk(fkeyed, seen_main),
                    harvest_conjuncts=out + cong, harvest_nodes=nodes, harvest_split=split)
 

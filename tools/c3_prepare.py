@@ -13,6 +13,7 @@ a whole-set prepare in a fresh context (checked once).
     python tools/c3_prepare.py [--reps 15] [--file NAME] [--out FILE]
 """
 import argparse
+import gc
 import json
 import os
 import statistics
@@ -42,7 +43,9 @@ def main():
     s = parse_file(os.path.join(ROOT, "tests", "golden", "solver_log", a.file))
     text = to_smt2(s.asserts)
     rows = []
+    sc = q = None
     for rep in range(a.reps):
+        sc = q = None        # the previous repetition's context is freed here, not inside the timed calls
         ws = parse_script(text)         # fresh nodes, fresh stand-in ASTs per repetition
         raws = [z.ast(n) for n in ws.asserts]
         cache = z3bridge.ConjunctCache()
@@ -54,6 +57,7 @@ def main():
             import cProfile
             pr = cProfile.Profile()
             pr.enable()
+        gc.collect()         # the parent's deferred collection (prepare pauses the collector) is not the child's
         t0 = time.perf_counter()
         sc = cache.to_ir(raws)
         t1 = time.perf_counter()
