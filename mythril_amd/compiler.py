@@ -22,6 +22,7 @@ the drop-in ``get_model`` turns into "fall back to z3" (fail closed).
 from __future__ import annotations
 
 import math
+import os
 import zlib
 from array import array
 from dataclasses import dataclass, field
@@ -926,6 +927,9 @@ def _schedule_narrow_early(insns: List[MInsn]) -> List[MInsn]:
 
 
 # --------------------------------------------------------------------------- register allocation
+REMAT_LEAVES = os.environ.get("MYTHRIL_AMD_REMAT_LEAVES", "1") != "0"
+
+
 def _allocate(insns: List[MInsn], slots: Optional[Tuple[int, int]] = None):
     """Belady allocation of W/N vregs to MW_NW/MW_NN slots (slots: fewer,
     (W, N) - mw_compile.cpp mw_compile_slots); returns (insns, n_spill)."""
@@ -958,6 +962,12 @@ def _allocate(insns: List[MInsn], slots: Optional[Tuple[int, int]] = None):
     spill_free: Dict[str, List[int]] = {"W": [], "N": []}
     slot_cls: List[str] = []
     out: List[MInsn] = []
+    # wide leaves are drawn again where they are needed instead of spilled and
+    # filled (REMAT_LEAVES): the candidate generator is a function of the
+    # candidate and the leaf alone, and a W spill is eight words each way
+    remat = {ins.dst.id: ins for ins in insns if ins.op == "LEAF_W" and ins.dst is not None} \
+        if REMAT_LEAVES else {}
+    rematted: set = set()
 
     def get_spill_slot(cls: str) -> int:
         if spill_free[cls]:
@@ -977,7 +987,9 @@ def _allocate(insns: List[MInsn], slots: Optional[Tuple[int, int]] = None):
             raise Unsupported("register pressure: too many simultaneous operands")
         slot = reg_of.pop(best.id)
         del resident[cls][best.id]
-        if best_nu < (1 << 60) and best.id not in spill_of:
+        if best_nu < (1 << 60) and best.id in remat:
+            rematted.add(best.id)
+        elif best_nu < (1 << 60) and best.id not in spill_of:
             sp = get_spill_slot(cls)
             spill_of[best.id] = sp
             m = MInsn("SPILL_W" if cls == "W" else "SPILL_N", 0, None, [("phys", slot)], imm=sp)
@@ -994,6 +1006,13 @@ def _allocate(insns: List[MInsn], slots: Optional[Tuple[int, int]] = None):
         # bring every source into a register
         for s in ins.srcs:
             if isinstance(s, VReg) and s.id not in reg_of:
+                if s.id in rematted:
+                    slot = take(s.cls, i, pinned)
+                    r = remat[s.id]
+                    out.append(MInsn("LEAF_W", r.width, ("phys", slot), [], r.imm, chain=r.chain))
+                    reg_of[s.id] = slot
+                    resident[s.cls][s.id] = s
+                    continue
                 if s.id not in spill_of:
                     raise AssertionError("use of undefined vreg")
                 slot = take(s.cls, i, pinned)

@@ -13,6 +13,7 @@
 // The Python prepare() spent most of its time here; this
 // runs the same passes in a few microseconds per node.
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -122,6 +123,16 @@ struct Insn {
   bool grid = false;  // SPILL_N of a grid table entry (form_grids): a fixed word, not a spill slot
   bool cdleaf = false;  // a LEAF_N kept beside the W_CDINS that draws it again (fuse_checks)
 };
+
+// MYTHRIL_AMD_REMAT_LEAVES=0 turns leaf rematerialisation off (read once, as
+// compiler.py reads it at import)
+bool remat_leaves() {
+  static const bool on = [] {
+    const char* e = getenv("MYTHRIL_AMD_REMAT_LEAVES");
+    return !(e && strcmp(e, "0") == 0);
+  }();
+  return on;
+}
 
 int dst_cls(int op) {   // 'W', 'N' or 0 (isa.SHAPES[op][0])
   if (op >= MW_W_ADD && op <= MW_W_CDINS) return 'W';
@@ -1059,6 +1070,13 @@ struct Compiler {
     for (int s = n_slots - 1; s >= 0; --s)
       if ((s & 31) != MW_N_RESERVED) freeN.push_back(s);
     std::vector<int> reg_of(nv, -1), spill_of(nv, -1);
+    // wide leaves are drawn again where they are needed instead of spilled
+    // and filled (compiler.py REMAT_LEAVES): remat_def = the defining LEAF_W
+    std::vector<int> remat_def(nv, -1);
+    std::vector<char> rematted(nv, 0);
+    if (remat_leaves())
+      for (size_t i = 0; i < in.size(); ++i)
+        if (in[i].op == MW_LEAF_W && in[i].dst >= 0) remat_def[in[i].dst] = (int)i;
     std::vector<int> resW, resN;   // insertion-ordered resident vregs (compiler.py dict order)
     std::vector<int> spill_freeW, spill_freeN;
     std::vector<char> slot_cls;
@@ -1098,7 +1116,9 @@ struct Compiler {
       int slot = reg_of[best];
       reg_of[best] = -1;
       erase(RES(c), best);
-      if (best_nu < NEVER && spill_of[best] < 0) {
+      if (best_nu < NEVER && remat_def[best] >= 0) {
+        rematted[best] = 1;
+      } else if (best_nu < NEVER && spill_of[best] < 0) {
         int sp = get_spill_slot(c);
         spill_of[best] = sp;
         Insn m;
@@ -1124,6 +1144,16 @@ struct Compiler {
         if (is_v(x.s[j])) pinned[np++] = x.s[j].v;
       for (int j = 0; j < x.ns; ++j) {
         const Opnd& s = x.s[j];
+        if (is_v(s) && reg_of[s.v] < 0 && rematted[s.v]) {
+          int c = vcls[s.v];
+          int slot = take(c, (long long)i, pinned, np);
+          Insn r = in[remat_def[s.v]];
+          r.dst = slot;
+          out.push_back(r);
+          reg_of[s.v] = slot;
+          RES(c).push_back(s.v);
+          continue;
+        }
         if (is_v(s) && reg_of[s.v] < 0) {
           if (spill_of[s.v] < 0) throw BadInput{"use of undefined vreg"};
           int c = vcls[s.v];

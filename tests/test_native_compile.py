@@ -98,16 +98,40 @@ def test_random_dags_byte_identical(seed):
 
 
 def test_register_pressure_spills_identical():
-    """Forty wide values live at once: the W file (7 slots) spills and fills,
-    the narrow file too; spill slots laid out hottest-first."""
+    """Forty wide products live at once (both folds read all of them): the W
+    file (7 slots) spills and fills, the narrow file too; spill slots laid
+    out hottest-first."""
+    import functools
     c = Ctx()
     xs = [c.var(f"x{i}", 256) for i in range(40)]
-    ys = [c.app("bvadd", x, c.const(i + 1, 256)) for i, x in enumerate(xs)]
-    conj = [c.app("bvult", y, z) for y, z in zip(ys, ys[::-1])]
-    ns = [c.app("extract", y, params=(7, 0)) for y in ys]
+    ws = [c.app("bvmul", x, xs[(i + 1) % 40]) for i, x in enumerate(xs)]
+    f1 = functools.reduce(lambda a, b: c.app("bvadd", a, b), ws)
+    f2 = functools.reduce(lambda a, b: c.app("bvxor", a, b), ws[::-1])
+    conj = [c.app("bvult", f1, c.const(5, 256)), c.app("bvult", f2, c.const(7, 256))]
+    ns = [c.app("extract", w, params=(7, 0)) for w in ws]
     conj += [c.app("=", c.app("bvxor", *ns), c.const(3, 8))]
     a, b = _both(conj)
     assert a.stats["spills"] > 0 and a.stats["fills"] > 0
+
+
+def test_wide_leaves_redrawn_not_spilled():
+    """Forty wide leaves live across two folds: with REMAT_LEAVES (the
+    default) the allocators draw an evicted leaf again at its next use
+    instead of spilling it (the same LEAF_W, same leaf), identically."""
+    import functools
+    from mythril_amd import compiler
+    c = Ctx()
+    xs = [c.var(f"x{i}", 256) for i in range(40)]
+    f1 = functools.reduce(lambda a, b: c.app("bvadd", a, b), xs)
+    f2 = functools.reduce(lambda a, b: c.app("bvxor", a, b), xs[::-1])
+    conj = [c.app("bvult", f1, c.const(5, 256)), c.app("bvult", f2, c.const(7, 256))]
+    a, b = _both(conj)
+    inv = {v: k for k, v in isa.OPCODES.items()}
+    ops = [inv[int(r[0]) & 0xFF] for r in a.code.reshape(-1, 4)]
+    if compiler.REMAT_LEAVES:
+        assert a.stats["spills"] == 0 and ops.count("LEAF_W") > 40
+    else:
+        assert a.stats["spills"] > 0
 
 
 def test_superinstructions_identical():

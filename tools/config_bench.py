@@ -84,6 +84,7 @@ def main():
     ap.add_argument("--no-jit", action="store_true")
     ap.add_argument("--warm", action="store_true", help="only compile the specialised kernels into build/jit (CPU)")
     ap.add_argument("--only", default=None, help="comma-separated config names (default: all)")
+    ap.add_argument("--engines", default=None, help="comma-separated engines (default: asm,asmjit,interp[,jit])")
     a = ap.parse_args()
     import bench
     from mythril_amd import isa, jit
@@ -116,7 +117,10 @@ def main():
                 first = [x if x is not None else y for x, y in zip(first, found)]
                 pos += SLICE
             ttfw = time.perf_counter() - t0
-            for engine in (["asm", "asmjit", "interp"] if a.no_jit else ["asm", "asmjit", "interp", "jit"]):
+            engines = ["asm", "asmjit", "interp"] if a.no_jit else ["asm", "asmjit", "interp", "jit"]
+            if a.engines:
+                engines = a.engines.split(",")
+            for engine in engines:
                 compile_s = None
                 # asm: the threaded-dispatch interpreter (the default for these
                 # programs); asmjit: each program's assembled kernel
