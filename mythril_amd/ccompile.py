@@ -94,11 +94,14 @@ def why_unavailable() -> Optional[str]:
     return _why
 
 
-def serialize(conj: Sequence[Node], trace: Sequence[Node], nodes: Optional[List[Node]] = None):
+def serialize(conj: Sequence[Node], trace: Sequence[Node], nodes: Optional[List[Node]] = None,
+              memo: Optional[dict] = None):
     """(records, number of nodes, constant bytes, roots, nodes): the DAG below
     the (flattened) conjuncts and traced terms in the mythril_compile.h
     format, operand-first (``topo`` order, the node set compile_program
-    counts ops over; `nodes` when the caller has that walk already)."""
+    counts ops over; `nodes` when the caller has that walk already).
+    memo: an operation node's record head by node id, kept with a long-lived
+    context (the head depends on the node alone; operand indices do not)."""
     if nodes is None:
         nodes = topo(list(conj) + list(trace))
     idx: Dict[int, int] = {}
@@ -107,6 +110,7 @@ def serialize(conj: Sequence[Node], trace: Sequence[Node], nodes: Optional[List[
     names: Dict[str, int] = {}
     nk = 0
     ext, put, opc = recs.extend, recs.append, _OPC.get
+    hget = memo.get if memo is not None else None
     for i, n in enumerate(nodes):
         idx[n.id] = i
         op = n.op
@@ -123,11 +127,16 @@ def serialize(conj: Sequence[Node], trace: Sequence[Node], nodes: Optional[List[
             continue
         args = n.args
         na = len(args)
-        pr = n.params
-        if pr:
-            ext((opc(op, -1), n.width, 0 if n.dom is None else 1, pr[0], pr[1] if len(pr) > 1 else 0, na))
-        else:
-            ext((opc(op, -1), n.width, 0 if n.dom is None else 1, 0, 0, na))
+        h = hget(n.id) if hget is not None else None
+        if h is None:
+            pr = n.params
+            if pr:
+                h = (opc(op, -1), n.width, 0 if n.dom is None else 1, pr[0], pr[1] if len(pr) > 1 else 0, na)
+            else:
+                h = (opc(op, -1), n.width, 0 if n.dom is None else 1, 0, 0, na)
+            if memo is not None:
+                memo[n.id] = h
+        ext(h)
         if na == 2:   # the common arities without a comprehension
             a, b = args
             ext((idx[a.id], idx[b.id]))
@@ -145,23 +154,25 @@ def _addr(buf) -> int:
 
 def compile_native(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, LeafSpec]] = None,
                    trace: Sequence[Node] = (), pools: Optional[Dict[str, List[Optional[int]]]] = None,
-                   reach=None, slots: Optional[Tuple[int, int]] = None) -> Program:
+                   reach=None, slots: Optional[Tuple[int, int]] = None, memo: Optional[dict] = None) -> Program:
     """compile_program(conjuncts, leaf_specs, trace, pools, slots), natively.
     reach: (flattened conjuncts, their topo) when the caller has them and
-    nothing is traced (prepare: Lowered.flat, Lowered.nodes)."""
+    nothing is traced (prepare: Lowered.flat, Lowered.nodes).  memo: a
+    long-lived context's record heads (serialize)."""
     fns = _bind()
     if fns is None:
         raise RuntimeError(f"native compiler unavailable: {_why}")
     trace = list(trace)
     if reach is not None and not trace:
         conj, nodes = reach
-        recs, nn, kb, nk, roots, nodes, idx, names = serialize(conj, trace, nodes)
+        recs, nn, kb, nk, roots, nodes, idx, names = serialize(conj, trace, nodes, memo)
     else:
         conj = _flatten(conjuncts)
         recs, nn, kb, nk, roots, nodes, idx, names = serialize(conj, trace)
     info, code, consts, leaves, tr = _run(fns, recs, nn, kb, nk, roots, len(conj), len(trace), slots)
     leaf_nodes = [nodes[i] for i in leaves.tolist()]
-    specs, leaf_words, pool_words, in_row = layout_leaves(leaf_nodes, leaf_specs, pools)
+    specs, leaf_words, pool_words, in_row = layout_leaves(leaf_nodes, leaf_specs, pools,
+                                                          memo.setdefault("_pools", {}) if memo is not None else None)
     t = tr.tolist()
     trace_map = {nodes[t[k]].id: (t[k + 1], "W" if t[k + 2] else "N") for k in range(0, len(t), 3)}
     n_insn = int(info.ncode_words) // 4
@@ -309,9 +320,10 @@ USE_PYTHON = os.environ.get("MYTHRIL_AMD_PY_COMPILE", "0") == "1"
 
 
 def compile_query(conjuncts: Sequence[Node], leaf_specs: Optional[Dict[str, LeafSpec]] = None,
-                  trace: Sequence[Node] = (), pools=None, reach=None, slots=None) -> Program:
+                  trace: Sequence[Node] = (), pools=None, reach=None, slots=None, memo=None) -> Program:
     """The product's compiler: native when the library is built (always, on
-    a GPU box: the device path needs the same library), else compiler.py."""
+    a GPU box: the device path needs the same library), else compiler.py.
+    memo: a long-lived context's serialisation memo (compile_native)."""
     if not USE_PYTHON and available():
-        return compile_native(conjuncts, leaf_specs, trace, pools, reach, slots)
+        return compile_native(conjuncts, leaf_specs, trace, pools, reach, slots, memo)
     return compile_program(conjuncts, leaf_specs=leaf_specs, trace=trace, pools=pools, slots=slots)

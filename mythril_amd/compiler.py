@@ -1084,7 +1084,7 @@ def _limbs(v: int) -> List[int]:
 
 
 def layout_leaves(leaf_nodes: Sequence[Node], leaf_specs: Optional[Dict[str, LeafSpec]] = None,
-                  pools: Optional[Dict[str, List[Optional[int]]]] = None):
+                  pools: Optional[Dict[str, List[Optional[int]]]] = None, memo: Optional[dict] = None):
     """Leaf table + pool words for `leaf_nodes` (in leaf-index order).
 
     Default layout: bit-interleaved (Morton) digits over the first
@@ -1092,7 +1092,8 @@ def layout_leaves(leaf_nodes: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
     best proposals of all leaves are tried together first; leaves that do not
     fit are sampled with hashed digits.  Returns (specs, leaf words, pool
     words, input rows).  The code refers to leaves by index only, so a program
-    whose leaf set grows (incremental.py) re-lays its table with this."""
+    whose leaf set grows (incremental.py) re-lays its table with this.
+    memo: a long-lived context's pool bytes by (width, entries)."""
     specs: List[LeafSpec] = []
     leaf_words: List[int] = []
     pool_words = bytearray()   # u32 words, little-endian
@@ -1158,12 +1159,20 @@ def layout_leaves(leaf_nodes: Sequence[Node], leaf_specs: Optional[Dict[str, Lea
                     spec.bits = nb
             pshift, pbits, poff, pstride = spec.shift, spec.bits, len(pool_words) // 4, spec.stride
             bit = max(bit, spec.shift + (spec.bits - 1) * max(spec.stride, 1) + 1 if spec.bits else 0)
-            m = (1 << w) - 1
-            if w < 32:   # one word per entry (mw_isa.h MW_POOL_NARROW_RANDOM)
-                pool_words += array("I", [isa.POOL_NARROW_RANDOM if e is None else e & m for e in spec.pool]).tobytes()
-            else:        # flags word + 8 limbs, little-endian
-                for e in spec.pool:
-                    pool_words += _POOL_RANDOM_W if e is None else b"\0\0\0\0" + (e & m).to_bytes(32, "little")
+            key = (w, tuple(spec.pool)) if memo is not None else None
+            pb = memo.get(key) if key is not None else None
+            if pb is None:
+                m = (1 << w) - 1
+                if w < 32:   # one word per entry (mw_isa.h MW_POOL_NARROW_RANDOM)
+                    pb = array("I", [isa.POOL_NARROW_RANDOM if e is None else e & m for e in spec.pool]).tobytes()
+                else:        # flags word + 8 limbs, little-endian
+                    pb = b"".join([_POOL_RANDOM_W if e is None else b"\0\0\0\0" + (e & m).to_bytes(32, "little")
+                                   for e in spec.pool])
+                if key is not None:
+                    if len(memo) >= 1 << 16:
+                        memo.clear()
+                    memo[key] = pb
+            pool_words += pb
         leaf_words.extend([w, kind, spec.key_salt(), pshift, pbits, poff, in_row, pstride])
         in_row += (w + 31) // 32
         specs.append(spec)

@@ -128,7 +128,8 @@ def _prepare(conjuncts, ctx, use_pools, timings) -> Query:
                     split=low.harvest_split) \
         if use_pools else {}
     t2 = time.perf_counter()
-    prog = compile_query(low.conjuncts, leaf_specs=specs, reach=(low.flat, low.nodes))
+    prog = compile_query(low.conjuncts, leaf_specs=specs, reach=(low.flat, low.nodes),
+                         memo=ctx.__dict__.setdefault("_records", {}) if getattr(ctx, "long_lived", False) else None)
     if timings is not None:
         timings.update(lower=t1 - t0, pools=t2 - t1, compile=time.perf_counter() - t2)
     # trace every array index / function argument (wider than 256 bits: as 256-bit chunks)
@@ -149,11 +150,29 @@ def _prepare(conjuncts, ctx, use_pools, timings) -> Query:
     # then the variables only a cell index reads (traced too: the witness
     # carries their values, so the cell and the formula agree)
     have = {n.id for n in prog.leaf_nodes}
-    extra = [v for v in free_vars(arg_terms) if v.op == "var" and v.id not in have]
+    extra = [v for v in _free_vars(arg_terms, ctx) if v.op == "var" and v.id not in have]
     traced = list(prog.leaf_nodes) + extra + arg_terms
     q = Query(ctx, conj, low, prog, lambda: _witness_program(prog, traced), arg_terms)
     q.arg_chunks = arg_chunks
     return q
+
+
+def _free_vars(terms: List[Node], ctx: Ctx) -> List[Node]:
+    """free_vars(terms); in a long-lived context from each term's own list,
+    kept per term id and merged by first occurrence (the same list: see
+    lower._topo_memo)."""
+    if not getattr(ctx, "long_lived", False):
+        return free_vars(terms)
+    memo = ctx.__dict__.setdefault("_free_vars", {})
+    out: Dict[int, Node] = {}
+    for t in terms:
+        fv = memo.get(t.id)
+        if fv is None:
+            fv = memo[t.id] = tuple(free_vars([t]))
+        for v in fv:
+            if v.id not in out:
+                out[v.id] = v
+    return list(out.values())
 
 
 # Python-side phase times of WitnessEngine.search (tools/dropin_profile.py):

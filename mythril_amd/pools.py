@@ -631,6 +631,7 @@ def harvest(conjuncts: List[Node], leaves: Optional[List[Node]], pool_size: int 
     specs: Dict[str, LeafSpec] = {}
     uniq_consts = list(dict.fromkeys(consts))[:256]
     tails: Dict[int, List[int]] = {}   # width -> the constants' proposals, deduplicated
+    plain_pools: Dict[int, List[int]] = {}   # width -> the pool of a leaf with no proposals of its own
     nfixed = max(1, int(pool_size * (1 - random_share)))
     # word ties first: their bytes' pools are the word's (no pool of their own to build)
     tied = _tie_words(concats, {lf.name for lf in leaves if lf.op == "var"}, word_props, set(exact), uniq_consts,
@@ -647,21 +648,29 @@ def harvest(conjuncts: List[Node], leaves: Optional[List[Node]], pool_size: int 
         actors = ACTORS if w >= 160 and any(t in leaf.name.lower() for t in _ADDRESS_WORDS) else ()
         # lazily: the pool fills after a few dozen values, and the byte split of
         # 256 constants for every calldata byte leaf was most of prepare()'s time
-        tail = tails.get(w)
-        if tail is None:
-            tail = tails[w] = list(dict.fromkeys(_const_props(uniq_consts, m, w == 8)))
-        cand = itertools.chain(proposals.get(leaf.name, ()), actors, (0, 1, 2, m, 1 << (w - 1), m - 1), tail)
-        pool: List[Optional[int]] = []
-        seen = set()
-        add, put, k = seen.add, pool.append, 0
-        for v in itertools.chain((c[leaf.name] for c in combos if leaf.name in c), cand) if combos else cand:
-            v &= m
-            if v not in seen:
-                add(v)
-                put(v)
-                k += 1
-                if k >= nfixed:
-                    break
+        props = proposals.get(leaf.name, ())
+        plain = not props and not actors and not (combos and any(leaf.name in c for c in combos))
+        got = plain_pools.get(w) if plain else None     # a leaf nothing proposes: its width's pool
+        if got is not None:
+            pool = list(got)
+        else:
+            tail = tails.get(w)
+            if tail is None:
+                tail = tails[w] = list(dict.fromkeys(_const_props(uniq_consts, m, w == 8)))
+            cand = itertools.chain(props, actors, (0, 1, 2, m, 1 << (w - 1), m - 1), tail)
+            pool = []
+            seen = set()
+            add, put, k = seen.add, pool.append, 0
+            for v in itertools.chain((c[leaf.name] for c in combos if leaf.name in c), cand) if combos else cand:
+                v &= m
+                if v not in seen:
+                    add(v)
+                    put(v)
+                    k += 1
+                    if k >= nfixed:
+                        break
+            if plain:
+                plain_pools[w] = list(pool)
         if w == 1:
             pool = [0, 1]
         else:
