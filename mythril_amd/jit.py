@@ -56,6 +56,17 @@ CHECK_SYNC = os.environ.get("MW_JIT_CHECK_SYNC", "0") == "1"
 # v_mad_u64_u32 carry-outs counted per column) instead of mul8's rows; C5
 # 17.51 -> 17.40 ms per 2^22 launch (profiles/r6k/ab_c5_mulcols.json)
 MUL_COLS = os.environ.get("MW_JIT_MUL_COLS", "1") == "1"
+# An LDS leaf's reload is placed this many body lines before its use (not
+# before the leaf's own store), so its latency overlaps the instructions in
+# between; 0 reloads right before the use.  C5 per 2^22 launch (tools/ab_c5.py,
+# profiles/r6p): 0 lines 17.41 ms, 8 lines 16.91, 16 lines 16.88, 32 lines
+# 16.85, 64 lines 20.93 ms; every line of distance keeps a reloaded leaf live
+# longer, and past 8 LLVM spills to scratch (HBM writes per launch +25 MB at
+# 8 lines, +300 MB at 16, +350 MB at 32), so 8 it is
+LDS_AHEAD = int(os.environ.get("MW_JIT_LDS_AHEAD", "8"))
+# ... or (when > 0) as far back as that much estimated work (insn_weight, in
+# machine instructions) of the lines in between
+LDS_AHEAD_W = int(os.environ.get("MW_JIT_LDS_AHEAD_W", "0"))
 M32 = 0xFFFFFFFF
 
 _WBIN = {"W_ADD": "w_add", "W_SUB": "w_sub", "W_MUL": "w_mul", "W_AND": "w_and", "W_OR": "w_or",
@@ -172,6 +183,8 @@ class _Gen:
         self.lines: List[str] = []
         self.since_split = 0
         self.nf = 0
+        self.put_at: Dict[int, int] = {}     # LDS leaf vreg -> index of its store line
+        self.line_w: List[int] = []          # estimated work of each line (_place_reloads)
 
     def W(self, s) -> str:
         if isinstance(s, Const):
@@ -186,7 +199,7 @@ class _Gen:
         slot = self.lds_slot.get(s.id)
         if slot is not None:
             self.nl += 1
-            self.pre.append(f"u32 L{self.nl}[8]; jit::lds_get8({slot}u, L{self.nl});")
+            self.pre.append(("R", f"u32 L{self.nl}[8]; jit::lds_get8({slot}u, L{self.nl});", s.id))
             return f"L{self.nl}"
         return f"v{s.id}"
 
@@ -204,6 +217,13 @@ class _Gen:
                 f"pool, seed, cand, {dst});")
 
     def emit(self, ins) -> None:
+        n0 = len(self.lines)
+        self._emit(ins)
+        self.line_w.extend([0] * (len(self.lines) - len(self.line_w)))
+        if len(self.lines) > n0:
+            self.line_w[-1] = insn_weight(ins)
+
+    def _emit(self, ins) -> None:
         op, w, d, S, imm = ins.op, ins.width, ins.dst, ins.srcs, ins.imm
         self.since_split += 1
         if self.since_split > SPLIT_EVERY and op != "CHECK":
@@ -239,6 +259,7 @@ class _Gen:
             self.since_split = 0
         elif op == "LEAF_W" and d.id in self.lds_slot:
             out(f"{{ u32 t_[8]; {self.leaf(imm, 't_')} jit::lds_put8({self.lds_slot[d.id]}u, t_); }}")
+            self.put_at[d.id] = len(self.lines)
         elif op == "LEAF_W":
             out(f"u32 {dn}[8]; {self.leaf(imm, dn)}")
         elif op == "LEAF_N":
@@ -307,9 +328,44 @@ class _Gen:
         else:
             raise ValueError(f"jit: no emitter for {op}")
 
+    def _place_reloads(self) -> List[str]:
+        """self.lines with every LDS reload ("R", text, leaf) moved LDS_AHEAD
+        lines earlier (never above its leaf's store): it goes before the
+        first other line at or after that point, in the order met."""
+        if LDS_AHEAD <= 0 and LDS_AHEAD_W <= 0:
+            return [x[1] if isinstance(x, tuple) else x for x in self.lines]
+        before: Dict[int, List[str]] = {}
+        rest: List[Tuple[int, str]] = []
+        for i, x in enumerate(self.lines):
+            if isinstance(x, tuple):
+                floor = self.put_at.get(x[2], -1) + 1
+                if LDS_AHEAD_W > 0:
+                    j, acc = i, 0
+                    while j > floor and acc < LDS_AHEAD_W:
+                        j -= 1
+                        acc += self.line_w[j]
+                else:
+                    j = max(i - LDS_AHEAD, floor)
+                before.setdefault(j, []).append(x[1])
+            else:
+                rest.append((i, x))
+        out: List[str] = []
+        pend = sorted(before)
+        k = 0
+        for i, x in rest:
+            while k < len(pend) and pend[k] <= i:
+                out += before[pend[k]]
+                k += 1
+            out.append(x)
+        while k < len(pend):
+            out += before[pend[k]]
+            k += 1
+        return out
+
     def body(self) -> str:
         for ins in self.insns:
             self.emit(ins)
+        self.lines = self._place_reloads()
         head = [f"template <bool EARLY>",
                 f"MW_HD bool {self.name}_body(const u32* __restrict__ pool, u64 seed, u64 cand, bool alive,",
                 f"                             u32 ctl, u32* __restrict__ trace, u64 tstride, u64 tidx,",

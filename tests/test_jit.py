@@ -196,3 +196,39 @@ def test_host_build_parts_and_to_whole_program():
     whole, _ = emu_eval(p, None, n, seed=s.seed, begin=begin)
     assert np.array_equal(acc, whole)
     assert acc[300] == 1  # the planted witness
+
+
+@pytest.mark.parametrize("ahead", [0, 8, 32])
+def test_lds_reloads_ahead_of_use(monkeypatch, ahead):
+    """jit.LDS_AHEAD: a leaf's LDS reload moves up to `ahead` body lines
+    before its use, never above the leaf's own store; the host build with
+    the reloads moved still gives the oracle's verdicts."""
+    import re
+    monkeypatch.setattr(jit, "LDS_AHEAD", ahead)
+    progs = _random_programs(4, 7400)
+    src = jit.generate([p for *_, p in progs], [f"t{k}" for k in range(len(progs))], "", lds_leaves=3)
+    bodies = src.split("template <bool EARLY>")[1:]     # names restart in every program's body
+    assert len(bodies) == len(progs)
+    for text in bodies:
+        body = text.splitlines()
+        decl, put = {}, {}
+        for i, ln in enumerate(body):
+            for m in re.finditer(r"u32 (L\d+)\[8\]; jit::lds_get8\((\d+)u", ln):
+                decl[m.group(1)] = (i, int(m.group(2)))
+            for m in re.finditer(r"jit::lds_put8\((\d+)u", ln):
+                put.setdefault(int(m.group(1)), []).append(i)
+        assert decl
+        for i, ln in enumerate(body):
+            for m in re.finditer(r"\b(L\d+)\b(?!\[8\])", ln):
+                at, slot = decl[m.group(1)]
+                assert at <= i, (m.group(1), at, i)
+                # the reload follows a store of its slot
+                assert any(p < at for p in put.get(slot, [])), (m.group(1), slot)
+    path, names = jit.compile_host([p for *_, p in progs], lds_leaves=3)
+    lib = ctypes.CDLL(str(path))
+    seed, begin, n = 0x5EED000A, 91, 24
+    for (dag, conj, extra, nodes, p), name in zip(progs, names):
+        v, _ = host_run(lib, name, p, seed, begin, n)
+        for j, m in enumerate(oracle_models(p, seed, begin, n)):
+            vals = eval_nodes(conj, m)
+            assert v[j] == int(all(vals[c.id] for c in conj)), f"{name} verdict {j}"

@@ -48,10 +48,21 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             # optimisation levels that trade instructions for code size (instruction-fetch wait)
             "os": {"EXTRA_FLAGS": ["-Os"]}, "o2": {"EXTRA_FLAGS": ["-O2"]},
             # 256-bit products by columns with v_mad_u64_u32 carry-outs (mw_jit.h mul8_cols)
-            "mulcols": {"EXTRA_FLAGS": [], "MUL_COLS": True}, "rows": {"EXTRA_FLAGS": [], "MUL_COLS": False}}
+            "mulcols": {"EXTRA_FLAGS": [], "MUL_COLS": True}, "rows": {"EXTRA_FLAGS": [], "MUL_COLS": False},
+            # LDS leaf reloads placed k body lines ahead of their use (jit.LDS_AHEAD)
+            "ahead8": {"EXTRA_FLAGS": [], "LDS_AHEAD": 8}, "ahead16": {"EXTRA_FLAGS": [], "LDS_AHEAD": 16},
+            "ahead32": {"EXTRA_FLAGS": [], "LDS_AHEAD": 32}, "ahead64": {"EXTRA_FLAGS": [], "LDS_AHEAD": 64},
+            "a32l12": {"EXTRA_FLAGS": [], "LDS_AHEAD": 32, "lds": 12},
+            "a32l14": {"EXTRA_FLAGS": [], "LDS_AHEAD": 32, "lds": 14},
+            "a32l8": {"EXTRA_FLAGS": [], "LDS_AHEAD": 32, "lds": 8},
+            # ... by estimated work instead of lines (jit.LDS_AHEAD_W)
+            "w60": {"EXTRA_FLAGS": [], "LDS_AHEAD_W": 60}, "w120": {"EXTRA_FLAGS": [], "LDS_AHEAD_W": 120},
+            "w240": {"EXTRA_FLAGS": [], "LDS_AHEAD_W": 240}, "w480": {"EXTRA_FLAGS": [], "LDS_AHEAD_W": 480}}
 
 
 MUL_COLS_DEFAULT = jit.MUL_COLS
+LDS_AHEAD_DEFAULT = jit.LDS_AHEAD
+LDS_AHEAD_W_DEFAULT = jit.LDS_AHEAD_W
 
 
 def main():
@@ -66,7 +77,8 @@ def main():
     p = compile_program(syn.conjuncts)
     images = {}
     for v in a.variants.split(","):
-        opts = {"MUL_COLS": MUL_COLS_DEFAULT, **VARIANTS[v]}
+        opts = {"MUL_COLS": MUL_COLS_DEFAULT, "LDS_AHEAD": LDS_AHEAD_DEFAULT, "LDS_AHEAD_W": LDS_AHEAD_W_DEFAULT,
+                **VARIANTS[v]}
         il = opts.pop("interleave", 1)
         waves, lds = opts.pop("waves", 2), opts.pop("lds", 10)
         for k, val in opts.items():
