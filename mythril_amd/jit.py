@@ -67,6 +67,9 @@ LDS_AHEAD = int(os.environ.get("MW_JIT_LDS_AHEAD", "8"))
 # ... or (when > 0) as far back as that much estimated work (insn_weight, in
 # machine instructions) of the lines in between
 LDS_AHEAD_W = int(os.environ.get("MW_JIT_LDS_AHEAD_W", "0"))
+# ... and never above a line at least this heavy (insn_weight: the divisions,
+# where LLVM already runs short of registers)
+LDS_AHEAD_STOP = int(os.environ.get("MW_JIT_LDS_AHEAD_STOP", str(1 << 30)))
 M32 = 0xFFFFFFFF
 
 _WBIN = {"W_ADD": "w_add", "W_SUB": "w_sub", "W_MUL": "w_mul", "W_AND": "w_and", "W_OR": "w_or",
@@ -344,6 +347,10 @@ class _Gen:
                     while j > floor and acc < LDS_AHEAD_W:
                         j -= 1
                         acc += self.line_w[j]
+                elif LDS_AHEAD_STOP < (1 << 30):
+                    j = i
+                    while j > floor and i - j < LDS_AHEAD and self.line_w[j - 1] < LDS_AHEAD_STOP:
+                        j -= 1
                 else:
                     j = max(i - LDS_AHEAD, floor)
                 before.setdefault(j, []).append(x[1])

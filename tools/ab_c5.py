@@ -57,12 +57,19 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             "a32l8": {"EXTRA_FLAGS": [], "LDS_AHEAD": 32, "lds": 8},
             # ... by estimated work instead of lines (jit.LDS_AHEAD_W)
             "w60": {"EXTRA_FLAGS": [], "LDS_AHEAD_W": 60}, "w120": {"EXTRA_FLAGS": [], "LDS_AHEAD_W": 120},
-            "w240": {"EXTRA_FLAGS": [], "LDS_AHEAD_W": 240}, "w480": {"EXTRA_FLAGS": [], "LDS_AHEAD_W": 480}}
+            "w240": {"EXTRA_FLAGS": [], "LDS_AHEAD_W": 240}, "w480": {"EXTRA_FLAGS": [], "LDS_AHEAD_W": 480},
+            # ... not above a division (jit.LDS_AHEAD_STOP)
+            "a8s": {"EXTRA_FLAGS": [], "LDS_AHEAD": 8, "LDS_AHEAD_STOP": 500},
+            "a16s": {"EXTRA_FLAGS": [], "LDS_AHEAD": 16, "LDS_AHEAD_STOP": 500},
+            "a8m": {"EXTRA_FLAGS": [], "LDS_AHEAD": 8, "LDS_AHEAD_STOP": 100},
+            "a4": {"EXTRA_FLAGS": [], "LDS_AHEAD": 4},
+            "a32s": {"EXTRA_FLAGS": [], "LDS_AHEAD": 32, "LDS_AHEAD_STOP": 500}}
 
 
 MUL_COLS_DEFAULT = jit.MUL_COLS
 LDS_AHEAD_DEFAULT = jit.LDS_AHEAD
 LDS_AHEAD_W_DEFAULT = jit.LDS_AHEAD_W
+LDS_AHEAD_STOP_DEFAULT = jit.LDS_AHEAD_STOP
 
 
 def main():
@@ -78,7 +85,7 @@ def main():
     images = {}
     for v in a.variants.split(","):
         opts = {"MUL_COLS": MUL_COLS_DEFAULT, "LDS_AHEAD": LDS_AHEAD_DEFAULT, "LDS_AHEAD_W": LDS_AHEAD_W_DEFAULT,
-                **VARIANTS[v]}
+                "LDS_AHEAD_STOP": LDS_AHEAD_STOP_DEFAULT, **VARIANTS[v]}
         il = opts.pop("interleave", 1)
         waves, lds = opts.pop("waves", 2), opts.pop("lds", 10)
         for k, val in opts.items():
