@@ -56,20 +56,22 @@ CHECK_SYNC = os.environ.get("MW_JIT_CHECK_SYNC", "0") == "1"
 # v_mad_u64_u32 carry-outs counted per column) instead of mul8's rows; C5
 # 17.51 -> 17.40 ms per 2^22 launch (profiles/r6k/ab_c5_mulcols.json)
 MUL_COLS = os.environ.get("MW_JIT_MUL_COLS", "1") == "1"
-# An LDS leaf's reload is placed this many body lines before its use (not
-# before the leaf's own store), so its latency overlaps the instructions in
-# between; 0 reloads right before the use.  C5 per 2^22 launch (tools/ab_c5.py,
-# profiles/r6p): 0 lines 17.41 ms, 8 lines 16.91, 16 lines 16.88, 32 lines
-# 16.85, 64 lines 20.93 ms; every line of distance keeps a reloaded leaf live
-# longer, and past 8 LLVM spills to scratch (HBM writes per launch +25 MB at
-# 8 lines, +300 MB at 16, +350 MB at 32), so 8 it is
-LDS_AHEAD = int(os.environ.get("MW_JIT_LDS_AHEAD", "8"))
+# An LDS leaf's reload is placed up to this many body lines before its use
+# (not before the leaf's own store, and not above a division: LDS_AHEAD_STOP),
+# so its latency overlaps the instructions in between; 0 reloads right before
+# the use.  C5 per 2^22 launch (tools/ab_c5.py, profiles/r6p): right before
+# the use 17.41 ms; 8 / 16 / 32 lines 16.91 / 16.88 / 16.85 ms, but hoisted
+# into the divisions' register pressure LLVM spills to scratch (+25 / +300 /
+# +350 MB of HBM writes per launch) and 64 lines spill so much it is slower
+# (20.93 ms); 32 lines stopping at divisions 16.93 ms with the spills of the
+# unhoisted kernel (12 bytes per lane), so that is the default
+LDS_AHEAD = int(os.environ.get("MW_JIT_LDS_AHEAD", "32"))
 # ... or (when > 0) as far back as that much estimated work (insn_weight, in
 # machine instructions) of the lines in between
 LDS_AHEAD_W = int(os.environ.get("MW_JIT_LDS_AHEAD_W", "0"))
 # ... and never above a line at least this heavy (insn_weight: the divisions,
 # where LLVM already runs short of registers)
-LDS_AHEAD_STOP = int(os.environ.get("MW_JIT_LDS_AHEAD_STOP", str(1 << 30)))
+LDS_AHEAD_STOP = int(os.environ.get("MW_JIT_LDS_AHEAD_STOP", "500"))
 M32 = 0xFFFFFFFF
 
 _WBIN = {"W_ADD": "w_add", "W_SUB": "w_sub", "W_MUL": "w_mul", "W_AND": "w_and", "W_OR": "w_or",
