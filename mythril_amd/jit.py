@@ -63,9 +63,10 @@ MUL_COLS = os.environ.get("MW_JIT_MUL_COLS", "1") == "1"
 # the use 17.41 ms; 8 / 16 / 32 lines 16.91 / 16.88 / 16.85 ms, but hoisted
 # into the divisions' register pressure LLVM spills to scratch (+25 / +300 /
 # +350 MB of HBM writes per launch) and 64 lines spill so much it is slower
-# (20.93 ms); 32 lines stopping at divisions 16.93 ms with the spills of the
-# unhoisted kernel (12 bytes per lane), so that is the default
-LDS_AHEAD = int(os.environ.get("MW_JIT_LDS_AHEAD", "32"))
+# (20.93 ms).  Stopping at divisions: 8 / 16 / 32 lines 16.98 / 16.95 /
+# 16.94 ms with 3 / 2 / 11 VGPRs spilled (the unhoisted kernel: 2); 16 lines
+# keeps the unhoisted kernel's 12 scratch bytes per lane, so that is the default
+LDS_AHEAD = int(os.environ.get("MW_JIT_LDS_AHEAD", "16"))
 # ... or (when > 0) as far back as that much estimated work (insn_weight, in
 # machine instructions) of the lines in between
 LDS_AHEAD_W = int(os.environ.get("MW_JIT_LDS_AHEAD_W", "0"))
