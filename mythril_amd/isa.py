@@ -170,15 +170,6 @@ ASM_FUSED = [
     ("CHECK", "LEAF_W"),
     ("LEAF_N", "N_ITE"),
     ("LEAF_W", "N_ULT"),
-    # round 6 (tools/opcode_ngrams.py on the corpus after leaf rematerialisation,
-    # sequences without a chaining handler): 0.579 -> 0.52 dispatches per instruction
-    ("N_OR", "N_OR", "N_OR", "W_ZEXTN"),
-    ("W_ITE", "W_ITE"),
-    ("N_EQ", "CHECK", "LEAF_W"),
-    ("SPILL_N", "SPILL_N", "SPILL_N", "SPILL_N"),
-    ("N_EQ", "LEAF_W"),
-    ("LEAF_N", "CHECK_GRID", "LEAF_N", "CHECK_GRID"),
-    ("N_EQ", "N_OR", "CHECK", "LEAF_W"),
 ]
 assert all(2 <= len(t) <= ASM_FUSED_MAX and not {"W_CDINS", "END"} & set(t)
            and set(t) <= set(ASM_OPCODES) for t in ASM_FUSED)
