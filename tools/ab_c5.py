@@ -63,13 +63,18 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             "a16s": {"EXTRA_FLAGS": [], "LDS_AHEAD": 16, "LDS_AHEAD_STOP": 500},
             "a8m": {"EXTRA_FLAGS": [], "LDS_AHEAD": 8, "LDS_AHEAD_STOP": 100},
             "a4": {"EXTRA_FLAGS": [], "LDS_AHEAD": 4},
-            "a32s": {"EXTRA_FLAGS": [], "LDS_AHEAD": 32, "LDS_AHEAD_STOP": 500}}
+            "a32s": {"EXTRA_FLAGS": [], "LDS_AHEAD": 32, "LDS_AHEAD_STOP": 500},
+            # basic-block length of the straight-line body (jit.SPLIT_EVERY, default 48)
+            "sp32": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 32}, "sp64": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 64},
+            "sp96": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 96}, "sp128": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 128},
+            "sp192": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 192}, "sp256": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 256}}
 
 
 MUL_COLS_DEFAULT = jit.MUL_COLS
 LDS_AHEAD_DEFAULT = jit.LDS_AHEAD
 LDS_AHEAD_W_DEFAULT = jit.LDS_AHEAD_W
 LDS_AHEAD_STOP_DEFAULT = jit.LDS_AHEAD_STOP
+SPLIT_EVERY_DEFAULT = jit.SPLIT_EVERY
 
 
 def main():
@@ -85,7 +90,7 @@ def main():
     images = {}
     for v in a.variants.split(","):
         opts = {"MUL_COLS": MUL_COLS_DEFAULT, "LDS_AHEAD": LDS_AHEAD_DEFAULT, "LDS_AHEAD_W": LDS_AHEAD_W_DEFAULT,
-                "LDS_AHEAD_STOP": LDS_AHEAD_STOP_DEFAULT, **VARIANTS[v]}
+                "LDS_AHEAD_STOP": LDS_AHEAD_STOP_DEFAULT, "SPLIT_EVERY": SPLIT_EVERY_DEFAULT, **VARIANTS[v]}
         il = opts.pop("interleave", 1)
         waves, lds = opts.pop("waves", 2), opts.pop("lds", 10)
         for k, val in opts.items():
