@@ -52,6 +52,7 @@ SPLIT_KIND = os.environ.get("MW_JIT_SPLIT", "branch")
 # experiments (tools/ab_c5.py): a workgroup barrier after every conjunct of the
 # exhaustive variant, keeping a block's waves at the same place in the code
 CHECK_SYNC = os.environ.get("MW_JIT_CHECK_SYNC", "0") == "1"
+CHECK_SYNC_EVERY = int(os.environ.get("MW_JIT_CHECK_SYNC_EVERY", "1"))   # ... after every k-th conjunct
 # 256-bit products of two register operands by columns (mw_jit.h mul8_cols:
 # v_mad_u64_u32 carry-outs counted per column) instead of mul8's rows; C5
 # 17.51 -> 17.40 ms per 2^22 launch (profiles/r6k/ab_c5_mulcols.json)
@@ -191,6 +192,7 @@ class _Gen:
         self.nf = 0
         self.put_at: Dict[int, int] = {}     # LDS leaf vreg -> index of its store line
         self.line_w: List[int] = []          # estimated work of each line (_place_reloads)
+        self.nchecks = 0
 
     def W(self, s) -> str:
         if isinstance(s, Const):
@@ -260,7 +262,9 @@ class _Gen:
         if d is not None:
             dn = f"v{d.id}" if d.cls == "W" else f"n{d.id}"
         if op == "CHECK":
-            tail = "{ JIT_SPLIT(); JIT_SYNC(); }" if CHECK_SYNC else "JIT_SPLIT();"
+            self.nchecks += 1
+            sync = CHECK_SYNC and self.nchecks % CHECK_SYNC_EVERY == 0
+            tail = "{ JIT_SPLIT(); JIT_SYNC(); }" if sync else "JIT_SPLIT();"
             out(f"alive = jit::check(alive, {A[0]}); if (EARLY) {{ if (jit::none(alive)) break; }} else {tail}")
             self.since_split = 0
         elif op == "LEAF_W" and d.id in self.lds_slot:

@@ -67,7 +67,11 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             # basic-block length of the straight-line body (jit.SPLIT_EVERY, default 48)
             "sp32": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 32}, "sp64": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 64},
             "sp96": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 96}, "sp128": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 128},
-            "sp192": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 192}, "sp256": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 256}}
+            "sp192": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 192}, "sp256": {"EXTRA_FLAGS": [], "SPLIT_EVERY": 256},
+            # a workgroup barrier after every k-th conjunct (the block's waves fetch the same code)
+            "sync8": {"EXTRA_FLAGS": [], "CHECK_SYNC": True, "CHECK_SYNC_EVERY": 8},
+            "sync32": {"EXTRA_FLAGS": [], "CHECK_SYNC": True, "CHECK_SYNC_EVERY": 32},
+            "sync128": {"EXTRA_FLAGS": [], "CHECK_SYNC": True, "CHECK_SYNC_EVERY": 128}}
 
 
 MUL_COLS_DEFAULT = jit.MUL_COLS
@@ -89,7 +93,7 @@ def main():
     p = compile_program(syn.conjuncts)
     images = {}
     for v in a.variants.split(","):
-        opts = {"MUL_COLS": MUL_COLS_DEFAULT, "LDS_AHEAD": LDS_AHEAD_DEFAULT, "LDS_AHEAD_W": LDS_AHEAD_W_DEFAULT,
+        opts = {"CHECK_SYNC": False, "CHECK_SYNC_EVERY": 1, "MUL_COLS": MUL_COLS_DEFAULT, "LDS_AHEAD": LDS_AHEAD_DEFAULT, "LDS_AHEAD_W": LDS_AHEAD_W_DEFAULT,
                 "LDS_AHEAD_STOP": LDS_AHEAD_STOP_DEFAULT, "SPLIT_EVERY": SPLIT_EVERY_DEFAULT, **VARIANTS[v]}
         il = opts.pop("interleave", 1)
         waves, lds = opts.pop("waves", 2), opts.pop("lds", 10)
