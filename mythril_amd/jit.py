@@ -74,6 +74,12 @@ LDS_AHEAD_W = int(os.environ.get("MW_JIT_LDS_AHEAD_W", "0"))
 # ... and never above a line at least this heavy (insn_weight: the divisions,
 # where LLVM already runs short of registers)
 LDS_AHEAD_STOP = int(os.environ.get("MW_JIT_LDS_AHEAD_STOP", "500"))
+# A use within this many body lines of the leaf's last reload reads that
+# copy instead of reloading (0: every use reloads).  C5 per 2^22 launch
+# (profiles/r6ze-r6zg, against 0 on the same box): 4 / 12 / 24 / 48 / 96 / 192
+# lines -0.5 / -0.8 / -1.0 / -1.5 / -2.1 / -2.3 %, with the unreused kernel's
+# spills up to 96 lines (12 bytes per lane) and 68 bytes at 192: 96
+LDS_REUSE = int(os.environ.get("MW_JIT_LDS_REUSE", "96"))
 M32 = 0xFFFFFFFF
 
 _WBIN = {"W_ADD": "w_add", "W_SUB": "w_sub", "W_MUL": "w_mul", "W_AND": "w_and", "W_OR": "w_or",
@@ -193,6 +199,7 @@ class _Gen:
         self.put_at: Dict[int, int] = {}     # LDS leaf vreg -> index of its store line
         self.line_w: List[int] = []          # estimated work of each line (_place_reloads)
         self.nchecks = 0
+        self.last_reload: Dict[int, Tuple[str, int]] = {}   # LDS leaf -> (its last reload, line)
 
     def W(self, s) -> str:
         if isinstance(s, Const):
@@ -206,7 +213,11 @@ class _Gen:
             raise ValueError("N register in a W operand")
         slot = self.lds_slot.get(s.id)
         if slot is not None:
+            last = self.last_reload.get(s.id)
+            if LDS_REUSE and last is not None and len(self.lines) - last[1] <= LDS_REUSE:
+                return last[0]      # reloaded a few lines ago: that copy again
             self.nl += 1
+            self.last_reload[s.id] = (f"L{self.nl}", len(self.lines))
             self.pre.append(("R", f"u32 L{self.nl}[8]; jit::lds_get8({slot}u, L{self.nl});", s.id))
             return f"L{self.nl}"
         return f"v{s.id}"

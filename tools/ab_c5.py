@@ -71,7 +71,11 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             # a workgroup barrier after every k-th conjunct (the block's waves fetch the same code)
             "sync8": {"EXTRA_FLAGS": [], "CHECK_SYNC": True, "CHECK_SYNC_EVERY": 8},
             "sync32": {"EXTRA_FLAGS": [], "CHECK_SYNC": True, "CHECK_SYNC_EVERY": 32},
-            "sync128": {"EXTRA_FLAGS": [], "CHECK_SYNC": True, "CHECK_SYNC_EVERY": 128}}
+            "sync128": {"EXTRA_FLAGS": [], "CHECK_SYNC": True, "CHECK_SYNC_EVERY": 128},
+            # a leaf's recent LDS reload read again instead of reloading (jit.LDS_REUSE)
+            "reuse4": {"EXTRA_FLAGS": [], "LDS_REUSE": 4}, "reuse12": {"EXTRA_FLAGS": [], "LDS_REUSE": 12},
+            "reuse24": {"EXTRA_FLAGS": [], "LDS_REUSE": 24}, "reuse48": {"EXTRA_FLAGS": [], "LDS_REUSE": 48},
+            "reuse96": {"EXTRA_FLAGS": [], "LDS_REUSE": 96}, "reuse192": {"EXTRA_FLAGS": [], "LDS_REUSE": 192}}
 
 
 MUL_COLS_DEFAULT = jit.MUL_COLS
@@ -93,7 +97,7 @@ def main():
     p = compile_program(syn.conjuncts)
     images = {}
     for v in a.variants.split(","):
-        opts = {"CHECK_SYNC": False, "CHECK_SYNC_EVERY": 1, "MUL_COLS": MUL_COLS_DEFAULT, "LDS_AHEAD": LDS_AHEAD_DEFAULT, "LDS_AHEAD_W": LDS_AHEAD_W_DEFAULT,
+        opts = {"CHECK_SYNC": False, "CHECK_SYNC_EVERY": 1, "LDS_REUSE": 0, "MUL_COLS": MUL_COLS_DEFAULT, "LDS_AHEAD": LDS_AHEAD_DEFAULT, "LDS_AHEAD_W": LDS_AHEAD_W_DEFAULT,
                 "LDS_AHEAD_STOP": LDS_AHEAD_STOP_DEFAULT, "SPLIT_EVERY": SPLIT_EVERY_DEFAULT, **VARIANTS[v]}
         il = opts.pop("interleave", 1)
         waves, lds = opts.pop("waves", 2), opts.pop("lds", 10)
