@@ -75,7 +75,10 @@ VARIANTS = {"base": {"EXTRA_FLAGS": []},
             # a leaf's recent LDS reload read again instead of reloading (jit.LDS_REUSE)
             "reuse4": {"EXTRA_FLAGS": [], "LDS_REUSE": 4}, "reuse12": {"EXTRA_FLAGS": [], "LDS_REUSE": 12},
             "reuse24": {"EXTRA_FLAGS": [], "LDS_REUSE": 24}, "reuse48": {"EXTRA_FLAGS": [], "LDS_REUSE": 48},
-            "reuse96": {"EXTRA_FLAGS": [], "LDS_REUSE": 96}, "reuse192": {"EXTRA_FLAGS": [], "LDS_REUSE": 192}}
+            "reuse96": {"EXTRA_FLAGS": [], "LDS_REUSE": 96}, "reuse192": {"EXTRA_FLAGS": [], "LDS_REUSE": 192},
+            "reuse128": {"EXTRA_FLAGS": [], "LDS_REUSE": 128},
+            "l8r96": {"EXTRA_FLAGS": [], "LDS_REUSE": 96, "lds": 8},
+            "a32r96": {"EXTRA_FLAGS": [], "LDS_REUSE": 96, "LDS_AHEAD": 32}}
 
 
 MUL_COLS_DEFAULT = jit.MUL_COLS
@@ -83,6 +86,7 @@ LDS_AHEAD_DEFAULT = jit.LDS_AHEAD
 LDS_AHEAD_W_DEFAULT = jit.LDS_AHEAD_W
 LDS_AHEAD_STOP_DEFAULT = jit.LDS_AHEAD_STOP
 SPLIT_EVERY_DEFAULT = jit.SPLIT_EVERY
+LDS_REUSE_DEFAULT = jit.LDS_REUSE
 
 
 def main():
@@ -97,7 +101,7 @@ def main():
     p = compile_program(syn.conjuncts)
     images = {}
     for v in a.variants.split(","):
-        opts = {"CHECK_SYNC": False, "CHECK_SYNC_EVERY": 1, "LDS_REUSE": 0, "MUL_COLS": MUL_COLS_DEFAULT, "LDS_AHEAD": LDS_AHEAD_DEFAULT, "LDS_AHEAD_W": LDS_AHEAD_W_DEFAULT,
+        opts = {"CHECK_SYNC": False, "CHECK_SYNC_EVERY": 1, "LDS_REUSE": LDS_REUSE_DEFAULT, "MUL_COLS": MUL_COLS_DEFAULT, "LDS_AHEAD": LDS_AHEAD_DEFAULT, "LDS_AHEAD_W": LDS_AHEAD_W_DEFAULT,
                 "LDS_AHEAD_STOP": LDS_AHEAD_STOP_DEFAULT, "SPLIT_EVERY": SPLIT_EVERY_DEFAULT, **VARIANTS[v]}
         il = opts.pop("interleave", 1)
         waves, lds = opts.pop("waves", 2), opts.pop("lds", 10)
